@@ -1,0 +1,267 @@
+// Gather / scatter kernels around the neighbour indices (HBM-bound):
+//   group fwd/bwd     reference `group` gather + centroid subtract (+ /r)      common.py:62-71
+//   maxk fwd/bwd      reference `reduce(..., 'max')` over the K axis              common.py:85-86
+//   interp fwd/bwd    reference `interpolate` IDW sum over the 3 neighbours       common.py:115-122
+//   edge fwd/bwd      reference `get_graph_feature` cat(x_j - x_i, x_i)           dgcnn.py:41-53
+//
+// Layout: point-major rows, (rows, channels) row-contiguous fp32, so every
+// neighbour fetch is one contiguous channel vector (coalesced across lanes).
+// Backward scatters use fp32 atomics (global_atomic_add_f32); forward results
+// are bit-exact with the reference's CPU arithmetic order.
+#include "pcs_common.hpp"
+
+namespace pcs {
+
+__device__ __forceinline__ long long gtid() { return (long long)blockIdx.x * blockDim.x + threadIdx.x; }
+__device__ __forceinline__ long long gstride() { return (long long)gridDim.x * blockDim.x; }
+
+static inline dim3 grid_for(long long n, int block = 256) {
+    long long g = (n + block - 1) / block;
+    if (g > 65536) g = 65536;
+    if (g < 1) g = 1;
+    return dim3((unsigned)g);
+}
+
+// ------------------------------------------------------------------ group
+__global__ void group_fwd_kernel(const float* __restrict__ xyz, const float* __restrict__ feats,
+                                 const float* __restrict__ cent, const int* __restrict__ idx, int C, int N, int K,
+                                 int D, float r, int normalize, float* __restrict__ out, long long total) {
+    const int W = 3 + D;
+    for (long long t = gtid(); t < total; t += gstride()) {
+        const long long row = t / W;
+        const int ch = (int)(t - row * W);
+        const long long g = row / K;          // centroid row b*C + c
+        const int b = (int)(g / C);
+        const int p = idx[row];
+        float v;
+        if (ch < 3) {
+            v = xyz[((long long)b * N + p) * 3 + ch] - cent[g * 3 + ch];
+            if (normalize) v = v / r;
+        } else {
+            v = feats[((long long)b * N + p) * D + (ch - 3)];
+        }
+        out[t] = v;
+    }
+}
+
+__global__ void group_bwd_kernel(const float* __restrict__ gout, const int* __restrict__ idx, int C, int N, int K,
+                                 int D, float* __restrict__ gfeats, long long total) {
+    const int W = 3 + D;
+    for (long long t = gtid(); t < total; t += gstride()) {
+        const long long row = t / D;
+        const int ch = (int)(t - row * D);
+        const int b = (int)(row / ((long long)K * C));
+        const int p = idx[row];
+        atomicAdd(&gfeats[((long long)b * N + p) * D + ch], gout[row * W + 3 + ch]);
+    }
+}
+
+// ------------------------------------------------------------------ max over K
+__global__ void maxk_fwd_kernel(const float* __restrict__ x, int K, int Ch, float* __restrict__ out,
+                                unsigned char* __restrict__ arg, long long total) {
+    for (long long t = gtid(); t < total; t += gstride()) {
+        const long long g = t / Ch;
+        const int ch = (int)(t - g * Ch);
+        const float* base = x + g * K * Ch + ch;
+        float m = base[0];
+        int a = 0;
+        for (int k = 1; k < K; ++k) {
+            const float v = base[(long long)k * Ch];
+            if (v > m || (v != v && m == m)) { m = v; a = k; }   // first max; NaN propagates like torch.max
+        }
+        out[t] = m;
+        arg[t] = (unsigned char)a;
+    }
+}
+
+__global__ void maxk_bwd_kernel(const float* __restrict__ gout, const unsigned char* __restrict__ arg, int K,
+                                int Ch, float* __restrict__ gx, long long total) {
+    for (long long t = gtid(); t < total; t += gstride()) {
+        const long long row = t / Ch;           // g*K + k
+        const int ch = (int)(t - row * Ch);
+        const long long g = row / K;
+        const int k = (int)(row - g * K);
+        const long long o = g * Ch + ch;
+        gx[t] = (arg[o] == k) ? gout[o] : 0.f;
+    }
+}
+
+// ------------------------------------------------------------------ 3-NN IDW interpolation
+// out[b,n, col_off + ch] (row stride ld_out) = sum_k (p[idx_k] * w_k) / norm,  w_k = 1/(d_k + 1e-9)
+__global__ void interp_fwd_kernel(const float* __restrict__ pts, const int* __restrict__ idx,
+                                  const float* __restrict__ dist, int N, int M, int D, float* __restrict__ out,
+                                  int ld_out, int col_off, long long total) {
+    for (long long t = gtid(); t < total; t += gstride()) {
+        const long long row = t / D;            // b*N + n
+        const int ch = (int)(t - row * D);
+        const int b = (int)(row / N);
+        const float w0 = 1.0f / (dist[row * 3 + 0] + 1e-9f);
+        const float w1 = 1.0f / (dist[row * 3 + 1] + 1e-9f);
+        const float w2 = 1.0f / (dist[row * 3 + 2] + 1e-9f);
+        const float nrm = (w0 + w1) + w2;
+        const float* P = pts + (long long)b * M * D + ch;
+        const float t0 = (P[(long long)idx[row * 3 + 0] * D] * w0) / nrm;
+        const float t1 = (P[(long long)idx[row * 3 + 1] * D] * w1) / nrm;
+        const float t2 = (P[(long long)idx[row * 3 + 2] * D] * w2) / nrm;
+        out[row * ld_out + col_off + ch] = (t0 + t1) + t2;
+    }
+}
+
+__global__ void interp_bwd_kernel(const float* __restrict__ gout, const int* __restrict__ idx,
+                                  const float* __restrict__ dist, int N, int M, int D, int ld_gout, int col_off,
+                                  float* __restrict__ gpts, long long total) {
+    for (long long t = gtid(); t < total; t += gstride()) {
+        const long long row = t / D;
+        const int ch = (int)(t - row * D);
+        const int b = (int)(row / N);
+        const float w0 = 1.0f / (dist[row * 3 + 0] + 1e-9f);
+        const float w1 = 1.0f / (dist[row * 3 + 1] + 1e-9f);
+        const float w2 = 1.0f / (dist[row * 3 + 2] + 1e-9f);
+        const float nrm = (w0 + w1) + w2;
+        const float gq = gout[row * ld_gout + col_off + ch] / nrm;
+        float* G = gpts + (long long)b * M * D + ch;
+        atomicAdd(&G[(long long)idx[row * 3 + 0] * D], gq * w0);
+        atomicAdd(&G[(long long)idx[row * 3 + 1] * D], gq * w1);
+        atomicAdd(&G[(long long)idx[row * 3 + 2] * D], gq * w2);
+    }
+}
+
+// ------------------------------------------------------------------ EdgeConv graph feature
+// out row (b,i,j) = [x[nbr] - x[i], x[i]]  (2D channels), x point-major (B, N, D)
+__global__ void edge_fwd_kernel(const float* __restrict__ x, const int* __restrict__ idx, int N, int k, int D,
+                                float* __restrict__ out, long long total) {
+    const int W = 2 * D;
+    for (long long t = gtid(); t < total; t += gstride()) {
+        const long long row = t / W;            // (b*N + i)*k + j
+        const int ch = (int)(t - row * W);
+        const long long pi = row / k;           // b*N + i
+        const int b = (int)(pi / N);
+        const float xi = x[pi * D + (ch < D ? ch : ch - D)];
+        if (ch < D) {
+            const int p = idx[row];
+            out[t] = x[((long long)b * N + p) * D + ch] - xi;
+        } else {
+            out[t] = xi;
+        }
+    }
+}
+
+// gx[i] += sum_j (g_b[i,j] - g_a[i,j]);  gx[nbr] += g_a[i,j]
+__global__ void edge_bwd_kernel(const float* __restrict__ gout, const int* __restrict__ idx, int N, int k, int D,
+                                float* __restrict__ gx, long long total) {
+    const int W = 2 * D;
+    for (long long t = gtid(); t < total; t += gstride()) {
+        const long long pi = t / D;             // b*N + i
+        const int ch = (int)(t - pi * D);
+        const int b = (int)(pi / N);
+        float acc = 0.f;
+        for (int j = 0; j < k; ++j) {
+            const long long row = pi * k + j;
+            const float ga = gout[row * W + ch];
+            const float gb = gout[row * W + D + ch];
+            acc += gb - ga;
+            atomicAdd(&gx[((long long)b * N + idx[row]) * D + ch], ga);
+        }
+        atomicAdd(&gx[pi * D + ch], acc);
+    }
+}
+
+}  // namespace pcs
+
+using namespace pcs;
+
+// Reference: models/utils/common.py:62-71.  out (B*C*K, 3+D).
+PCS_API int pcs_group_fwd(const float* xyz, const float* feats, const float* centroids, const int32_t* idx, int B,
+                          int N, int C, int K, int D, float r, int normalize, float* out, void* stream) {
+    PCS_CHECK_ARG(B >= 0 && N >= 1 && C >= 0 && K >= 1 && D >= 0, "pcs_group_fwd: bad sizes");
+    PCS_CHECK_ARG(xyz && centroids && idx && out && (D == 0 || feats), "pcs_group_fwd: null pointer");
+    const long long total = (long long)B * C * K * (3 + D);
+    if (total == 0) return 0;
+    hipLaunchKernelGGL(group_fwd_kernel, grid_for(total), dim3(256), 0, as_stream(stream), xyz, feats, centroids,
+                       idx, C, N, K, D, r, normalize, out, total);
+    return launch_status("pcs_group_fwd");
+}
+
+// Backward of the feature gather: grad_feats (B, N, D) += scatter of grad_out[..., 3:]
+// (grad_feats must be zeroed by the caller).
+PCS_API int pcs_group_bwd(const float* grad_out, const int32_t* idx, int B, int N, int C, int K, int D,
+                          float* grad_feats, void* stream) {
+    PCS_CHECK_ARG(B >= 0 && N >= 1 && C >= 0 && K >= 1 && D >= 0, "pcs_group_bwd: bad sizes");
+    const long long total = (long long)B * C * K * D;
+    if (total == 0) return 0;
+    PCS_CHECK_ARG(grad_out && idx && grad_feats, "pcs_group_bwd: null pointer");
+    hipLaunchKernelGGL(group_bwd_kernel, grid_for(total), dim3(256), 0, as_stream(stream), grad_out, idx, C, N, K, D,
+                       grad_feats, total);
+    return launch_status("pcs_group_bwd");
+}
+
+// Reference: common.py:85-86.  x (G*K, Ch) -> out (G, Ch), argmax (G, Ch) u8 (first max).
+PCS_API int pcs_maxk_fwd(const float* x, long long G, int K, int Ch, float* out, uint8_t* argmax, void* stream) {
+    PCS_CHECK_ARG(G >= 0 && K >= 1 && K <= 256 && Ch >= 1, "pcs_maxk_fwd: bad sizes (K must be 1..256)");
+    const long long total = G * Ch;
+    if (total == 0) return 0;
+    PCS_CHECK_ARG(x && out && argmax, "pcs_maxk_fwd: null pointer");
+    hipLaunchKernelGGL(maxk_fwd_kernel, grid_for(total), dim3(256), 0, as_stream(stream), x, K, Ch, out, argmax,
+                       total);
+    return launch_status("pcs_maxk_fwd");
+}
+
+PCS_API int pcs_maxk_bwd(const float* grad_out, const uint8_t* argmax, long long G, int K, int Ch, float* grad_x,
+                         void* stream) {
+    PCS_CHECK_ARG(G >= 0 && K >= 1 && K <= 256 && Ch >= 1, "pcs_maxk_bwd: bad sizes");
+    const long long total = G * K * Ch;
+    if (total == 0) return 0;
+    PCS_CHECK_ARG(grad_out && argmax && grad_x, "pcs_maxk_bwd: null pointer");
+    hipLaunchKernelGGL(maxk_bwd_kernel, grid_for(total), dim3(256), 0, as_stream(stream), grad_out, argmax, K, Ch,
+                       grad_x, total);
+    return launch_status("pcs_maxk_bwd");
+}
+
+// Reference: common.py:115-122.  pts (B, M, D); idx/dist (B, N, 3) from pcs_knn_select;
+// out[(b*N+n)*ld_out + col_off + ch].
+PCS_API int pcs_interp_fwd(const float* pts, const int32_t* idx, const float* dist, int B, int N, int M, int D,
+                           float* out, int ld_out, int col_off, void* stream) {
+    PCS_CHECK_ARG(B >= 0 && N >= 0 && M >= 3 && D >= 1 && ld_out >= col_off + D && col_off >= 0,
+                  "pcs_interp_fwd: bad sizes");
+    const long long total = (long long)B * N * D;
+    if (total == 0) return 0;
+    PCS_CHECK_ARG(pts && idx && dist && out, "pcs_interp_fwd: null pointer");
+    hipLaunchKernelGGL(interp_fwd_kernel, grid_for(total), dim3(256), 0, as_stream(stream), pts, idx, dist, N, M, D,
+                       out, ld_out, col_off, total);
+    return launch_status("pcs_interp_fwd");
+}
+
+// grad_pts (B, M, D) += IDW-weighted scatter (caller zeroes grad_pts).
+PCS_API int pcs_interp_bwd(const float* grad_out, const int32_t* idx, const float* dist, int B, int N, int M, int D,
+                           int ld_gout, int col_off, float* grad_pts, void* stream) {
+    PCS_CHECK_ARG(B >= 0 && N >= 0 && M >= 3 && D >= 1 && ld_gout >= col_off + D && col_off >= 0,
+                  "pcs_interp_bwd: bad sizes");
+    const long long total = (long long)B * N * D;
+    if (total == 0) return 0;
+    PCS_CHECK_ARG(grad_out && idx && dist && grad_pts, "pcs_interp_bwd: null pointer");
+    hipLaunchKernelGGL(interp_bwd_kernel, grid_for(total), dim3(256), 0, as_stream(stream), grad_out, idx, dist, N, M,
+                       D, ld_gout, col_off, grad_pts, total);
+    return launch_status("pcs_interp_bwd");
+}
+
+// Reference: dgcnn.py:41-53.  x (B, N, D) point-major; idx (B, N, k); out (B*N*k, 2D).
+PCS_API int pcs_edge_fwd(const float* x, const int32_t* idx, int B, int N, int k, int D, float* out, void* stream) {
+    PCS_CHECK_ARG(B >= 0 && N >= 1 && k >= 1 && D >= 1, "pcs_edge_fwd: bad sizes");
+    const long long total = (long long)B * N * k * 2 * D;
+    if (total == 0) return 0;
+    PCS_CHECK_ARG(x && idx && out, "pcs_edge_fwd: null pointer");
+    hipLaunchKernelGGL(edge_fwd_kernel, grid_for(total), dim3(256), 0, as_stream(stream), x, idx, N, k, D, out, total);
+    return launch_status("pcs_edge_fwd");
+}
+
+// grad_x (B, N, D) += backward of the graph feature (caller zeroes grad_x).
+PCS_API int pcs_edge_bwd(const float* grad_out, const int32_t* idx, int B, int N, int k, int D, float* grad_x,
+                         void* stream) {
+    PCS_CHECK_ARG(B >= 0 && N >= 1 && k >= 1 && D >= 1, "pcs_edge_bwd: bad sizes");
+    const long long total = (long long)B * N * D;
+    if (total == 0) return 0;
+    PCS_CHECK_ARG(grad_out && idx && grad_x, "pcs_edge_bwd: null pointer");
+    hipLaunchKernelGGL(edge_bwd_kernel, grid_for(total), dim3(256), 0, as_stream(stream), grad_out, idx, N, k, D,
+                       grad_x, total);
+    return launch_status("pcs_edge_bwd");
+}

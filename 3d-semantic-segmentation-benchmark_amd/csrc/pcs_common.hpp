@@ -1,0 +1,74 @@
+// Shared helpers for the pcseg HIP library (gfx950 / CDNA4, wave64).
+//
+// Conventions of the C ABI (include/pcseg.h):
+//   * every entry point takes caller-owned device pointers, plain sizes and a
+//     hipStream_t passed as void*; no allocation, no host sync inside;
+//   * returns 0 on success, otherwise a hipError_t-compatible code, with a
+//     thread-local message readable through pcs_last_error().
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#define PCS_API extern "C" __attribute__((visibility("default")))
+
+namespace pcs {
+
+// ------------------------------------------------------------ error plumbing
+void set_error(const char* fmt, ...);
+int launch_status(const char* what);   // reads hipGetLastError after a launch
+
+#define PCS_CHECK_ARG(cond, ...)                                   \
+    do {                                                           \
+        if (!(cond)) {                                             \
+            ::pcs::set_error(__VA_ARGS__);                         \
+            return (int)hipErrorInvalidValue;                      \
+        }                                                          \
+    } while (0)
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// ------------------------------------------------------------ device helpers
+constexpr int kWave = 64;
+
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+__device__ __forceinline__ unsigned long long ballot(bool p) { return __ballot(p); }
+
+// lanes strictly below this one
+__device__ __forceinline__ unsigned long long lanemask_lt() {
+    const int l = lane_id();
+    return l == 0 ? 0ull : (~0ull >> (64 - l));
+}
+
+__device__ __forceinline__ int popc64(unsigned long long m) { return __popcll(m); }
+
+__device__ __forceinline__ int ffs64(unsigned long long m) { return __ffsll((long long)m) - 1; }
+
+// wave-uniform read of lane `l` (l must be wave-uniform)
+__device__ __forceinline__ unsigned readlane_u(unsigned v, int l) {
+    return (unsigned)__builtin_amdgcn_readlane((int)v, l);
+}
+// lane `l` (wave-uniform) takes v: one v_cmp + v_cndmask, visible to the compiler
+__device__ __forceinline__ unsigned writelane_u(unsigned old, unsigned v, int l) {
+    return lane_id() == l ? v : old;
+}
+__device__ __forceinline__ float readlane_f(float v, int l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
+// bit pattern of a non-negative float (incl. +inf) orders like the float
+__device__ __forceinline__ unsigned fbits(float x) { return __float_as_uint(x); }
+
+// un-fused squared distance, evaluated exactly like the reference's
+// ((p - c) ** 2).sum(-1) on the CPU: ((dx*dx + dy*dy) + dz*dz), no FMA.
+__device__ __forceinline__ float sqdist_unfused(float px, float py, float pz, float cx, float cy, float cz) {
+    const float dx = __fsub_rn(px, cx);
+    const float dy = __fsub_rn(py, cy);
+    const float dz = __fsub_rn(pz, cz);
+    return __fadd_rn(__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)), __fmul_rn(dz, dz));
+}
+
+}  // namespace pcs

@@ -1,0 +1,84 @@
+"""ctypes binding of libpcseg.so, the gfx950 HIP library behind include/pcseg.h.
+
+The library is built in-tree by `csrc/Makefile` (see `__graft_entry__.build`).
+There is no CPU fallback: if the library is missing or a GPU op is called on a
+CPU tensor, the call raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, 'libpcseg.so')
+
+P = ctypes.c_void_p
+I32 = ctypes.c_int
+I64 = ctypes.c_longlong
+F32 = ctypes.c_float
+
+# name -> argtypes (all return int status), mirrors include/pcseg.h
+SIGNATURES = {
+    'pcs_fps': [P, I32, I32, I32, P, P, P, P],
+    'pcs_ball_query': [P, P, I32, I32, I32, F32, I32, P, P],
+    'pcs_knn_select': [P, P, I32, I32, I32, I32, P, P, P],
+    'pcs_knn': [P, I32, I32, I32, I32, P, P],
+    'pcs_group_fwd': [P, P, P, P, I32, I32, I32, I32, I32, F32, I32, P, P],
+    'pcs_group_bwd': [P, P, I32, I32, I32, I32, I32, P, P],
+    'pcs_maxk_fwd': [P, I64, I32, I32, P, P, P],
+    'pcs_maxk_bwd': [P, P, I64, I32, I32, P, P],
+    'pcs_interp_fwd': [P, P, P, I32, I32, I32, I32, P, I32, I32, P],
+    'pcs_interp_bwd': [P, P, P, I32, I32, I32, I32, I32, I32, P, P],
+    'pcs_edge_fwd': [P, P, I32, I32, I32, I32, P, P],
+    'pcs_edge_bwd': [P, P, I32, I32, I32, I32, P, P],
+}
+
+_lock = threading.Lock()
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Load (once) and type the library; raises if it was not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise RuntimeError(f'pcseg: HIP library not built ({LIB_PATH} missing); '
+                                   'run `python -c "import __graft_entry__ as g; g.build()"` or '
+                                   '`make -C 3d-semantic-segmentation-benchmark_amd/csrc`')
+            lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+            lib.pcs_last_error.restype = ctypes.c_char_p
+            lib.pcs_last_error.argtypes = []
+            lib.pcs_abi_version.restype = ctypes.c_int
+            for name, args in SIGNATURES.items():
+                fn = getattr(lib, name)
+                fn.argtypes = args
+                fn.restype = ctypes.c_int
+            _lib = lib
+    return _lib
+
+
+def stream_ptr(device: torch.device | None = None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def call(name: str, *args) -> None:
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        raise RuntimeError(f'{name} failed ({rc}): {lib.pcs_last_error().decode(errors="replace")}')
+
+
+def ptr(t: torch.Tensor | None) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+def check_cuda(*tensors: torch.Tensor) -> None:
+    for t in tensors:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError('pcseg ops run only on the GPU (no CPU fallback); got a CPU tensor')

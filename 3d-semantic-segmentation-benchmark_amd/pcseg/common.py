@@ -1,0 +1,195 @@
+"""Point-op library and PointNet++ building blocks -- drop-in for the reference's
+`models/utils/common.py` (same function/class names, signatures, parameter
+names, return conventions), executed by the gfx950 HIP kernels in libpcseg.so.
+
+Internally every activation is point-major rows (rows, channels); the
+reference's channel-first permutes become views at the module boundary.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from . import ops
+from .mlp import mlp_rows
+from .replay import active as _replay
+
+
+# --------------------------------------------------------------------------- functional API
+def _fps_start(B: int, N: int, device) -> torch.Tensor:
+    rp = _replay()
+    if rp is not None and rp.fps_starts:
+        return rp.fps_starts.pop(0).to(device=device, dtype=torch.int32)
+    # the reference draws its start exactly like this (common.py:22)
+    return torch.randint(0, N, (B,), dtype=torch.int, device=device)
+
+
+def sample_indices(coords: torch.Tensor, C: int):
+    """FPS -> (idx (B,C) int32, centroid coords (B,C,3))."""
+    B, N, _ = coords.shape
+    start = _fps_start(B, N, coords.device)
+    idx, cent = ops.fps(coords, C, start)
+    rp = _replay()
+    if rp is not None:
+        rp.rec_fps_starts.append(start.detach().cpu())
+        rp.rec_fps_idx.append(idx.detach().cpu())
+    return idx, cent
+
+
+def sample(coords: torch.Tensor, C: int) -> torch.Tensor:
+    """Reference `sample` (common.py:6-34): farthest point sampling, returns (B, C, 3)."""
+    return sample_indices(coords, C)[1]
+
+
+def _ball(cent, coords, r, K):
+    idx = ops.ball_query(cent, coords, r, K)
+    rp = _replay()
+    if rp is not None:
+        rp.rec_group_idx.append(idx.detach().cpu())
+    return idx
+
+
+def group(centroid_coords: torch.Tensor, coords: torch.Tensor, features: torch.Tensor, r: float, K: int,
+          normalize: bool = False) -> torch.Tensor:
+    """Reference `group` (common.py:37-71) -> (B, C, K, 3+D)."""
+    B, C, _ = centroid_coords.shape
+    idx = _ball(centroid_coords, coords, r, K)
+    rows = ops.group_rows(coords, features, centroid_coords, idx, r, normalize)
+    return rows.view(B, C, K, rows.shape[1])
+
+
+def reduce(x: torch.Tensor, type: str) -> torch.Tensor:
+    """Reference `reduce` (common.py:74-91).  x (B, C, K, D') -> (B, C, D')."""
+    if type == 'max':
+        B, C, K, D = x.shape
+        return ops.maxk(x.reshape(B * C * K, D), K).view(B, C, D)
+    if type == 'avg':
+        # kept bug-compatible with the reference (common.py:89 indexes [0] after the mean)
+        return torch.mean(x, dim=2)[0]
+    raise ValueError(f"'{type}' pooling not supported; use 'max' or 'avg'.")
+
+
+def interpolate(points: torch.Tensor, coords_1: torch.Tensor, coords_2: torch.Tensor, k: int = 3) -> torch.Tensor:
+    """Reference `interpolate` (common.py:94-122) -> (B, N, D).  k == 3 as in the reference's callers."""
+    if k != 3:
+        raise ValueError('pcseg interpolate supports k=3 (the reference default)')
+    B, N, _ = coords_1.shape
+    idx, dist = ops.knn_select(coords_1, coords_2, 3)
+    rp = _replay()
+    if rp is not None:
+        rp.rec_interp_idx.append(idx.detach().cpu())
+    return ops.interp_cat_rows(None, points, idx, dist).view(B, N, points.shape[2])
+
+
+# --------------------------------------------------------------------------- MLP blocks
+class MiniPointNet(nn.Module):
+    """Reference common.py:125-150 (Conv2d 1x1 -> BatchNorm2d -> ReLU)."""
+
+    def __init__(self, in_channels: int, mlps: list[int]):
+        super().__init__()
+        self.conv = nn.ModuleList()
+        self.batch = nn.ModuleList()
+        prev = in_channels
+        for m in mlps:
+            self.conv.append(nn.Conv2d(prev, m, (1, 1)))
+            self.batch.append(nn.BatchNorm2d(m))
+            prev = m
+
+    def forward_rows(self, x: torch.Tensor) -> torch.Tensor:
+        return mlp_rows(x, self.conv, self.batch)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        B, Cin, H, W = x.shape
+        rows = x.permute(0, 2, 3, 1).reshape(B * H * W, Cin)
+        return self.forward_rows(rows).view(B, H, W, -1).permute(0, 3, 1, 2)
+
+
+class UnitPointNet(nn.Module):
+    """Reference common.py:153-178 (Conv1d 1x1 -> BatchNorm1d -> ReLU)."""
+
+    def __init__(self, in_channels: int, mlps: list[int]):
+        super().__init__()
+        self.conv = nn.ModuleList()
+        self.batch = nn.ModuleList()
+        prev = in_channels
+        for m in mlps:
+            self.conv.append(nn.Conv1d(prev, m, 1))
+            self.batch.append(nn.BatchNorm1d(m))
+            prev = m
+
+    def forward_rows(self, x: torch.Tensor) -> torch.Tensor:
+        return mlp_rows(x, self.conv, self.batch)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        B, Cin, N = x.shape
+        rows = x.permute(0, 2, 1).reshape(B * N, Cin)
+        return self.forward_rows(rows).view(B, N, -1).permute(0, 2, 1)
+
+
+class SetAbstraction(nn.Module):
+    """Reference common.py:180-214: FPS -> ball query + group -> shared MLP -> max over K."""
+
+    def __init__(self, C: int, radius: float, in_channels: int, mlps: list[int], K: int = 32,
+                 pooling_type: str = 'max', grouping_norm: bool = False):
+        super().__init__()
+        self.point_net = MiniPointNet(in_channels, mlps)
+        self.C = C
+        self.radius = radius
+        self.K = K
+        self.pooling_type = pooling_type
+        self.grouping_norm = grouping_norm
+
+    def forward(self, coords: torch.Tensor, features: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+        B = coords.shape[0]
+        _, cent = sample_indices(coords, self.C)
+        idx = _ball(cent, coords, self.radius, self.K)
+        rows = ops.group_rows(coords, features, cent, idx, self.radius, self.grouping_norm)
+        act = self.point_net.forward_rows(rows)
+        if self.pooling_type == 'max':
+            out = ops.maxk(act, self.K).view(B, self.C, -1)
+        else:
+            out = reduce(act.view(B, self.C, self.K, -1), self.pooling_type)
+        return cent, out
+
+
+class FeaturePropagation(nn.Module):
+    """Reference common.py:217-243: 3-NN IDW interpolation, concat skip, shared MLP."""
+
+    def __init__(self, in_channels: int, mlps: list[int]):
+        super().__init__()
+        self.point_net = UnitPointNet(in_channels, mlps)
+
+    def forward(self, coords_1: torch.Tensor, coords_2: torch.Tensor, features_1: torch.Tensor | None,
+                features_2: torch.Tensor) -> torch.Tensor:
+        B, N, _ = coords_1.shape
+        idx, dist = ops.knn_select(coords_1, coords_2, 3)
+        rp = _replay()
+        if rp is not None:
+            rp.rec_interp_idx.append(idx.detach().cpu())
+        rows = ops.interp_cat_rows(features_1, features_2, idx, dist)
+        return self.point_net.forward_rows(rows).view(B, N, -1)
+
+
+class InvResMLP(nn.Module):
+    """Reference common.py:246-301: group (C=N, normalised) -> 1-layer MLP -> max -> 2-layer MLP -> + residual."""
+
+    def __init__(self, radius: int, in_channels: int, mlp_size: int, K: int, pooling_type: str = 'max'):
+        super().__init__()
+        self.radius = radius
+        self.K = K
+        self.pooling_type = pooling_type
+        self.neighbour_features_mlp = MiniPointNet(in_channels, [mlp_size])
+        self.point_features_mlp = UnitPointNet(mlp_size, [4 * mlp_size, mlp_size])
+
+    def forward(self, centroid_coords: torch.Tensor, coords: torch.Tensor,
+                features: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+        B, C, _ = centroid_coords.shape
+        idx = _ball(centroid_coords, coords, self.radius, self.K)
+        rows = ops.group_rows(coords, features, centroid_coords, idx, self.radius, True)
+        act = self.neighbour_features_mlp.forward_rows(rows)
+        if self.pooling_type == 'max':
+            pooled = ops.maxk(act, self.K)
+        else:
+            pooled = reduce(act.view(B, C, self.K, -1), self.pooling_type).reshape(B * C, -1)
+        out = self.point_features_mlp.forward_rows(pooled).view(B, C, -1)
+        return centroid_coords, out + features

@@ -1,0 +1,94 @@
+"""Data-parallel training over RCCL (torch.distributed backend "nccl" on ROCm).
+
+S3DIS blocks are independent samples, so the only exchange step is the
+gradient all-reduce after backward.  Gradients live in ONE flat
+fp32 buffer (every `param.grad` is a view into it), split into a few
+contiguous buckets that are all-reduced as soon as autograd has produced every
+gradient in them -- overlapping the collective with the rest of backward on
+RCCL's own stream.  BatchNorm statistics stay local per rank (DDP's default;
+the reference has no SyncBN); parameters and buffers are broadcast from rank 0
+once.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+
+def broadcast_model(model: torch.nn.Module, src: int = 0) -> None:
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return
+    with torch.no_grad():
+        for t in list(model.parameters()) + list(model.buffers()):
+            dist.broadcast(t.data, src)
+
+
+class FlatGradAllReduce:
+    """Flat gradient buffer + bucketed, backward-overlapped all-reduce (mean)."""
+
+    def __init__(self, model: torch.nn.Module, bucket_bytes: int = 4 << 20, overlap: bool = True):
+        self.params = [p for p in model.parameters() if p.requires_grad]
+        total = sum(p.numel() for p in self.params)
+        dev = self.params[0].device
+        self.flat = torch.zeros(total, dtype=torch.float32, device=dev)
+        self.world = dist.get_world_size() if dist.is_initialized() else 1
+        # buckets are laid out in REVERSE parameter order: backward produces the
+        # last layers' gradients first, so the first bucket completes earliest.
+        order = list(reversed(self.params))
+        self.views = {}
+        off = 0
+        self.buckets: list[tuple[int, int, list[torch.nn.Parameter]]] = []
+        cur_start, cur = 0, []
+        for p in order:
+            n = p.numel()
+            self.views[p] = self.flat[off:off + n].view_as(p)
+            cur.append(p)
+            off += n
+            if (off - cur_start) * 4 >= bucket_bytes:
+                self.buckets.append((cur_start, off, cur))
+                cur_start, cur = off, []
+        if cur:
+            self.buckets.append((cur_start, off, cur))
+        self._bucket_of = {p: i for i, (_, _, ps) in enumerate(self.buckets) for p in ps}
+        self._pending = [len(ps) for _, _, ps in self.buckets]
+        self._handles: list = []
+        self.overlap = overlap and self.world > 1
+        self.attach()
+        if self.overlap:
+            for p in self.params:
+                p.register_post_accumulate_grad_hook(self._hook)
+
+    def attach(self) -> None:
+        """(Re)bind every param.grad to its view of the flat buffer."""
+        for p in self.params:
+            p.grad = self.views[p]
+
+    def zero_grad(self) -> None:
+        self.flat.zero_()
+        self.attach()
+        self._pending = [len(ps) for _, _, ps in self.buckets]
+        self._handles = []
+
+    def _hook(self, p: torch.Tensor) -> None:
+        b = self._bucket_of[p]
+        self._pending[b] -= 1
+        if self._pending[b] == 0:
+            s, e, _ = self.buckets[b]
+            self._handles.append(dist.all_reduce(self.flat[s:e], op=dist.ReduceOp.SUM, async_op=True))
+
+    def synchronize(self) -> None:
+        """Finish all bucket reductions and average (call before optimizer.step())."""
+        if self.world == 1:
+            return
+        if self.overlap:
+            for h in self._handles:
+                h.wait()
+            # any bucket whose hook did not fire (unused params) is reduced now
+            for b, (s, e, _) in enumerate(self.buckets):
+                if self._pending[b] != 0:
+                    dist.all_reduce(self.flat[s:e], op=dist.ReduceOp.SUM)
+        else:
+            dist.all_reduce(self.flat, op=dist.ReduceOp.SUM)
+        self.flat.div_(self.world)
+        self._handles = []
+        self._pending = [len(ps) for _, _, ps in self.buckets]

@@ -1,0 +1,404 @@
+"""Segmentation models with the reference's constructors, forward signatures,
+return conventions and state_dict keys.
+
+  PointNetpp        models/PointNetpp/PointNetpp.py:6-48     (B,N,9) -> (B,N,classes)
+  PointNetppMSG     (not in the reference; composed from the same SA/FP blocks)
+  PointNeXt         models/PointNeXt/PointNeXt.py:17-147     (B,N,9) -> (B,N,classes)
+  DGCNN             models/dgcnn/dgcnn.py:80-162             (B,3|6,N) -> (logits, x5, None)
+  DGCNNWithColor    models/dgcnn/dgcnn.py:165-257            (B,6,N)   -> (logits, x5, None)
+  get_model/get_loss models/dgcnn/dgcnn.py:260-280
+  PointNetSeg       models/PointNet/PointNet.py:119-150      (B,N,9) -> probabilities
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import ops
+from .common import SetAbstraction, FeaturePropagation, InvResMLP, UnitPointNet, sample_indices, _ball
+from .mlp import conv_rows, bn_rows
+from .replay import active as _replay
+
+
+def _head_rows(x_rows: torch.Tensor, drop: nn.Module, conv: nn.Module) -> torch.Tensor:
+    return conv_rows(drop(x_rows), conv)
+
+
+class PointNetpp(nn.Module):
+    """PointNet++ SSG semantic segmentation (reference PointNetpp.py:6-48)."""
+
+    def __init__(self, part_classes: int):
+        super().__init__()
+        self.sa1 = SetAbstraction(1024, 0.1, 9, [32, 32, 64])
+        self.sa2 = SetAbstraction(256, 0.2, 64 + 3, [64, 64, 128])
+        self.sa3 = SetAbstraction(64, 0.4, 128 + 3, [128, 128, 256])
+        self.sa4 = SetAbstraction(16, 0.8, 256 + 3, [256, 256, 512])
+        self.fp4 = FeaturePropagation(512 + 256, [256, 256])
+        self.fp3 = FeaturePropagation(256 + 128, [256, 256])
+        self.fp2 = FeaturePropagation(256 + 64, [256, 128])
+        self.fp1 = FeaturePropagation(128, [128, 128, 128, 128])
+        self.drop = nn.Dropout(0.5)
+        self.conv = nn.Conv1d(128, part_classes, 1)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        B, N, _ = x.shape
+        c0 = x[:, :, :3].contiguous()
+        f0 = x[:, :, 3:].contiguous()
+        c1, f1 = self.sa1(c0, f0)
+        c2, f2 = self.sa2(c1, f1)
+        c3, f3 = self.sa3(c2, f2)
+        c4, f4 = self.sa4(c3, f3)
+        f3 = self.fp4(c3, c4, f3, f4)
+        f2 = self.fp3(c2, c3, f2, f3)
+        f1 = self.fp2(c1, c2, f1, f2)
+        f0 = self.fp1(c0, c1, None, f1)
+        return _head_rows(f0.reshape(B * N, -1), self.drop, self.conv).view(B, N, -1)
+
+
+class PointNetppMSG(nn.Module):
+    """PointNet++ MSG (multi-scale grouping) segmentation.
+
+    Not in the reference (BASELINE.json config 4 names it); composed from the
+    reference's own SetAbstraction / FeaturePropagation semantics with the
+    standard semantic-segmentation MSG widths: each level
+    samples its centroids ONCE and groups them at two radii, concatenating the
+    two pooled branches.
+    """
+
+    CFG = [  # (C, radii, Ks, [mlp per scale])
+        (1024, (0.05, 0.1), (16, 32), ([16, 16, 32], [32, 32, 64])),
+        (256, (0.1, 0.2), (16, 32), ([64, 64, 128], [64, 96, 128])),
+        (64, (0.2, 0.4), (16, 32), ([128, 196, 256], [128, 196, 256])),
+        (16, (0.4, 0.8), (16, 32), ([256, 256, 512], [256, 384, 512])),
+    ]
+
+    def __init__(self, part_classes: int):
+        super().__init__()
+        self.levels = nn.ModuleList()
+        d = 6
+        skips = [6]
+        for C, radii, Ks, mlps in self.CFG:
+            branches = nn.ModuleList([SetAbstraction(C, r, d + 3, m, K=k) for r, k, m in zip(radii, Ks, mlps)])
+            self.levels.append(branches)
+            d = sum(m[-1] for m in mlps)
+            skips.append(d)
+        self.fp4 = FeaturePropagation(skips[4] + skips[3], [256, 256])
+        self.fp3 = FeaturePropagation(256 + skips[2], [256, 256])
+        self.fp2 = FeaturePropagation(256 + skips[1], [256, 128])
+        self.fp1 = FeaturePropagation(128, [128, 128, 128])
+        self.drop = nn.Dropout(0.5)
+        self.conv = nn.Conv1d(128, part_classes, 1)
+
+    def _sa_level(self, branches, coords, feats):
+        C = branches[0].C
+        B = coords.shape[0]
+        _, cent = sample_indices(coords, C)
+        outs = []
+        for sa in branches:
+            idx = _ball(cent, coords, sa.radius, sa.K)
+            rows = ops.group_rows(coords, feats, cent, idx, sa.radius, sa.grouping_norm)
+            act = sa.point_net.forward_rows(rows)
+            outs.append(ops.maxk(act, sa.K).view(B, C, -1))
+        return cent, torch.cat(outs, dim=-1)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        B, N, _ = x.shape
+        cs, fs = [x[:, :, :3].contiguous()], [x[:, :, 3:].contiguous()]
+        for branches in self.levels:
+            c, f = self._sa_level(branches, cs[-1], fs[-1])
+            cs.append(c)
+            fs.append(f)
+        f3 = self.fp4(cs[3], cs[4], fs[3], fs[4])
+        f2 = self.fp3(cs[2], cs[3], fs[2], f3)
+        f1 = self.fp2(cs[1], cs[2], fs[1], f2)
+        f0 = self.fp1(cs[0], cs[1], None, f1)
+        return _head_rows(f0.reshape(B * N, -1), self.drop, self.conv).view(B, N, -1)
+
+
+class PointNeXt(nn.Module):
+    """PointNeXt(-B-like) segmentation (reference PointNeXt.py:17-147)."""
+
+    def __init__(self, part_classes: int, version: str = 'b'):
+        super().__init__()
+        self.num_classes = part_classes
+        self.mlp = UnitPointNet(9, [32])
+        mlp_last = self.mlp.conv[-1].out_channels
+        self.sa1 = SetAbstraction(1024, 0.1, mlp_last + 3, [32, 32, 64], grouping_norm=True)
+        sa1 = self.sa1.point_net.conv[-1].out_channels
+        self.irmlp1 = InvResMLP(0.1, sa1 + 3, sa1, 32)
+        self.sa2 = SetAbstraction(256, 0.2, sa1 + 3, [64, 64, 128], grouping_norm=True)
+        sa2 = self.sa2.point_net.conv[-1].out_channels
+        self.irmlp2 = InvResMLP(0.1, sa2 + 3, sa2, 32)
+        self.irmlp2_1 = InvResMLP(0.2, sa2 + 3, sa2, 32)
+        self.sa3 = SetAbstraction(64, 0.4, sa2 + 3, [128, 128, 256], grouping_norm=True)
+        sa3 = self.sa3.point_net.conv[-1].out_channels
+        self.irmlp3 = InvResMLP(0.4, sa3 + 3, sa3, 32)
+        self.sa4 = SetAbstraction(16, 0.8, sa3 + 3, [256, 256, 512], grouping_norm=True)
+        sa4 = self.sa4.point_net.conv[-1].out_channels
+        self.irmlp4 = InvResMLP(0.8, sa4 + 3, sa4, 16)
+        self.fp4 = FeaturePropagation(sa4 + sa3, [256, 256])
+        fp4 = self.fp4.point_net.conv[-1].out_channels
+        self.fp3 = FeaturePropagation(fp4 + sa2, [256, 256])
+        fp3 = self.fp3.point_net.conv[-1].out_channels
+        self.fp2 = FeaturePropagation(fp3 + sa1, [256, 128])
+        fp2 = self.fp2.point_net.conv[-1].out_channels
+        self.fp1 = FeaturePropagation(fp2 + mlp_last, [128, 128, 128, 128])
+        fp1 = self.fp1.point_net.conv[-1].out_channels
+        self.drop = nn.Dropout(0.5)
+        self.conv = nn.Conv1d(fp1, part_classes, 1)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        B, N, Cin = x.shape
+        x = x.contiguous()
+        f0 = self.mlp.forward_rows(x.view(B * N, Cin)).view(B, N, -1)
+        c0 = x[:, :, :3].contiguous()
+        c1, f1 = self.sa1(c0, f0)
+        c1, f1 = self.irmlp1(c1, c1, f1)
+        c2, f2 = self.sa2(c1, f1)
+        c2, f2 = self.irmlp2(c2, c2, f2)
+        c2, f2 = self.irmlp2_1(c2, c2, f2)
+        c3, f3 = self.sa3(c2, f2)
+        c3, f3 = self.irmlp3(c3, c3, f3)
+        c4, f4 = self.sa4(c3, f3)
+        c4, f4 = self.irmlp4(c4, c4, f4)
+        f3 = self.fp4(c3, c4, f3, f4)
+        f2 = self.fp3(c2, c3, f2, f3)
+        f1 = self.fp2(c1, c2, f1, f2)
+        f0 = self.fp1(c0, c1, f0, f1)
+        return _head_rows(f0.reshape(B * N, -1), self.drop, self.conv).view(B, N, -1)
+
+
+# ------------------------------------------------------------------------- DGCNN
+def _seq_rows(x_rows: torch.Tensor, seq: nn.Sequential) -> torch.Tensor:
+    """Conv1d(bias=False) -> BN1d -> LeakyReLU [-> Dropout] on rows."""
+    z = bn_rows(conv_rows(x_rows, seq[0]), seq[1])
+    y = F.leaky_relu(z, seq[2].negative_slope)
+    if len(seq) > 3:
+        y = seq[3](y)
+    return y
+
+
+class EdgeConv(nn.Module):
+    """Reference dgcnn.py:60-77.  forward takes/returns the reference's (B, C, N) layout."""
+
+    def __init__(self, in_channels, out_channels, k=20):
+        super().__init__()
+        self.k = k
+        self.conv = nn.Sequential(
+            nn.Conv2d(in_channels * 2, out_channels, kernel_size=1, bias=False),
+            nn.BatchNorm2d(out_channels),
+            nn.LeakyReLU(negative_slope=0.2))
+
+    def forward_points(self, xp: torch.Tensor) -> torch.Tensor:
+        """xp point-major (B, N, C) -> (B, N, Cout)."""
+        B, N, _ = xp.shape
+        rp = _replay()
+        if rp is not None and rp.knn_idx:
+            idx = rp.knn_idx.pop(0).to(device=xp.device, dtype=torch.int32).contiguous()
+        else:
+            idx = ops.knn(xp, self.k)
+        if rp is not None:
+            rp.rec_knn_idx.append(idx.detach().cpu())
+        rows = ops.edge_rows(xp, idx)
+        z = bn_rows(conv_rows(rows, self.conv[0]), self.conv[1])
+        y = F.leaky_relu(z, self.conv[2].negative_slope)
+        return ops.maxk(y, self.k).view(B, N, -1)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return self.forward_points(x.transpose(1, 2).contiguous()).transpose(1, 2)
+
+
+def _dgcnn_head(self, parts: list[torch.Tensor], B: int, N: int):
+    xc = torch.cat(parts, dim=-1)                      # (B, N, 320|384)
+    xr = xc.view(B * N, -1)
+    x5 = _seq_rows(xr, self.conv5)                      # (B*N, emb)
+    x6 = _seq_rows(torch.cat((xr, x5), dim=1), self.conv6)
+    x7 = _seq_rows(x6, self.conv7)
+    logits = conv_rows(x7, self.conv8).view(B, N, -1)
+    # the reference returns x5 as a contiguous (B, emb, N); a transposed view of
+    # the point-major tensor has the same shape and values without a 0.5 GB copy
+    return logits, x5.view(B, N, -1).transpose(1, 2), None
+
+
+def _head_seq(cin, cout, dropout):
+    return nn.Sequential(nn.Conv1d(cin, cout, kernel_size=1, bias=False), nn.BatchNorm1d(cout),
+                         nn.LeakyReLU(negative_slope=0.2), nn.Dropout(dropout))
+
+
+class DGCNN(nn.Module):
+    """Reference dgcnn.py:80-162 (xyz graph; 6-channel input uses xyz only)."""
+
+    def __init__(self, num_classes=13, k=20, emb_dims=1024, dropout=0.5):
+        super().__init__()
+        self.k = k
+        self.num_classes = num_classes
+        self.conv1 = EdgeConv(3, 64, k)
+        self.conv2 = EdgeConv(64, 64, k)
+        self.conv3 = EdgeConv(64, 64, k)
+        self.conv4 = EdgeConv(64, 128, k)
+        self.conv5 = nn.Sequential(nn.Conv1d(320, emb_dims, kernel_size=1, bias=False),
+                                   nn.BatchNorm1d(emb_dims), nn.LeakyReLU(negative_slope=0.2))
+        self.conv6 = _head_seq(emb_dims + 320, 512, dropout)
+        self.conv7 = _head_seq(512, 256, dropout)
+        self.conv8 = nn.Conv1d(256, num_classes, kernel_size=1)
+
+    def forward(self, x):
+        B, _, N = x.shape
+        xyz = x[:, :3, :] if x.size(1) == 6 else x
+        xp = xyz.transpose(1, 2).contiguous()
+        x1 = self.conv1.forward_points(xp)
+        x2 = self.conv2.forward_points(x1)
+        x3 = self.conv3.forward_points(x2)
+        x4 = self.conv4.forward_points(x3)
+        return _dgcnn_head(self, [x1, x2, x3, x4], B, N)
+
+
+class DGCNNWithColor(nn.Module):
+    """Reference dgcnn.py:165-257 (xyz graph + per-point colour branch)."""
+
+    def __init__(self, num_classes=13, k=20, emb_dims=1024, dropout=0.5):
+        super().__init__()
+        self.k = k
+        self.num_classes = num_classes
+        self.conv1 = EdgeConv(3, 64, k)
+        self.conv2 = EdgeConv(64, 64, k)
+        self.conv3 = EdgeConv(64, 64, k)
+        self.conv4 = EdgeConv(64, 128, k)
+        self.color_conv = nn.Sequential(nn.Conv1d(3, 64, kernel_size=1, bias=False),
+                                        nn.BatchNorm1d(64), nn.LeakyReLU(negative_slope=0.2))
+        self.conv5 = nn.Sequential(nn.Conv1d(384, emb_dims, kernel_size=1, bias=False),
+                                   nn.BatchNorm1d(emb_dims), nn.LeakyReLU(negative_slope=0.2))
+        self.conv6 = _head_seq(emb_dims + 384, 512, dropout)
+        self.conv7 = _head_seq(512, 256, dropout)
+        self.conv8 = nn.Conv1d(256, num_classes, kernel_size=1)
+
+    def forward(self, x):
+        if x.size(1) != 6:
+            raise ValueError("DGCNNWithColor expects 6-channel input (xyz + rgb)")
+        B, _, N = x.shape
+        xp = x.transpose(1, 2)                           # (B, N, 6) view of the (B,6,N) input
+        xyz = xp[:, :, :3].contiguous()
+        rgb = xp[:, :, 3:6].contiguous()
+        x1 = self.conv1.forward_points(xyz)
+        x2 = self.conv2.forward_points(x1)
+        x3 = self.conv3.forward_points(x2)
+        x4 = self.conv4.forward_points(x3)
+        color = _seq_rows(rgb.view(B * N, 3), self.color_conv).view(B, N, -1)
+        return _dgcnn_head(self, [x1, x2, x3, x4, color], B, N)
+
+
+def get_model(num_classes=13, use_color=True, **kwargs):
+    """Reference dgcnn.py:260-273."""
+    if use_color:
+        return DGCNNWithColor(num_classes=num_classes, **kwargs)
+    return DGCNN(num_classes=num_classes, **kwargs)
+
+
+def get_loss():
+    """Reference dgcnn.py:276-280."""
+    return nn.CrossEntropyLoss(ignore_index=-1)
+
+
+# ------------------------------------------------------------------------- PointNet (dense plumbing)
+class TNet(nn.Module):
+    """Reference PointNet.py:6-38."""
+
+    def __init__(self, k=9):
+        super().__init__()
+        self.k = k
+        self.conv1 = nn.Conv1d(k, 64, 1)
+        self.conv2 = nn.Conv1d(64, 128, 1)
+        self.conv3 = nn.Conv1d(128, 1024, 1)
+        self.fc1 = nn.Linear(1024, 512)
+        self.fc2 = nn.Linear(512, 256)
+        self.fc3 = nn.Linear(256, k * k)
+        self.bn1 = nn.BatchNorm1d(64)
+        self.bn2 = nn.BatchNorm1d(128)
+        self.bn3 = nn.BatchNorm1d(1024)
+        self.bn4 = nn.BatchNorm1d(512)
+        self.bn5 = nn.BatchNorm1d(256)
+
+    def forward_points(self, xp):
+        """xp (B, N, k) point-major."""
+        B, N, _ = xp.shape
+        r = xp.reshape(B * N, -1)
+        r = F.relu(bn_rows(conv_rows(r, self.conv1), self.bn1))
+        r = F.relu(bn_rows(conv_rows(r, self.conv2), self.bn2))
+        r = F.relu(bn_rows(conv_rows(r, self.conv3), self.bn3))
+        g = r.view(B, N, -1).max(dim=1)[0]
+        g = F.relu(self.bn4(self.fc1(g)))
+        g = F.relu(self.bn5(self.fc2(g)))
+        eye = torch.eye(self.k, device=g.device).view(1, self.k * self.k).repeat(B, 1)
+        return (self.fc3(g) + eye).view(B, self.k, self.k)
+
+    def forward(self, x):
+        return self.forward_points(x.transpose(1, 2))
+
+
+class PointNetEncoder(nn.Module):
+    """Reference PointNet.py:41-90."""
+
+    def __init__(self, global_feat=True, feature_transform=False, k=9):
+        super().__init__()
+        self.stn = TNet(k=k)
+        self.conv1 = nn.Conv1d(k, 64, 1)
+        self.bn1 = nn.BatchNorm1d(64)
+        self.feature_transform = feature_transform
+        if feature_transform:
+            self.fstn = TNet(k=64)
+        self.conv2 = nn.Conv1d(64, 128, 1)
+        self.bn2 = nn.BatchNorm1d(128)
+        self.conv3 = nn.Conv1d(128, 1024, 1)
+        self.bn3 = nn.BatchNorm1d(1024)
+        self.global_feat = global_feat
+
+    def forward_points(self, xp):
+        B, N, _ = xp.shape
+        trans = self.stn.forward_points(xp)
+        xp = torch.bmm(xp, trans)
+        r = F.relu(bn_rows(conv_rows(xp.reshape(B * N, -1), self.conv1), self.bn1))
+        trans_feat = None
+        if self.feature_transform:
+            trans_feat = self.fstn.forward_points(r.view(B, N, -1))
+            r = torch.bmm(r.view(B, N, -1), trans_feat).reshape(B * N, -1)
+        pf = r.view(B, N, -1)
+        r = F.relu(bn_rows(conv_rows(r, self.conv2), self.bn2))
+        r = bn_rows(conv_rows(r, self.conv3), self.bn3)
+        g = r.view(B, N, -1).max(dim=1)[0]
+        if self.global_feat:
+            return g, trans, trans_feat
+        return torch.cat([g.view(B, 1, 1024).expand(B, N, 1024), pf], dim=2), trans, trans_feat
+
+    def forward(self, x):
+        out, trans, tf = self.forward_points(x.transpose(1, 2))
+        if self.global_feat:
+            return out, trans, tf
+        return out.transpose(1, 2), trans, tf
+
+
+class PointNetSeg(nn.Module):
+    """Reference PointNet.py:119-150 ((B, N, 9) -> per-point class probabilities)."""
+
+    def __init__(self, part_classes=13, feature_transform=False):
+        super().__init__()
+        self.feature_transform = feature_transform
+        self.feat = PointNetEncoder(global_feat=False, feature_transform=feature_transform)
+        self.conv1 = nn.Conv1d(1088, 512, 1)
+        self.bn1 = nn.BatchNorm1d(512)
+        self.conv2 = nn.Conv1d(512, 256, 1)
+        self.bn2 = nn.BatchNorm1d(256)
+        self.conv3 = nn.Conv1d(256, 128, 1)
+        self.bn3 = nn.BatchNorm1d(128)
+        self.conv4 = nn.Conv1d(128, part_classes, 1)
+
+    def forward(self, x):
+        B, N, _ = x.shape
+        feat, _, _ = self.feat.forward_points(x)
+        r = feat.reshape(B * N, -1)
+        r = F.relu(bn_rows(conv_rows(r, self.conv1), self.bn1))
+        r = F.relu(bn_rows(conv_rows(r, self.conv2), self.bn2))
+        r = F.relu(bn_rows(conv_rows(r, self.conv3), self.bn3))
+        r = conv_rows(r, self.conv4).view(B, N, -1)
+        e = torch.exp(r)
+        return e / torch.sum(e, keepdim=True, dim=-1)

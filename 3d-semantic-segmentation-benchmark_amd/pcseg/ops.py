@@ -1,0 +1,210 @@
+"""Tensor-level wrappers (torch.autograd.Function) over the HIP C ABI.
+
+Every op runs on the current HIP stream of the input's device and is
+allocation-light (outputs come from PyTorch's caching allocator).  Shapes and
+devices are validated here, mirroring the reference's ValueError style; a
+non-zero ABI status raises RuntimeError with the library's message.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import call, ptr, stream_ptr, check_cuda
+
+
+def _c(t: torch.Tensor) -> torch.Tensor:
+    return t if t.is_contiguous() else t.contiguous()
+
+
+def radius_sq_f32(r: float) -> float:
+    """float32(r ** 2): the threshold the reference compares against (common.py:58)."""
+    return float(np.float32(r ** 2))
+
+
+# ------------------------------------------------------------------ neighbour search (no grad)
+def fps(xyz: torch.Tensor, C: int, start: torch.Tensor):
+    """xyz (B,N,3) -> (idx (B,C) int32, centroids (B,C,3))."""
+    check_cuda(xyz)
+    xyz = _c(xyz.float())
+    B, N, _ = xyz.shape
+    start = _c(start.to(device=xyz.device, dtype=torch.int32))
+    idx = torch.empty((B, C), dtype=torch.int32, device=xyz.device)
+    cent = torch.empty((B, C, 3), dtype=torch.float32, device=xyz.device)
+    call('pcs_fps', ptr(xyz), B, N, C, ptr(start), ptr(idx), ptr(cent), stream_ptr(xyz.device))
+    return idx, cent
+
+
+def ball_query(cent: torch.Tensor, xyz: torch.Tensor, r: float, K: int) -> torch.Tensor:
+    check_cuda(cent, xyz)
+    cent, xyz = _c(cent.float()), _c(xyz.float())
+    B, C, _ = cent.shape
+    N = xyz.shape[1]
+    if K > N:
+        raise RuntimeError(f'selected index k out of range (K={K} > N={N})')
+    out = torch.empty((B, C, K), dtype=torch.int32, device=xyz.device)
+    call('pcs_ball_query', ptr(cent), ptr(xyz), B, C, N, radius_sq_f32(r), K, ptr(out), stream_ptr(xyz.device))
+    return out
+
+
+def knn_select(query: torch.Tensor, ref: torch.Tensor, k: int = 3):
+    """(idx (B,N,k) int32, squared dist (B,N,k)) of the k nearest ref points."""
+    check_cuda(query, ref)
+    query, ref = _c(query.float()), _c(ref.float())
+    B, N, _ = query.shape
+    M = ref.shape[1]
+    if k > M:
+        raise RuntimeError(f'selected index k out of range (k={k} > M={M})')
+    idx = torch.empty((B, N, k), dtype=torch.int32, device=query.device)
+    dist = torch.empty((B, N, k), dtype=torch.float32, device=query.device)
+    call('pcs_knn_select', ptr(query), ptr(ref), B, N, M, k, ptr(idx), ptr(dist), stream_ptr(query.device))
+    return idx, dist
+
+
+def knn(x: torch.Tensor, k: int) -> torch.Tensor:
+    """DGCNN feature-space kNN; x point-major (B,N,F) -> idx (B,N,k) int32."""
+    check_cuda(x)
+    x = _c(x.float())
+    B, N, Fd = x.shape
+    out = torch.empty((B, N, k), dtype=torch.int32, device=x.device)
+    call('pcs_knn', ptr(x), B, N, Fd, k, ptr(out), stream_ptr(x.device))
+    return out
+
+
+# ------------------------------------------------------------------ differentiable gathers
+class GroupFn(torch.autograd.Function):
+    """(B*C*K, 3+D) rows [ (xyz[idx]-c) (/r), feats[idx] ]; grad flows to feats only."""
+
+    @staticmethod
+    def forward(ctx, xyz, feats, cent, idx, r, normalize):
+        B, N, _ = xyz.shape
+        C, K = idx.shape[1], idx.shape[2]
+        D = feats.shape[2] if feats is not None else 0
+        out = torch.empty((B * C * K, 3 + D), dtype=torch.float32, device=xyz.device)
+        call('pcs_group_fwd', ptr(xyz), ptr(feats), ptr(cent), ptr(idx), B, N, C, K, D, float(np.float32(r)),
+             int(bool(normalize)), ptr(out), stream_ptr(xyz.device))
+        ctx.save_for_backward(idx)
+        ctx.dims = (B, N, C, K, D)
+        ctx.has_feats = feats is not None
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        (idx,) = ctx.saved_tensors
+        B, N, C, K, D = ctx.dims
+        gfeats = None
+        if ctx.has_feats and ctx.needs_input_grad[1]:
+            gout = _c(gout)
+            gfeats = torch.zeros((B, N, D), dtype=torch.float32, device=gout.device)
+            call('pcs_group_bwd', ptr(gout), ptr(idx), B, N, C, K, D, ptr(gfeats), stream_ptr(gout.device))
+        return None, gfeats, None, None, None, None
+
+
+def group_rows(xyz, feats, cent, idx, r, normalize):
+    check_cuda(xyz, cent, idx)
+    xyz, cent = _c(xyz.float()), _c(cent.float())
+    feats = _c(feats.float()) if feats is not None else None
+    return GroupFn.apply(xyz, feats, cent, _c(idx), r, normalize)
+
+
+class MaxKFn(torch.autograd.Function):
+    """x (G*K, Ch) -> (G, Ch) max over K; backward routes to the first argmax."""
+
+    @staticmethod
+    def forward(ctx, x, K):
+        x = _c(x)
+        GK, Ch = x.shape
+        G = GK // K
+        out = torch.empty((G, Ch), dtype=torch.float32, device=x.device)
+        arg = torch.empty((G, Ch), dtype=torch.uint8, device=x.device)
+        call('pcs_maxk_fwd', ptr(x), G, K, Ch, ptr(out), ptr(arg), stream_ptr(x.device))
+        ctx.save_for_backward(arg)
+        ctx.K = K
+        ctx.mark_non_differentiable(arg)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        (arg,) = ctx.saved_tensors
+        gout = _c(gout)
+        G, Ch = gout.shape
+        gx = torch.empty((G * ctx.K, Ch), dtype=torch.float32, device=gout.device)
+        call('pcs_maxk_bwd', ptr(gout), ptr(arg), G, ctx.K, Ch, ptr(gx), stream_ptr(gout.device))
+        return gx, None
+
+
+def maxk(x, K):
+    check_cuda(x)
+    if x.shape[0] % K:
+        raise ValueError('maxk: rows not divisible by K')
+    if K > 256:
+        raise ValueError('maxk: K > 256 not supported')
+    return MaxKFn.apply(x.float(), K)
+
+
+class InterpCatFn(torch.autograd.Function):
+    """rows (B*N, D1+D2) = [f1, IDW-interpolate(f2)] (reference FeaturePropagation.forward)."""
+
+    @staticmethod
+    def forward(ctx, f1, f2, idx, dist):
+        B, M, D2 = f2.shape
+        N = idx.shape[1]
+        D1 = f1.shape[2] if f1 is not None else 0
+        W = D1 + D2
+        out = torch.empty((B * N, W), dtype=torch.float32, device=f2.device)
+        if f1 is not None:
+            out.view(B, N, W)[:, :, :D1].copy_(f1)
+        call('pcs_interp_fwd', ptr(f2), ptr(idx), ptr(dist), B, N, M, D2, ptr(out), W, D1, stream_ptr(f2.device))
+        ctx.save_for_backward(idx, dist)
+        ctx.dims = (B, N, M, D1, D2)
+        ctx.has_f1 = f1 is not None
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        idx, dist = ctx.saved_tensors
+        B, N, M, D1, D2 = ctx.dims
+        gout = _c(gout)
+        W = D1 + D2
+        g1 = gout.view(B, N, W)[:, :, :D1] if (ctx.has_f1 and ctx.needs_input_grad[0]) else None
+        g2 = None
+        if ctx.needs_input_grad[1]:
+            g2 = torch.zeros((B, M, D2), dtype=torch.float32, device=gout.device)
+            call('pcs_interp_bwd', ptr(gout), ptr(idx), ptr(dist), B, N, M, D2, W, D1, ptr(g2),
+                 stream_ptr(gout.device))
+        return g1, g2, None, None
+
+
+def interp_cat_rows(f1, f2, idx, dist):
+    check_cuda(f2, idx, dist)
+    f1 = _c(f1.float()) if f1 is not None else None
+    return InterpCatFn.apply(f1, _c(f2.float()), _c(idx), _c(dist))
+
+
+class EdgeFn(torch.autograd.Function):
+    """rows (B*N*k, 2D) = [x_j - x_i, x_i] (reference get_graph_feature, dgcnn.py:41-53)."""
+
+    @staticmethod
+    def forward(ctx, x, idx):
+        B, N, D = x.shape
+        k = idx.shape[2]
+        out = torch.empty((B * N * k, 2 * D), dtype=torch.float32, device=x.device)
+        call('pcs_edge_fwd', ptr(x), ptr(idx), B, N, k, D, ptr(out), stream_ptr(x.device))
+        ctx.save_for_backward(idx)
+        ctx.dims = (B, N, k, D)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        (idx,) = ctx.saved_tensors
+        B, N, k, D = ctx.dims
+        gout = _c(gout)
+        gx = torch.zeros((B, N, D), dtype=torch.float32, device=gout.device)
+        call('pcs_edge_bwd', ptr(gout), ptr(idx), B, N, k, D, ptr(gx), stream_ptr(gout.device))
+        return gx, None
+
+
+def edge_rows(x, idx):
+    check_cuda(x, idx)
+    return EdgeFn.apply(_c(x.float()), _c(idx))

@@ -1,0 +1,244 @@
+#!/usr/bin/env python3
+"""Throughput bench: points/s of one training step (forward + masked one-hot CE +
+backward + gradient all-reduce + Adam step) on 4096-point S3DIS-like blocks.
+
+Workload at N=1 (BASELINE.json configs[1]): PointNet++ SSG, batch 32 per GPU,
+4096 points, fp32, synthetic blocks resident in HBM before timing starts.
+Multi-GPU: one process per GPU (torchrun), data-parallel, RCCL all-reduce of the
+flat gradient buffer, fixed per-GPU batch ("weak" scaling).
+
+Also reported on the same JSON line:
+  roofline      -- the dominant HIP kernel's algorithmic bytes / its average
+                   launch time (HIP events on its stream) vs 8 TB/s HBM;
+  cpu_baseline  -- the CPU oracle (oracle/ref_ops.py, the reference algorithm
+                   restated on PyTorch-CPU) on a bounded sample of the same
+                   workload, in a subprocess with no GPU visible, rank 0 only.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.join(REPO, '3d-semantic-segmentation-benchmark_amd')
+for _p in (REPO, PKG_ROOT):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+MODELS = {
+    'pointnetpp': ('PointNetpp', lambda m: m.PointNetpp(14), 'points'),
+    'pointnetpp_msg': ('PointNetppMSG', lambda m: m.PointNetppMSG(14), 'points'),
+    'pointnext': ('PointNeXt', lambda m: m.PointNeXt(14), 'points'),
+    'dgcnn': ('DGCNNWithColor', lambda m: m.DGCNNWithColor(num_classes=14, k=20), 'chfirst6'),
+    'pointnet': ('PointNetSeg', lambda m: m.PointNetSeg(part_classes=14), 'points'),
+}
+HBM_PEAK_GBS = 8000.0           # MI355X HBM3E spec (MI355X_MICROARCH.md)
+FP32_PEAK_TFLOPS = 157.3
+
+
+def model_input(pts, kind):
+    if kind == 'chfirst6':
+        return pts[:, :, :6].contiguous().transpose(1, 2)   # (B,6,N) view, as harness B passes it
+    return pts
+
+
+def logits_of(out):
+    return out[0] if isinstance(out, tuple) else out
+
+
+# ----------------------------------------------------------------------------- CPU baseline worker
+def cpu_baseline_worker(args):
+    import torch
+    from oracle import ref_ops as R
+    from pcseg.synthetic import make_batch
+    torch.set_num_threads(args.cpu_threads)
+    name, ctor, kind = MODELS[args.model]
+    model = R.seeded_init_(ctor(R), 0)
+    model.train()
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+    pts, labels, lengths = make_batch(args.cpu_batch, args.npoints, seed=1000)
+    x = model_input(pts, kind)
+    lab = labels.float() if kind == 'chfirst6' else labels
+
+    def step():
+        opt.zero_grad()
+        loss = R.masked_onehot_cross_entropy(logits_of(model(x)), lab, lengths)
+        loss.backward()
+        opt.step()
+    step()
+    times = []
+    for _ in range(args.cpu_steps):
+        t0 = time.perf_counter()
+        step()
+        times.append(time.perf_counter() - t0)
+    best = min(times)
+    print(json.dumps({'value': args.cpu_batch * args.npoints / best, 'unit': 'points/s',
+                      'cores': torch.get_num_threads(), 'kind': 'port',
+                      'sample': f'{name} oracle (PyTorch-CPU restatement of the reference), batch {args.cpu_batch} x '
+                                f'{args.npoints} pts, 1 warm-up + best of {args.cpu_steps} steps '
+                                f'(fwd+CE+bwd+Adam), {sum(times):.1f} s timed'}))
+
+
+def run_cpu_baseline(args):
+    env = dict(os.environ)
+    env['HIP_VISIBLE_DEVICES'] = ''
+    env['CUDA_VISIBLE_DEVICES'] = ''
+    threads = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
+    env['OMP_NUM_THREADS'] = str(threads)
+    cmd = [sys.executable, os.path.abspath(__file__), '--cpu-baseline-worker', '--model', args.model,
+           '--npoints', str(args.npoints), '--cpu-batch', str(args.cpu_batch), '--cpu-steps', str(args.cpu_steps),
+           '--cpu-threads', str(threads)]
+    try:
+        out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=900, check=True).stdout
+        return json.loads(out.strip().splitlines()[-1])
+    except Exception as e:  # noqa: BLE001 -- the baseline is informative, never fatal
+        return {'value': None, 'unit': 'points/s', 'cores': threads, 'kind': 'port', 'sample': f'failed: {e}'}
+
+
+# ----------------------------------------------------------------------------- roofline of one kernel
+def kernel_roofline(args, dev):
+    """Time the dominant HIP kernel alone, on the stream it is launched on (HIP events)."""
+    import torch
+    from pcseg import ops
+    from pcseg.synthetic import make_batch
+    B, N = args.batch, args.npoints
+    pts, _, _ = make_batch(B, N, seed=7)
+    xyz = pts[:, :, :3].contiguous().to(dev)
+    feats = pts[:, :, 3:].contiguous().to(dev)
+    start = torch.zeros(B, dtype=torch.int32, device=dev)
+    C, K, r = 1024, 32, 0.1
+    _, cent = ops.fps(xyz, C, start)
+    idx = ops.ball_query(cent, xyz, r, K)
+    D = feats.shape[2]
+    out = torch.empty((B * C * K, 3 + D), device=dev)
+    from pcseg._lib import call, ptr, stream_ptr
+    s = stream_ptr(dev)
+
+    def launch():
+        call('pcs_group_fwd', ptr(xyz), ptr(feats), ptr(cent), ptr(idx), B, N, C, K, D, 0.1, 0, ptr(out), s)
+    for _ in range(5):
+        launch()
+    st = torch.cuda.current_stream(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = 50
+    e0.record(st)
+    for _ in range(reps):
+        launch()
+    e1.record(st)
+    e1.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    # algorithmic bytes: write the grouped rows, read their indices, read the cloud
+    # (xyz+feats once) and the centroids once.
+    M = B * C * K
+    algo = M * (3 + D) * 4 + M * 4 + B * N * (3 + D) * 4 + B * C * 3 * 4
+    gbs = algo / (ms * 1e-3) / 1e9
+    return {'kernel': 'group_fwd_kernel (SA1 gather: B=%d C=%d K=%d D=%d)' % (B, C, K, D), 'bound': 'hbm',
+            'achieved': round(gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': round(gbs / HBM_PEAK_GBS, 4),
+            'traffic': None, 'avg_launch_us': round(ms * 1e3, 2), 'algo_bytes_per_launch': algo}
+
+
+# ----------------------------------------------------------------------------- main bench
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--warmup', type=int, default=5)
+    ap.add_argument('--model', default='pointnetpp', choices=sorted(MODELS))
+    ap.add_argument('--batch', type=int, default=32, help='per-GPU batch')
+    ap.add_argument('--npoints', type=int, default=4096)
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--cpu-batch', type=int, default=8)
+    ap.add_argument('--cpu-steps', type=int, default=2)
+    ap.add_argument('--cpu-threads', type=int, default=0)
+    ap.add_argument('--cpu-baseline-worker', action='store_true')
+    ap.add_argument('--no-roofline', action='store_true')
+    args = ap.parse_args()
+    if args.cpu_baseline_worker:
+        cpu_baseline_worker(args)
+        return
+
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    dev = torch.device('cuda', local)
+
+    cpu_res = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu_res = run_cpu_baseline(args)     # before the GPU run: the host is otherwise idle
+
+    import pcseg
+    from pcseg.ddp import FlatGradAllReduce, broadcast_model
+    from pcseg.synthetic import make_batch
+    from oracle.ref_ops import seeded_init_
+
+    name, ctor, kind = MODELS[args.model]
+    model = seeded_init_(ctor(pcseg), 0).to(dev).train()
+    broadcast_model(model)
+    grads = FlatGradAllReduce(model)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+    pts, labels, lengths = make_batch(args.batch, args.npoints, seed=1000 * 2 + rank)
+    x = model_input(pts.to(dev), kind)
+    lab = (labels.float() if kind == 'chfirst6' else labels).to(dev)
+    lengths = lengths.to(dev)
+
+    def step():
+        grads.zero_grad()
+        loss = pcseg.masked_onehot_cross_entropy(logits_of(model(x)), lab, lengths)
+        loss.backward()
+        grads.synchronize()
+        opt.step()
+        return loss
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t)
+    if not torch.isfinite(loss):
+        raise RuntimeError('non-finite loss')
+    roof = None
+    if rank == 0 and not args.no_roofline and args.model in ('pointnetpp', 'pointnetpp_msg', 'pointnext'):
+        roof = kernel_roofline(args, dev)
+    if rank == 0:
+        ms = dt / args.steps * 1e3
+        value = world * args.batch * args.npoints * args.steps / dt
+        res = {
+            'metric': 'points/sec fwd+bwd, 4096-pt S3DIS blocks, PointNet++/DGCNN @1/2/4/8 GPU',
+            'value': round(value, 1), 'unit': 'points/s', 'n_gpus': world, 'steps': args.steps,
+            'warmup': args.warmup, 'ms_per_step': round(ms, 3), 'higher_is_better': True, 'scaling': 'weak',
+            'vs_baseline': None, 'dtype': 'fp32', 'data': 'synthetic S3DIS-like blocks (pcseg.synthetic), '
+                                                          'random-init weights',
+            'config': {'workload': f'{name} seg, {args.npoints} pts, batch {args.batch}/GPU, fwd+CE+bwd'
+                                   f'{"+allreduce" if world > 1 else ""}+Adam',
+                       'model': name, 'global_batch': world * args.batch, 'npoints': args.npoints,
+                       'parallelism': f'dp{world}'},
+            'roofline': roof,
+            'cpu_baseline': cpu_res,
+        }
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

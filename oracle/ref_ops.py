@@ -30,9 +30,13 @@ import torch.nn.functional as F
 class Replay:
     """Queues of FPS starts / kNN indices consumed in call order, plus records."""
 
-    def __init__(self, fps_starts=None, knn_idx=None):
+    def __init__(self, fps_starts=None, knn_idx=None, fps_idx=None, group_idx=None, interp_idx=None):
         self.fps_starts = list(fps_starts) if fps_starts is not None else None
         self.knn_idx = list(knn_idx) if knn_idx is not None else None
+        # full index replay (used to run the oracle in float64 on the float32 run's neighbour choices)
+        self.fps_idx = list(fps_idx) if fps_idx is not None else None
+        self.group_idx = list(group_idx) if group_idx is not None else None
+        self.interp_idx = list(interp_idx) if interp_idx is not None else None
         self.rec_fps_starts: list[torch.Tensor] = []
         self.rec_fps_idx: list[torch.Tensor] = []
         self.rec_group_idx: list[torch.Tensor] = []
@@ -90,9 +94,13 @@ def sample(coords: torch.Tensor, C: int) -> torch.Tensor:
     if rp is not None and rp.fps_starts is not None:
         start = rp.fps_starts.pop(0)
     B, N, _ = coords.shape
-    if start is None:
-        start = torch.randint(0, N, (B,), dtype=torch.int)
-    idx = fps_indices(coords, C, start)
+    if rp is not None and rp.fps_idx:
+        idx = rp.fps_idx.pop(0)
+        start = idx[:, 0].clone()
+    else:
+        if start is None:
+            start = torch.randint(0, N, (B,), dtype=torch.int)
+        idx = fps_indices(coords, C, start)
     if rp is not None:
         rp.rec_fps_starts.append(start.clone())
         rp.rec_fps_idx.append(idx.clone())
@@ -117,8 +125,11 @@ def group(centroid_coords, coords, features, r, K, normalize=False):
     """Reference `group` (common.py:37-71) -> (B, C, K, 3+D)."""
     B, N, _ = features.shape
     C = centroid_coords.shape[1]
-    idx = ball_query(centroid_coords, coords, r, K)
     rp = _rp()
+    if rp is not None and rp.group_idx:
+        idx = rp.group_idx.pop(0).long()
+    else:
+        idx = ball_query(centroid_coords, coords, r, K)
     if rp is not None:
         rp.rec_group_idx.append(idx.clone())
     bi = torch.arange(B).view(B, 1, 1).expand(B, C, K)
@@ -155,8 +166,13 @@ def three_nn(coords_1, coords_2, k=3):
 
 def interpolate(points, coords_1, coords_2, k=3):
     B, N, _ = coords_1.shape
-    dist, idx = three_nn(coords_1, coords_2, k)
     rp = _rp()
+    if rp is not None and rp.interp_idx:
+        idx = rp.interp_idx.pop(0).long()
+        bj = torch.arange(B).view(B, 1, 1).expand_as(idx)
+        dist = ((coords_2[bj, idx] - coords_1.unsqueeze(2)) ** 2).sum(dim=-1)
+    else:
+        dist, idx = three_nn(coords_1, coords_2, k)
     if rp is not None:
         rp.rec_interp_idx.append(idx.clone())
     bi = torch.arange(B).view(B, 1, 1).expand(B, N, k)

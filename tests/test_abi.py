@@ -1,0 +1,104 @@
+"""CPU-side checks of the boundary: the C-ABI library loads and exports every symbol
+include/pcseg.h declares; the product API mirrors the reference's (names,
+signatures, state_dict keys); ops refuse CPU tensors (no silent fallback)."""
+import ctypes
+import inspect
+import os
+import re
+
+import pytest
+import torch
+
+from conftest import REPO
+
+import pcseg
+from pcseg import _lib
+from oracle import ref_ops as R
+
+HEADER = os.path.join(REPO, 'include', 'pcseg.h')
+
+
+def header_symbols():
+    txt = open(HEADER).read()
+    txt = re.sub(r'/\*.*?\*/', '', txt, flags=re.S)
+    return sorted(set(re.findall(r'\b(pcs_[a-z0-9_]+)\s*\(', txt)))
+
+
+def test_library_exports_every_header_symbol():
+    lib = _lib.load()
+    syms = header_symbols()
+    assert len(syms) >= 14
+    for s in syms:
+        assert hasattr(lib, s), s
+    # every typed binding corresponds to a header declaration and vice versa
+    assert set(_lib.SIGNATURES) | {'pcs_last_error', 'pcs_abi_version'} == set(syms)
+    assert lib.pcs_abi_version() == 1
+
+
+def test_nm_exports_are_c_abi():
+    so = _lib.LIB_PATH
+    out = os.popen(f'nm -D --defined-only {so}').read()
+    for s in header_symbols():
+        assert re.search(rf'\bT {s}$', out, flags=re.M), s
+
+
+def test_error_path_without_gpu_compute():
+    """A bad-size call returns an error code + message without touching the device."""
+    lib = _lib.load()
+    rc = lib.pcs_fps(None, 1, 0, 4, None, None, None, None)
+    assert rc != 0
+    assert b'pcs_fps' in lib.pcs_last_error()
+
+
+def test_ops_refuse_cpu_tensors():
+    x = torch.rand(1, 64, 3)
+    with pytest.raises(RuntimeError, match='GPU'):
+        pcseg.ops.fps(x, 8, torch.zeros(1, dtype=torch.int32))
+    with pytest.raises(RuntimeError, match='GPU'):
+        pcseg.ops.ball_query(x[:, :8], x, 0.1, 4)
+
+
+@pytest.mark.parametrize('name', ['PointNetpp', 'PointNeXt', 'DGCNN', 'DGCNNWithColor', 'PointNetSeg',
+                                  'SetAbstraction', 'FeaturePropagation', 'InvResMLP', 'MiniPointNet',
+                                  'UnitPointNet', 'EdgeConv'])
+def test_constructor_signatures_match_reference(name):
+    a = inspect.signature(getattr(pcseg, name).__init__)
+    b = inspect.signature(getattr(R, name).__init__)
+    assert [(p.name, p.default) for p in a.parameters.values()] == \
+        [(p.name, p.default) for p in b.parameters.values()]
+
+
+@pytest.mark.parametrize('ctor', [lambda m: m.PointNetpp(14), lambda m: m.PointNeXt(14),
+                                  lambda m: m.DGCNNWithColor(14), lambda m: m.DGCNN(13),
+                                  lambda m: m.PointNetSeg(14)])
+def test_state_dict_layout_matches_reference(ctor):
+    a, b = ctor(pcseg).state_dict(), ctor(R).state_dict()
+    assert list(a) == list(b)
+    for k in a:
+        assert a[k].shape == b[k].shape and a[k].dtype == b[k].dtype, k
+    # checkpoints interchange
+    ctor(pcseg).load_state_dict(b)
+
+
+def test_functional_signatures_match_reference():
+    for fn in ['sample', 'group', 'reduce', 'interpolate']:
+        a = inspect.signature(getattr(pcseg, fn))
+        b = inspect.signature(getattr(R, fn))
+        assert list(a.parameters) == list(b.parameters), fn
+
+
+def test_loss_matches_oracle_on_cpu(golden):
+    import numpy as np
+    z = golden('loss.npz')
+    logits, onehot, lengths = (torch.from_numpy(np.array(z[k])) for k in ('logits', 'onehot', 'lengths'))
+    assert torch.allclose(pcseg.masked_onehot_cross_entropy(logits, onehot, lengths), torch.from_numpy(z['loss']),
+                          rtol=1e-6)
+    assert float(pcseg.masked_onehot_cross_entropy(logits, onehot, torch.zeros(3, dtype=torch.int64))) == 0.0
+    lf = logits.clone().requires_grad_(True)
+    pcseg.masked_onehot_cross_entropy(lf, onehot.float(), lengths.to(torch.int32)).backward()
+    assert torch.allclose(lf.grad, torch.from_numpy(z['grad']), rtol=1e-6, atol=1e-9)
+
+
+def test_reduce_rejects_unknown_pooling():
+    with pytest.raises(ValueError):
+        pcseg.reduce(torch.zeros(1, 2, 3, 4), 'sum')

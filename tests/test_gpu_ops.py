@@ -1,0 +1,202 @@
+"""GPU parity of every HIP primitive against the CPU oracle (oracle/ref_ops.py),
+through the C ABI.  Index work must be bit-exact; float outputs exact where the
+kernel replays the reference's arithmetic order, else within the stated tolerance.
+"""
+import numpy as np
+import pytest
+import torch
+
+import pcseg
+from pcseg import ops
+from pcseg.synthetic import make_batch
+from oracle import ref_ops as R
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda'
+
+
+def T(a):
+    return torch.from_numpy(np.array(a))
+
+
+def cloud(B, N, seed, kind='surface'):
+    if kind == 'dup':
+        pts, _, _ = make_batch(B, max(8, N // 3), seed)
+        g = torch.Generator().manual_seed(seed)
+        return pts[:, torch.randint(0, pts.shape[1], (N,), generator=g), :3].contiguous()
+    pts, _, _ = make_batch(B, N, seed, uniform=(kind == 'uniform'))
+    return pts[:, :, :3].contiguous()
+
+
+def sorted_rows(idx):
+    return idx.long().sort(-1).values
+
+
+# ----------------------------------------------------------------------------- FPS
+@pytest.mark.parametrize('B,N,C,kind', [(2, 4096, 1024, 'surface'), (3, 1024, 256, 'surface'), (2, 256, 64, 'uniform'),
+                                        (2, 64, 16, 'surface'), (2, 1000, 333, 'dup'), (1, 24576, 1024, 'surface'),
+                                        (2, 5000, 1200, 'uniform'), (1, 37, 37, 'dup'), (4, 2048, 512, 'dup')])
+def test_fps_bit_exact(B, N, C, kind):
+    xyz = cloud(B, N, seed=N + C, kind=kind)
+    start = torch.randint(0, N, (B,), dtype=torch.int32, generator=torch.Generator().manual_seed(N))
+    ref = R.fps_indices(xyz, C, start)
+    idx, cent = ops.fps(xyz.to(DEV), C, start.to(DEV))
+    assert torch.equal(idx.cpu(), ref)
+    assert torch.equal(cent.cpu(), xyz[torch.arange(B).view(B, 1), ref.long()])
+
+
+def test_fps_golden(golden):
+    z = golden('fps.npz')
+    for sfx in ('', '_u', '_d'):
+        xyz = T(z['coords' + sfx])
+        _, cent = ops.fps(xyz.to(DEV), int(z['C' + sfx]), T(z['starts' + sfx]).to(DEV))
+        assert torch.equal(cent.cpu(), T(z['out' + sfx])), sfx
+
+
+# ----------------------------------------------------------------------------- ball query
+@pytest.mark.parametrize('case', ['sa1', 'sa2', 'sa3', 'sa4', 'irm1', 'irm4', 'uni', 'dup', 'big'])
+def test_ball_query_golden(golden, case):
+    z = golden('group.npz')
+    B, N, C, K, norm = [int(v) for v in z[f'{case}/meta']]
+    r = float(z[f'{case}/r'])
+    coords, cent = T(z[f'{case}/coords']), T(z[f'{case}/cent'])
+    idx = ops.ball_query(cent.to(DEV), coords.to(DEV), r, K)
+    ref_idx = T(z[f'{case}/out'])[..., 3].long()
+    assert torch.equal(sorted_rows(idx.cpu()), ref_idx.sort(-1).values)
+
+
+@pytest.mark.parametrize('B,N,C,r,K,kind', [
+    (4, 4096, 1024, 0.1, 32, 'surface'), (4, 1024, 256, 0.2, 32, 'surface'), (4, 256, 64, 0.4, 32, 'surface'),
+    (4, 64, 16, 0.8, 32, 'surface'), (2, 1024, 1024, 0.1, 32, 'surface'), (2, 4096, 512, 0.1, 32, 'uniform'),
+    (2, 2047, 300, 0.3, 32, 'dup'), (2, 2048, 300, 0.3, 32, 'dup'), (2, 16, 16, 0.8, 16, 'surface'),
+    (2, 3000, 100, 0.05, 16, 'surface'), (1, 24576, 1024, 0.1, 32, 'surface'), (2, 100, 50, 2.0, 32, 'uniform')])
+def test_ball_query_matches_oracle(B, N, C, r, K, kind):
+    xyz = cloud(B, N, seed=7 * N + C, kind=kind)
+    start = torch.zeros(B, dtype=torch.int32)
+    cent = xyz[torch.arange(B).view(B, 1), R.fps_indices(xyz, C, start).long()]
+    ref = R.ball_query(cent, xyz, r, K)
+    got = ops.ball_query(cent.to(DEV), xyz.to(DEV), r, K).cpu()
+    assert torch.equal(sorted_rows(got), sorted_rows(ref))
+
+
+# ----------------------------------------------------------------------------- 3-NN
+@pytest.mark.parametrize('case', ['fp1', 'fp2', 'fp3', 'fp4'])
+def test_interpolate_golden_bit_exact(golden, case):
+    z = golden('interp.npz')
+    out = pcseg.interpolate(T(z[f'{case}/f2']).to(DEV), T(z[f'{case}/c1']).to(DEV), T(z[f'{case}/c2']).to(DEV))
+    assert torch.equal(out.cpu(), T(z[f'{case}/out']))
+
+
+@pytest.mark.parametrize('B,N,M,kind', [(4, 4096, 1024, 'surface'), (4, 1024, 256, 'surface'),
+                                        (4, 256, 64, 'surface'), (4, 64, 16, 'surface'), (2, 24576, 1024, 'surface'),
+                                        (2, 2000, 191, 'dup'), (2, 2000, 192, 'dup'), (2, 500, 3, 'uniform')])
+def test_three_nn_matches_oracle(B, N, M, kind):
+    c1 = cloud(B, N, seed=N + M, kind=kind)
+    c2 = c1[torch.arange(B).view(B, 1), R.fps_indices(c1, M, torch.zeros(B, dtype=torch.int32)).long()]
+    dref, iref = R.three_nn(c1, c2)
+    idx, dist = ops.knn_select(c1.to(DEV), c2.to(DEV), 3)
+    assert torch.equal(sorted_rows(idx.cpu()), sorted_rows(iref))
+    assert torch.equal(dist.cpu().sort(-1).values, dref.sort(-1).values)
+
+
+# ----------------------------------------------------------------------------- gathers
+@pytest.mark.parametrize('normalize', [False, True])
+def test_group_fwd_bwd(normalize):
+    B, N, C, K, D, r = 3, 1024, 256, 32, 19, 0.2
+    xyz = cloud(B, N, seed=5)
+    g = torch.Generator().manual_seed(6)
+    feats = torch.randn(B, N, D, generator=g)
+    cent = xyz[:, :C].contiguous()
+    ri = R.ball_query(cent, xyz, r, K)
+    gi = ops.ball_query(cent.to(DEV), xyz.to(DEV), r, K).cpu().long()
+    assert torch.equal(gi.sort(-1).values, ri.sort(-1).values)
+    ref_in = feats.clone().requires_grad_(True)
+    ref = R.group(cent, xyz, ref_in, r, K, normalize)
+    fd = feats.to(DEV).requires_grad_(True)
+    got = pcseg.group(cent.to(DEV), xyz.to(DEV), fd, r, K, normalize)
+    # same neighbour set; canonical order may differ among ties -> align by index
+    ps, pr = gi.argsort(-1), ri.argsort(-1)
+    gs = got.detach().cpu().gather(2, ps.unsqueeze(-1).expand(B, C, K, 3 + D))
+    rs = ref.detach().gather(2, pr.unsqueeze(-1).expand(B, C, K, 3 + D))
+    assert torch.equal(gs, rs)
+
+    def weights(idx):   # order-independent loss weights: a function of (b, c, point, channel)
+        b = torch.arange(B).view(B, 1, 1, 1).double()
+        c = torch.arange(C).view(1, C, 1, 1).double()
+        ch = torch.arange(3 + D).view(1, 1, 1, 3 + D).double()
+        return torch.sin(0.37 * idx.unsqueeze(-1).double() + 1.3 * ch + 0.11 * c + 2.9 * b).float()
+    (ref * weights(ri)).sum().backward()
+    (got * weights(gi).to(DEV)).sum().backward()
+    assert torch.allclose(fd.grad.cpu(), ref_in.grad, rtol=1e-5, atol=1e-5)
+
+
+def test_maxk_fwd_bwd():
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(64, 32, 48, generator=g)
+    x[:, 5] = x[:, 2]                       # exact ties -> first index
+    x = torch.relu(x)                        # many zero ties
+    xr = x.clone().requires_grad_(True)
+    ref = torch.max(xr, dim=1)[0]
+    xd = x.to(DEV).reshape(64 * 32, 48).requires_grad_(True)
+    got = ops.maxk(xd, 32)
+    assert torch.equal(got.detach().cpu(), ref.detach())
+    w = torch.randn(ref.shape, generator=g)
+    (ref * w).sum().backward()
+    (got * w.to(DEV)).sum().backward()
+    assert torch.equal(xd.grad.cpu().view(64, 32, 48), xr.grad)
+
+
+def test_interp_cat_fwd_bwd():
+    B, N, M, D1, D2 = 2, 1024, 256, 7, 13
+    c1 = cloud(B, N, seed=9)
+    c2 = c1[:, :M]
+    g = torch.Generator().manual_seed(9)
+    f1, f2 = torch.randn(B, N, D1, generator=g), torch.randn(B, M, D2, generator=g)
+    r1, r2 = f1.clone().requires_grad_(True), f2.clone().requires_grad_(True)
+    ref = torch.cat([r1, R.interpolate(r2, c1, c2)], dim=-1)
+    d1, d2 = f1.to(DEV).requires_grad_(True), f2.to(DEV).requires_grad_(True)
+    idx, dist = ops.knn_select(c1.to(DEV), c2.to(DEV), 3)
+    got = ops.interp_cat_rows(d1, d2, idx, dist).view(B, N, D1 + D2)
+    assert torch.allclose(got.detach().cpu(), ref.detach(), rtol=1e-6, atol=1e-6)
+    w = torch.randn(ref.shape, generator=g)
+    (ref * w).sum().backward()
+    (got * w.to(DEV)).sum().backward()
+    assert torch.allclose(d1.grad.cpu(), r1.grad)
+    assert torch.allclose(d2.grad.cpu(), r2.grad, rtol=1e-5, atol=1e-5)
+
+
+def test_edge_fwd_bwd():
+    B, N, D, k = 2, 512, 8, 20
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(B, D, N, generator=g)
+    idx = R.knn(x, k)
+    xr = x.clone().requires_grad_(True)
+    ref = R.get_graph_feature(xr, k=k, idx=idx)            # (B, 2D, N, k)
+    xd = x.transpose(1, 2).contiguous().to(DEV).requires_grad_(True)
+    got = ops.edge_rows(xd, idx.to(torch.int32).to(DEV)).view(B, N, k, 2 * D).permute(0, 3, 1, 2)
+    assert torch.equal(got.detach().cpu(), ref.detach())
+    w = torch.randn(ref.shape, generator=g)
+    (ref * w).sum().backward()
+    (got * w.to(DEV)).sum().backward()
+    assert torch.allclose(xd.grad.cpu().transpose(1, 2), xr.grad, rtol=1e-5, atol=1e-5)
+
+
+# ----------------------------------------------------------------------------- DGCNN kNN
+@pytest.mark.parametrize('F_,seed', [(3, 1), (64, 2)])
+def test_dgcnn_knn_agrees_with_oracle(F_, seed):
+    B, N, k = 2, 2048, 20
+    if F_ == 3:
+        x = cloud(B, N, seed).transpose(1, 2).contiguous()
+    else:
+        x = torch.randn(B, F_, N, generator=torch.Generator().manual_seed(seed))
+    ref = R.knn(x, k)
+    got = ops.knn(x.transpose(1, 2).contiguous().to(DEV), k).cpu().long()
+    same = (got.sort(-1).values == ref.sort(-1).values).all(-1)
+    assert same.float().mean() > 0.99
+    # rows that differ may only swap near-ties: compare the k-th best distance
+    xp = x.transpose(1, 2)
+    d = torch.cdist(xp.double(), xp.double()) ** 2
+    kth_ref = d.gather(2, ref).max(-1).values
+    kth_got = d.gather(2, got).max(-1).values
+    assert torch.allclose(kth_got, kth_ref, rtol=1e-4, atol=1e-5)
+    assert (got[..., 0] == torch.arange(N)).float().mean() > 0.99   # self first
