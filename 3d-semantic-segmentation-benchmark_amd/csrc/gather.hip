@@ -25,16 +25,17 @@ static inline dim3 grid_for(long long n, int block = 256) {
 // ------------------------------------------------------------------ group
 __global__ void group_fwd_kernel(const float* __restrict__ xyz, const float* __restrict__ feats,
                                  const float* __restrict__ cent, const int* __restrict__ idx, int C, int N, int K,
-                                 int D, float r, int normalize, float* __restrict__ out, long long total) {
-    const int W = 3 + D;
+                                 int D, float r, int normalize, float* __restrict__ out, int ld, long long total) {
     for (long long t = gtid(); t < total; t += gstride()) {
-        const long long row = t / W;
-        const int ch = (int)(t - row * W);
+        const long long row = t / ld;
+        const int ch = (int)(t - row * ld);
         const long long g = row / K;          // centroid row b*C + c
         const int b = (int)(g / C);
         const int p = idx[row];
         float v;
-        if (ch < 3) {
+        if (ch >= 3 + D) {
+            v = 0.f;                          // row padding (keeps rows 16-B aligned for the GEMM)
+        } else if (ch < 3) {
             v = xyz[((long long)b * N + p) * 3 + ch] - cent[g * 3 + ch];
             if (normalize) v = v / r;
         } else {
@@ -45,8 +46,7 @@ __global__ void group_fwd_kernel(const float* __restrict__ xyz, const float* __r
 }
 
 __global__ void group_bwd_kernel(const float* __restrict__ gout, const int* __restrict__ idx, int C, int N, int K,
-                                 int D, float* __restrict__ gfeats, long long total) {
-    const int W = 3 + D;
+                                 int D, int W, float* __restrict__ gfeats, long long total) {
     for (long long t = gtid(); t < total; t += gstride()) {
         const long long row = t / D;
         const int ch = (int)(t - row * D);
@@ -127,15 +127,16 @@ __global__ void interp_bwd_kernel(const float* __restrict__ gout, const int* __r
 }
 
 // ------------------------------------------------------------------ EdgeConv graph feature
-// out row (b,i,j) = [x[nbr] - x[i], x[i]]  (2D channels), x point-major (B, N, D)
+// out row (b,i,j) = [x[nbr] - x[i], x[i]]  (2D channels, row stride W >= 2D, pad zeroed),
+// x point-major (B, N, D)
 __global__ void edge_fwd_kernel(const float* __restrict__ x, const int* __restrict__ idx, int N, int k, int D,
-                                float* __restrict__ out, long long total) {
-    const int W = 2 * D;
+                                int W, float* __restrict__ out, long long total) {
     for (long long t = gtid(); t < total; t += gstride()) {
         const long long row = t / W;            // (b*N + i)*k + j
         const int ch = (int)(t - row * W);
         const long long pi = row / k;           // b*N + i
         const int b = (int)(pi / N);
+        if (ch >= 2 * D) { out[t] = 0.f; continue; }
         const float xi = x[pi * D + (ch < D ? ch : ch - D)];
         if (ch < D) {
             const int p = idx[row];
@@ -148,8 +149,7 @@ __global__ void edge_fwd_kernel(const float* __restrict__ x, const int* __restri
 
 // gx[i] += sum_j (g_b[i,j] - g_a[i,j]);  gx[nbr] += g_a[i,j]
 __global__ void edge_bwd_kernel(const float* __restrict__ gout, const int* __restrict__ idx, int N, int k, int D,
-                                float* __restrict__ gx, long long total) {
-    const int W = 2 * D;
+                                int W, float* __restrict__ gx, long long total) {
     for (long long t = gtid(); t < total; t += gstride()) {
         const long long pi = t / D;             // b*N + i
         const int ch = (int)(t - pi * D);
@@ -172,26 +172,26 @@ using namespace pcs;
 
 // Reference: models/utils/common.py:62-71.  out (B*C*K, 3+D).
 PCS_API int pcs_group_fwd(const float* xyz, const float* feats, const float* centroids, const int32_t* idx, int B,
-                          int N, int C, int K, int D, float r, int normalize, float* out, void* stream) {
-    PCS_CHECK_ARG(B >= 0 && N >= 1 && C >= 0 && K >= 1 && D >= 0, "pcs_group_fwd: bad sizes");
+                          int N, int C, int K, int D, float r, int normalize, float* out, int ld_out, void* stream) {
+    PCS_CHECK_ARG(B >= 0 && N >= 1 && C >= 0 && K >= 1 && D >= 0 && ld_out >= 3 + D, "pcs_group_fwd: bad sizes");
     PCS_CHECK_ARG(xyz && centroids && idx && out && (D == 0 || feats), "pcs_group_fwd: null pointer");
-    const long long total = (long long)B * C * K * (3 + D);
+    const long long total = (long long)B * C * K * ld_out;
     if (total == 0) return 0;
     hipLaunchKernelGGL(group_fwd_kernel, grid_for(total), dim3(256), 0, as_stream(stream), xyz, feats, centroids,
-                       idx, C, N, K, D, r, normalize, out, total);
+                       idx, C, N, K, D, r, normalize, out, ld_out, total);
     return launch_status("pcs_group_fwd");
 }
 
 // Backward of the feature gather: grad_feats (B, N, D) += scatter of grad_out[..., 3:]
 // (grad_feats must be zeroed by the caller).
-PCS_API int pcs_group_bwd(const float* grad_out, const int32_t* idx, int B, int N, int C, int K, int D,
+PCS_API int pcs_group_bwd(const float* grad_out, int ld_gout, const int32_t* idx, int B, int N, int C, int K, int D,
                           float* grad_feats, void* stream) {
-    PCS_CHECK_ARG(B >= 0 && N >= 1 && C >= 0 && K >= 1 && D >= 0, "pcs_group_bwd: bad sizes");
+    PCS_CHECK_ARG(B >= 0 && N >= 1 && C >= 0 && K >= 1 && D >= 0 && ld_gout >= 3 + D, "pcs_group_bwd: bad sizes");
     const long long total = (long long)B * C * K * D;
     if (total == 0) return 0;
     PCS_CHECK_ARG(grad_out && idx && grad_feats, "pcs_group_bwd: null pointer");
     hipLaunchKernelGGL(group_bwd_kernel, grid_for(total), dim3(256), 0, as_stream(stream), grad_out, idx, C, N, K, D,
-                       grad_feats, total);
+                       ld_gout, grad_feats, total);
     return launch_status("pcs_group_bwd");
 }
 
@@ -245,23 +245,25 @@ PCS_API int pcs_interp_bwd(const float* grad_out, const int32_t* idx, const floa
 }
 
 // Reference: dgcnn.py:41-53.  x (B, N, D) point-major; idx (B, N, k); out (B*N*k, 2D).
-PCS_API int pcs_edge_fwd(const float* x, const int32_t* idx, int B, int N, int k, int D, float* out, void* stream) {
-    PCS_CHECK_ARG(B >= 0 && N >= 1 && k >= 1 && D >= 1, "pcs_edge_fwd: bad sizes");
-    const long long total = (long long)B * N * k * 2 * D;
+PCS_API int pcs_edge_fwd(const float* x, const int32_t* idx, int B, int N, int k, int D, float* out, int ld_out,
+                         void* stream) {
+    PCS_CHECK_ARG(B >= 0 && N >= 1 && k >= 1 && D >= 1 && ld_out >= 2 * D, "pcs_edge_fwd: bad sizes");
+    const long long total = (long long)B * N * k * ld_out;
     if (total == 0) return 0;
     PCS_CHECK_ARG(x && idx && out, "pcs_edge_fwd: null pointer");
-    hipLaunchKernelGGL(edge_fwd_kernel, grid_for(total), dim3(256), 0, as_stream(stream), x, idx, N, k, D, out, total);
+    hipLaunchKernelGGL(edge_fwd_kernel, grid_for(total), dim3(256), 0, as_stream(stream), x, idx, N, k, D, ld_out, out,
+                       total);
     return launch_status("pcs_edge_fwd");
 }
 
 // grad_x (B, N, D) += backward of the graph feature (caller zeroes grad_x).
-PCS_API int pcs_edge_bwd(const float* grad_out, const int32_t* idx, int B, int N, int k, int D, float* grad_x,
-                         void* stream) {
-    PCS_CHECK_ARG(B >= 0 && N >= 1 && k >= 1 && D >= 1, "pcs_edge_bwd: bad sizes");
+PCS_API int pcs_edge_bwd(const float* grad_out, int ld_gout, const int32_t* idx, int B, int N, int k, int D,
+                         float* grad_x, void* stream) {
+    PCS_CHECK_ARG(B >= 0 && N >= 1 && k >= 1 && D >= 1 && ld_gout >= 2 * D, "pcs_edge_bwd: bad sizes");
     const long long total = (long long)B * N * D;
     if (total == 0) return 0;
     PCS_CHECK_ARG(grad_out && idx && grad_x, "pcs_edge_bwd: null pointer");
     hipLaunchKernelGGL(edge_bwd_kernel, grid_for(total), dim3(256), 0, as_stream(stream), grad_out, idx, N, k, D,
-                       grad_x, total);
+                       ld_gout, grad_x, total);
     return launch_status("pcs_edge_bwd");
 }

@@ -26,14 +26,29 @@ SIGNATURES = {
     'pcs_ball_query': [P, P, I32, I32, I32, F32, I32, P, P],
     'pcs_knn_select': [P, P, I32, I32, I32, I32, P, P, P],
     'pcs_knn': [P, I32, I32, I32, I32, P, P],
-    'pcs_group_fwd': [P, P, P, P, I32, I32, I32, I32, I32, F32, I32, P, P],
-    'pcs_group_bwd': [P, P, I32, I32, I32, I32, I32, P, P],
+    'pcs_group_fwd': [P, P, P, P, I32, I32, I32, I32, I32, F32, I32, P, I32, P],
+    'pcs_group_bwd': [P, I32, P, I32, I32, I32, I32, I32, P, P],
     'pcs_maxk_fwd': [P, I64, I32, I32, P, P, P],
     'pcs_maxk_bwd': [P, P, I64, I32, I32, P, P],
     'pcs_interp_fwd': [P, P, P, I32, I32, I32, I32, P, I32, I32, P],
     'pcs_interp_bwd': [P, P, P, I32, I32, I32, I32, I32, I32, P, P],
-    'pcs_edge_fwd': [P, P, I32, I32, I32, I32, P, P],
-    'pcs_edge_bwd': [P, P, I32, I32, I32, I32, P, P],
+    'pcs_edge_fwd': [P, P, I32, I32, I32, I32, P, I32, P],
+    'pcs_edge_bwd': [P, I32, P, I32, I32, I32, I32, P, P],
+    # shared-MLP engine
+    'pcs_gemm_row_blocks': [I32, I32],
+    'pcs_gemm_rows': [P, I32, I32, I32, P, P, I32, F32, P, I32, I32, P, P, I32, I32, P,
+                      P, I32, P, P, P, P, I32, F32, P, P],
+    'pcs_wgrad': [P, I32, I32, P, I32, I32, P, P, I32, F32, I32, P, P, P],
+    'pcs_bn_finalize': [P, I32, I32, I64, P, P, F32, F32, P, P, P, P, P, P, P],
+    'pcs_bn_bwd_finalize': [P, I32, I32, I64, P, P, P, P, P, P],
+    'pcs_bn_bwd_reduce_blocks': [I32],
+    'pcs_bn_bwd_reduce': [P, I32, P, I32, I32, I32, P, P, P, P, I32, F32, P, P],
+    'pcs_bn_bwd_dz': [P, I32, P, I32, I32, I32, P, P, P, P, P, P, I32, F32, P, P],
+    'pcs_pool_fwd': [P, I32, I64, I32, P, P, I32, F32, P, P, P],
+    'pcs_pool_bwd_reduce_blocks': [I64],
+    'pcs_pool_bwd_reduce': [P, P, P, I32, I64, I32, P, P, P, P, I32, F32, P, P],
+    'pcs_pool_bwd_dz': [P, P, P, I32, I64, I32, P, P, P, P, P, P, I32, F32, P, P],
+    'pcs_bn_act': [P, I32, I32, I32, P, P, I32, F32, P, I32, P],
 }
 
 _lock = threading.Lock()

@@ -11,7 +11,7 @@ import torch
 import torch.nn as nn
 
 from . import ops
-from .mlp import mlp_rows
+from .engine import shared_mlp, pad_rows
 from .replay import active as _replay
 
 
@@ -55,7 +55,8 @@ def group(centroid_coords: torch.Tensor, coords: torch.Tensor, features: torch.T
     B, C, _ = centroid_coords.shape
     idx = _ball(centroid_coords, coords, r, K)
     rows = ops.group_rows(coords, features, centroid_coords, idx, r, normalize)
-    return rows.view(B, C, K, rows.shape[1])
+    D = features.shape[2] if features is not None else 0
+    return rows.view(B, C, K, rows.shape[1])[..., :3 + D]
 
 
 def reduce(x: torch.Tensor, type: str) -> torch.Tensor:
@@ -95,13 +96,14 @@ class MiniPointNet(nn.Module):
             self.batch.append(nn.BatchNorm2d(m))
             prev = m
 
-    def forward_rows(self, x: torch.Tensor) -> torch.Tensor:
-        return mlp_rows(x, self.conv, self.batch)
+    def forward_rows(self, x: torch.Tensor, kin: int | None = None, pool_k: int = 0) -> torch.Tensor:
+        """rows (M, ld) -> (M, C_L), or (M/pool_k, C_L) max-pooled over consecutive groups of pool_k rows."""
+        return shared_mlp(x, kin or x.shape[1], self.conv, self.batch, 'relu', 0.0, pool_k)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         B, Cin, H, W = x.shape
         rows = x.permute(0, 2, 3, 1).reshape(B * H * W, Cin)
-        return self.forward_rows(rows).view(B, H, W, -1).permute(0, 3, 1, 2)
+        return self.forward_rows(pad_rows(rows), Cin).view(B, H, W, -1).permute(0, 3, 1, 2)
 
 
 class UnitPointNet(nn.Module):
@@ -117,13 +119,13 @@ class UnitPointNet(nn.Module):
             self.batch.append(nn.BatchNorm1d(m))
             prev = m
 
-    def forward_rows(self, x: torch.Tensor) -> torch.Tensor:
-        return mlp_rows(x, self.conv, self.batch)
+    def forward_rows(self, x: torch.Tensor, kin: int | None = None) -> torch.Tensor:
+        return shared_mlp(x, kin or x.shape[1], self.conv, self.batch, 'relu', 0.0, 0)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         B, Cin, N = x.shape
         rows = x.permute(0, 2, 1).reshape(B * N, Cin)
-        return self.forward_rows(rows).view(B, N, -1).permute(0, 2, 1)
+        return self.forward_rows(pad_rows(rows), Cin).view(B, N, -1).permute(0, 2, 1)
 
 
 class SetAbstraction(nn.Module):
@@ -144,10 +146,11 @@ class SetAbstraction(nn.Module):
         _, cent = sample_indices(coords, self.C)
         idx = _ball(cent, coords, self.radius, self.K)
         rows = ops.group_rows(coords, features, cent, idx, self.radius, self.grouping_norm)
-        act = self.point_net.forward_rows(rows)
+        kin = 3 + features.shape[2]
         if self.pooling_type == 'max':
-            out = ops.maxk(act, self.K).view(B, self.C, -1)
+            out = self.point_net.forward_rows(rows, kin, pool_k=self.K).view(B, self.C, -1)
         else:
+            act = self.point_net.forward_rows(rows, kin)
             out = reduce(act.view(B, self.C, self.K, -1), self.pooling_type)
         return cent, out
 
@@ -186,10 +189,11 @@ class InvResMLP(nn.Module):
         B, C, _ = centroid_coords.shape
         idx = _ball(centroid_coords, coords, self.radius, self.K)
         rows = ops.group_rows(coords, features, centroid_coords, idx, self.radius, True)
-        act = self.neighbour_features_mlp.forward_rows(rows)
+        kin = 3 + features.shape[2]
         if self.pooling_type == 'max':
-            pooled = ops.maxk(act, self.K)
+            pooled = self.neighbour_features_mlp.forward_rows(rows, kin, pool_k=self.K)
         else:
+            act = self.neighbour_features_mlp.forward_rows(rows, kin)
             pooled = reduce(act.view(B, C, self.K, -1), self.pooling_type).reshape(B * C, -1)
         out = self.point_features_mlp.forward_rows(pooled).view(B, C, -1)
         return centroid_coords, out + features

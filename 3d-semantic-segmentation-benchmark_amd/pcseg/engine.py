@@ -1,0 +1,219 @@
+"""Shared-MLP engine: a stack of (1x1 conv -> training-mode BN -> ReLU/LeakyReLU)
+layers on point-major rows, optionally max-pooled over groups of K rows, run
+entirely by the HIP kernels of csrc/mlp.hip (MFMA fp32 GEMMs with fused BN
+statistics / BN-apply / pooling, fp64 statistics).
+
+Reference semantics: MiniPointNet / UnitPointNet (models/utils/common.py:125-178)
+followed by `reduce(..., 'max')` (common.py:211-212), EdgeConv
+(models/dgcnn/dgcnn.py:67-76), DGCNN conv5..conv7 (dgcnn.py:188-207).
+
+Only pre-BN activations Z are kept for backward; the BN-applied activation of
+layer l is recomputed inside layer l+1's GEMM A-load, so it never touches HBM.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from ._lib import call, load, ptr, stream_ptr
+
+ACT = {'relu': 0, 'lrelu': 1, 'none': 2}
+BM = 128  # row tile of pcs_gemm_rows (must match csrc/mlp.hip)
+
+
+def ld4(n: int) -> int:
+    return (n + 3) // 4 * 4
+
+
+def pad_rows(x: torch.Tensor) -> torch.Tensor:
+    """(M, C) -> contiguous rows with a stride that is a multiple of 4 (zero pad)."""
+    M, C = x.shape
+    ld = ld4(C)
+    if ld == C and x.is_contiguous():
+        return x
+    out = torch.zeros((M, ld), dtype=torch.float32, device=x.device)
+    out[:, :C] = x
+    return out
+
+
+def _f64(shape, dev):
+    return torch.empty(shape, dtype=torch.float64, device=dev)
+
+
+def _f32(shape, dev):
+    return torch.empty(shape, dtype=torch.float32, device=dev)
+
+
+class SharedMLPFn(torch.autograd.Function):
+    """rows X (M, ld) with Kin logical channels -> pooled (M/pool_K, C_L) or activation (M, C_L)."""
+
+    @staticmethod
+    def forward(ctx, X, Kin, pool_K, act, slope, bns, *params):
+        dev = X.device
+        st = stream_ptr(dev)
+        M, lda = X.shape
+        a_code = ACT[act]
+        A, lda_cur, K_cur, s_prev, t_prev = X, lda, Kin, None, None
+        Zs, stats = [], []
+        nl = len(bns)
+        for li in range(nl):
+            W, b, g, be = params[4 * li:4 * li + 4]
+            bn = bns[li]
+            Cout = W.shape[0]
+            Wm = W.reshape(Cout, -1)
+            if not Wm.is_contiguous():
+                Wm = Wm.contiguous()
+            if Cout % 4:
+                raise ValueError(f'engine: layer width {Cout} must be a multiple of 4')
+            Z = _f32((M, Cout), dev)
+            use_batch = bn.training or bn.running_mean is None
+            s, t, mean, inv = (_f32((Cout,), dev) for _ in range(4))
+            if use_batch:
+                nb = (M + BM - 1) // BM
+                part = _f64((nb, 2, Cout), dev)
+                call('pcs_gemm_rows', ptr(A), lda_cur, M, K_cur, ptr(s_prev), ptr(t_prev), a_code, slope,
+                     ptr(Wm), Wm.shape[1], 1, ptr(b), ptr(Z), Cout, Cout, ptr(part),
+                     None, 0, None, None, None, None, 0, 0.0, None, st)
+                momentum = 0.0
+                rm = rv = None
+                if bn.training and bn.track_running_stats and bn.running_mean is not None:
+                    bn.num_batches_tracked.add_(1)
+                    momentum = bn.momentum if bn.momentum is not None else 1.0 / float(bn.num_batches_tracked)
+                    rm, rv = bn.running_mean, bn.running_var
+                call('pcs_bn_finalize', ptr(part), nb, Cout, M, ptr(g), ptr(be), float(bn.eps), float(momentum),
+                     ptr(rm), ptr(rv), ptr(s), ptr(t), ptr(mean), ptr(inv), st)
+            else:
+                call('pcs_gemm_rows', ptr(A), lda_cur, M, K_cur, ptr(s_prev), ptr(t_prev), a_code, slope,
+                     ptr(Wm), Wm.shape[1], 1, ptr(b), ptr(Z), Cout, Cout, None,
+                     None, 0, None, None, None, None, 0, 0.0, None, st)
+                with torch.no_grad():
+                    inv.copy_(torch.rsqrt(bn.running_var + bn.eps))
+                    mean.copy_(bn.running_mean)
+                    s.copy_((g if g is not None else 1.0) * inv)
+                    t.copy_((be if be is not None else 0.0) - mean * s)
+            Zs.append(Z)
+            stats.append((s, t, mean, inv, use_batch))
+            A, lda_cur, K_cur, s_prev, t_prev = Z, Cout, Cout, s, t
+        CL = Zs[-1].shape[1]
+        s, t = stats[-1][0], stats[-1][1]
+        if pool_K:
+            G = M // pool_K
+            out = _f32((G, CL), dev)
+            arg = torch.empty((G, CL), dtype=torch.uint8, device=dev)
+            call('pcs_pool_fwd', ptr(Zs[-1]), CL, G, pool_K, ptr(s), ptr(t), a_code, slope, ptr(out), ptr(arg), st)
+            ctx.mark_non_differentiable(arg)
+        else:
+            out = _f32((M, CL), dev)
+            arg = None
+            call('pcs_bn_act', ptr(Zs[-1]), CL, M, CL, ptr(s), ptr(t), a_code, slope, ptr(out), CL, st)
+        ctx.save_for_backward(X, *Zs, *[x for st_ in stats for x in st_[:4]], *(p for p in params if p is not None),
+                              *([arg] if arg is not None else []))
+        ctx.meta = (Kin, pool_K, a_code, slope, nl, [st_[4] for st_ in stats],
+                    [p is not None for p in params], arg is not None)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        Kin, pool_K, a_code, slope, nl, use_batch, present, has_arg = ctx.meta
+        saved = list(ctx.saved_tensors)
+        X = saved[0]
+        Zs = saved[1:1 + nl]
+        flat = saved[1 + nl:1 + nl + 4 * nl]
+        stats = [tuple(flat[4 * i:4 * i + 4]) for i in range(nl)]
+        rest = saved[1 + nl + 4 * nl:]
+        params = []
+        it = iter(rest)
+        for pr in present:
+            params.append(next(it) if pr else None)
+        arg = next(it) if has_arg else None
+        dev = gout.device
+        st = stream_ptr(dev)
+        lib = load()
+        M, lda = X.shape
+        gout = gout.contiguous()
+        CL = Zs[-1].shape[1]
+        s, t, mean, inv = stats[-1]
+        grads = [None] * len(params)
+
+        # ---- top layer: BN-backward sums and dZ
+        if pool_K:
+            G = M // pool_K
+            nb = lib.pcs_pool_bwd_reduce_blocks(G)
+            part = _f64((nb, 2, CL), dev)
+            call('pcs_pool_bwd_reduce', ptr(gout), ptr(arg), ptr(Zs[-1]), CL, G, pool_K, ptr(s), ptr(t), ptr(mean),
+                 ptr(inv), a_code, slope, ptr(part), st)
+        else:
+            nb = lib.pcs_bn_bwd_reduce_blocks(M)
+            part = _f64((nb, 2, CL), dev)
+            call('pcs_bn_bwd_reduce', ptr(gout), CL, ptr(Zs[-1]), CL, M, CL, ptr(s), ptr(t), ptr(mean), ptr(inv),
+                 a_code, slope, ptr(part), st)
+        dgam, dbet, kB, kC = (_f32((CL,), dev) for _ in range(4))
+        call('pcs_bn_bwd_finalize', ptr(part), nb, CL, M, ptr(s), ptr(dgam), ptr(dbet), ptr(kB), ptr(kC), st)
+        if not use_batch[-1]:
+            kB.zero_()
+            kC.zero_()
+        dZ = _f32((M, CL), dev)
+        if pool_K:
+            call('pcs_pool_bwd_dz', ptr(gout), ptr(arg), ptr(Zs[-1]), CL, M // pool_K, pool_K, ptr(s), ptr(t),
+                 ptr(mean), ptr(inv), ptr(kB), ptr(kC), a_code, slope, ptr(dZ), st)
+        else:
+            call('pcs_bn_bwd_dz', ptr(gout), CL, ptr(Zs[-1]), CL, M, CL, ptr(s), ptr(t), ptr(mean), ptr(inv),
+                 ptr(kB), ptr(kC), a_code, slope, ptr(dZ), st)
+        bn_grads = {nl - 1: (dgam, dbet)}
+        dX = None
+        for li in range(nl - 1, -1, -1):
+            W, b = params[4 * li], params[4 * li + 1]
+            Cout = W.shape[0]
+            Wm = W.reshape(Cout, -1)
+            Cin = Wm.shape[1]
+            dW = torch.zeros((Cout, Cin), dtype=torch.float32, device=dev)
+            db = torch.zeros((Cout,), dtype=torch.float32, device=dev) if b is not None else None
+            if li > 0:
+                sp, tp, mp, ip = stats[li - 1]
+                call('pcs_wgrad', ptr(dZ), Cout, Cout, ptr(Zs[li - 1]), Cin, Cin, ptr(sp), ptr(tp), a_code, slope, M,
+                     ptr(dW), ptr(db), st)
+            else:
+                call('pcs_wgrad', ptr(dZ), Cout, Cout, ptr(X), lda, Kin, None, None, 0, 0.0, M, ptr(dW), ptr(db), st)
+            grads[4 * li] = dW.view_as(W)
+            grads[4 * li + 1] = db
+            if li > 0:
+                sp, tp, mp, ip = stats[li - 1]
+                dA = _f32((M, Cin), dev)
+                nbg = (M + BM - 1) // BM
+                bpart = _f64((nbg, 2, Cin), dev)
+                call('pcs_gemm_rows', ptr(dZ), Cout, M, Cout, None, None, 0, 0.0, ptr(Wm), Cin, 0, None, ptr(dA), Cin,
+                     Cin, None, ptr(Zs[li - 1]), Cin, ptr(sp), ptr(tp), ptr(mp), ptr(ip), a_code, slope, ptr(bpart),
+                     st)
+                g2, b2, kB2, kC2 = (_f32((Cin,), dev) for _ in range(4))
+                call('pcs_bn_bwd_finalize', ptr(bpart), nbg, Cin, M, ptr(sp), ptr(g2), ptr(b2), ptr(kB2), ptr(kC2), st)
+                if not use_batch[li - 1]:
+                    kB2.zero_()
+                    kC2.zero_()
+                bn_grads[li - 1] = (g2, b2)
+                dZ = _f32((M, Cin), dev)
+                call('pcs_bn_bwd_dz', ptr(dA), Cin, ptr(Zs[li - 1]), Cin, M, Cin, ptr(sp), ptr(tp), ptr(mp), ptr(ip),
+                     ptr(kB2), ptr(kC2), a_code, slope, ptr(dZ), st)
+            elif ctx.needs_input_grad[0]:
+                dX = torch.zeros((M, lda), dtype=torch.float32, device=dev) if lda != Kin else _f32((M, lda), dev)
+                call('pcs_gemm_rows', ptr(dZ), Cout, M, Cout, None, None, 0, 0.0, ptr(Wm), Cin, 0, None, ptr(dX), lda,
+                     Kin, None, None, 0, None, None, None, None, 0, 0.0, None, st)
+        for li, (dg, dbb) in bn_grads.items():
+            if params[4 * li + 2] is not None:
+                grads[4 * li + 2] = dg
+            if params[4 * li + 3] is not None:
+                grads[4 * li + 3] = dbb
+        return (dX, None, None, None, None, None, *grads)
+
+
+def shared_mlp(x_rows: torch.Tensor, kin: int, convs, bns, act: str = 'relu', slope: float = 0.0,
+               pool_k: int = 0) -> torch.Tensor:
+    """Run a conv/BN/act stack on rows.  x_rows (M, ld) with `kin` logical channels, ld % 4 == 0."""
+    if not x_rows.is_cuda:
+        raise RuntimeError('pcseg ops run only on the GPU (no CPU fallback); got a CPU tensor')
+    if x_rows.shape[1] % 4 or not x_rows.is_contiguous():
+        x_rows = pad_rows(x_rows[:, :kin])
+    params = []
+    for conv, bn in zip(convs, bns):
+        params += [conv.weight, conv.bias, bn.weight, bn.bias]
+    return SharedMLPFn.apply(x_rows, kin, pool_k, act, float(slope), list(bns), *params)

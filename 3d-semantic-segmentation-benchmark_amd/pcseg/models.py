@@ -18,6 +18,7 @@ import torch.nn.functional as F
 from . import ops
 from .common import SetAbstraction, FeaturePropagation, InvResMLP, UnitPointNet, sample_indices, _ball
 from .mlp import conv_rows, bn_rows
+from .engine import shared_mlp, pad_rows
 from .replay import active as _replay
 
 
@@ -98,8 +99,7 @@ class PointNetppMSG(nn.Module):
         for sa in branches:
             idx = _ball(cent, coords, sa.radius, sa.K)
             rows = ops.group_rows(coords, feats, cent, idx, sa.radius, sa.grouping_norm)
-            act = sa.point_net.forward_rows(rows)
-            outs.append(ops.maxk(act, sa.K).view(B, C, -1))
+            outs.append(sa.point_net.forward_rows(rows, 3 + feats.shape[2], pool_k=sa.K).view(B, C, -1))
         return cent, torch.cat(outs, dim=-1)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
@@ -151,7 +151,7 @@ class PointNeXt(nn.Module):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         B, N, Cin = x.shape
         x = x.contiguous()
-        f0 = self.mlp.forward_rows(x.view(B * N, Cin)).view(B, N, -1)
+        f0 = self.mlp.forward_rows(pad_rows(x.view(B * N, Cin)), Cin).view(B, N, -1)
         c0 = x[:, :, :3].contiguous()
         c1, f1 = self.sa1(c0, f0)
         c1, f1 = self.irmlp1(c1, c1, f1)
@@ -170,10 +170,9 @@ class PointNeXt(nn.Module):
 
 
 # ------------------------------------------------------------------------- DGCNN
-def _seq_rows(x_rows: torch.Tensor, seq: nn.Sequential) -> torch.Tensor:
-    """Conv1d(bias=False) -> BN1d -> LeakyReLU [-> Dropout] on rows."""
-    z = bn_rows(conv_rows(x_rows, seq[0]), seq[1])
-    y = F.leaky_relu(z, seq[2].negative_slope)
+def _seq_rows(x_rows: torch.Tensor, seq: nn.Sequential, kin: int | None = None) -> torch.Tensor:
+    """Conv1d(bias=False) -> BN1d -> LeakyReLU [-> Dropout] on rows (HIP shared-MLP engine)."""
+    y = shared_mlp(x_rows, kin or x_rows.shape[1], [seq[0]], [seq[1]], 'lrelu', seq[2].negative_slope, 0)
     if len(seq) > 3:
         y = seq[3](y)
     return y
@@ -201,9 +200,9 @@ class EdgeConv(nn.Module):
         if rp is not None:
             rp.rec_knn_idx.append(idx.detach().cpu())
         rows = ops.edge_rows(xp, idx)
-        z = bn_rows(conv_rows(rows, self.conv[0]), self.conv[1])
-        y = F.leaky_relu(z, self.conv[2].negative_slope)
-        return ops.maxk(y, self.k).view(B, N, -1)
+        pooled = shared_mlp(rows, 2 * xp.shape[2], [self.conv[0]], [self.conv[1]], 'lrelu',
+                            self.conv[2].negative_slope, pool_k=self.k)
+        return pooled.view(B, N, -1)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         return self.forward_points(x.transpose(1, 2).contiguous()).transpose(1, 2)
@@ -284,7 +283,7 @@ class DGCNNWithColor(nn.Module):
         x2 = self.conv2.forward_points(x1)
         x3 = self.conv3.forward_points(x2)
         x4 = self.conv4.forward_points(x3)
-        color = _seq_rows(rgb.view(B * N, 3), self.color_conv).view(B, N, -1)
+        color = _seq_rows(pad_rows(rgb.view(B * N, 3)), self.color_conv, 3).view(B, N, -1)
         return _dgcnn_head(self, [x1, x2, x3, x4, color], B, N)
 
 

@@ -73,31 +73,37 @@ def knn(x: torch.Tensor, k: int) -> torch.Tensor:
 
 
 # ------------------------------------------------------------------ differentiable gathers
+def ld4(n: int) -> int:
+    return (n + 3) // 4 * 4
+
+
 class GroupFn(torch.autograd.Function):
-    """(B*C*K, 3+D) rows [ (xyz[idx]-c) (/r), feats[idx] ]; grad flows to feats only."""
+    """(B*C*K, ld) rows [ (xyz[idx]-c) (/r), feats[idx], 0-pad ], ld = 3+D rounded up to 4;
+    grad flows to feats only (coords never require grad in the reference)."""
 
     @staticmethod
     def forward(ctx, xyz, feats, cent, idx, r, normalize):
         B, N, _ = xyz.shape
         C, K = idx.shape[1], idx.shape[2]
         D = feats.shape[2] if feats is not None else 0
-        out = torch.empty((B * C * K, 3 + D), dtype=torch.float32, device=xyz.device)
+        ld = ld4(3 + D)
+        out = torch.empty((B * C * K, ld), dtype=torch.float32, device=xyz.device)
         call('pcs_group_fwd', ptr(xyz), ptr(feats), ptr(cent), ptr(idx), B, N, C, K, D, float(np.float32(r)),
-             int(bool(normalize)), ptr(out), stream_ptr(xyz.device))
+             int(bool(normalize)), ptr(out), ld, stream_ptr(xyz.device))
         ctx.save_for_backward(idx)
-        ctx.dims = (B, N, C, K, D)
+        ctx.dims = (B, N, C, K, D, ld)
         ctx.has_feats = feats is not None
         return out
 
     @staticmethod
     def backward(ctx, gout):
         (idx,) = ctx.saved_tensors
-        B, N, C, K, D = ctx.dims
+        B, N, C, K, D, ld = ctx.dims
         gfeats = None
         if ctx.has_feats and ctx.needs_input_grad[1]:
             gout = _c(gout)
             gfeats = torch.zeros((B, N, D), dtype=torch.float32, device=gout.device)
-            call('pcs_group_bwd', ptr(gout), ptr(idx), B, N, C, K, D, ptr(gfeats), stream_ptr(gout.device))
+            call('pcs_group_bwd', ptr(gout), ld, ptr(idx), B, N, C, K, D, ptr(gfeats), stream_ptr(gout.device))
         return None, gfeats, None, None, None, None
 
 
@@ -183,25 +189,26 @@ def interp_cat_rows(f1, f2, idx, dist):
 
 
 class EdgeFn(torch.autograd.Function):
-    """rows (B*N*k, 2D) = [x_j - x_i, x_i] (reference get_graph_feature, dgcnn.py:41-53)."""
+    """rows (B*N*k, ld) = [x_j - x_i, x_i, 0-pad] (reference get_graph_feature, dgcnn.py:41-53)."""
 
     @staticmethod
     def forward(ctx, x, idx):
         B, N, D = x.shape
         k = idx.shape[2]
-        out = torch.empty((B * N * k, 2 * D), dtype=torch.float32, device=x.device)
-        call('pcs_edge_fwd', ptr(x), ptr(idx), B, N, k, D, ptr(out), stream_ptr(x.device))
+        ld = ld4(2 * D)
+        out = torch.empty((B * N * k, ld), dtype=torch.float32, device=x.device)
+        call('pcs_edge_fwd', ptr(x), ptr(idx), B, N, k, D, ptr(out), ld, stream_ptr(x.device))
         ctx.save_for_backward(idx)
-        ctx.dims = (B, N, k, D)
+        ctx.dims = (B, N, k, D, ld)
         return out
 
     @staticmethod
     def backward(ctx, gout):
         (idx,) = ctx.saved_tensors
-        B, N, k, D = ctx.dims
+        B, N, k, D, ld = ctx.dims
         gout = _c(gout)
         gx = torch.zeros((B, N, D), dtype=torch.float32, device=gout.device)
-        call('pcs_edge_bwd', ptr(gout), ptr(idx), B, N, k, D, ptr(gx), stream_ptr(gout.device))
+        call('pcs_edge_bwd', ptr(gout), ld, ptr(idx), B, N, k, D, ptr(gx), stream_ptr(gout.device))
         return gx, None
 
 

@@ -114,12 +114,13 @@ def kernel_roofline(args, dev):
     _, cent = ops.fps(xyz, C, start)
     idx = ops.ball_query(cent, xyz, r, K)
     D = feats.shape[2]
-    out = torch.empty((B * C * K, 3 + D), device=dev)
+    ld = (3 + D + 3) // 4 * 4
+    out = torch.empty((B * C * K, ld), device=dev)
     from pcseg._lib import call, ptr, stream_ptr
     s = stream_ptr(dev)
 
     def launch():
-        call('pcs_group_fwd', ptr(xyz), ptr(feats), ptr(cent), ptr(idx), B, N, C, K, D, 0.1, 0, ptr(out), s)
+        call('pcs_group_fwd', ptr(xyz), ptr(feats), ptr(cent), ptr(idx), B, N, C, K, D, 0.1, 0, ptr(out), ld, s)
     for _ in range(5):
         launch()
     st = torch.cuda.current_stream(dev)
@@ -134,7 +135,7 @@ def kernel_roofline(args, dev):
     # algorithmic bytes: write the grouped rows, read their indices, read the cloud
     # (xyz+feats once) and the centroids once.
     M = B * C * K
-    algo = M * (3 + D) * 4 + M * 4 + B * N * (3 + D) * 4 + B * C * 3 * 4
+    algo = M * ld * 4 + M * 4 + B * N * (3 + D) * 4 + B * C * 3 * 4
     gbs = algo / (ms * 1e-3) / 1e9
     return {'kernel': 'group_fwd_kernel (SA1 gather: B=%d C=%d K=%d D=%d)' % (B, C, K, D), 'bound': 'hbm',
             'achieved': round(gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': round(gbs / HBM_PEAK_GBS, 4),

@@ -62,10 +62,11 @@ int pcs_knn(const float* x, int B, int N, int F, int k, int32_t* out_idx,
  * [ (xyz[idx]-centroid) (/ r if normalize), feats[idx] ]. */
 int pcs_group_fwd(const float* xyz, const float* feats, const float* centroids,
                   const int32_t* idx, int B, int N, int C, int K, int D,
-                  float r, int normalize, float* out, void* stream);
-/* grad_feats (B,N,D) += scatter(grad_out[:, 3:])   (accumulating) */
-int pcs_group_bwd(const float* grad_out, const int32_t* idx, int B, int N,
-                  int C, int K, int D, float* grad_feats, void* stream);
+                  float r, int normalize, float* out, int ld_out, void* stream);
+/* grad_feats (B,N,D) += scatter(grad_out[:, 3:3+D])   (accumulating);
+ * rows of grad_out have stride ld_gout (>= 3+D; pad columns zeroed by fwd) */
+int pcs_group_bwd(const float* grad_out, int ld_gout, const int32_t* idx, int B,
+                  int N, int C, int K, int D, float* grad_feats, void* stream);
 
 /* models/utils/common.py:85-86 `reduce(x,'max')` over K:
  * x (G*K, Ch) -> out (G, Ch), argmax (G, Ch) uint8 (first max). */
@@ -88,10 +89,74 @@ int pcs_interp_bwd(const float* grad_out, const int32_t* idx, const float* dist,
 /* models/dgcnn/dgcnn.py:41-53 `get_graph_feature`: x (B,N,D) point-major,
  * idx (B,N,k); out (B*N*k, 2D) rows [x_j - x_i, x_i]. */
 int pcs_edge_fwd(const float* x, const int32_t* idx, int B, int N, int k,
-                 int D, float* out, void* stream);
+                 int D, float* out, int ld_out, void* stream);
 /* grad_x (B,N,D) += backward of the above   (accumulating) */
-int pcs_edge_bwd(const float* grad_out, const int32_t* idx, int B, int N,
-                 int k, int D, float* grad_x, void* stream);
+int pcs_edge_bwd(const float* grad_out, int ld_gout, const int32_t* idx, int B,
+                 int N, int k, int D, float* grad_x, void* stream);
+
+/* ---- shared-MLP engine: 1x1 conv + training-mode BN + ReLU/LeakyReLU ------
+ * models/utils/common.py:125-178 (MiniPointNet/UnitPointNet), dgcnn.py:67-76,
+ * dgcnn.py:188-207.  act: 0 = ReLU, 1 = LeakyReLU(slope), 2 = identity.
+ * BN partial-sum workspaces are fp64 [blocks][2][N]. */
+
+/* row blocks of pcs_gemm_rows (sizes its stats/bstats workspace) */
+int pcs_gemm_row_blocks(int M, int N);
+/* C (M x N, ldc) = act_in(A*s_in + t_in) . op(W) (+bias): op(W) = W^T (trans_w,
+ * W is N x K) or W (K x N).  A rows have stride lda (multiple of 4).
+ * stats: partial (sum, sum^2) of C per channel.  bstats: fused BN-backward
+ * partials (sum dy, sum dy*xhat) of the layer whose pre-BN output is zp
+ * (dy = C * act'(zp*sp+tp), xhat = (zp-meanp)*invp). */
+int pcs_gemm_rows(const float* A, int lda, int M, int K, const float* s_in,
+                  const float* t_in, int act_in, float slope_in, const float* W,
+                  int ldw, int trans_w, const float* bias, float* C, int ldc,
+                  int N, double* stats, const float* zp, int ldzp,
+                  const float* sp, const float* tp, const float* meanp,
+                  const float* invp, int actp, float slopep, double* bstats,
+                  void* stream);
+/* dW (N x K) += X^T . act(Y*s+t) over M rows (s,t nullable = identity);
+ * db (N, nullable) += column sums of X.   (accumulating) */
+int pcs_wgrad(const float* X, int ldx, int N, const float* Y, int ldy, int K,
+              const float* s, const float* t, int act, float slope, int M,
+              float* dW, float* db, void* stream);
+/* BN forward finalize: partials -> scale s, shift t, mean, invstd; running
+ * mean/var updated with `momentum` and the unbiased variance (nullable). */
+int pcs_bn_finalize(const double* part, int nb, int N, long long M,
+                    const float* gamma, const float* beta, float eps,
+                    float momentum, float* run_mean, float* run_var, float* s,
+                    float* t, float* mean, float* invstd, void* stream);
+/* BN backward finalize: partials -> dgamma, dbeta, kB = s*sum_dy/M,
+ * kC = s*sum(dy*xhat)/M  (dZ = s*dy - kB - kC*xhat). */
+int pcs_bn_bwd_finalize(const double* part, int nb, int N, long long M,
+                        const float* s, float* dgamma, float* dbeta, float* kB,
+                        float* kC, void* stream);
+int pcs_bn_bwd_reduce_blocks(int M);
+int pcs_bn_bwd_reduce(const float* dA, int ldd, const float* Z, int ldz, int M,
+                      int N, const float* s, const float* t, const float* mean,
+                      const float* inv, int act, float slope, double* part,
+                      void* stream);
+int pcs_bn_bwd_dz(const float* dA, int ldd, const float* Z, int ldz, int M,
+                  int N, const float* s, const float* t, const float* mean,
+                  const float* inv, const float* kB, const float* kC, int act,
+                  float slope, float* dZ, void* stream);
+/* common.py:211-212 / dgcnn.py:76: pooled (G x N) = max_k act(Z*s+t), first
+ * argmax (u8); Z rows are (g*K + k). */
+int pcs_pool_fwd(const float* Z, int N, long long G, int K, const float* s,
+                 const float* t, int act, float slope, float* out,
+                 uint8_t* arg, void* stream);
+int pcs_pool_bwd_reduce_blocks(long long G);
+int pcs_pool_bwd_reduce(const float* dpool, const uint8_t* arg, const float* Z,
+                        int N, long long G, int K, const float* s,
+                        const float* t, const float* mean, const float* inv,
+                        int act, float slope, double* part, void* stream);
+int pcs_pool_bwd_dz(const float* dpool, const uint8_t* arg, const float* Z,
+                    int N, long long G, int K, const float* s, const float* t,
+                    const float* mean, const float* inv, const float* kB,
+                    const float* kC, int act, float slope, float* dZ,
+                    void* stream);
+/* out (M x N, ldo) = act(Z*s + t) */
+int pcs_bn_act(const float* Z, int ldz, int M, int N, const float* s,
+               const float* t, int act, float slope, float* out, int ldo,
+               void* stream);
 
 #ifdef __cplusplus
 }

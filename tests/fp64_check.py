@@ -25,15 +25,21 @@ def _dropout_off(m):
             mod.eval()
 
 
-def three_way(prod_ctor, ref_ctor, B, N, seed, uniform=False, pad=0, dev='cuda', chfirst=False):
-    pts, labels, lengths = make_batch(B, N, seed=seed, uniform=uniform)
-    if pad:
-        lengths = torch.tensor([N - pad * (i % 2) for i in range(B)], dtype=torch.uint64)
-        for i in range(B):
-            pts[i, int(lengths[i]):] = 0.0
-    x = pts[:, :, :6].contiguous().transpose(1, 2) if chfirst else pts
-    lab = labels.float() if chfirst else labels
-    ref32 = R.seeded_init_(ref_ctor(), seed)
+def three_way(prod_ctor, ref_ctor, B, N, seed, uniform=False, pad=0, dev='cuda', chfirst=False,
+              inputs=None, init_seed=None, fps_starts=None, knn_idx=None):
+    """inputs=(x, labels, lengths) overrides the synthetic batch; fps_starts / knn_idx seed the
+    fp32 oracle run (e.g. a golden fixture's recorded draws)."""
+    if inputs is None:
+        pts, labels, lengths = make_batch(B, N, seed=seed, uniform=uniform)
+        if pad:
+            lengths = torch.tensor([N - pad * (i % 2) for i in range(B)], dtype=torch.uint64)
+            for i in range(B):
+                pts[i, int(lengths[i]):] = 0.0
+        x = pts[:, :, :6].contiguous().transpose(1, 2) if chfirst else pts
+        lab = labels.float() if chfirst else labels
+    else:
+        x, lab, lengths = inputs
+    ref32 = R.seeded_init_(ref_ctor(), seed if init_seed is None else init_seed)
     ref64 = copy.deepcopy(ref32).double()
     prod = prod_ctor()
     prod.load_state_dict(ref32.state_dict())
@@ -45,7 +51,7 @@ def three_way(prod_ctor, ref_ctor, B, N, seed, uniform=False, pad=0, dev='cuda',
     def logits_of(o):
         return o[0] if isinstance(o, tuple) else o
 
-    rp = R.Replay()
+    rp = R.Replay(fps_starts=fps_starts, knn_idx=knn_idx)
     with R.replay(rp):
         l32 = logits_of(ref32(x))
     R.masked_onehot_cross_entropy(l32, lab, lengths).backward()

@@ -14,9 +14,10 @@ Two anchors:
     tensor passes when the GPU error vs fp64 is <= 1e-3 of its norm OR no more
     than 10x the CPU reference's own fp32 error (tests/fp64_check.py).  In
     practice the GPU error is at or below the CPU reference's on every tensor.
-Gradient summaries against the golden fixtures use a 2e-2 norm-relative bound
-(catches wrong indices / scatters, which give O(1) errors) because the
-fixture holds only the reference's fp32 values.
+On the golden fixtures the gradients get the same three-way check (weights,
+inputs and FPS draws of the fixture), plus a coarse 2e-2 / 5e-2 norm-relative
+comparison with the fixture's own gradient summaries (catches wrong indices /
+scatters, which give O(1) errors).
 """
 import numpy as np
 import pytest
@@ -56,7 +57,12 @@ def prepare(prod_ctor, ref_ctor, seed):
 GRAD_RTOL_GOLDEN = 2e-2
 
 
-def check_grad_summaries(model, z):
+def _assert_three_way(rows):
+    bad = failures(rows, rtol=RTOL, factor=10.0)
+    assert not bad, bad
+
+
+def check_grad_summaries(model, z, rtol=GRAD_RTOL_GOLDEN):
     g = torch.Generator().manual_seed(7)
     gmax = max(float(z['g_l2/' + k]) for k, _ in model.named_parameters())
     for k, p in sorted(model.named_parameters()):
@@ -65,9 +71,9 @@ def check_grad_summaries(model, z):
         flat = gr.reshape(-1).double()
         scale = max(float(z['g_l2/' + k]), 1e-3 * gmax)
         d_l2 = abs(float(flat.norm()) - float(z['g_l2/' + k]))
-        assert d_l2 <= GRAD_RTOL_GOLDEN * scale, (k, d_l2, scale)
+        assert d_l2 <= rtol * scale, (k, d_l2, scale)
         d_dot = abs(float((flat * probe.reshape(-1).double()).sum()) - float(z['g_dot/' + k]))
-        assert d_dot <= GRAD_RTOL_GOLDEN * scale * max(1.0, flat.numel() ** 0.5), (k, d_dot, scale)
+        assert d_dot <= rtol * scale * max(1.0, flat.numel() ** 0.5), (k, d_dot, scale)
 
 
 def check_buffers(model, z):
@@ -127,8 +133,11 @@ def test_pointnet2_family_vs_reference_golden(golden, name, prod, ref, seed):
     loss = pcseg.masked_onehot_cross_entropy(logits, T(z['labels']).to(DEV), T(z['lengths']).to(DEV))
     assert abs(float(loss) - float(z['loss'])) <= RTOL * abs(float(z['loss']))
     loss.backward()
-    check_grad_summaries(model, z)
     check_buffers(model, z)
+    # every gradient tensor, on the golden inputs/weights/FPS draws: three-way vs fp64 truth
+    _assert_three_way(three_way(prod, ref, 0, 0, 0, inputs=(T(z['x']), T(z['labels']), T(z['lengths'])),
+                                init_seed=seed, fps_starts=fps_starts(z)))
+    check_grad_summaries(model, z, rtol=5e-2)
 
 
 def test_dgcnn_color_vs_reference_golden(golden):
@@ -146,8 +155,13 @@ def test_dgcnn_color_vs_reference_golden(golden):
                                              T(z['lengths']).to(torch.int32).to(DEV))
     assert abs(float(loss) - float(z['loss'])) <= RTOL * abs(float(z['loss']))
     loss.backward()
-    check_grad_summaries(model, z)
     check_buffers(model, z)
+    check_grad_summaries(model, z)
+    xin = T(z['x']).transpose(1, 2).contiguous().transpose(1, 2)
+    _assert_three_way(three_way(lambda: pcseg.DGCNNWithColor(num_classes=14, k=20),
+                                lambda: R.DGCNNWithColor(num_classes=14, k=20), 0, 0, 0,
+                                inputs=(xin, T(z['labels']).float(), T(z['lengths']).to(torch.int32)),
+                                init_seed=999, knn_idx=[T(z[f'knn{i}']).long() for i in range(4)]))
 
 
 def test_pointnet_vs_reference_golden(golden):
@@ -160,11 +174,6 @@ def test_pointnet_vs_reference_golden(golden):
     # gradients: the fixture's B=2 makes the TNet's BatchNorm1d degenerate (2 samples), so its
     # gradients are cancellation noise in the reference itself; they are covered by the B=4
     # three-way test below instead.
-
-
-def _assert_three_way(rows):
-    bad = failures(rows, rtol=RTOL, factor=10.0)
-    assert not bad, bad
 
 
 @pytest.mark.parametrize('B,N,seed,uniform,pad', [(4, 4096, 101, False, 0), (2, 4096, 102, True, 0),
