@@ -11,34 +11,95 @@
 // live in registers (PPT points per thread), so a step touches no memory except
 // one 16-B LDS slot per wave.  The running minimum is kept SQUARED (sqrt is
 // monotone, so min commutes with it); each thread takes its local maximum M,
-// computes S = sqrtf(M) once (correctly rounded) and the lowest of its points
-// whose sqrt rounds to S -- so the key (S, lowest index) reproduces the
-// reference's argmax over sqrt'ed distances, ties included, with one sqrt per
-// thread per step instead of one per point.  Keys are reduced wave-wide with
-// shuffles, then across waves through a double-buffered LDS slot array.
+// and the wave reduces them with DPP row ops + v_readlane; only the wave-level
+// maximum is square-rooted (correctly rounded), and the lowest index whose
+// sqrt ties it is found by a threshold compare -- so the pick reproduces the
+// reference's argmax over sqrt'ed distances, ties included.  Waves combine
+// through a double-buffered LDS slot array (one barrier per step).
 #include "pcs_common.hpp"
+
+#include <stdlib.h>
 
 namespace pcs {
 
-__device__ __forceinline__ void umax64(unsigned& hi, unsigned& lo, unsigned h2, unsigned l2) {
-    const bool take = (h2 > hi) || (h2 == hi && l2 > lo);
-    hi = take ? h2 : hi;
-    lo = take ? l2 : lo;
+template <int CTRL>
+__device__ __forceinline__ unsigned dpp_u(unsigned v) {
+    return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
 }
 
+// wave-wide max / min of an unsigned value, result wave-uniform: DPP inside 16-lane
+// rows (quad xor1, quad xor2, half-row mirror, row mirror) + v_readlane of the four
+// row results.  No LDS round trips.
+__device__ __forceinline__ unsigned wave_umax(unsigned v) {
+    v = max(v, dpp_u<0xB1>(v));
+    v = max(v, dpp_u<0x4E>(v));
+    v = max(v, dpp_u<0x141>(v));
+    v = max(v, dpp_u<0x140>(v));
+    return max(max(readlane_u(v, 0), readlane_u(v, 16)), max(readlane_u(v, 32), readlane_u(v, 48)));
+}
+__device__ __forceinline__ unsigned wave_umin(unsigned v) {
+    v = min(v, dpp_u<0xB1>(v));
+    v = min(v, dpp_u<0x4E>(v));
+    v = min(v, dpp_u<0x141>(v));
+    v = min(v, dpp_u<0x140>(v));
+    return min(min(readlane_u(v, 0), readlane_u(v, 16)), min(readlane_u(v, 32), readlane_u(v, 48)));
+}
+
+constexpr int kFpsLdsOut = 2048;   // centroids buffered in LDS (written once at the end)
+
+#ifdef PCS_FPS_STAMPS
+// diagnostic build only (scripts/fps_stamps.py): per-segment s_memtime cycles of wave 0, block 0
+__device__ unsigned long long g_fps_stamps[8];
+#define FPS_STAMP(k)                                                                      \
+    do {                                                                                  \
+        __builtin_amdgcn_sched_barrier(0);                                                \
+        unsigned long long tn_;                                                           \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(tn_)::"memory");       \
+        __builtin_amdgcn_sched_barrier(0);                                                \
+        st_acc[k] += tn_ - st_prev;                                                       \
+        st_prev = tn_;                                                                    \
+    } while (0)
+#else
+#define FPS_STAMP(k) \
+    do {             \
+    } while (0)
+#endif
+
+constexpr int kFpsLdsCloud = 8192;   // clouds up to this size keep a coordinate copy in LDS
+
+// One step per loop iteration:
+//  1. each thread folds the new distances into its squared running minima and takes
+//     its local max (squared);
+//  2. wave max M* (exact, as float bits) -> S = sqrtf(M*) and lo = the smallest
+//     float whose sqrt rounds to S (wave-uniform, sqrts in parallel);
+//  3. the wave's candidate = lowest point index with best >= lo, i.e. the lowest
+//     index among ALL its points whose reference distance sqrt(best) equals S;
+//  4. lane 0 of every wave publishes (S, index) in one LDS slot; after the barrier
+//     lane l of every wave reads slot l and the waves redo the (max S, min index)
+//     reduction with DPP -- no serial compare chain -- and fetch the winner's
+//     coordinates from the LDS copy of the cloud.
+// This is exactly the reference's "first index of max(sqrt distances)".
 template <int BLOCK, int PPT>
 __global__ __launch_bounds__(BLOCK) void fps_kernel(const float* __restrict__ xyz, int N, int C,
                                                     const int* __restrict__ start, int* __restrict__ out_idx,
                                                     float* __restrict__ out_xyz) {
     constexpr int NW = BLOCK / kWave;
-    __shared__ unsigned s_khi[2][NW];
-    __shared__ unsigned s_klo[2][NW];
-    __shared__ float4 s_pos[2][NW];
+    static_assert(NW <= 64, "one slot per lane");
+    __shared__ __attribute__((aligned(16))) uint2 s_key[2][NW];   // (sqrt bits + 1, index); 0 = empty
+    // Per-step global stores would make every __syncthreads wait for them (the
+    // barrier's fence drains vmcnt): keep the picked centroids in LDS instead.
+    __shared__ float4 s_out[kFpsLdsOut];
+    __shared__ float s_cloud[3 * kFpsLdsCloud];
+    const bool lds_out = C <= kFpsLdsOut;
+    const bool lds_cloud = N <= kFpsLdsCloud;
 
     const int b = blockIdx.x;
     const int t = threadIdx.x;
-    const int w = t >> 6;
+    const int w = t >> 6, lane = t & 63;
     const float* P = xyz + (size_t)b * N * 3;
+
+    if (lds_cloud)
+        for (int e = t; e < 3 * N; e += BLOCK) s_cloud[e] = P[e];
 
     float px[PPT], py[PPT], pz[PPT], best[PPT];
 #pragma unroll
@@ -51,21 +112,31 @@ __global__ __launch_bounds__(BLOCK) void fps_kernel(const float* __restrict__ xy
             best[j] = __int_as_float(0x7f800000);
         } else {
             px[j] = py[j] = pz[j] = 0.f;
-            best[j] = -1.f;  // never a candidate
+            best[j] = -1.f;  // never a candidate: fminf(d >= 0, -1) keeps -1
         }
     }
 
     int far = start[b];
     far = far < 0 ? 0 : (far >= N ? N - 1 : far);
     float cx = P[3 * far + 0], cy = P[3 * far + 1], cz = P[3 * far + 2];
+    if (lds_cloud) __syncthreads();
 
+#ifdef PCS_FPS_STAMPS
+    unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long st_prev = __builtin_amdgcn_s_memtime();
+#endif
     for (int i = 0; i < C; ++i) {
+        FPS_STAMP(0);
         if (t == 0) {
-            out_idx[(size_t)b * C + i] = far;
-            float* o = out_xyz + ((size_t)b * C + i) * 3;
-            o[0] = cx;
-            o[1] = cy;
-            o[2] = cz;
+            if (lds_out) {
+                s_out[i] = make_float4(cx, cy, cz, __int_as_float(far));
+            } else {
+                out_idx[(size_t)b * C + i] = far;
+                float* o = out_xyz + ((size_t)b * C + i) * 3;
+                o[0] = cx;
+                o[1] = cy;
+                o[2] = cz;
+            }
         }
         if (i == C - 1) break;
 
@@ -74,58 +145,71 @@ __global__ __launch_bounds__(BLOCK) void fps_kernel(const float* __restrict__ xy
         for (int j = 0; j < PPT; ++j) {
             const float dx = px[j] - cx, dy = py[j] - cy, dz = pz[j] - cz;
             const float d = __fmaf_rn(dz, dz, __fmaf_rn(dy, dy, __fmul_rn(dx, dx)));
-            if (best[j] >= 0.f) best[j] = d < best[j] ? d : best[j];
+            best[j] = fminf(d, best[j]);                  // == (d < best ? d : best): no NaN, no -0 here
             M = fmaxf(M, best[j]);
         }
-
-        unsigned khi = 0, klo = 0;
-        int jsel = 0;
-        if (M >= 0.f) {
-            const float S = __fsqrt_rn(M);
-            float lo = M;
-            for (int it = 0; it < 4 && lo > 0.f; ++it) {
-                const float pl = __uint_as_float(__float_as_uint(lo) - 1u);
-                if (__fsqrt_rn(pl) == S) lo = pl; else break;
-            }
-            jsel = PPT;
+        FPS_STAMP(1);
+        const unsigned wk = wave_umax(M >= 0.f ? __float_as_uint(M) + 1u : 0u);
+        FPS_STAMP(2);
+        const int buf = i & 1;
+        if (wk != 0) {
+            const unsigned mb = wk - 1u;
+            const float Mw = __uint_as_float(mb);
+            const float S = __fsqrt_rn(Mw);
+            // at most 3 floats below Mw share its sqrt (sqrt halves relative spacing):
+            // test them in parallel instead of a dependent chain of sqrts
+            const float p1 = mb >= 1u ? __uint_as_float(mb - 1u) : -1.f;
+            const float p2 = mb >= 2u ? __uint_as_float(mb - 2u) : -1.f;
+            const float p3 = mb >= 3u ? __uint_as_float(mb - 3u) : -1.f;
+            const bool e1 = p1 >= 0.f && __fsqrt_rn(p1) == S;
+            const bool e2 = p2 >= 0.f && __fsqrt_rn(p2) == S;
+            const bool e3 = p3 >= 0.f && __fsqrt_rn(p3) == S;
+            const float lo = e1 ? (e2 ? (e3 ? p3 : p2) : p1) : Mw;
+            unsigned cand = 0xFFFFFFFFu;
 #pragma unroll
             for (int j = PPT - 1; j >= 0; --j)
-                if (best[j] >= lo) jsel = j;
-            khi = __float_as_uint(S) + 1u;
-            klo = 0xFFFFFFFFu - (unsigned)(jsel * BLOCK + t);
+                cand = best[j] >= lo ? (unsigned)(j * BLOCK + t) : cand;
+            FPS_STAMP(3);
+            const unsigned widx = wave_umin(cand);
+            FPS_STAMP(4);
+            if (lane == 0) s_key[buf][w] = make_uint2(__float_as_uint(S) + 1u, widx);
+        } else if (lane == 0) {
+            s_key[buf][w] = make_uint2(0u, 0xFFFFFFFFu);
         }
-        unsigned mhi = khi, mlo = klo;
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) {
-            const unsigned h2 = (unsigned)__shfl_xor((int)mhi, o);
-            const unsigned l2 = (unsigned)__shfl_xor((int)mlo, o);
-            umax64(mhi, mlo, h2, l2);
-        }
-        const int buf = i & 1;
-        if ((t & 63) == 0) {
-            s_khi[buf][w] = mhi;
-            s_klo[buf][w] = mlo;
-        }
-        if (khi != 0 && khi == mhi && klo == mlo) {
-            float x = 0.f, y = 0.f, z = 0.f;
-#pragma unroll
-            for (int j = 0; j < PPT; ++j)
-                if (j == jsel) { x = px[j]; y = py[j]; z = pz[j]; }
-            s_pos[buf][w] = make_float4(x, y, z, 0.f);
-        }
+        FPS_STAMP(5);
         __syncthreads();
-        unsigned bh = s_khi[buf][0], bl = s_klo[buf][0];
-        int bw = 0;
-#pragma unroll
-        for (int ww = 1; ww < NW; ++ww) {
-            const unsigned h2 = s_khi[buf][ww], l2 = s_klo[buf][ww];
-            if ((h2 > bh) || (h2 == bh && l2 > bl)) { bh = h2; bl = l2; bw = ww; }
+        FPS_STAMP(6);
+        const uint2 k2 = lane < NW ? s_key[buf][lane] : make_uint2(0u, 0xFFFFFFFFu);
+        const unsigned bs = wave_umax(k2.x);
+        far = (int)wave_umin(k2.x == bs ? k2.y : 0xFFFFFFFFu);
+        if (lds_cloud) {
+            cx = s_cloud[3 * far + 0];
+            cy = s_cloud[3 * far + 1];
+            cz = s_cloud[3 * far + 2];
+        } else {
+            cx = P[3 * far + 0];
+            cy = P[3 * far + 1];
+            cz = P[3 * far + 2];
         }
-        far = (int)(0xFFFFFFFFu - bl);
-        const float4 q = s_pos[buf][bw];
-        cx = q.x;
-        cy = q.y;
-        cz = q.z;
+#ifdef PCS_FPS_STAMPS
+        asm volatile("" ::"v"(cx), "v"(cy), "v"(cz));
+        FPS_STAMP(7);
+#endif
+    }
+#ifdef PCS_FPS_STAMPS
+    if (blockIdx.x == 0 && t == 0)
+        for (int k = 0; k < 8; ++k) g_fps_stamps[k] = st_acc[k];
+#endif
+    if (lds_out) {
+        __syncthreads();
+        for (int i = t; i < C; i += BLOCK) {
+            const float4 q = s_out[i];
+            out_idx[(size_t)b * C + i] = __float_as_int(q.w);
+            float* o = out_xyz + ((size_t)b * C + i) * 3;
+            o[0] = q.x;
+            o[1] = q.y;
+            o[2] = q.z;
+        }
     }
 }
 
@@ -146,16 +230,27 @@ PCS_API int pcs_fps(const float* xyz, int B, int N, int C, const int32_t* start,
     PCS_CHECK_ARG(xyz && start && out_idx && out_xyz, "pcs_fps: null pointer");
     if (B == 0) return 0;
     hipStream_t s = as_stream(stream);
-    if (N <= 64) launch_fps<64, 1>(xyz, B, N, C, start, out_idx, out_xyz, s);
-    else if (N <= 256) launch_fps<256, 1>(xyz, B, N, C, start, out_idx, out_xyz, s);
-    else if (N <= 1024) launch_fps<256, 4>(xyz, B, N, C, start, out_idx, out_xyz, s);
-    else if (N <= 4096) launch_fps<512, 8>(xyz, B, N, C, start, out_idx, out_xyz, s);
-    else if (N <= 8192) launch_fps<512, 16>(xyz, B, N, C, start, out_idx, out_xyz, s);
-    else if (N <= 16384) launch_fps<1024, 16>(xyz, B, N, C, start, out_idx, out_xyz, s);
-    else if (N <= 32768) launch_fps<1024, 32>(xyz, B, N, C, start, out_idx, out_xyz, s);
-    else {
-        set_error("pcs_fps: N=%d exceeds the 32768-point limit", N);
+    // threads per cloud: PCS_FPS_BLOCK (64/256/512/1024) overrides the default, for tuning
+    static const int forced = [] { const char* e = getenv("PCS_FPS_BLOCK"); return e ? atoi(e) : 0; }();
+    const int blk = forced ? forced : (N <= 256 ? 64 : (N <= 2048 ? 256 : (N <= 8192 ? 512 : 1024)));
+    const int ppt = (N + blk - 1) / blk;
+#define PCS_FPS_CASE(BL, PP) if (blk == BL && ppt <= PP) { launch_fps<BL, PP>(xyz, B, N, C, start, out_idx, out_xyz, s); } else
+    PCS_FPS_CASE(64, 1) PCS_FPS_CASE(64, 2) PCS_FPS_CASE(64, 4) PCS_FPS_CASE(64, 8)
+    PCS_FPS_CASE(256, 1) PCS_FPS_CASE(256, 2) PCS_FPS_CASE(256, 4) PCS_FPS_CASE(256, 8) PCS_FPS_CASE(256, 16)
+    PCS_FPS_CASE(512, 2) PCS_FPS_CASE(512, 4) PCS_FPS_CASE(512, 8) PCS_FPS_CASE(512, 16)
+    PCS_FPS_CASE(1024, 1) PCS_FPS_CASE(1024, 2) PCS_FPS_CASE(1024, 4) PCS_FPS_CASE(1024, 8)
+    PCS_FPS_CASE(1024, 16) PCS_FPS_CASE(1024, 24) PCS_FPS_CASE(1024, 32)
+    {
+        set_error("pcs_fps: N=%d not supported with %d threads per cloud (max 32768 points)", N, blk);
         return (int)hipErrorInvalidValue;
     }
+#undef PCS_FPS_CASE
     return launch_status("pcs_fps");
 }
+
+#ifdef PCS_FPS_STAMPS
+PCS_API int pcs_debug_fps_stamps(unsigned long long* host_out) {
+    return (int)hipMemcpyFromSymbol(host_out, HIP_SYMBOL(pcs::g_fps_stamps), sizeof(unsigned long long) * 8, 0,
+                                    hipMemcpyDeviceToHost);
+}
+#endif

@@ -43,7 +43,7 @@ struct GemmArgs {
     const float* A; int lda; int M; int K;     // A rows (M x K), row stride lda
     const float* s_in; const float* t_in;      // A transform: act(a*s+t) per K channel (or null)
     int act_in; float slope_in;
-    const float* W; int ldw;                   // BT: B[k][n] = W[n*ldw+k]; else B[k][n] = W[k*ldw+n]
+    const float* W; int ldw;                   // B[k][n] = W[n*ldw + k]
     const float* bias;                         // per n (or null)
     float* C; int ldc; int N;                  // output rows (M x N)
     double* stats;                             // [gridDim.x][2][N]: sum, sum of squares of C (or null)
@@ -55,20 +55,35 @@ struct GemmArgs {
 };
 
 // ------------------------------------------------------------------ row GEMM
-template <int BM, int BN, int WM, int WN, bool BT, bool AXF>
-__global__ __launch_bounds__(256) void gemm_rows_kernel(GemmArgs g) {
-    constexpr int BK = 32;
+// C[M x N] = T(A)[M x K] . B[K x N],  B[k][n] = W[n*ldw + k]  (W row-major N x K).
+//
+// 256 threads = 4 waves in a WM x WN grid; each wave owns TM x TN 32x32 MFMA tiles.
+// K is consumed in 32-deep slabs staged through a double-buffered LDS ring with the
+// next slab's global loads in flight (registers) while the current slab is computed.
+// Inside a slab the k order is permuted so that lane half h takes k = 16h + s
+// (s = 0..15): each lane's A/B fragments are then 16 CONSECUTIVE floats of one LDS
+// row, read with ds_read_b128; the 144-B row stride (BK + 4 floats) makes those
+// reads bank-conflict free.  The MFMA sums over k, so the permutation only
+// reorders the fp32 accumulation.
+constexpr int GBK = 32;
+constexpr int GLDK = GBK + 4;
+
+template <int BM, int BN, int WM, int WN, bool AXF>
+__global__ __launch_bounds__(256, 2) void gemm_rows_kernel(GemmArgs g) {
     constexpr int WTM = BM / WM, WTN = BN / WN;
     constexpr int TM = WTM / 32, TN = WTN / 32;
-    static_assert(WM * WN == 4, "4 waves");
-    static_assert(TM >= 1 && TN >= 1, "tile");
-    __shared__ float As[BM][BK + 1];
-    __shared__ float Bs[BK][BN + 1];
+    constexpr int AV = BM * GBK / 4 / 256;
+    constexpr int BV = (BN * GBK / 4 + 255) / 256;
+    static_assert(WM * WN == 4 && TM >= 1 && TN >= 1, "tile");
+    __shared__ __attribute__((aligned(16))) float As[2][BM][GLDK];
+    __shared__ __attribute__((aligned(16))) float Bs[2][BN][GLDK];
     __shared__ double red[2][WM][BN];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave / WN, wn = wave % WN;
     const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+    const int h = lane >> 5, l32 = lane & 31;
+    const bool wvec = (g.ldw & 3) == 0;
 
     f32x16 acc[TM][TN];
 #pragma unroll
@@ -78,62 +93,103 @@ __global__ __launch_bounds__(256) void gemm_rows_kernel(GemmArgs g) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-    for (int k0 = 0; k0 < g.K; k0 += BK) {
-        // ---- A tile (BM x BK), float4 loads along K (lda % 4 == 0)
+    float4 ra[AV], rb[BV];
+    // every A float4 of this thread sits at the same k offset 4*(tid&7) of a slab, so one
+    // (scale, shift) quad per slab serves all of them
+    float4 rs = make_float4(0.f, 0.f, 0.f, 0.f), rt = rs;
+    auto gload = [&](int k0) {
+        if (AXF) {
+            const int gk = k0 + 4 * (tid & 7);
+            rs.x = gk + 0 < g.K ? g.s_in[gk + 0] : 0.f;
+            rs.y = gk + 1 < g.K ? g.s_in[gk + 1] : 0.f;
+            rs.z = gk + 2 < g.K ? g.s_in[gk + 2] : 0.f;
+            rs.w = gk + 3 < g.K ? g.s_in[gk + 3] : 0.f;
+            rt.x = gk + 0 < g.K ? g.t_in[gk + 0] : 0.f;
+            rt.y = gk + 1 < g.K ? g.t_in[gk + 1] : 0.f;
+            rt.z = gk + 2 < g.K ? g.t_in[gk + 2] : 0.f;
+            rt.w = gk + 3 < g.K ? g.t_in[gk + 3] : 0.f;
+        }
 #pragma unroll
-        for (int it = 0; it < BM * BK / 4 / 256; ++it) {
+        for (int it = 0; it < AV; ++it) {
             const int e = it * 256 + tid;
-            const int r = e / (BK / 4), c4 = e % (BK / 4);
-            const int gr = m0 + r, gk = k0 + c4 * 4;
-            float v[4] = {0.f, 0.f, 0.f, 0.f};
-            if (gr < g.M && gk < g.K) {
-                const float4 q = *reinterpret_cast<const float4*>(g.A + (size_t)gr * g.lda + gk);
-                v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    if (gk + i >= g.K) v[i] = 0.f;
-                    else if (AXF) v[i] = act_f(v[i] * g.s_in[gk + i] + g.t_in[gk + i], g.act_in, g.slope_in);
-                }
-            }
-#pragma unroll
-            for (int i = 0; i < 4; ++i) As[r][c4 * 4 + i] = v[i];
+            const int r = e >> 3, c4 = e & 7;
+            const int gr = m0 + r, gk = k0 + 4 * c4;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (gr < g.M && gk < g.K) v = *reinterpret_cast<const float4*>(g.A + (size_t)gr * g.lda + gk);
+            ra[it] = v;
         }
-        // ---- B tile (BK x BN)
-        if (BT) {
 #pragma unroll
-            for (int it = 0; it < (BK * BN + 255) / 256; ++it) {
-                const int e = it * 256 + tid;
-                if (e < BK * BN) {
-                    const int n = e / BK, kk = e % BK;
-                    const int gn = n0 + n, gk = k0 + kk;
-                    Bs[kk][n] = (gn < g.N && gk < g.K) ? g.W[(size_t)gn * g.ldw + gk] : 0.f;
+        for (int it = 0; it < BV; ++it) {
+            const int e = it * 256 + tid;
+            const int n = e >> 3, c4 = e & 7;
+            const int gn = n0 + n, gk = k0 + 4 * c4;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (e < BN * GBK / 4 && gn < g.N && gk < g.K) {
+                const float* w = g.W + (size_t)gn * g.ldw + gk;
+                if (wvec && gk + 3 < g.K) v = *reinterpret_cast<const float4*>(w);
+                else {
+                    v.x = w[0];
+                    v.y = gk + 1 < g.K ? w[1] : 0.f;
+                    v.z = gk + 2 < g.K ? w[2] : 0.f;
+                    v.w = gk + 3 < g.K ? w[3] : 0.f;
                 }
             }
-        } else {
-#pragma unroll
-            for (int it = 0; it < (BK * BN + 255) / 256; ++it) {
-                const int e = it * 256 + tid;
-                if (e < BK * BN) {
-                    const int kk = e / BN, n = e % BN;
-                    const int gn = n0 + n, gk = k0 + kk;
-                    Bs[kk][n] = (gn < g.N && gk < g.K) ? g.W[(size_t)gk * g.ldw + gn] : 0.f;
-                }
-            }
+            rb[it] = v;
         }
-        __syncthreads();
+    };
+    auto sstore = [&](int buf, int k0) {
 #pragma unroll
-        for (int kk = 0; kk < BK; kk += 2) {
-            float a[TM], b[TN];
+        for (int it = 0; it < AV; ++it) {
+            const int e = it * 256 + tid;
+            const int r = e >> 3, c4 = e & 7;
+            const int gk = k0 + 4 * c4;
+            float4 v = ra[it];
+            if (AXF) {
+                v.x = gk + 0 < g.K ? act_f(v.x * rs.x + rt.x, g.act_in, g.slope_in) : 0.f;
+                v.y = gk + 1 < g.K ? act_f(v.y * rs.y + rt.y, g.act_in, g.slope_in) : 0.f;
+                v.z = gk + 2 < g.K ? act_f(v.z * rs.z + rt.z, g.act_in, g.slope_in) : 0.f;
+                v.w = gk + 3 < g.K ? act_f(v.w * rs.w + rt.w, g.act_in, g.slope_in) : 0.f;
+            } else {
+                v.y = gk + 1 < g.K ? v.y : 0.f;
+                v.z = gk + 2 < g.K ? v.z : 0.f;
+                v.w = gk + 3 < g.K ? v.w : 0.f;
+            }
+            *reinterpret_cast<float4*>(&As[buf][r][4 * c4]) = v;
+        }
 #pragma unroll
-            for (int i = 0; i < TM; ++i) a[i] = As[wm * WTM + i * 32 + (lane & 31)][kk + (lane >> 5)];
+        for (int it = 0; it < BV; ++it) {
+            const int e = it * 256 + tid;
+            if (e < BN * GBK / 4) *reinterpret_cast<float4*>(&Bs[buf][e >> 3][4 * (e & 7)]) = rb[it];
+        }
+    };
+
+    const int nk = (g.K + GBK - 1) / GBK;
+    gload(0);
+    sstore(0, 0);
+    __syncthreads();
+    for (int ks = 0; ks < nk; ++ks) {
+        const int buf = ks & 1;
+        if (ks + 1 < nk) gload((ks + 1) * GBK);
 #pragma unroll
-            for (int j = 0; j < TN; ++j) b[j] = Bs[kk + (lane >> 5)][wn * WTN + j * 32 + (lane & 31)];
+        for (int q = 0; q < 4; ++q) {
+            float4 a[TM], b[TN];
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+                a[i] = *reinterpret_cast<const float4*>(&As[buf][wm * WTM + i * 32 + l32][16 * h + 4 * q]);
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+                b[j] = *reinterpret_cast<const float4*>(&Bs[buf][wn * WTN + j * 32 + l32][16 * h + 4 * q]);
 #pragma unroll
             for (int i = 0; i < TM; ++i)
 #pragma unroll
-                for (int j = 0; j < TN; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+                for (int j = 0; j < TN; ++j) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].x, b[j].x, acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].y, b[j].y, acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].z, b[j].z, acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].w, b[j].w, acc[i][j], 0, 0, 0);
+                }
         }
+        if (ks + 1 < nk) sstore(buf ^ 1, (ks + 1) * GBK);
         __syncthreads();
     }
 
@@ -142,7 +198,7 @@ __global__ __launch_bounds__(256) void gemm_rows_kernel(GemmArgs g) {
     const bool want_b = g.bstats != nullptr;
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-        const int lc = wn * WTN + j * 32 + (lane & 31);
+        const int lc = wn * WTN + j * 32 + l32;
         const int col = n0 + lc;
         const bool cok = col < g.N;
         const float bv = (g.bias && cok) ? g.bias[col] : 0.f;
@@ -153,7 +209,7 @@ __global__ __launch_bounds__(256) void gemm_rows_kernel(GemmArgs g) {
         for (int i = 0; i < TM; ++i) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const int row = m0 + wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                const int row = m0 + wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
                 if (row < g.M && cok) {
                     const float v = acc[i][j][r] + bv;
                     g.C[(size_t)row * g.ldc + col] = v;
@@ -198,62 +254,169 @@ __global__ __launch_bounds__(256) void gemm_rows_kernel(GemmArgs g) {
 
 // ------------------------------------------------------------------ weight gradient
 // dW[n][k] += sum_r X[r][n] * T(Y)[r][k] ; db[n] += sum_r X[r][n]   (rows split over gridDim.x)
-template <bool YXF>
-__global__ __launch_bounds__(256) void wgrad_kernel(const float* __restrict__ X, int ldx, int N,
-                                                    const float* __restrict__ Y, int ldy, int K,
-                                                    const float* __restrict__ s, const float* __restrict__ t,
-                                                    int act, float slope, int M, int rows_per_block,
-                                                    float* __restrict__ dW, float* __restrict__ db) {
-    constexpr int BR = 32, BO = 64, BI = 64;
-    __shared__ float Xs[BR][BO + 1];
-    __shared__ float Ys[BR][BI + 1];
+// Same LDS/fragment scheme as the row GEMM with the ROW index as the reduction
+// axis: X and T(Y) slabs of 32 rows are stored transposed ([channel][row], 144-B
+// stride) so each lane's fragment is 16 consecutive rows.  fp32 partial sums are
+// flushed every 8 slabs (256 rows) into a second accumulator to bound the
+// accumulation error, and blocks combine with fp32 atomics.
+template <int BO, int BI, bool YXF>
+__global__ __launch_bounds__(256, 2) void wgrad_kernel(const float* __restrict__ X, int ldx, int N,
+                                                       const float* __restrict__ Y, int ldy, int K,
+                                                       const float* __restrict__ s, const float* __restrict__ t,
+                                                       int act, float slope, int M, int rows_per_block,
+                                                       float* __restrict__ dW, float* __restrict__ db) {
+    constexpr int BR = 32, LDR = BR + 4;
+    constexpr int TM = BO / 64, TN = BI / 64;
+    constexpr int XV = BR * BO / 4 / 256, YV = BR * BI / 4 / 256;
+    __shared__ __attribute__((aligned(16))) float Xs[2][BO][LDR];
+    __shared__ __attribute__((aligned(16))) float Ys[2][BI][LDR];
+    __shared__ float dbs[256 / (BO / 4)][BO];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wo = wave >> 1, wi = wave & 1;
+    const int h = lane >> 5, l32 = lane & 31;
     const int tiles_i = (K + BI - 1) / BI;
     const int n0 = (blockIdx.y / tiles_i) * BO;
     const int k0 = (blockIdx.y % tiles_i) * BI;
     const int rb = blockIdx.x * rows_per_block;
     const int re = min(M, rb + rows_per_block);
-    f32x16 acc;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-    float dbacc = 0.f;
     const bool do_db = (db != nullptr) && (k0 == 0);
-    for (int r0 = rb; r0 < re; r0 += BR) {
+
+    // this thread's fixed channel quads
+    const int xc4 = tid % (BO / 4), yc4 = tid % (BI / 4);
+    float ys[4] = {1.f, 1.f, 1.f, 1.f}, yt[4] = {0.f, 0.f, 0.f, 0.f};
+    if (YXF) {
 #pragma unroll
-        for (int it = 0; it < BR * BO / 256; ++it) {
+        for (int j = 0; j < 4; ++j) {
+            const int gk = k0 + 4 * yc4 + j;
+            if (gk < K) { ys[j] = s[gk]; yt[j] = t[gk]; }
+        }
+    }
+    float dbv[4] = {0.f, 0.f, 0.f, 0.f};
+
+    f32x16 acc[TM][TN], tot[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) { acc[i][j][r] = 0.f; tot[i][j][r] = 0.f; }
+
+    float4 rx[XV], ry[YV];
+    auto gload = [&](int r0) {
+#pragma unroll
+        for (int it = 0; it < XV; ++it) {
             const int e = it * 256 + tid;
-            const int rr = e / BO, c = e % BO;
-            const int gr = r0 + rr, gn = n0 + c;
-            Xs[rr][c] = (gr < re && gn < N) ? X[(size_t)gr * ldx + gn] : 0.f;
-            const int gk = k0 + c;
-            float y = 0.f;
-            if (gr < re && gk < K) {
-                y = Y[(size_t)gr * ldy + gk];
-                if (YXF) y = act_f(y * s[gk] + t[gk], act, slope);
+            const int r = e / (BO / 4);
+            const int gr = r0 + r, gn = n0 + 4 * xc4;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (gr < re && gn < N) v = *reinterpret_cast<const float4*>(X + (size_t)gr * ldx + gn);
+            rx[it] = v;
+        }
+#pragma unroll
+        for (int it = 0; it < YV; ++it) {
+            const int e = it * 256 + tid;
+            const int r = e / (BI / 4);
+            const int gr = r0 + r, gk = k0 + 4 * yc4;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (gr < re && gk < K) v = *reinterpret_cast<const float4*>(Y + (size_t)gr * ldy + gk);
+            ry[it] = v;
+        }
+    };
+    auto sstore = [&](int buf) {
+#pragma unroll
+        for (int it = 0; it < XV; ++it) {
+            const int e = it * 256 + tid;
+            const int r = e / (BO / 4);
+            const float4 v = rx[it];
+            Xs[buf][4 * xc4 + 0][r] = v.x;
+            Xs[buf][4 * xc4 + 1][r] = v.y;
+            Xs[buf][4 * xc4 + 2][r] = v.z;
+            Xs[buf][4 * xc4 + 3][r] = v.w;
+            if (do_db) { dbv[0] += v.x; dbv[1] += v.y; dbv[2] += v.z; dbv[3] += v.w; }
+        }
+#pragma unroll
+        for (int it = 0; it < YV; ++it) {
+            const int e = it * 256 + tid;
+            const int r = e / (BI / 4);
+            float4 v = ry[it];
+            if (YXF) {
+                const int gk = k0 + 4 * yc4;
+                v.x = gk + 0 < K ? act_f(v.x * ys[0] + yt[0], act, slope) : 0.f;
+                v.y = gk + 1 < K ? act_f(v.y * ys[1] + yt[1], act, slope) : 0.f;
+                v.z = gk + 2 < K ? act_f(v.z * ys[2] + yt[2], act, slope) : 0.f;
+                v.w = gk + 3 < K ? act_f(v.w * ys[3] + yt[3], act, slope) : 0.f;
             }
-            Ys[rr][c] = y;
+            Ys[buf][4 * yc4 + 0][r] = v.x;
+            Ys[buf][4 * yc4 + 1][r] = v.y;
+            Ys[buf][4 * yc4 + 2][r] = v.z;
+            Ys[buf][4 * yc4 + 3][r] = v.w;
         }
-        __syncthreads();
-        if (do_db && tid < BO) {
-#pragma unroll 8
-            for (int rr = 0; rr < BR; ++rr) dbacc += Xs[rr][tid];
-        }
+    };
+
+    const int nslab = (re - rb + BR - 1) / BR;
+    if (nslab > 0) {
+        gload(rb);
+        sstore(0);
+    }
+    __syncthreads();
+    for (int sl = 0; sl < nslab; ++sl) {
+        const int buf = sl & 1;
+        if (sl + 1 < nslab) gload(rb + (sl + 1) * BR);
 #pragma unroll
-        for (int kk = 0; kk < BR; kk += 2) {
-            const float a = Xs[kk + (lane >> 5)][wo * 32 + (lane & 31)];
-            const float b = Ys[kk + (lane >> 5)][wi * 32 + (lane & 31)];
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+        for (int q = 0; q < 4; ++q) {
+            float4 a[TM], b[TN];
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+                a[i] = *reinterpret_cast<const float4*>(&Xs[buf][wo * (BO / 2) + i * 32 + l32][16 * h + 4 * q]);
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+                b[j] = *reinterpret_cast<const float4*>(&Ys[buf][wi * (BI / 2) + j * 32 + l32][16 * h + 4 * q]);
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].x, b[j].x, acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].y, b[j].y, acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].z, b[j].z, acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].w, b[j].w, acc[i][j], 0, 0, 0);
+                }
         }
+        if ((sl & 7) == 7) {
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) { tot[i][j][r] += acc[i][j][r]; acc[i][j][r] = 0.f; }
+        }
+        if (sl + 1 < nslab) sstore(buf ^ 1);
         __syncthreads();
     }
-    const int kcol = k0 + wi * 32 + (lane & 31);
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const int n = n0 + wo * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        if (n < N && kcol < K) atomicAdd(&dW[(size_t)n * K + kcol], acc[r]);
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int kcol = k0 + wi * (BI / 2) + j * 32 + l32;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int n = n0 + wo * (BO / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (n < N && kcol < K) atomicAdd(&dW[(size_t)n * K + kcol], tot[i][j][r] + acc[i][j][r]);
+            }
+        }
+    if (do_db) {
+        const int grp = tid / (BO / 4);
+        dbs[grp][4 * xc4 + 0] = dbv[0];
+        dbs[grp][4 * xc4 + 1] = dbv[1];
+        dbs[grp][4 * xc4 + 2] = dbv[2];
+        dbs[grp][4 * xc4 + 3] = dbv[3];
+        __syncthreads();
+        if (tid < BO && n0 + tid < N) {
+            float a = 0.f;
+#pragma unroll
+            for (int gi = 0; gi < 256 / (BO / 4); ++gi) a += dbs[gi][tid];
+            atomicAdd(&db[n0 + tid], a);
+        }
     }
-    if (do_db && tid < BO && n0 + tid < N) atomicAdd(&db[n0 + tid], dbacc);
 }
 
 // ------------------------------------------------------------------ BN finalize (forward)
@@ -302,12 +465,13 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const double* __restri
 }
 
 // ------------------------------------------------------------------ BN finalize (backward)
-// sums (sum dy, sum dy*xhat) -> dgamma, dbeta and dZ coefficients kB = s*sum_dy/M, kC = s*sum_dyx/M
+// sums (sum dy, sum dy*xhat) -> dgamma, dbeta (added when `accum`) and the dZ coefficients
+// kB = s*sum_dy/M, kC = s*sum_dyx/M
 __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const double* __restrict__ part, int nb, int N,
                                                               long long M, const float* __restrict__ s,
                                                               float* __restrict__ dgamma, float* __restrict__ dbeta,
                                                               float* __restrict__ kB, float* __restrict__ kC,
-                                                              const float* __restrict__ inv) {
+                                                              int accum) {
     __shared__ double r1[256], r2[256];
     const int n = blockIdx.x;
     double a = 0.0, b = 0.0;
@@ -326,11 +490,11 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const double* __re
         __syncthreads();
     }
     if (threadIdx.x == 0) {
-        if (dbeta) dbeta[n] = (float)r1[0];
-        if (dgamma) dgamma[n] = (float)r2[0];
-        kB[n] = (float)((double)s[n] * r1[0] / (double)M);
-        kC[n] = (float)((double)s[n] * r2[0] / (double)M);
-        (void)inv;
+        const double S1 = r1[0], S2 = r2[0];
+        if (dbeta) dbeta[n] = accum ? dbeta[n] + (float)S1 : (float)S1;
+        if (dgamma) dgamma[n] = accum ? dgamma[n] + (float)S2 : (float)S2;
+        kB[n] = (float)((double)s[n] * S1 / (double)M);
+        kC[n] = (float)((double)s[n] * S2 / (double)M);
     }
 }
 
@@ -480,11 +644,20 @@ static inline unsigned ew_grid(long long total) {
     return (unsigned)(g < 1 ? 1 : g);
 }
 
-template <int BM, int BN, int WM, int WN, bool BT>
+template <int BM, int BN, int WM, int WN>
 static void launch_gemm(const GemmArgs& g, hipStream_t s) {
     const dim3 grid((g.M + BM - 1) / BM, (g.N + BN - 1) / BN);
-    if (g.s_in) hipLaunchKernelGGL((gemm_rows_kernel<BM, BN, WM, WN, BT, true>), grid, dim3(256), 0, s, g);
-    else hipLaunchKernelGGL((gemm_rows_kernel<BM, BN, WM, WN, BT, false>), grid, dim3(256), 0, s, g);
+    if (g.s_in) hipLaunchKernelGGL((gemm_rows_kernel<BM, BN, WM, WN, true>), grid, dim3(256), 0, s, g);
+    else hipLaunchKernelGGL((gemm_rows_kernel<BM, BN, WM, WN, false>), grid, dim3(256), 0, s, g);
+}
+
+template <int BO, int BI>
+static void launch_wgrad(dim3 grid, hipStream_t st, const float* X, int ldx, int N, const float* Y, int ldy, int K,
+                         const float* s, const float* t, int act, float slope, int M, int rows, float* dW, float* db) {
+    if (s) hipLaunchKernelGGL((wgrad_kernel<BO, BI, true>), grid, dim3(256), 0, st, X, ldx, N, Y, ldy, K, s, t, act,
+                              slope, M, rows, dW, db);
+    else hipLaunchKernelGGL((wgrad_kernel<BO, BI, false>), grid, dim3(256), 0, st, X, ldx, N, Y, ldy, K, s, t, act,
+                            slope, M, rows, dW, db);
 }
 
 }  // namespace pcs
@@ -497,12 +670,12 @@ PCS_API int pcs_gemm_row_blocks(int M, int N) {
     return (M + 127) / 128;
 }
 
-// C = act_in(A*s_in+t_in) . B (+bias), B = W^T (trans_w=1, W is N x K) or W (trans_w=0, W is K x N).
+// C = act_in(A*s_in+t_in) . W^T (+bias), W row-major N x K (row stride ldw).
 // stats (nullable): [row_blocks][2][N] fp64 partial (sum, sumsq) of C.
 // bstats (nullable): fused BN-backward partials of the layer whose pre-BN output is zp (same shape as C):
 //   [row_blocks][2][N] of (sum dy, sum dy*xhat), dy = C * act'(zp*sp+tp), xhat = (zp-meanp)*invp.
 PCS_API int pcs_gemm_rows(const float* A, int lda, int M, int K, const float* s_in, const float* t_in, int act_in,
-                          float slope_in, const float* W, int ldw, int trans_w, const float* bias, float* C, int ldc,
+                          float slope_in, const float* W, int ldw, const float* bias, float* C, int ldc,
                           int N, double* stats, const float* zp, int ldzp, const float* sp, const float* tp,
                           const float* meanp, const float* invp, int actp, float slopep, double* bstats,
                           void* stream) {
@@ -512,19 +685,14 @@ PCS_API int pcs_gemm_rows(const float* A, int lda, int M, int K, const float* s_
     PCS_CHECK_ARG(!(stats && bstats), "pcs_gemm_rows: stats and bstats are exclusive");
     PCS_CHECK_ARG(!bstats || (zp && sp && tp && meanp && invp), "pcs_gemm_rows: bstats needs zp/sp/tp/meanp/invp");
     PCS_CHECK_ARG((s_in == nullptr) == (t_in == nullptr), "pcs_gemm_rows: s_in/t_in must both be set or null");
+    PCS_CHECK_ARG(ldw >= K, "pcs_gemm_rows: ldw=%d < K=%d", ldw, K);
     if (M == 0) return 0;
     GemmArgs g{A, lda, M, K, s_in, t_in, act_in, slope_in, W, ldw, bias, C, ldc, N, stats,
                zp, ldzp, sp, tp, meanp, invp, actp, slopep, bstats};
     hipStream_t s = as_stream(stream);
-    if (trans_w) {
-        if (N <= 32) launch_gemm<128, 32, 4, 1, true>(g, s);
-        else if (N <= 64) launch_gemm<128, 64, 4, 1, true>(g, s);
-        else launch_gemm<128, 128, 2, 2, true>(g, s);
-    } else {
-        if (N <= 32) launch_gemm<128, 32, 4, 1, false>(g, s);
-        else if (N <= 64) launch_gemm<128, 64, 4, 1, false>(g, s);
-        else launch_gemm<128, 128, 2, 2, false>(g, s);
-    }
+    if (N <= 32) launch_gemm<128, 32, 4, 1>(g, s);
+    else if (N <= 64) launch_gemm<128, 64, 4, 1>(g, s);
+    else launch_gemm<128, 128, 2, 2>(g, s);
     return launch_status("pcs_gemm_rows");
 }
 
@@ -533,18 +701,21 @@ PCS_API int pcs_wgrad(const float* X, int ldx, int N, const float* Y, int ldy, i
                       int act, float slope, int M, float* dW, float* db, void* stream) {
     PCS_CHECK_ARG(M >= 0 && N >= 1 && K >= 1, "pcs_wgrad: bad sizes");
     PCS_CHECK_ARG(X && Y && dW, "pcs_wgrad: null pointer");
+    PCS_CHECK_ARG(ldx % 4 == 0 && ldy % 4 == 0 && N % 4 == 0, "pcs_wgrad: ldx/ldy/N must be multiples of 4");
     if (M == 0) return 0;
-    const int tiles = ((N + 63) / 64) * ((K + 63) / 64);
-    int splits = (2048 + tiles - 1) / tiles;
+    const int BO = N > 64 ? 128 : 64, BI = K > 64 ? 128 : 64;
+    const int tiles = ((N + BO - 1) / BO) * ((K + BI - 1) / BI);
+    int splits = (1024 + tiles - 1) / tiles;
     int rows = (M + splits - 1) / splits;
-    rows = ((rows + 31) / 32) * 32;
+    rows = ((rows + 255) / 256) * 256;
     if (rows < 256) rows = 256;
     splits = (M + rows - 1) / rows;
     const dim3 grid(splits, tiles);
-    if (s) hipLaunchKernelGGL(wgrad_kernel<true>, grid, dim3(256), 0, as_stream(stream), X, ldx, N, Y, ldy, K, s, t,
-                              act, slope, M, rows, dW, db);
-    else hipLaunchKernelGGL(wgrad_kernel<false>, grid, dim3(256), 0, as_stream(stream), X, ldx, N, Y, ldy, K, s, t,
-                            act, slope, M, rows, dW, db);
+    hipStream_t st = as_stream(stream);
+    if (BO == 128 && BI == 128) launch_wgrad<128, 128>(grid, st, X, ldx, N, Y, ldy, K, s, t, act, slope, M, rows, dW, db);
+    else if (BO == 128) launch_wgrad<128, 64>(grid, st, X, ldx, N, Y, ldy, K, s, t, act, slope, M, rows, dW, db);
+    else if (BI == 128) launch_wgrad<64, 128>(grid, st, X, ldx, N, Y, ldy, K, s, t, act, slope, M, rows, dW, db);
+    else launch_wgrad<64, 64>(grid, st, X, ldx, N, Y, ldy, K, s, t, act, slope, M, rows, dW, db);
     return launch_status("pcs_wgrad");
 }
 
@@ -558,12 +729,12 @@ PCS_API int pcs_bn_finalize(const double* part, int nb, int N, long long M, cons
     return launch_status("pcs_bn_finalize");
 }
 
-// BN backward finalize: part [nb][2][N] of (sum dy, sum dy*xhat) -> dgamma, dbeta, kB, kC.
+// BN backward finalize: part [nb][2][N] of (sum dy, sum dy*xhat) -> dgamma, dbeta (+= when accum), kB, kC.
 PCS_API int pcs_bn_bwd_finalize(const double* part, int nb, int N, long long M, const float* s, float* dgamma,
-                                float* dbeta, float* kB, float* kC, void* stream) {
+                                float* dbeta, float* kB, float* kC, int accum, void* stream) {
     PCS_CHECK_ARG(nb >= 1 && N >= 1 && M >= 1, "pcs_bn_bwd_finalize: bad sizes");
     hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(N), dim3(256), 0, as_stream(stream), part, nb, N, M, s, dgamma,
-                       dbeta, kB, kC, (const float*)nullptr);
+                       dbeta, kB, kC, accum);
     return launch_status("pcs_bn_bwd_finalize");
 }
 

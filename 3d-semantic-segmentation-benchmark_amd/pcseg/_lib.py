@@ -36,11 +36,11 @@ SIGNATURES = {
     'pcs_edge_bwd': [P, I32, P, I32, I32, I32, I32, P, P],
     # shared-MLP engine
     'pcs_gemm_row_blocks': [I32, I32],
-    'pcs_gemm_rows': [P, I32, I32, I32, P, P, I32, F32, P, I32, I32, P, P, I32, I32, P,
+    'pcs_gemm_rows': [P, I32, I32, I32, P, P, I32, F32, P, I32, P, P, I32, I32, P,
                       P, I32, P, P, P, P, I32, F32, P, P],
     'pcs_wgrad': [P, I32, I32, P, I32, I32, P, P, I32, F32, I32, P, P, P],
     'pcs_bn_finalize': [P, I32, I32, I64, P, P, F32, F32, P, P, P, P, P, P, P],
-    'pcs_bn_bwd_finalize': [P, I32, I32, I64, P, P, P, P, P, P],
+    'pcs_bn_bwd_finalize': [P, I32, I32, I64, P, P, P, P, P, I32, P],
     'pcs_bn_bwd_reduce_blocks': [I32],
     'pcs_bn_bwd_reduce': [P, I32, P, I32, I32, I32, P, P, P, P, I32, F32, P, P],
     'pcs_bn_bwd_dz': [P, I32, P, I32, I32, I32, P, P, P, P, P, P, I32, F32, P, P],

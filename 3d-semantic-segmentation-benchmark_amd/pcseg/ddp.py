@@ -56,7 +56,10 @@ class FlatGradAllReduce:
         self.attach()
         if self.overlap:
             for p in self.params:
+                # autograd-accumulated params fire the post-accumulate hook; params whose
+                # gradients the HIP engine writes in place call _pcs_grad_ready instead
                 p.register_post_accumulate_grad_hook(self._hook)
+                p._pcs_grad_ready = self._hook
 
     def attach(self) -> None:
         """(Re)bind every param.grad to its view of the flat buffer."""

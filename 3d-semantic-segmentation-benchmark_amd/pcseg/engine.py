@@ -37,6 +37,32 @@ def pad_rows(x: torch.Tensor) -> torch.Tensor:
     return out
 
 
+def grad_target(p: torch.Tensor | None) -> torch.Tensor | None:
+    """The buffer the engine accumulates p's gradient into (p.grad itself, created zeroed if absent).
+
+    The engine writes parameter gradients directly (fp32 atomics / accumulate flag) instead
+    of returning them, so autograd issues no AccumulateGrad add (and no zero fill) per
+    parameter; hooks registered through `_pcs_grad_ready` (pcseg.ddp) are called after.
+    """
+    if p is None or not p.requires_grad:
+        return None
+    g = p.grad
+    if g is None:
+        g = torch.zeros_like(p, memory_format=torch.contiguous_format)
+        p.grad = g
+    elif not g.is_contiguous() or g.dtype != torch.float32:
+        raise RuntimeError('pcseg engine: parameter .grad must be a contiguous fp32 tensor')
+    return g
+
+
+def notify_grad_ready(params) -> None:
+    for p in params:
+        if p is not None:
+            cb = getattr(p, '_pcs_grad_ready', None)
+            if cb is not None:
+                cb(p)
+
+
 def _f64(shape, dev):
     return torch.empty(shape, dtype=torch.float64, device=dev)
 
@@ -73,7 +99,7 @@ class SharedMLPFn(torch.autograd.Function):
                 nb = (M + BM - 1) // BM
                 part = _f64((nb, 2, Cout), dev)
                 call('pcs_gemm_rows', ptr(A), lda_cur, M, K_cur, ptr(s_prev), ptr(t_prev), a_code, slope,
-                     ptr(Wm), Wm.shape[1], 1, ptr(b), ptr(Z), Cout, Cout, ptr(part),
+                     ptr(Wm), Wm.shape[1], ptr(b), ptr(Z), Cout, Cout, ptr(part),
                      None, 0, None, None, None, None, 0, 0.0, None, st)
                 momentum = 0.0
                 rm = rv = None
@@ -85,7 +111,7 @@ class SharedMLPFn(torch.autograd.Function):
                      ptr(rm), ptr(rv), ptr(s), ptr(t), ptr(mean), ptr(inv), st)
             else:
                 call('pcs_gemm_rows', ptr(A), lda_cur, M, K_cur, ptr(s_prev), ptr(t_prev), a_code, slope,
-                     ptr(Wm), Wm.shape[1], 1, ptr(b), ptr(Z), Cout, Cout, None,
+                     ptr(Wm), Wm.shape[1], ptr(b), ptr(Z), Cout, Cout, None,
                      None, 0, None, None, None, None, 0, 0.0, None, st)
                 with torch.no_grad():
                     inv.copy_(torch.rsqrt(bn.running_var + bn.eps))
@@ -148,8 +174,9 @@ class SharedMLPFn(torch.autograd.Function):
             part = _f64((nb, 2, CL), dev)
             call('pcs_bn_bwd_reduce', ptr(gout), CL, ptr(Zs[-1]), CL, M, CL, ptr(s), ptr(t), ptr(mean), ptr(inv),
                  a_code, slope, ptr(part), st)
-        dgam, dbet, kB, kC = (_f32((CL,), dev) for _ in range(4))
-        call('pcs_bn_bwd_finalize', ptr(part), nb, CL, M, ptr(s), ptr(dgam), ptr(dbet), ptr(kB), ptr(kC), st)
+        kB, kC = _f32((CL,), dev), _f32((CL,), dev)
+        gg, gb = grad_target(params[4 * (nl - 1) + 2]), grad_target(params[4 * (nl - 1) + 3])
+        call('pcs_bn_bwd_finalize', ptr(part), nb, CL, M, ptr(s), ptr(gg), ptr(gb), ptr(kB), ptr(kC), 1, st)
         if not use_batch[-1]:
             kB.zero_()
             kC.zero_()
@@ -160,49 +187,46 @@ class SharedMLPFn(torch.autograd.Function):
         else:
             call('pcs_bn_bwd_dz', ptr(gout), CL, ptr(Zs[-1]), CL, M, CL, ptr(s), ptr(t), ptr(mean), ptr(inv),
                  ptr(kB), ptr(kC), a_code, slope, ptr(dZ), st)
-        bn_grads = {nl - 1: (dgam, dbet)}
         dX = None
         for li in range(nl - 1, -1, -1):
             W, b = params[4 * li], params[4 * li + 1]
             Cout = W.shape[0]
             Wm = W.reshape(Cout, -1)
             Cin = Wm.shape[1]
-            dW = torch.zeros((Cout, Cin), dtype=torch.float32, device=dev)
-            db = torch.zeros((Cout,), dtype=torch.float32, device=dev) if b is not None else None
-            if li > 0:
-                sp, tp, mp, ip = stats[li - 1]
-                call('pcs_wgrad', ptr(dZ), Cout, Cout, ptr(Zs[li - 1]), Cin, Cin, ptr(sp), ptr(tp), a_code, slope, M,
-                     ptr(dW), ptr(db), st)
-            else:
-                call('pcs_wgrad', ptr(dZ), Cout, Cout, ptr(X), lda, Kin, None, None, 0, 0.0, M, ptr(dW), ptr(db), st)
-            grads[4 * li] = dW.view_as(W)
-            grads[4 * li + 1] = db
+            Wt = Wm.t().contiguous()          # (Cin x Cout): dgrad B[k=cout][n=cin] = Wt[n][k]
+            dW = grad_target(W)
+            db = grad_target(b)
+            if dW is not None:
+                if li > 0:
+                    sp, tp, mp, ip = stats[li - 1]
+                    call('pcs_wgrad', ptr(dZ), Cout, Cout, ptr(Zs[li - 1]), Cin, Cin, ptr(sp), ptr(tp), a_code, slope,
+                         M, ptr(dW), ptr(db), st)
+                else:
+                    call('pcs_wgrad', ptr(dZ), Cout, Cout, ptr(X), lda, Kin, None, None, 0, 0.0, M, ptr(dW), ptr(db),
+                         st)
             if li > 0:
                 sp, tp, mp, ip = stats[li - 1]
                 dA = _f32((M, Cin), dev)
                 nbg = (M + BM - 1) // BM
                 bpart = _f64((nbg, 2, Cin), dev)
-                call('pcs_gemm_rows', ptr(dZ), Cout, M, Cout, None, None, 0, 0.0, ptr(Wm), Cin, 0, None, ptr(dA), Cin,
+                call('pcs_gemm_rows', ptr(dZ), Cout, M, Cout, None, None, 0, 0.0, ptr(Wt), Cout, None, ptr(dA), Cin,
                      Cin, None, ptr(Zs[li - 1]), Cin, ptr(sp), ptr(tp), ptr(mp), ptr(ip), a_code, slope, ptr(bpart),
                      st)
-                g2, b2, kB2, kC2 = (_f32((Cin,), dev) for _ in range(4))
-                call('pcs_bn_bwd_finalize', ptr(bpart), nbg, Cin, M, ptr(sp), ptr(g2), ptr(b2), ptr(kB2), ptr(kC2), st)
+                kB2, kC2 = _f32((Cin,), dev), _f32((Cin,), dev)
+                g2, b2 = grad_target(params[4 * (li - 1) + 2]), grad_target(params[4 * (li - 1) + 3])
+                call('pcs_bn_bwd_finalize', ptr(bpart), nbg, Cin, M, ptr(sp), ptr(g2), ptr(b2), ptr(kB2), ptr(kC2), 1,
+                     st)
                 if not use_batch[li - 1]:
                     kB2.zero_()
                     kC2.zero_()
-                bn_grads[li - 1] = (g2, b2)
                 dZ = _f32((M, Cin), dev)
                 call('pcs_bn_bwd_dz', ptr(dA), Cin, ptr(Zs[li - 1]), Cin, M, Cin, ptr(sp), ptr(tp), ptr(mp), ptr(ip),
                      ptr(kB2), ptr(kC2), a_code, slope, ptr(dZ), st)
             elif ctx.needs_input_grad[0]:
                 dX = torch.zeros((M, lda), dtype=torch.float32, device=dev) if lda != Kin else _f32((M, lda), dev)
-                call('pcs_gemm_rows', ptr(dZ), Cout, M, Cout, None, None, 0, 0.0, ptr(Wm), Cin, 0, None, ptr(dX), lda,
+                call('pcs_gemm_rows', ptr(dZ), Cout, M, Cout, None, None, 0, 0.0, ptr(Wt), Cout, None, ptr(dX), lda,
                      Kin, None, None, 0, None, None, None, None, 0, 0.0, None, st)
-        for li, (dg, dbb) in bn_grads.items():
-            if params[4 * li + 2] is not None:
-                grads[4 * li + 2] = dg
-            if params[4 * li + 3] is not None:
-                grads[4 * li + 3] = dbb
+        notify_grad_ready(params)
         return (dX, None, None, None, None, None, *grads)
 
 

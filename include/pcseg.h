@@ -101,14 +101,14 @@ int pcs_edge_bwd(const float* grad_out, int ld_gout, const int32_t* idx, int B,
 
 /* row blocks of pcs_gemm_rows (sizes its stats/bstats workspace) */
 int pcs_gemm_row_blocks(int M, int N);
-/* C (M x N, ldc) = act_in(A*s_in + t_in) . op(W) (+bias): op(W) = W^T (trans_w,
- * W is N x K) or W (K x N).  A rows have stride lda (multiple of 4).
+/* C (M x N, ldc) = act_in(A*s_in + t_in) . W^T (+bias), W row-major N x K with
+ * row stride ldw.  A rows have stride lda (multiple of 4).
  * stats: partial (sum, sum^2) of C per channel.  bstats: fused BN-backward
  * partials (sum dy, sum dy*xhat) of the layer whose pre-BN output is zp
  * (dy = C * act'(zp*sp+tp), xhat = (zp-meanp)*invp). */
 int pcs_gemm_rows(const float* A, int lda, int M, int K, const float* s_in,
                   const float* t_in, int act_in, float slope_in, const float* W,
-                  int ldw, int trans_w, const float* bias, float* C, int ldc,
+                  int ldw, const float* bias, float* C, int ldc,
                   int N, double* stats, const float* zp, int ldzp,
                   const float* sp, const float* tp, const float* meanp,
                   const float* invp, int actp, float slopep, double* bstats,
@@ -124,11 +124,12 @@ int pcs_bn_finalize(const double* part, int nb, int N, long long M,
                     const float* gamma, const float* beta, float eps,
                     float momentum, float* run_mean, float* run_var, float* s,
                     float* t, float* mean, float* invstd, void* stream);
-/* BN backward finalize: partials -> dgamma, dbeta, kB = s*sum_dy/M,
- * kC = s*sum(dy*xhat)/M  (dZ = s*dy - kB - kC*xhat). */
+/* BN backward finalize: partials -> dgamma, dbeta (written, or added when
+ * accum != 0), kB = s*sum_dy/M, kC = s*sum(dy*xhat)/M
+ * (dZ = s*dy - kB - kC*xhat). */
 int pcs_bn_bwd_finalize(const double* part, int nb, int N, long long M,
                         const float* s, float* dgamma, float* dbeta, float* kB,
-                        float* kC, void* stream);
+                        float* kC, int accum, void* stream);
 int pcs_bn_bwd_reduce_blocks(int M);
 int pcs_bn_bwd_reduce(const float* dA, int ldd, const float* Z, int ldz, int M,
                       int N, const float* s, const float* t, const float* mean,

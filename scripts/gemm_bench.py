@@ -1,0 +1,54 @@
+"""Per-shape timing of the engine GEMMs (pcs_gemm_rows fwd/dgrad, pcs_wgrad) on the GPU."""
+import os
+import sys
+
+sys.path[:0] = [os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                             '3d-semantic-segmentation-benchmark_amd')]
+import torch  # noqa: E402
+from pcseg._lib import call, ptr, stream_ptr  # noqa: E402
+
+dev = 'cuda'
+SHAPES = [  # (name, M, K, N)
+    ('sa1.l1', 1048576, 9, 32), ('sa1.l2', 1048576, 32, 32), ('sa1.l3', 1048576, 32, 64),
+    ('sa2.l1', 262144, 67, 64), ('sa2.l3', 262144, 64, 128),
+    ('sa3.l1', 65536, 131, 128), ('sa3.l3', 65536, 128, 256),
+    ('sa4.l1', 16384, 259, 256), ('sa4.l3', 16384, 256, 512),
+    ('fp3.l1', 8192, 384, 256), ('fp2.l1', 32768, 320, 256), ('fp1.lx', 131072, 128, 128),
+    ('dg.e2', 2621440, 128, 64), ('dg.c5', 131072, 384, 1024), ('dg.c6', 131072, 1408, 512),
+]
+
+
+def timeit(fn, reps=10):
+    for _ in range(2):
+        fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    e1.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+st = stream_ptr(torch.device(dev))
+for name, M, K, N in SHAPES:
+    lda = (K + 3) // 4 * 4
+    A = torch.randn(M, lda, device=dev)
+    W = torch.randn(N, K, device=dev)
+    s = torch.rand(K, device=dev) + 0.5
+    t = torch.randn(K, device=dev) * 0.1
+    b = torch.randn(N, device=dev)
+    C = torch.empty(M, N, device=dev)
+    part = torch.empty((M + 127) // 128, 2, N, dtype=torch.float64, device=dev)
+    fwd = lambda: call('pcs_gemm_rows', ptr(A), lda, M, K, ptr(s), ptr(t), 0, 0.0, ptr(W), K, ptr(b), ptr(C), N, N,  # noqa
+                       ptr(part), None, 0, None, None, None, None, 0, 0.0, None, st)
+    ms = timeit(fwd)
+    fl = 2.0 * M * K * N
+    by = 4.0 * M * (lda + N)
+    dW = torch.zeros(N, K, device=dev)
+    db = torch.zeros(N, device=dev)
+    wg = lambda: call('pcs_wgrad', ptr(C), N, N, ptr(A), lda, K, ptr(s), ptr(t), 0, 0.0, M, ptr(dW), ptr(db), st)  # noqa
+    ms2 = timeit(wg)
+    print(f'{name:8s} M={M:8d} K={K:5d} N={N:5d}  fwd {ms*1e3:8.1f} us {fl/ms/1e9:6.1f} TF/s {by/ms/1e6:6.0f} GB/s'
+          f' | wgrad {ms2*1e3:8.1f} us {fl/ms2/1e9:6.1f} TF/s', flush=True)

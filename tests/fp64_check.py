@@ -89,9 +89,22 @@ def three_way(prod_ctor, ref_ctor, B, N, seed, uniform=False, pad=0, dev='cuda',
     return rows
 
 
-def failures(rows, rtol=1e-3, factor=10.0):
+def failures(rows, rtol=1e-3, factor=10.0, floor=1e-3):
+    """A tensor passes when its GPU error vs the fp64 truth is
+      <= rtol x its norm, or
+      <= factor x the CPU fp32 reference's own error, or
+      <= floor x the largest gradient norm in the same top-level module (sa3, fp1, conv2, ...):
+         the survey's floor for sums that are pure cancellation (pre-BN conv biases,
+         BN betas of pooled layers), whose value is decided by a handful of ReLU/argmax
+         flips at |y| ~ 1e-7 in ANY fp32 evaluation order."""
+    top = {}
+    for name, _, _, n in rows:
+        if name != 'logits' and 'running' not in name:
+            key = name.split('.')[0]
+            top[key] = max(top.get(key, 0.0), n)
     bad = []
     for name, eg, ec, n in rows:
-        if not (eg <= rtol * n or eg <= factor * ec):
+        fl = floor * top.get(name.split('.')[0], 0.0) if 'running' not in name else 0.0
+        if not (eg <= rtol * n or eg <= factor * ec or eg <= fl):
             bad.append((name, eg, ec, n))
     return bad
