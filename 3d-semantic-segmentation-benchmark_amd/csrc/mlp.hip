@@ -498,82 +498,139 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const double* __re
     }
 }
 
+// ------------------------------------------------------------------ elementwise helpers (float4 over channels)
+// All engine tensors have N % 4 == 0, row stride == N (dense) unless stated; one
+// thread owns one float4 of channels (c4) in one row.
+struct F4 {
+    float v[4];
+};
+__device__ __forceinline__ F4 ld4(const float* p) {
+    const float4 q = *reinterpret_cast<const float4*>(p);
+    return F4{{q.x, q.y, q.z, q.w}};
+}
+__device__ __forceinline__ void st4(float* p, const F4& a) {
+    *reinterpret_cast<float4*>(p) = make_float4(a.v[0], a.v[1], a.v[2], a.v[3]);
+}
+
 // ------------------------------------------------------------------ column reduce of (dy, dy*xhat)
-// standalone BN-backward reduce when dA comes from outside the engine
+// standalone BN-backward reduce when dA comes from outside the engine.  Block =
+// 256 threads = (N/4 channel quads) x (rows in flight); partial [blockIdx.x][2][N].
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restrict__ dA, int ldd,
                                                             const float* __restrict__ Z, int ldz, int M, int N,
                                                             const float* __restrict__ s, const float* __restrict__ t,
                                                             const float* __restrict__ mean,
                                                             const float* __restrict__ inv, int act, float slope,
                                                             int rows_per_block, double* __restrict__ part) {
-    __shared__ double r1[4][64], r2[4][64];
-    const int lane = threadIdx.x & 63, ph = threadIdx.x >> 6;
-    const int col = blockIdx.y * 64 + lane;
+    extern __shared__ double red_dyn[];   // [2][256][4]
+    const int nq = N / 4;                 // channel quads; blockIdx.y walks 256-quad column tiles
+    const int q0 = blockIdx.y * 256;
+    const int tq = threadIdx.x % min(nq - q0, 256);
+    const int rstep = 256 / min(nq - q0, 256);
+    const int rlane = threadIdx.x / min(nq - q0, 256);
+    const int c = 4 * (q0 + tq);
+    double a[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0};
     const int rb = blockIdx.x * rows_per_block;
     const int re = min(M, rb + rows_per_block);
-    double a = 0.0, b = 0.0;
-    if (col < N) {
-        const float sc = s[col], tc = t[col], mc = mean[col], ic = inv[col];
-        for (int r = rb + ph; r < re; r += 4) {
-            const float z = Z[(size_t)r * ldz + col];
-            const float dy = dA[(size_t)r * ldd + col] * dact_f(z * sc + tc, act, slope);
-            a += (double)dy;
-            b += (double)dy * (double)((z - mc) * ic);
+    if (rlane < rstep) {
+        float sc[4], tc[4], mc[4], ic[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { sc[j] = s[c + j]; tc[j] = t[c + j]; mc[j] = mean[c + j]; ic[j] = inv[c + j]; }
+        for (int r = rb + rlane; r < re; r += rstep) {
+            const F4 z = ld4(Z + (size_t)r * ldz + c);
+            const F4 g = ld4(dA + (size_t)r * ldd + c);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float dy = g.v[j] * dact_f(z.v[j] * sc[j] + tc[j], act, slope);
+                a[j] += (double)dy;
+                b[j] += (double)dy * (double)((z.v[j] - mc[j]) * ic[j]);
+            }
         }
     }
-    r1[ph][lane] = a;
-    r2[ph][lane] = b;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        red_dyn[(0 * 256 + threadIdx.x) * 4 + j] = a[j];
+        red_dyn[(1 * 256 + threadIdx.x) * 4 + j] = b[j];
+    }
     __syncthreads();
-    if (ph == 0 && col < N) {
-        part[((size_t)blockIdx.x * 2 + 0) * N + col] = r1[0][lane] + r1[1][lane] + r1[2][lane] + r1[3][lane];
-        part[((size_t)blockIdx.x * 2 + 1) * N + col] = r2[0][lane] + r2[1][lane] + r2[2][lane] + r2[3][lane];
+    if (rlane == 0) {
+        for (int rr = 1; rr < rstep; ++rr) {
+            const int o = rr * min(nq - q0, 256) + tq;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                a[j] += red_dyn[(0 * 256 + o) * 4 + j];
+                b[j] += red_dyn[(1 * 256 + o) * 4 + j];
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            part[((size_t)blockIdx.x * 2 + 0) * N + c + j] = a[j];
+            part[((size_t)blockIdx.x * 2 + 1) * N + c + j] = b[j];
+        }
     }
 }
 
-// dZ = s*dy - kB - kC*xhat   (dy = dA * act'(z*s+t), xhat = (z-mean)*inv)
+// dZ = s*dy - kB - kC*xhat   (dy = dA * act'(z*s+t), xhat = (z-mean)*inv), dense rows
 __global__ __launch_bounds__(256) void bn_bwd_dz_kernel(const float* __restrict__ dA, int ldd,
-                                                        const float* __restrict__ Z, int ldz, long long total, int N,
+                                                        const float* __restrict__ Z, int ldz, int total4, int nq,
                                                         const float* __restrict__ s, const float* __restrict__ t,
                                                         const float* __restrict__ mean, const float* __restrict__ inv,
                                                         const float* __restrict__ kB, const float* __restrict__ kC,
                                                         int act, float slope, float* __restrict__ dZ) {
-    for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
-        const long long r = e / N;
-        const int c = (int)(e - r * N);
-        const float z = Z[r * ldz + c];
-        const float dy = dA[r * ldd + c] * dact_f(z * s[c] + t[c], act, slope);
-        const float xh = (z - mean[c]) * inv[c];
-        dZ[e] = s[c] * dy - kB[c] - kC[c] * xh;
+    for (int e = blockIdx.x * 256 + threadIdx.x; e < total4; e += gridDim.x * 256) {
+        const int r = e / nq;
+        const int c = 4 * (e - r * nq);
+        const F4 z = ld4(Z + (size_t)r * ldz + c);
+        const F4 g = ld4(dA + (size_t)r * ldd + c);
+        F4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float dy = g.v[j] * dact_f(z.v[j] * s[c + j] + t[c + j], act, slope);
+            const float xh = (z.v[j] - mean[c + j]) * inv[c + j];
+            o.v[j] = s[c + j] * dy - kB[c + j] - kC[c + j] * xh;
+        }
+        st4(dZ + (size_t)r * 4 * nq + c, o);
     }
 }
 
 // ------------------------------------------------------------------ pooling over K with BN + act
 // pooled[g][c] = max_k act(z*s+t) (first max), argmax u8
-__global__ __launch_bounds__(256) void pool_fwd_kernel(const float* __restrict__ Z, int N, long long G, int K,
+__global__ __launch_bounds__(256) void pool_fwd_kernel(const float* __restrict__ Z, int nq, int G, int K,
                                                        const float* __restrict__ s, const float* __restrict__ t,
                                                        int act, float slope, float* __restrict__ out,
                                                        unsigned char* __restrict__ arg) {
-    const long long total = G * N;
-    for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
-        const long long g = e / N;
-        const int c = (int)(e - g * N);
-        const float sc = s[c], tc = t[c];
-        const float* z = Z + g * K * N + c;
-        float m = act_f(z[0] * sc + tc, act, slope);
-        int a = 0;
-        for (int k = 1; k < K; ++k) {
-            const float v = act_f(z[(long long)k * N] * sc + tc, act, slope);
-            if (v > m) { m = v; a = k; }
+    const int N = 4 * nq;
+    const int total4 = G * nq;
+    for (int e = blockIdx.x * 256 + threadIdx.x; e < total4; e += gridDim.x * 256) {
+        const int g = e / nq;
+        const int c = 4 * (e - g * nq);
+        float sc[4], tc[4], m[4];
+        int a[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { sc[j] = s[c + j]; tc[j] = t[c + j]; }
+        const float* z = Z + (size_t)g * K * N + c;
+        {
+            const F4 v = ld4(z);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) m[j] = act_f(v.v[j] * sc[j] + tc[j], act, slope);
         }
-        out[e] = m;
-        arg[e] = (unsigned char)a;
+        for (int k = 1; k < K; ++k) {
+            const F4 v = ld4(z + (size_t)k * N);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float y = act_f(v.v[j] * sc[j] + tc[j], act, slope);
+                if (y > m[j]) { m[j] = y; a[j] = k; }
+            }
+        }
+        st4(out + (size_t)g * N + c, F4{{m[0], m[1], m[2], m[3]}});
+        *reinterpret_cast<uchar4*>(arg + (size_t)g * N + c) =
+            make_uchar4((unsigned char)a[0], (unsigned char)a[1], (unsigned char)a[2], (unsigned char)a[3]);
     }
 }
 
 // BN-backward sums for a pooled layer: only the argmax row of each (g, c) carries dy
 __global__ __launch_bounds__(256) void pool_bwd_reduce_kernel(const float* __restrict__ dpool,
                                                               const unsigned char* __restrict__ arg,
-                                                              const float* __restrict__ Z, int N, long long G, int K,
+                                                              const float* __restrict__ Z, int N, int G, int K,
                                                               const float* __restrict__ s,
                                                               const float* __restrict__ t,
                                                               const float* __restrict__ mean,
@@ -582,15 +639,16 @@ __global__ __launch_bounds__(256) void pool_bwd_reduce_kernel(const float* __res
     __shared__ double r1[4][64], r2[4][64];
     const int lane = threadIdx.x & 63, ph = threadIdx.x >> 6;
     const int col = blockIdx.y * 64 + lane;
-    const long long gb = (long long)blockIdx.x * groups_per_block;
-    const long long ge = min(G, gb + groups_per_block);
+    const int gb = blockIdx.x * groups_per_block;
+    const int ge = min(G, gb + groups_per_block);
     double a = 0.0, b = 0.0;
     if (col < N) {
         const float sc = s[col], tc = t[col], mc = mean[col], ic = inv[col];
-        for (long long g = gb + ph; g < ge; g += 4) {
-            const int k = arg[g * N + col];
-            const float z = Z[(g * K + k) * N + col];
-            const float dy = dpool[g * N + col] * dact_f(z * sc + tc, act, slope);
+#pragma unroll 4
+        for (int g = gb + ph; g < ge; g += 4) {
+            const int k = arg[(size_t)g * N + col];
+            const float z = Z[((size_t)g * K + k) * N + col];
+            const float dy = dpool[(size_t)g * N + col] * dact_f(z * sc + tc, act, slope);
             a += (double)dy;
             b += (double)dy * (double)((z - mc) * ic);
         }
@@ -607,40 +665,52 @@ __global__ __launch_bounds__(256) void pool_bwd_reduce_kernel(const float* __res
 // dZ of a pooled layer: dy is dpool at the argmax row, 0 elsewhere
 __global__ __launch_bounds__(256) void pool_bwd_dz_kernel(const float* __restrict__ dpool,
                                                           const unsigned char* __restrict__ arg,
-                                                          const float* __restrict__ Z, int N, long long G, int K,
+                                                          const float* __restrict__ Z, int nq, int G, int K,
                                                           const float* __restrict__ s, const float* __restrict__ t,
                                                           const float* __restrict__ mean,
                                                           const float* __restrict__ inv,
                                                           const float* __restrict__ kB, const float* __restrict__ kC,
                                                           int act, float slope, float* __restrict__ dZ) {
-    const long long total = G * K * N;
-    for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
-        const long long r = e / N;
-        const int c = (int)(e - r * N);
-        const long long g = r / K;
-        const int k = (int)(r - g * K);
-        const float z = Z[e];
-        float dy = 0.f;
-        if (arg[g * N + c] == k) dy = dpool[g * N + c] * dact_f(z * s[c] + t[c], act, slope);
-        const float xh = (z - mean[c]) * inv[c];
-        dZ[e] = s[c] * dy - kB[c] - kC[c] * xh;
+    const int N = 4 * nq;
+    const long long total4 = (long long)G * K * nq;
+    for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < total4; e += (long long)gridDim.x * 256) {
+        const int r = (int)(e / nq);
+        const int c = 4 * (int)(e - (long long)r * nq);
+        const int g = r / K;
+        const int k = r - g * K;
+        const F4 z = ld4(Z + (size_t)r * N + c);
+        const uchar4 aq = *reinterpret_cast<const uchar4*>(arg + (size_t)g * N + c);
+        const F4 dp = ld4(dpool + (size_t)g * N + c);
+        const unsigned char av[4] = {aq.x, aq.y, aq.z, aq.w};
+        F4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float dy = av[j] == k ? dp.v[j] * dact_f(z.v[j] * s[c + j] + t[c + j], act, slope) : 0.f;
+            const float xh = (z.v[j] - mean[c + j]) * inv[c + j];
+            o.v[j] = s[c + j] * dy - kB[c + j] - kC[c + j] * xh;
+        }
+        st4(dZ + (size_t)r * N + c, o);
     }
 }
 
 // a = act(z*s + t) materialised (outputs consumed outside the engine)
-__global__ __launch_bounds__(256) void bn_act_kernel(const float* __restrict__ Z, int ldz, long long total, int N,
+__global__ __launch_bounds__(256) void bn_act_kernel(const float* __restrict__ Z, int ldz, int total4, int nq,
                                                      const float* __restrict__ s, const float* __restrict__ t,
                                                      int act, float slope, float* __restrict__ out, int ldo) {
-    for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
-        const long long r = e / N;
-        const int c = (int)(e - r * N);
-        out[r * ldo + c] = act_f(Z[r * ldz + c] * s[c] + t[c], act, slope);
+    for (int e = blockIdx.x * 256 + threadIdx.x; e < total4; e += gridDim.x * 256) {
+        const int r = e / nq;
+        const int c = 4 * (e - r * nq);
+        const F4 z = ld4(Z + (size_t)r * ldz + c);
+        F4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o.v[j] = act_f(z.v[j] * s[c + j] + t[c + j], act, slope);
+        st4(out + (size_t)r * ldo + c, o);
     }
 }
 
 static inline unsigned ew_grid(long long total) {
     long long g = (total + 255) / 256;
-    if (g > 16384) g = 16384;
+    if (g > 8192) g = 8192;
     return (unsigned)(g < 1 ? 1 : g);
 }
 
@@ -738,70 +808,77 @@ PCS_API int pcs_bn_bwd_finalize(const double* part, int nb, int N, long long M, 
     return launch_status("pcs_bn_bwd_finalize");
 }
 
-PCS_API int pcs_bn_bwd_reduce_blocks(int M) { return (M + 1023) / 1024; }
+static const int kRedRows = 256;
+
+PCS_API int pcs_bn_bwd_reduce_blocks(int M) { return (M + kRedRows - 1) / kRedRows; }
 
 PCS_API int pcs_bn_bwd_reduce(const float* dA, int ldd, const float* Z, int ldz, int M, int N, const float* s,
                               const float* t, const float* mean, const float* inv, int act, float slope, double* part,
                               void* stream) {
-    PCS_CHECK_ARG(M >= 1 && N >= 1, "pcs_bn_bwd_reduce: bad sizes");
-    const int rows = 1024;
-    const dim3 grid((M + rows - 1) / rows, (N + 63) / 64);
-    hipLaunchKernelGGL(bn_bwd_reduce_kernel, grid, dim3(256), 0, as_stream(stream), dA, ldd, Z, ldz, M, N, s, t, mean,
-                       inv, act, slope, rows, part);
+    PCS_CHECK_ARG(M >= 1 && N >= 4 && N % 4 == 0 && ldd % 4 == 0 && ldz % 4 == 0,
+                  "pcs_bn_bwd_reduce: bad sizes (N, strides must be multiples of 4)");
+    const int nq = N / 4;
+    const dim3 grid((M + kRedRows - 1) / kRedRows, (nq + 255) / 256);
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel, grid, dim3(256), 2 * 256 * 4 * sizeof(double), as_stream(stream), dA, ldd,
+                       Z, ldz, M, N, s, t, mean, inv, act, slope, kRedRows, part);
     return launch_status("pcs_bn_bwd_reduce");
 }
 
 PCS_API int pcs_bn_bwd_dz(const float* dA, int ldd, const float* Z, int ldz, int M, int N, const float* s,
                           const float* t, const float* mean, const float* inv, const float* kB, const float* kC,
                           int act, float slope, float* dZ, void* stream) {
-    PCS_CHECK_ARG(M >= 0 && N >= 1, "pcs_bn_bwd_dz: bad sizes");
-    const long long total = (long long)M * N;
+    PCS_CHECK_ARG(M >= 0 && N >= 4 && N % 4 == 0 && ldd % 4 == 0 && ldz % 4 == 0, "pcs_bn_bwd_dz: bad sizes");
+    const long long total = (long long)M * N / 4;
+    PCS_CHECK_ARG(total < (1ll << 31), "pcs_bn_bwd_dz: too many elements");
     if (total == 0) return 0;
-    hipLaunchKernelGGL(bn_bwd_dz_kernel, dim3(ew_grid(total)), dim3(256), 0, as_stream(stream), dA, ldd, Z, ldz, total,
-                       N, s, t, mean, inv, kB, kC, act, slope, dZ);
+    hipLaunchKernelGGL(bn_bwd_dz_kernel, dim3(ew_grid(total)), dim3(256), 0, as_stream(stream), dA, ldd, Z, ldz,
+                       (int)total, N / 4, s, t, mean, inv, kB, kC, act, slope, dZ);
     return launch_status("pcs_bn_bwd_dz");
 }
 
 PCS_API int pcs_pool_fwd(const float* Z, int N, long long G, int K, const float* s, const float* t, int act,
                          float slope, float* out, uint8_t* arg, void* stream) {
-    PCS_CHECK_ARG(G >= 0 && K >= 1 && K <= 256 && N >= 1, "pcs_pool_fwd: bad sizes");
-    const long long total = G * N;
+    PCS_CHECK_ARG(G >= 0 && K >= 1 && K <= 256 && N >= 4 && N % 4 == 0, "pcs_pool_fwd: bad sizes");
+    const long long total = G * N / 4;
+    PCS_CHECK_ARG(G * K * (long long)N < (1ll << 40) && total < (1ll << 31), "pcs_pool_fwd: too many elements");
     if (total == 0) return 0;
-    hipLaunchKernelGGL(pool_fwd_kernel, dim3(ew_grid(total)), dim3(256), 0, as_stream(stream), Z, N, G, K, s, t, act,
-                       slope, out, arg);
+    hipLaunchKernelGGL(pool_fwd_kernel, dim3(ew_grid(total)), dim3(256), 0, as_stream(stream), Z, N / 4, (int)G, K, s,
+                       t, act, slope, out, arg);
     return launch_status("pcs_pool_fwd");
 }
 
-PCS_API int pcs_pool_bwd_reduce_blocks(long long G) { return (int)((G + 255) / 256); }
+PCS_API int pcs_pool_bwd_reduce_blocks(long long G) { return (int)((G + 63) / 64); }
 
 PCS_API int pcs_pool_bwd_reduce(const float* dpool, const uint8_t* arg, const float* Z, int N, long long G, int K,
                                 const float* s, const float* t, const float* mean, const float* inv, int act,
                                 float slope, double* part, void* stream) {
-    PCS_CHECK_ARG(G >= 1 && K >= 1 && N >= 1, "pcs_pool_bwd_reduce: bad sizes");
-    const int gpb = 256;
+    PCS_CHECK_ARG(G >= 1 && G < (1ll << 31) && K >= 1 && N >= 1, "pcs_pool_bwd_reduce: bad sizes");
+    const int gpb = 64;
     const dim3 grid((unsigned)((G + gpb - 1) / gpb), (N + 63) / 64);
-    hipLaunchKernelGGL(pool_bwd_reduce_kernel, grid, dim3(256), 0, as_stream(stream), dpool, arg, Z, N, G, K, s, t,
-                       mean, inv, act, slope, gpb, part);
+    hipLaunchKernelGGL(pool_bwd_reduce_kernel, grid, dim3(256), 0, as_stream(stream), dpool, arg, Z, N, (int)G, K, s,
+                       t, mean, inv, act, slope, gpb, part);
     return launch_status("pcs_pool_bwd_reduce");
 }
 
 PCS_API int pcs_pool_bwd_dz(const float* dpool, const uint8_t* arg, const float* Z, int N, long long G, int K,
                             const float* s, const float* t, const float* mean, const float* inv, const float* kB,
                             const float* kC, int act, float slope, float* dZ, void* stream) {
-    PCS_CHECK_ARG(G >= 0 && K >= 1 && N >= 1, "pcs_pool_bwd_dz: bad sizes");
-    const long long total = G * K * N;
+    PCS_CHECK_ARG(G >= 0 && G < (1ll << 31) && K >= 1 && K <= 256 && N >= 4 && N % 4 == 0,
+                  "pcs_pool_bwd_dz: bad sizes");
+    const long long total = G * K * N / 4;
     if (total == 0) return 0;
-    hipLaunchKernelGGL(pool_bwd_dz_kernel, dim3(ew_grid(total)), dim3(256), 0, as_stream(stream), dpool, arg, Z, N, G,
-                       K, s, t, mean, inv, kB, kC, act, slope, dZ);
+    hipLaunchKernelGGL(pool_bwd_dz_kernel, dim3(ew_grid(total)), dim3(256), 0, as_stream(stream), dpool, arg, Z, N / 4,
+                       (int)G, K, s, t, mean, inv, kB, kC, act, slope, dZ);
     return launch_status("pcs_pool_bwd_dz");
 }
 
 PCS_API int pcs_bn_act(const float* Z, int ldz, int M, int N, const float* s, const float* t, int act, float slope,
                        float* out, int ldo, void* stream) {
-    PCS_CHECK_ARG(M >= 0 && N >= 1, "pcs_bn_act: bad sizes");
-    const long long total = (long long)M * N;
+    PCS_CHECK_ARG(M >= 0 && N >= 4 && N % 4 == 0 && ldz % 4 == 0 && ldo % 4 == 0, "pcs_bn_act: bad sizes");
+    const long long total = (long long)M * N / 4;
+    PCS_CHECK_ARG(total < (1ll << 31), "pcs_bn_act: too many elements");
     if (total == 0) return 0;
-    hipLaunchKernelGGL(bn_act_kernel, dim3(ew_grid(total)), dim3(256), 0, as_stream(stream), Z, ldz, total, N, s, t,
-                       act, slope, out, ldo);
+    hipLaunchKernelGGL(bn_act_kernel, dim3(ew_grid(total)), dim3(256), 0, as_stream(stream), Z, ldz, (int)total, N / 4,
+                       s, t, act, slope, out, ldo);
     return launch_status("pcs_bn_act");
 }
