@@ -39,18 +39,91 @@ __device__ __forceinline__ float dact_f(float y, int act, float slope) {
     return 1.f;
 }
 
+// Operand descriptor (layout-identical to pcs_operand in include/pcseg.h).  The
+// value fed to the MFMA for channel c of row r is
+//   PLAIN   : data[r][c]
+//   BNACT   : act(data[r][c]*s[c] + t[c])                  (forward: previous layer's BN + act)
+//   BNBWD   : s*dy - kb - alpha*(z - mean),  dy = data[r][c]*act'(z*s+t), z = Z[r][c]
+//   POOLBWD : as BNBWD with data[r][c] = (arg[g][c] == k) ? dpool[g][c] : 0, g = r / pool_k, k = r % pool_k
+// i.e. BNBWD/POOLBWD rebuild the layer's dZ (BatchNorm backward) on the fly from its
+// output gradient and pre-BN Z, so dZ is never written to HBM.
+struct Operand {
+    const float* data; int ld; int mode;
+    const float* s; const float* t; int act; float slope;
+    const float* z; int ldz;
+    const float* mean; const float* inv; const float* alpha; const float* kb;
+    const unsigned char* arg; int pool_k;
+};
+enum { OP_PLAIN = 0, OP_BNACT = 1, OP_BNBWD = 2, OP_POOLBWD = 3 };
+
+// per-channel coefficients of a transform, for 4 consecutive channels
+struct Quad {
+    float4 s, t, mean, alpha, kb;
+};
+
+template <int MODE>
+__device__ __forceinline__ void load_quad(const Operand& o, int c, int K, Quad& q) {
+    auto get = [&](const float* p, int j, float dflt) { return c + j < K ? p[c + j] : dflt; };
+    if (MODE >= OP_BNACT) {
+        q.s = make_float4(get(o.s, 0, 0.f), get(o.s, 1, 0.f), get(o.s, 2, 0.f), get(o.s, 3, 0.f));
+        q.t = make_float4(get(o.t, 0, 0.f), get(o.t, 1, 0.f), get(o.t, 2, 0.f), get(o.t, 3, 0.f));
+    }
+    if (MODE >= OP_BNBWD) {
+        q.mean = make_float4(get(o.mean, 0, 0.f), get(o.mean, 1, 0.f), get(o.mean, 2, 0.f), get(o.mean, 3, 0.f));
+        q.alpha = make_float4(get(o.alpha, 0, 0.f), get(o.alpha, 1, 0.f), get(o.alpha, 2, 0.f),
+                              get(o.alpha, 3, 0.f));
+        q.kb = make_float4(get(o.kb, 0, 0.f), get(o.kb, 1, 0.f), get(o.kb, 2, 0.f), get(o.kb, 3, 0.f));
+    }
+}
+
+// raw global loads of one float4 (row r, channels c..c+3); z only for BNBWD/POOLBWD
+template <int MODE>
+__device__ __forceinline__ void load_raw(const Operand& o, int r, int c, float4& v, float4& z) {
+    if (MODE == OP_POOLBWD) {
+        const int g = r / o.pool_k, k = r - g * o.pool_k;
+        const float4 d = *reinterpret_cast<const float4*>(o.data + (size_t)g * o.ld + c);
+        const uchar4 a = *reinterpret_cast<const uchar4*>(o.arg + (size_t)g * o.ld + c);
+        v.x = a.x == k ? d.x : 0.f;
+        v.y = a.y == k ? d.y : 0.f;
+        v.z = a.z == k ? d.z : 0.f;
+        v.w = a.w == k ? d.w : 0.f;
+    } else {
+        v = *reinterpret_cast<const float4*>(o.data + (size_t)r * o.ld + c);
+    }
+    if (MODE >= OP_BNBWD) z = *reinterpret_cast<const float4*>(o.z + (size_t)r * o.ldz + c);
+}
+
+template <int MODE>
+__device__ __forceinline__ float xform1(const Operand& o, float v, float z, float s, float t, float mean, float alpha,
+                                        float kb) {
+    if (MODE == OP_BNACT) return act_f(v * s + t, o.act, o.slope);
+    if (MODE >= OP_BNBWD) {
+        const float dy = v * dact_f(z * s + t, o.act, o.slope);
+        return s * dy - kb - alpha * (z - mean);
+    }
+    return v;
+}
+
+// transformed float4; channels >= K give 0
+template <int MODE>
+__device__ __forceinline__ float4 xform4(const Operand& o, float4 v, float4 z, const Quad& q, int c, int K) {
+    float4 r;
+    r.x = c + 0 < K ? xform1<MODE>(o, v.x, z.x, q.s.x, q.t.x, q.mean.x, q.alpha.x, q.kb.x) : 0.f;
+    r.y = c + 1 < K ? xform1<MODE>(o, v.y, z.y, q.s.y, q.t.y, q.mean.y, q.alpha.y, q.kb.y) : 0.f;
+    r.z = c + 2 < K ? xform1<MODE>(o, v.z, z.z, q.s.z, q.t.z, q.mean.z, q.alpha.z, q.kb.z) : 0.f;
+    r.w = c + 3 < K ? xform1<MODE>(o, v.w, z.w, q.s.w, q.t.w, q.mean.w, q.alpha.w, q.kb.w) : 0.f;
+    return r;
+}
+
 struct GemmArgs {
-    const float* A; int lda; int M; int K;     // A rows (M x K), row stride lda
-    const float* s_in; const float* t_in;      // A transform: act(a*s+t) per K channel (or null)
-    int act_in; float slope_in;
+    Operand a; int M; int K;                   // A rows (M x K) through its transform
     const float* W; int ldw;                   // B[k][n] = W[n*ldw + k]
     const float* bias;                         // per n (or null)
     float* C; int ldc; int N;                  // output rows (M x N)
     double* stats;                             // [gridDim.x][2][N]: sum, sum of squares of C (or null)
-    // fused backward reduce for the layer that produced A's *output* space (dgrad epilogue):
-    const float* zp; int ldzp;                 // that layer's pre-BN Z (M x N)
-    const float* sp; const float* tp; const float* meanp; const float* invp;
-    int actp; float slopep;
+    // fused BN-backward reduce of the layer whose OUTPUT space C lives in (dgrad epilogue):
+    // uses e.z (its pre-BN Z, M x N), e.s, e.t, e.mean, e.inv, e.act, e.slope
+    Operand e;
     double* bstats;                            // [gridDim.x][2][N]: sum dy, sum dy*xhat (or null)
 };
 
@@ -68,13 +141,13 @@ struct GemmArgs {
 constexpr int GBK = 32;
 constexpr int GLDK = GBK + 4;
 
-template <int BM, int BN, int WM, int WN, bool AXF>
+template <int BM, int BN, int WM, int WN, int AM>
 __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(GemmArgs g) {
     constexpr int WTM = BM / WM, WTN = BN / WN;
     constexpr int TM = WTM / 32, TN = WTN / 32;
     constexpr int AV = BM * GBK / 4 / 256;
     constexpr int BV = (BN * GBK / 4 + 255) / 256;
-    static_assert(WM * WN == 4 && TM >= 1 && TN >= 1, "tile");
+    static_assert(WM * WN == 4 && TM >= 1 && TN >= 1 && AV >= 1, "tile");
     __shared__ __attribute__((aligned(16))) float As[2][BM][GLDK];
     __shared__ __attribute__((aligned(16))) float Bs[2][BN][GLDK];
     __shared__ double red[2][WM][BN];
@@ -93,68 +166,47 @@ __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(GemmArgs g) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-    float4 ra[AV], rb[BV];
+    float4 ra[AV], rz[AV], rb[BV];
     // every A float4 of this thread sits at the same k offset 4*(tid&7) of a slab, so one
-    // (scale, shift) quad per slab serves all of them
-    float4 rs = make_float4(0.f, 0.f, 0.f, 0.f), rt = rs;
+    // coefficient quad per slab serves all of them
+    Quad q;
     auto gload = [&](int k0) {
-        if (AXF) {
-            const int gk = k0 + 4 * (tid & 7);
-            rs.x = gk + 0 < g.K ? g.s_in[gk + 0] : 0.f;
-            rs.y = gk + 1 < g.K ? g.s_in[gk + 1] : 0.f;
-            rs.z = gk + 2 < g.K ? g.s_in[gk + 2] : 0.f;
-            rs.w = gk + 3 < g.K ? g.s_in[gk + 3] : 0.f;
-            rt.x = gk + 0 < g.K ? g.t_in[gk + 0] : 0.f;
-            rt.y = gk + 1 < g.K ? g.t_in[gk + 1] : 0.f;
-            rt.z = gk + 2 < g.K ? g.t_in[gk + 2] : 0.f;
-            rt.w = gk + 3 < g.K ? g.t_in[gk + 3] : 0.f;
-        }
+        const int gk = k0 + 4 * (tid & 7);
+        load_quad<AM>(g.a, gk, g.K, q);
 #pragma unroll
         for (int it = 0; it < AV; ++it) {
-            const int e = it * 256 + tid;
-            const int r = e >> 3, c4 = e & 7;
-            const int gr = m0 + r, gk = k0 + 4 * c4;
-            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (gr < g.M && gk < g.K) v = *reinterpret_cast<const float4*>(g.A + (size_t)gr * g.lda + gk);
+            const int r = (it * 256 + tid) >> 3;
+            const int gr = m0 + r;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f), z = v;
+            if (gr < g.M && gk < g.K) load_raw<AM>(g.a, gr, gk, v, z);
             ra[it] = v;
+            rz[it] = z;
         }
 #pragma unroll
         for (int it = 0; it < BV; ++it) {
             const int e = it * 256 + tid;
             const int n = e >> 3, c4 = e & 7;
-            const int gn = n0 + n, gk = k0 + 4 * c4;
+            const int gn = n0 + n, gk2 = k0 + 4 * c4;
             float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (e < BN * GBK / 4 && gn < g.N && gk < g.K) {
-                const float* w = g.W + (size_t)gn * g.ldw + gk;
-                if (wvec && gk + 3 < g.K) v = *reinterpret_cast<const float4*>(w);
+            if (e < BN * GBK / 4 && gn < g.N && gk2 < g.K) {
+                const float* w = g.W + (size_t)gn * g.ldw + gk2;
+                if (wvec && gk2 + 3 < g.K) v = *reinterpret_cast<const float4*>(w);
                 else {
                     v.x = w[0];
-                    v.y = gk + 1 < g.K ? w[1] : 0.f;
-                    v.z = gk + 2 < g.K ? w[2] : 0.f;
-                    v.w = gk + 3 < g.K ? w[3] : 0.f;
+                    v.y = gk2 + 1 < g.K ? w[1] : 0.f;
+                    v.z = gk2 + 2 < g.K ? w[2] : 0.f;
+                    v.w = gk2 + 3 < g.K ? w[3] : 0.f;
                 }
             }
             rb[it] = v;
         }
     };
     auto sstore = [&](int buf, int k0) {
+        const int gk = k0 + 4 * (tid & 7);
 #pragma unroll
         for (int it = 0; it < AV; ++it) {
-            const int e = it * 256 + tid;
-            const int r = e >> 3, c4 = e & 7;
-            const int gk = k0 + 4 * c4;
-            float4 v = ra[it];
-            if (AXF) {
-                v.x = gk + 0 < g.K ? act_f(v.x * rs.x + rt.x, g.act_in, g.slope_in) : 0.f;
-                v.y = gk + 1 < g.K ? act_f(v.y * rs.y + rt.y, g.act_in, g.slope_in) : 0.f;
-                v.z = gk + 2 < g.K ? act_f(v.z * rs.z + rt.z, g.act_in, g.slope_in) : 0.f;
-                v.w = gk + 3 < g.K ? act_f(v.w * rs.w + rt.w, g.act_in, g.slope_in) : 0.f;
-            } else {
-                v.y = gk + 1 < g.K ? v.y : 0.f;
-                v.z = gk + 2 < g.K ? v.z : 0.f;
-                v.w = gk + 3 < g.K ? v.w : 0.f;
-            }
-            *reinterpret_cast<float4*>(&As[buf][r][4 * c4]) = v;
+            const int r = (it * 256 + tid) >> 3;
+            *reinterpret_cast<float4*>(&As[buf][r][4 * (tid & 7)]) = xform4<AM>(g.a, ra[it], rz[it], q, gk, g.K);
         }
 #pragma unroll
         for (int it = 0; it < BV; ++it) {
@@ -171,14 +223,14 @@ __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(GemmArgs g) {
         const int buf = ks & 1;
         if (ks + 1 < nk) gload((ks + 1) * GBK);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
+        for (int qq = 0; qq < 4; ++qq) {
             float4 a[TM], b[TN];
 #pragma unroll
             for (int i = 0; i < TM; ++i)
-                a[i] = *reinterpret_cast<const float4*>(&As[buf][wm * WTM + i * 32 + l32][16 * h + 4 * q]);
+                a[i] = *reinterpret_cast<const float4*>(&As[buf][wm * WTM + i * 32 + l32][16 * h + 4 * qq]);
 #pragma unroll
             for (int j = 0; j < TN; ++j)
-                b[j] = *reinterpret_cast<const float4*>(&Bs[buf][wn * WTN + j * 32 + l32][16 * h + 4 * q]);
+                b[j] = *reinterpret_cast<const float4*>(&Bs[buf][wn * WTN + j * 32 + l32][16 * h + 4 * qq]);
 #pragma unroll
             for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -203,7 +255,7 @@ __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(GemmArgs g) {
         const bool cok = col < g.N;
         const float bv = (g.bias && cok) ? g.bias[col] : 0.f;
         float sp = 0.f, tp = 0.f, mp = 0.f, ip = 0.f;
-        if (want_b && cok) { sp = g.sp[col]; tp = g.tp[col]; mp = g.meanp[col]; ip = g.invp[col]; }
+        if (want_b && cok) { sp = g.e.s[col]; tp = g.e.t[col]; mp = g.e.mean[col]; ip = g.e.inv[col]; }
         double s1 = 0.0, s2 = 0.0;
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
@@ -218,8 +270,8 @@ __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(GemmArgs g) {
                         s2 += (double)v * (double)v;
                     }
                     if (want_b) {
-                        const float z = g.zp[(size_t)row * g.ldzp + col];
-                        const float dy = v * dact_f(z * sp + tp, g.actp, g.slopep);
+                        const float z = g.e.z[(size_t)row * g.e.ldz + col];
+                        const float dy = v * dact_f(z * sp + tp, g.e.act, g.e.slope);
                         const float xh = (z - mp) * ip;
                         s1 += (double)dy;
                         s2 += (double)dy * (double)xh;
@@ -253,18 +305,18 @@ __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(GemmArgs g) {
 }
 
 // ------------------------------------------------------------------ weight gradient
-// dW[n][k] += sum_r X[r][n] * T(Y)[r][k] ; db[n] += sum_r X[r][n]   (rows split over gridDim.x)
+// dW[n][k] += sum_r X[r][n] * Y[r][k] ; db[n] += sum_r X[r][n]   (rows split over gridDim.x)
+// X = the layer's dZ (through its BNBWD/POOLBWD transform: rebuilt from the output
+// gradient and Z on load), Y = the layer's input (through the previous layer's BNACT).
 // Same LDS/fragment scheme as the row GEMM with the ROW index as the reduction
-// axis: X and T(Y) slabs of 32 rows are stored transposed ([channel][row], 144-B
+// axis: X and Y slabs of 32 rows are stored transposed ([channel][row], 144-B
 // stride) so each lane's fragment is 16 consecutive rows.  fp32 partial sums are
 // flushed every 8 slabs (256 rows) into a second accumulator to bound the
 // accumulation error, and blocks combine with fp32 atomics.
-template <int BO, int BI, bool YXF>
-__global__ __launch_bounds__(256, 2) void wgrad_kernel(const float* __restrict__ X, int ldx, int N,
-                                                       const float* __restrict__ Y, int ldy, int K,
-                                                       const float* __restrict__ s, const float* __restrict__ t,
-                                                       int act, float slope, int M, int rows_per_block,
-                                                       float* __restrict__ dW, float* __restrict__ db) {
+template <int BO, int BI, int XM, int YM>
+__global__ __launch_bounds__(256, 2) void wgrad_kernel(Operand xo, int N, Operand yo, int K, int M,
+                                                       int rows_per_block, float* __restrict__ dW,
+                                                       float* __restrict__ db) {
     constexpr int BR = 32, LDR = BR + 4;
     constexpr int TM = BO / 64, TN = BI / 64;
     constexpr int XV = BR * BO / 4 / 256, YV = BR * BI / 4 / 256;
@@ -281,16 +333,12 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const float* __restrict__
     const int re = min(M, rb + rows_per_block);
     const bool do_db = (db != nullptr) && (k0 == 0);
 
-    // this thread's fixed channel quads
+    // this thread's fixed channel quads and their transform coefficients
     const int xc4 = tid % (BO / 4), yc4 = tid % (BI / 4);
-    float ys[4] = {1.f, 1.f, 1.f, 1.f}, yt[4] = {0.f, 0.f, 0.f, 0.f};
-    if (YXF) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int gk = k0 + 4 * yc4 + j;
-            if (gk < K) { ys[j] = s[gk]; yt[j] = t[gk]; }
-        }
-    }
+    const int gn = n0 + 4 * xc4, gk = k0 + 4 * yc4;
+    Quad qx, qy;
+    load_quad<XM>(xo, gn, N, qx);
+    load_quad<YM>(yo, gk, K, qy);
     float dbv[4] = {0.f, 0.f, 0.f, 0.f};
 
     f32x16 acc[TM][TN], tot[TM][TN];
@@ -301,33 +349,31 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const float* __restrict__
 #pragma unroll
             for (int r = 0; r < 16; ++r) { acc[i][j][r] = 0.f; tot[i][j][r] = 0.f; }
 
-    float4 rx[XV], ry[YV];
+    float4 rx[XV], rxz[XV], ry[YV], ryz[YV];
     auto gload = [&](int r0) {
 #pragma unroll
         for (int it = 0; it < XV; ++it) {
-            const int e = it * 256 + tid;
-            const int r = e / (BO / 4);
-            const int gr = r0 + r, gn = n0 + 4 * xc4;
-            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (gr < re && gn < N) v = *reinterpret_cast<const float4*>(X + (size_t)gr * ldx + gn);
+            const int gr = r0 + (it * 256 + tid) / (BO / 4);
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f), z = v;
+            if (gr < re && gn < N) load_raw<XM>(xo, gr, gn, v, z);
             rx[it] = v;
+            rxz[it] = z;
         }
 #pragma unroll
         for (int it = 0; it < YV; ++it) {
-            const int e = it * 256 + tid;
-            const int r = e / (BI / 4);
-            const int gr = r0 + r, gk = k0 + 4 * yc4;
-            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (gr < re && gk < K) v = *reinterpret_cast<const float4*>(Y + (size_t)gr * ldy + gk);
+            const int gr = r0 + (it * 256 + tid) / (BI / 4);
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f), z = v;
+            if (gr < re && gk < K) load_raw<YM>(yo, gr, gk, v, z);
             ry[it] = v;
+            ryz[it] = z;
         }
     };
-    auto sstore = [&](int buf) {
+    auto sstore = [&](int buf, int r0) {
 #pragma unroll
         for (int it = 0; it < XV; ++it) {
-            const int e = it * 256 + tid;
-            const int r = e / (BO / 4);
-            const float4 v = rx[it];
+            const int r = (it * 256 + tid) / (BO / 4);
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (r0 + r < re) v = xform4<XM>(xo, rx[it], rxz[it], qx, gn, N);
             Xs[buf][4 * xc4 + 0][r] = v.x;
             Xs[buf][4 * xc4 + 1][r] = v.y;
             Xs[buf][4 * xc4 + 2][r] = v.z;
@@ -336,16 +382,9 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const float* __restrict__
         }
 #pragma unroll
         for (int it = 0; it < YV; ++it) {
-            const int e = it * 256 + tid;
-            const int r = e / (BI / 4);
-            float4 v = ry[it];
-            if (YXF) {
-                const int gk = k0 + 4 * yc4;
-                v.x = gk + 0 < K ? act_f(v.x * ys[0] + yt[0], act, slope) : 0.f;
-                v.y = gk + 1 < K ? act_f(v.y * ys[1] + yt[1], act, slope) : 0.f;
-                v.z = gk + 2 < K ? act_f(v.z * ys[2] + yt[2], act, slope) : 0.f;
-                v.w = gk + 3 < K ? act_f(v.w * ys[3] + yt[3], act, slope) : 0.f;
-            }
+            const int r = (it * 256 + tid) / (BI / 4);
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (r0 + r < re) v = xform4<YM>(yo, ry[it], ryz[it], qy, gk, K);
             Ys[buf][4 * yc4 + 0][r] = v.x;
             Ys[buf][4 * yc4 + 1][r] = v.y;
             Ys[buf][4 * yc4 + 2][r] = v.z;
@@ -356,7 +395,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const float* __restrict__
     const int nslab = (re - rb + BR - 1) / BR;
     if (nslab > 0) {
         gload(rb);
-        sstore(0);
+        sstore(0, rb);
     }
     __syncthreads();
     for (int sl = 0; sl < nslab; ++sl) {
@@ -389,7 +428,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const float* __restrict__
 #pragma unroll
                     for (int r = 0; r < 16; ++r) { tot[i][j][r] += acc[i][j][r]; acc[i][j][r] = 0.f; }
         }
-        if (sl + 1 < nslab) sstore(buf ^ 1);
+        if (sl + 1 < nslab) sstore(buf ^ 1, rb + (sl + 1) * BR);
         __syncthreads();
     }
 #pragma unroll
@@ -469,6 +508,7 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const double* __restri
 // kB = s*sum_dy/M, kC = s*sum_dyx/M
 __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const double* __restrict__ part, int nb, int N,
                                                               long long M, const float* __restrict__ s,
+                                                              const float* __restrict__ inv,
                                                               float* __restrict__ dgamma, float* __restrict__ dbeta,
                                                               float* __restrict__ kB, float* __restrict__ kC,
                                                               int accum) {
@@ -494,7 +534,7 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const double* __re
         if (dbeta) dbeta[n] = accum ? dbeta[n] + (float)S1 : (float)S1;
         if (dgamma) dgamma[n] = accum ? dgamma[n] + (float)S2 : (float)S2;
         kB[n] = (float)((double)s[n] * S1 / (double)M);
-        kC[n] = (float)((double)s[n] * S2 / (double)M);
+        kC[n] = (float)((double)s[n] * S2 / (double)M * (inv ? (double)inv[n] : 1.0));
     }
 }
 
@@ -569,29 +609,6 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restr
     }
 }
 
-// dZ = s*dy - kB - kC*xhat   (dy = dA * act'(z*s+t), xhat = (z-mean)*inv), dense rows
-__global__ __launch_bounds__(256) void bn_bwd_dz_kernel(const float* __restrict__ dA, int ldd,
-                                                        const float* __restrict__ Z, int ldz, int total4, int nq,
-                                                        const float* __restrict__ s, const float* __restrict__ t,
-                                                        const float* __restrict__ mean, const float* __restrict__ inv,
-                                                        const float* __restrict__ kB, const float* __restrict__ kC,
-                                                        int act, float slope, float* __restrict__ dZ) {
-    for (int e = blockIdx.x * 256 + threadIdx.x; e < total4; e += gridDim.x * 256) {
-        const int r = e / nq;
-        const int c = 4 * (e - r * nq);
-        const F4 z = ld4(Z + (size_t)r * ldz + c);
-        const F4 g = ld4(dA + (size_t)r * ldd + c);
-        F4 o;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const float dy = g.v[j] * dact_f(z.v[j] * s[c + j] + t[c + j], act, slope);
-            const float xh = (z.v[j] - mean[c + j]) * inv[c + j];
-            o.v[j] = s[c + j] * dy - kB[c + j] - kC[c + j] * xh;
-        }
-        st4(dZ + (size_t)r * 4 * nq + c, o);
-    }
-}
-
 // ------------------------------------------------------------------ pooling over K with BN + act
 // pooled[g][c] = max_k act(z*s+t) (first max), argmax u8
 __global__ __launch_bounds__(256) void pool_fwd_kernel(const float* __restrict__ Z, int nq, int G, int K,
@@ -662,37 +679,6 @@ __global__ __launch_bounds__(256) void pool_bwd_reduce_kernel(const float* __res
     }
 }
 
-// dZ of a pooled layer: dy is dpool at the argmax row, 0 elsewhere
-__global__ __launch_bounds__(256) void pool_bwd_dz_kernel(const float* __restrict__ dpool,
-                                                          const unsigned char* __restrict__ arg,
-                                                          const float* __restrict__ Z, int nq, int G, int K,
-                                                          const float* __restrict__ s, const float* __restrict__ t,
-                                                          const float* __restrict__ mean,
-                                                          const float* __restrict__ inv,
-                                                          const float* __restrict__ kB, const float* __restrict__ kC,
-                                                          int act, float slope, float* __restrict__ dZ) {
-    const int N = 4 * nq;
-    const long long total4 = (long long)G * K * nq;
-    for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < total4; e += (long long)gridDim.x * 256) {
-        const int r = (int)(e / nq);
-        const int c = 4 * (int)(e - (long long)r * nq);
-        const int g = r / K;
-        const int k = r - g * K;
-        const F4 z = ld4(Z + (size_t)r * N + c);
-        const uchar4 aq = *reinterpret_cast<const uchar4*>(arg + (size_t)g * N + c);
-        const F4 dp = ld4(dpool + (size_t)g * N + c);
-        const unsigned char av[4] = {aq.x, aq.y, aq.z, aq.w};
-        F4 o;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const float dy = av[j] == k ? dp.v[j] * dact_f(z.v[j] * s[c + j] + t[c + j], act, slope) : 0.f;
-            const float xh = (z.v[j] - mean[c + j]) * inv[c + j];
-            o.v[j] = s[c + j] * dy - kB[c + j] - kC[c + j] * xh;
-        }
-        st4(dZ + (size_t)r * N + c, o);
-    }
-}
-
 // a = act(z*s + t) materialised (outputs consumed outside the engine)
 __global__ __launch_bounds__(256) void bn_act_kernel(const float* __restrict__ Z, int ldz, int total4, int nq,
                                                      const float* __restrict__ s, const float* __restrict__ t,
@@ -717,61 +703,121 @@ static inline unsigned ew_grid(long long total) {
 template <int BM, int BN, int WM, int WN>
 static void launch_gemm(const GemmArgs& g, hipStream_t s) {
     const dim3 grid((g.M + BM - 1) / BM, (g.N + BN - 1) / BN);
-    if (g.s_in) hipLaunchKernelGGL((gemm_rows_kernel<BM, BN, WM, WN, true>), grid, dim3(256), 0, s, g);
-    else hipLaunchKernelGGL((gemm_rows_kernel<BM, BN, WM, WN, false>), grid, dim3(256), 0, s, g);
+    switch (g.a.mode) {
+    case OP_PLAIN: hipLaunchKernelGGL((gemm_rows_kernel<BM, BN, WM, WN, OP_PLAIN>), grid, dim3(256), 0, s, g); break;
+    case OP_BNACT: hipLaunchKernelGGL((gemm_rows_kernel<BM, BN, WM, WN, OP_BNACT>), grid, dim3(256), 0, s, g); break;
+    case OP_BNBWD: hipLaunchKernelGGL((gemm_rows_kernel<BM, BN, WM, WN, OP_BNBWD>), grid, dim3(256), 0, s, g); break;
+    default: hipLaunchKernelGGL((gemm_rows_kernel<BM, BN, WM, WN, OP_POOLBWD>), grid, dim3(256), 0, s, g); break;
+    }
+}
+
+template <int BO, int BI, int XM>
+static void launch_wgrad_y(dim3 grid, hipStream_t st, const Operand& x, int N, const Operand& y, int K, int M,
+                           int rows, float* dW, float* db) {
+    if (y.mode == OP_BNACT)
+        hipLaunchKernelGGL((wgrad_kernel<BO, BI, XM, OP_BNACT>), grid, dim3(256), 0, st, x, N, y, K, M, rows, dW, db);
+    else
+        hipLaunchKernelGGL((wgrad_kernel<BO, BI, XM, OP_PLAIN>), grid, dim3(256), 0, st, x, N, y, K, M, rows, dW, db);
 }
 
 template <int BO, int BI>
-static void launch_wgrad(dim3 grid, hipStream_t st, const float* X, int ldx, int N, const float* Y, int ldy, int K,
-                         const float* s, const float* t, int act, float slope, int M, int rows, float* dW, float* db) {
-    if (s) hipLaunchKernelGGL((wgrad_kernel<BO, BI, true>), grid, dim3(256), 0, st, X, ldx, N, Y, ldy, K, s, t, act,
-                              slope, M, rows, dW, db);
-    else hipLaunchKernelGGL((wgrad_kernel<BO, BI, false>), grid, dim3(256), 0, st, X, ldx, N, Y, ldy, K, s, t, act,
-                            slope, M, rows, dW, db);
+static void launch_wgrad(dim3 grid, hipStream_t st, const Operand& x, int N, const Operand& y, int K, int M, int rows,
+                         float* dW, float* db) {
+    switch (x.mode) {
+    case OP_PLAIN: launch_wgrad_y<BO, BI, OP_PLAIN>(grid, st, x, N, y, K, M, rows, dW, db); break;
+    case OP_BNBWD: launch_wgrad_y<BO, BI, OP_BNBWD>(grid, st, x, N, y, K, M, rows, dW, db); break;
+    default: launch_wgrad_y<BO, BI, OP_POOLBWD>(grid, st, x, N, y, K, M, rows, dW, db); break;
+    }
 }
 
 }  // namespace pcs
 
 using namespace pcs;
 
-// number of row blocks the row GEMM uses for M rows and N outputs (sizes the stats workspace)
-PCS_API int pcs_gemm_row_blocks(int M, int N) {
-    (void)N;
-    return (M + 127) / 128;
+// row-GEMM tile (BM x BN) for M rows and N outputs: the largest tile that still
+// gives >= 2 blocks per CU (256 CUs), else the one with the most blocks
+static void gemm_tile(int M, int N, int* bm, int* bn) {
+    struct T { int bm, bn; };
+    static const T big[] = {{128, 128}, {64, 128}, {64, 64}, {32, 128}};
+    static const T mid[] = {{128, 64}, {64, 64}};
+    const T* c = N > 64 ? big : mid;
+    const int nc = N > 64 ? 4 : 2;
+    if (N <= 32) { *bm = 128; *bn = 32; return; }
+    long long best = -1;
+    for (int i = 0; i < nc; ++i) {
+        const long long blocks = (long long)((M + c[i].bm - 1) / c[i].bm) * ((N + c[i].bn - 1) / c[i].bn);
+        if (blocks >= 512) { *bm = c[i].bm; *bn = c[i].bn; return; }
+        if (blocks > best) { best = blocks; *bm = c[i].bm; *bn = c[i].bn; }
+    }
 }
 
-// C = act_in(A*s_in+t_in) . W^T (+bias), W row-major N x K (row stride ldw).
+// number of row blocks the row GEMM uses for M rows and N outputs (sizes the stats workspace)
+PCS_API int pcs_gemm_row_blocks(int M, int N) {
+    int bm, bn;
+    gemm_tile(M, N, &bm, &bn);
+    return (M + bm - 1) / bm;
+}
+
+static int check_operand(const pcs_operand* o, int K, const char* who, const char* which) {
+    PCS_CHECK_ARG(o && o->data, "%s: %s operand missing", who, which);
+    PCS_CHECK_ARG(o->mode >= PCS_OP_PLAIN && o->mode <= PCS_OP_POOLBWD, "%s: %s mode %d", who, which, o->mode);
+    PCS_CHECK_ARG(o->ld % 4 == 0 && o->ld >= K, "%s: %s ld=%d must be a multiple of 4 and >= %d", who, which, o->ld,
+                  K);
+    PCS_CHECK_ARG(o->mode < PCS_OP_BNACT || (o->s && o->t), "%s: %s needs s/t", who, which);
+    PCS_CHECK_ARG(o->mode < PCS_OP_BNBWD || (o->z && o->ldz % 4 == 0 && o->ldz >= K && o->mean && o->alpha && o->kb),
+                  "%s: %s needs z/ldz/mean/alpha/kb", who, which);
+    PCS_CHECK_ARG(o->mode != PCS_OP_POOLBWD || (o->arg && o->pool_k >= 1 && o->pool_k <= 256),
+                  "%s: %s needs arg and 1 <= pool_k <= 256", who, which);
+    return 0;
+}
+
+static Operand to_dev(const pcs_operand* o) {
+    Operand r{};
+    if (!o) return r;
+    r.data = o->data; r.ld = o->ld; r.mode = o->mode;
+    r.s = o->s; r.t = o->t; r.act = o->act; r.slope = o->slope;
+    r.z = o->z; r.ldz = o->ldz;
+    r.mean = o->mean; r.inv = o->inv; r.alpha = o->alpha; r.kb = o->kb;
+    r.arg = o->arg; r.pool_k = o->pool_k;
+    return r;
+}
+
+// C = T(A) . W^T (+bias), W row-major N x K (row stride ldw).
 // stats (nullable): [row_blocks][2][N] fp64 partial (sum, sumsq) of C.
-// bstats (nullable): fused BN-backward partials of the layer whose pre-BN output is zp (same shape as C):
-//   [row_blocks][2][N] of (sum dy, sum dy*xhat), dy = C * act'(zp*sp+tp), xhat = (zp-meanp)*invp.
-PCS_API int pcs_gemm_rows(const float* A, int lda, int M, int K, const float* s_in, const float* t_in, int act_in,
-                          float slope_in, const float* W, int ldw, const float* bias, float* C, int ldc,
-                          int N, double* stats, const float* zp, int ldzp, const float* sp, const float* tp,
-                          const float* meanp, const float* invp, int actp, float slopep, double* bstats,
-                          void* stream) {
+// bstats (nullable): fused BN-backward partials of the layer whose pre-BN output is epi->z (same shape as C):
+//   [row_blocks][2][N] of (sum dy, sum dy*xhat), dy = C * act'(z*s+t), xhat = (z-mean)*inv.
+PCS_API int pcs_gemm_rows(const pcs_operand* a, int M, int K, const float* W, int ldw, const float* bias, float* C,
+                          int ldc, int N, double* stats, const pcs_operand* epi, double* bstats, void* stream) {
     PCS_CHECK_ARG(M >= 0 && K >= 1 && N >= 1, "pcs_gemm_rows: bad sizes M=%d K=%d N=%d", M, K, N);
-    PCS_CHECK_ARG(lda % 4 == 0 && lda >= K, "pcs_gemm_rows: lda=%d must be a multiple of 4 and >= K=%d", lda, K);
-    PCS_CHECK_ARG(A && W && C, "pcs_gemm_rows: null pointer");
+    if (int e = check_operand(a, K, "pcs_gemm_rows", "A")) return e;
+    PCS_CHECK_ARG(W && C, "pcs_gemm_rows: null pointer");
     PCS_CHECK_ARG(!(stats && bstats), "pcs_gemm_rows: stats and bstats are exclusive");
-    PCS_CHECK_ARG(!bstats || (zp && sp && tp && meanp && invp), "pcs_gemm_rows: bstats needs zp/sp/tp/meanp/invp");
-    PCS_CHECK_ARG((s_in == nullptr) == (t_in == nullptr), "pcs_gemm_rows: s_in/t_in must both be set or null");
+    PCS_CHECK_ARG(!bstats || (epi && epi->z && epi->s && epi->t && epi->mean && epi->inv),
+                  "pcs_gemm_rows: bstats needs epi z/s/t/mean/inv");
     PCS_CHECK_ARG(ldw >= K, "pcs_gemm_rows: ldw=%d < K=%d", ldw, K);
     if (M == 0) return 0;
-    GemmArgs g{A, lda, M, K, s_in, t_in, act_in, slope_in, W, ldw, bias, C, ldc, N, stats,
-               zp, ldzp, sp, tp, meanp, invp, actp, slopep, bstats};
+    GemmArgs g{to_dev(a), M, K, W, ldw, bias, C, ldc, N, stats, to_dev(epi), bstats};
     hipStream_t s = as_stream(stream);
-    if (N <= 32) launch_gemm<128, 32, 4, 1>(g, s);
-    else if (N <= 64) launch_gemm<128, 64, 4, 1>(g, s);
-    else launch_gemm<128, 128, 2, 2>(g, s);
+    int bm, bn;
+    gemm_tile(M, N, &bm, &bn);
+    if (bn == 32) launch_gemm<128, 32, 4, 1>(g, s);
+    else if (bm == 128 && bn == 64) launch_gemm<128, 64, 4, 1>(g, s);
+    else if (bm == 128) launch_gemm<128, 128, 2, 2>(g, s);
+    else if (bm == 64 && bn == 128) launch_gemm<64, 128, 2, 2>(g, s);
+    else if (bm == 64) launch_gemm<64, 64, 2, 2>(g, s);
+    else launch_gemm<32, 128, 1, 4>(g, s);
     return launch_status("pcs_gemm_rows");
 }
 
-// dW (N x K) += X^T . act(Y*s+t) over M rows; db (N) += column sums of X. dW/db zeroed by caller.
-PCS_API int pcs_wgrad(const float* X, int ldx, int N, const float* Y, int ldy, int K, const float* s, const float* t,
-                      int act, float slope, int M, float* dW, float* db, void* stream) {
+// dW (N x K) += T(X)^T . T(Y) over M rows; db (N) += column sums of T(X). dW/db zeroed by caller.
+PCS_API int pcs_wgrad(const pcs_operand* x, int N, const pcs_operand* y, int K, int M, float* dW, float* db,
+                      void* stream) {
     PCS_CHECK_ARG(M >= 0 && N >= 1 && K >= 1, "pcs_wgrad: bad sizes");
-    PCS_CHECK_ARG(X && Y && dW, "pcs_wgrad: null pointer");
-    PCS_CHECK_ARG(ldx % 4 == 0 && ldy % 4 == 0 && N % 4 == 0, "pcs_wgrad: ldx/ldy/N must be multiples of 4");
+    if (int e = check_operand(x, N, "pcs_wgrad", "X")) return e;
+    if (int e = check_operand(y, K, "pcs_wgrad", "Y")) return e;
+    PCS_CHECK_ARG(x->mode != PCS_OP_BNACT, "pcs_wgrad: X operand cannot be BNACT");
+    PCS_CHECK_ARG(y->mode <= PCS_OP_BNACT, "pcs_wgrad: Y operand must be PLAIN or BNACT");
+    PCS_CHECK_ARG(dW && N % 4 == 0, "pcs_wgrad: dW null or N not a multiple of 4");
     if (M == 0) return 0;
     const int BO = N > 64 ? 128 : 64, BI = K > 64 ? 128 : 64;
     const int tiles = ((N + BO - 1) / BO) * ((K + BI - 1) / BI);
@@ -782,10 +828,11 @@ PCS_API int pcs_wgrad(const float* X, int ldx, int N, const float* Y, int ldy, i
     splits = (M + rows - 1) / rows;
     const dim3 grid(splits, tiles);
     hipStream_t st = as_stream(stream);
-    if (BO == 128 && BI == 128) launch_wgrad<128, 128>(grid, st, X, ldx, N, Y, ldy, K, s, t, act, slope, M, rows, dW, db);
-    else if (BO == 128) launch_wgrad<128, 64>(grid, st, X, ldx, N, Y, ldy, K, s, t, act, slope, M, rows, dW, db);
-    else if (BI == 128) launch_wgrad<64, 128>(grid, st, X, ldx, N, Y, ldy, K, s, t, act, slope, M, rows, dW, db);
-    else launch_wgrad<64, 64>(grid, st, X, ldx, N, Y, ldy, K, s, t, act, slope, M, rows, dW, db);
+    const Operand xd = to_dev(x), yd = to_dev(y);
+    if (BO == 128 && BI == 128) launch_wgrad<128, 128>(grid, st, xd, N, yd, K, M, rows, dW, db);
+    else if (BO == 128) launch_wgrad<128, 64>(grid, st, xd, N, yd, K, M, rows, dW, db);
+    else if (BI == 128) launch_wgrad<64, 128>(grid, st, xd, N, yd, K, M, rows, dW, db);
+    else launch_wgrad<64, 64>(grid, st, xd, N, yd, K, M, rows, dW, db);
     return launch_status("pcs_wgrad");
 }
 
@@ -800,11 +847,11 @@ PCS_API int pcs_bn_finalize(const double* part, int nb, int N, long long M, cons
 }
 
 // BN backward finalize: part [nb][2][N] of (sum dy, sum dy*xhat) -> dgamma, dbeta (+= when accum), kB, kC.
-PCS_API int pcs_bn_bwd_finalize(const double* part, int nb, int N, long long M, const float* s, float* dgamma,
-                                float* dbeta, float* kB, float* kC, int accum, void* stream) {
+PCS_API int pcs_bn_bwd_finalize(const double* part, int nb, int N, long long M, const float* s, const float* invstd,
+                                float* dgamma, float* dbeta, float* kB, float* kC, int accum, void* stream) {
     PCS_CHECK_ARG(nb >= 1 && N >= 1 && M >= 1, "pcs_bn_bwd_finalize: bad sizes");
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(N), dim3(256), 0, as_stream(stream), part, nb, N, M, s, dgamma,
-                       dbeta, kB, kC, accum);
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(N), dim3(256), 0, as_stream(stream), part, nb, N, M, s, invstd,
+                       dgamma, dbeta, kB, kC, accum);
     return launch_status("pcs_bn_bwd_finalize");
 }
 
@@ -822,18 +869,6 @@ PCS_API int pcs_bn_bwd_reduce(const float* dA, int ldd, const float* Z, int ldz,
     hipLaunchKernelGGL(bn_bwd_reduce_kernel, grid, dim3(256), 2 * 256 * 4 * sizeof(double), as_stream(stream), dA, ldd,
                        Z, ldz, M, N, s, t, mean, inv, act, slope, kRedRows, part);
     return launch_status("pcs_bn_bwd_reduce");
-}
-
-PCS_API int pcs_bn_bwd_dz(const float* dA, int ldd, const float* Z, int ldz, int M, int N, const float* s,
-                          const float* t, const float* mean, const float* inv, const float* kB, const float* kC,
-                          int act, float slope, float* dZ, void* stream) {
-    PCS_CHECK_ARG(M >= 0 && N >= 4 && N % 4 == 0 && ldd % 4 == 0 && ldz % 4 == 0, "pcs_bn_bwd_dz: bad sizes");
-    const long long total = (long long)M * N / 4;
-    PCS_CHECK_ARG(total < (1ll << 31), "pcs_bn_bwd_dz: too many elements");
-    if (total == 0) return 0;
-    hipLaunchKernelGGL(bn_bwd_dz_kernel, dim3(ew_grid(total)), dim3(256), 0, as_stream(stream), dA, ldd, Z, ldz,
-                       (int)total, N / 4, s, t, mean, inv, kB, kC, act, slope, dZ);
-    return launch_status("pcs_bn_bwd_dz");
 }
 
 PCS_API int pcs_pool_fwd(const float* Z, int N, long long G, int K, const float* s, const float* t, int act,
@@ -858,18 +893,6 @@ PCS_API int pcs_pool_bwd_reduce(const float* dpool, const uint8_t* arg, const fl
     hipLaunchKernelGGL(pool_bwd_reduce_kernel, grid, dim3(256), 0, as_stream(stream), dpool, arg, Z, N, (int)G, K, s,
                        t, mean, inv, act, slope, gpb, part);
     return launch_status("pcs_pool_bwd_reduce");
-}
-
-PCS_API int pcs_pool_bwd_dz(const float* dpool, const uint8_t* arg, const float* Z, int N, long long G, int K,
-                            const float* s, const float* t, const float* mean, const float* inv, const float* kB,
-                            const float* kC, int act, float slope, float* dZ, void* stream) {
-    PCS_CHECK_ARG(G >= 0 && G < (1ll << 31) && K >= 1 && K <= 256 && N >= 4 && N % 4 == 0,
-                  "pcs_pool_bwd_dz: bad sizes");
-    const long long total = G * K * N / 4;
-    if (total == 0) return 0;
-    hipLaunchKernelGGL(pool_bwd_dz_kernel, dim3(ew_grid(total)), dim3(256), 0, as_stream(stream), dpool, arg, Z, N / 4,
-                       (int)G, K, s, t, mean, inv, kB, kC, act, slope, dZ);
-    return launch_status("pcs_pool_bwd_dz");
 }
 
 PCS_API int pcs_bn_act(const float* Z, int ldz, int M, int N, const float* s, const float* t, int act, float slope,

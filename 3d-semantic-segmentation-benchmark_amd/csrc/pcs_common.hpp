@@ -12,6 +12,8 @@
 #include <stdio.h>
 #include <string.h>
 
+#include "../../include/pcseg.h"   // the ABI this library implements (prototype check)
+
 #define PCS_API extern "C" __attribute__((visibility("default")))
 
 namespace pcs {

@@ -20,6 +20,19 @@ I32 = ctypes.c_int
 I64 = ctypes.c_longlong
 F32 = ctypes.c_float
 
+
+class Operand(ctypes.Structure):
+    """pcs_operand (include/pcseg.h): an engine GEMM operand and its on-load transform."""
+    _fields_ = [('data', P), ('ld', ctypes.c_int), ('mode', ctypes.c_int),
+                ('s', P), ('t', P), ('act', ctypes.c_int), ('slope', ctypes.c_float),
+                ('z', P), ('ldz', ctypes.c_int),
+                ('mean', P), ('inv', P), ('alpha', P), ('kb', P),
+                ('arg', P), ('pool_k', ctypes.c_int)]
+
+
+OP_PLAIN, OP_BNACT, OP_BNBWD, OP_POOLBWD = 0, 1, 2, 3
+OPP = ctypes.POINTER(Operand)
+
 # name -> argtypes (all return int status), mirrors include/pcseg.h
 SIGNATURES = {
     'pcs_fps': [P, I32, I32, I32, P, P, P, P],
@@ -36,18 +49,16 @@ SIGNATURES = {
     'pcs_edge_bwd': [P, I32, P, I32, I32, I32, I32, P, P],
     # shared-MLP engine
     'pcs_gemm_row_blocks': [I32, I32],
-    'pcs_gemm_rows': [P, I32, I32, I32, P, P, I32, F32, P, I32, P, P, I32, I32, P,
-                      P, I32, P, P, P, P, I32, F32, P, P],
-    'pcs_wgrad': [P, I32, I32, P, I32, I32, P, P, I32, F32, I32, P, P, P],
+    'pcs_operand_size': [],
+    'pcs_gemm_rows': [OPP, I32, I32, P, I32, P, P, I32, I32, P, OPP, P, P],
+    'pcs_wgrad': [OPP, I32, OPP, I32, I32, P, P, P],
     'pcs_bn_finalize': [P, I32, I32, I64, P, P, F32, F32, P, P, P, P, P, P, P],
-    'pcs_bn_bwd_finalize': [P, I32, I32, I64, P, P, P, P, P, I32, P],
+    'pcs_bn_bwd_finalize': [P, I32, I32, I64, P, P, P, P, P, P, I32, P],
     'pcs_bn_bwd_reduce_blocks': [I32],
     'pcs_bn_bwd_reduce': [P, I32, P, I32, I32, I32, P, P, P, P, I32, F32, P, P],
-    'pcs_bn_bwd_dz': [P, I32, P, I32, I32, I32, P, P, P, P, P, P, I32, F32, P, P],
     'pcs_pool_fwd': [P, I32, I64, I32, P, P, I32, F32, P, P, P],
     'pcs_pool_bwd_reduce_blocks': [I64],
     'pcs_pool_bwd_reduce': [P, P, P, I32, I64, I32, P, P, P, P, I32, F32, P, P],
-    'pcs_pool_bwd_dz': [P, P, P, I32, I64, I32, P, P, P, P, P, P, I32, F32, P, P],
     'pcs_bn_act': [P, I32, I32, I32, P, P, I32, F32, P, I32, P],
 }
 

@@ -82,6 +82,106 @@ def interpolate(points: torch.Tensor, coords_1: torch.Tensor, coords_2: torch.Te
     return ops.interp_cat_rows(None, points, idx, dist).view(B, N, points.shape[2])
 
 
+# --------------------------------------------------------------------------- geometry on a side stream
+_side_streams: dict = {}
+
+
+def side_stream(device) -> torch.cuda.Stream:
+    """One long-lived side stream per device for the neighbour-search work."""
+    dev = torch.device(device)
+    key = dev.index if dev.index is not None else torch.cuda.current_device()
+    st = _side_streams.get(key)
+    if st is None:
+        st = torch.cuda.Stream(device=dev)
+        _side_streams[key] = st
+    return st
+
+
+class GeometryPlan:
+    """All neighbour structure of one PointNet++-family forward, enqueued up front
+    on a side stream so it overlaps the shared-MLP work of the main stream.
+
+    The geometry depends on coordinates only: level l's centroids are FPS of
+    level l-1's (reference SetAbstraction.forward, common.py:204-206), its ball
+    queries group them against level l-1 (SA) or against themselves (InvResMLP,
+    common.py:288), and FeaturePropagation's 3-NN pairs adjacent levels
+    (common.py:107-114).  `levels` = [(C, [(r, K, on_self), ...]), ...] in the
+    reference's call order, so FPS start draws and replay records keep the
+    reference's sequence.  Consumers wait on the per-level event before reading.
+    """
+
+    def __init__(self, coords: torch.Tensor, levels, interp: bool = True):
+        dev = coords.device
+        main = torch.cuda.current_stream(dev)
+        side = side_stream(dev)
+        side.wait_stream(main)
+        self.coords = [coords]
+        self.balls, self.events, self.nn = [], [], []
+        made = []
+        with torch.cuda.stream(side):
+            prev = coords
+            for C, queries in levels:
+                _, cent = sample_indices(prev, C)
+                bl = [_ball(cent, cent if on_self else prev, r, K) for r, K, on_self in queries]
+                ev = torch.cuda.Event()
+                ev.record(side)
+                self.coords.append(cent)
+                self.balls.append(bl)
+                self.events.append(ev)
+                made += [cent, *bl]
+                prev = cent
+            if interp:
+                nn_ = []
+                for lv in range(len(levels) - 1, -1, -1):      # FP_L ... FP_1, the reference's order
+                    idx, dist = ops.knn_select(self.coords[lv], self.coords[lv + 1], 3)
+                    rp = _replay()
+                    if rp is not None:
+                        rp.rec_interp_idx.append(idx.detach().cpu())
+                    nn_.append((idx, dist))
+                    made += [idx, dist]
+                self.nn = nn_[::-1]                             # nn[lv] pairs level lv with lv + 1
+                self.nn_event = torch.cuda.Event()
+                self.nn_event.record(side)
+        coords.record_stream(side)
+        for t in made:
+            t.record_stream(main)
+
+    @staticmethod
+    def _wait(ev):
+        torch.cuda.current_stream().wait_event(ev)
+
+    def sa(self, level: int, q: int = 0):
+        """(centroids, ball idx) of level >= 1 for its q-th query, after waiting for them."""
+        self._wait(self.events[level - 1])
+        return self.coords[level], self.balls[level - 1][q]
+
+    def fp(self, level: int):
+        """(idx, dist) of the 3-NN from level `level` points into level `level + 1`."""
+        self._wait(self.nn_event)
+        return self.nn[level]
+
+
+class GeometryPrefetch:
+    """Mixin: `model.prefetch_geometry(x)` enqueues the GeometryPlan of a future
+    forward(x) now (e.g. before the previous step's backward), so FPS / ball
+    query / 3-NN of the next batch overlap that backward.  The next forward with
+    the same, unmodified tensor consumes it; anything else recomputes."""
+
+    def prefetch_geometry(self, x: torch.Tensor) -> None:
+        self._pcs_prefetched = (x, x._version, self._plan_for(self._coords_of(x)))
+
+    def _geometry(self, x: torch.Tensor, coords: torch.Tensor) -> GeometryPlan:
+        pf = getattr(self, '_pcs_prefetched', None)
+        self._pcs_prefetched = None
+        if pf is not None and pf[0] is x and pf[1] == x._version:
+            return pf[2]
+        return self._plan_for(coords)
+
+    @staticmethod
+    def _coords_of(x: torch.Tensor) -> torch.Tensor:
+        return x[:, :, :3].contiguous()
+
+
 # --------------------------------------------------------------------------- MLP blocks
 class MiniPointNet(nn.Module):
     """Reference common.py:125-150 (Conv2d 1x1 -> BatchNorm2d -> ReLU)."""
@@ -141,10 +241,15 @@ class SetAbstraction(nn.Module):
         self.pooling_type = pooling_type
         self.grouping_norm = grouping_norm
 
-    def forward(self, coords: torch.Tensor, features: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+    def forward(self, coords: torch.Tensor, features: torch.Tensor,
+                geo: tuple | None = None) -> tuple[torch.Tensor, torch.Tensor]:
+        """geo = (centroids, ball idx) precomputed by a GeometryPlan, else computed here."""
         B = coords.shape[0]
-        _, cent = sample_indices(coords, self.C)
-        idx = _ball(cent, coords, self.radius, self.K)
+        if geo is None:
+            _, cent = sample_indices(coords, self.C)
+            idx = _ball(cent, coords, self.radius, self.K)
+        else:
+            cent, idx = geo
         rows = ops.group_rows(coords, features, cent, idx, self.radius, self.grouping_norm)
         kin = 3 + features.shape[2]
         if self.pooling_type == 'max':
@@ -163,12 +268,16 @@ class FeaturePropagation(nn.Module):
         self.point_net = UnitPointNet(in_channels, mlps)
 
     def forward(self, coords_1: torch.Tensor, coords_2: torch.Tensor, features_1: torch.Tensor | None,
-                features_2: torch.Tensor) -> torch.Tensor:
+                features_2: torch.Tensor, geo: tuple | None = None) -> torch.Tensor:
+        """geo = (3-NN idx, squared dist) precomputed by a GeometryPlan, else computed here."""
         B, N, _ = coords_1.shape
-        idx, dist = ops.knn_select(coords_1, coords_2, 3)
-        rp = _replay()
-        if rp is not None:
-            rp.rec_interp_idx.append(idx.detach().cpu())
+        if geo is None:
+            idx, dist = ops.knn_select(coords_1, coords_2, 3)
+            rp = _replay()
+            if rp is not None:
+                rp.rec_interp_idx.append(idx.detach().cpu())
+        else:
+            idx, dist = geo
         rows = ops.interp_cat_rows(features_1, features_2, idx, dist)
         return self.point_net.forward_rows(rows).view(B, N, -1)
 
@@ -185,9 +294,10 @@ class InvResMLP(nn.Module):
         self.point_features_mlp = UnitPointNet(mlp_size, [4 * mlp_size, mlp_size])
 
     def forward(self, centroid_coords: torch.Tensor, coords: torch.Tensor,
-                features: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+                features: torch.Tensor, geo: torch.Tensor | None = None) -> tuple[torch.Tensor, torch.Tensor]:
+        """geo = ball idx precomputed by a GeometryPlan, else computed here."""
         B, C, _ = centroid_coords.shape
-        idx = _ball(centroid_coords, coords, self.radius, self.K)
+        idx = _ball(centroid_coords, coords, self.radius, self.K) if geo is None else geo
         rows = ops.group_rows(coords, features, centroid_coords, idx, self.radius, True)
         kin = 3 + features.shape[2]
         if self.pooling_type == 'max':

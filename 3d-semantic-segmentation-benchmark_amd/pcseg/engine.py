@@ -9,6 +9,9 @@ followed by `reduce(..., 'max')` (common.py:211-212), EdgeConv
 
 Only pre-BN activations Z are kept for backward; the BN-applied activation of
 layer l is recomputed inside layer l+1's GEMM A-load, so it never touches HBM.
+Backward mirrors it: a layer's dZ (the BatchNorm-backward of its output
+gradient) is rebuilt on load by both consumers (weight-gradient and data-
+gradient GEMMs) from the output gradient and Z, so it is never stored either.
 """
 from __future__ import annotations
 
@@ -16,10 +19,9 @@ import math
 
 import torch
 
-from ._lib import call, load, ptr, stream_ptr
+from ._lib import call, load, ptr, stream_ptr, Operand, OP_PLAIN, OP_BNACT, OP_BNBWD, OP_POOLBWD
 
 ACT = {'relu': 0, 'lrelu': 1, 'none': 2}
-BM = 128  # row tile of pcs_gemm_rows (must match csrc/mlp.hip)
 
 
 def ld4(n: int) -> int:
@@ -63,6 +65,95 @@ def notify_grad_ready(params) -> None:
                 cb(p)
 
 
+# --------------------------------------------------------------------------- launch probe
+_probe: list | None = None
+
+
+class KernelProbe:
+    """Bracket every engine GEMM launch with HIP events on the stream it runs on.
+
+    Inside `with KernelProbe() as kp:` each pcs_gemm_rows / pcs_wgrad launch is
+    recorded as (kernel name as rocprof reports it, algorithmic flops,
+    algorithmic bytes, start event, end event).  Used by bench.py's roofline.
+    """
+
+    def __enter__(self):
+        global _probe
+        self.records = []
+        _probe = self.records
+        return self
+
+    def __exit__(self, *exc):
+        global _probe
+        _probe = None
+        return False
+
+    def summary(self):
+        """{kernel: (launches, flops, bytes, seconds)} (synchronises)."""
+        out = {}
+        for name, fl, by, e0, e1 in self.records:
+            e1.synchronize()
+            n, f, b, t = out.get(name, (0, 0, 0, 0.0))
+            out[name] = (n + 1, f + fl, b + by, t + e0.elapsed_time(e1) * 1e-3)
+        return out
+
+
+def _gemm_tile(M: int, N: int) -> tuple[int, int, int, int]:
+    """(BM, BN, WM, WN) of the row GEMM -- mirrors gemm_tile() in csrc/mlp.hip (used for naming only)."""
+    if N <= 32:
+        return 128, 32, 4, 1
+    cands = [(128, 128, 2, 2), (64, 128, 2, 2), (64, 64, 2, 2), (32, 128, 1, 4)] if N > 64 else \
+        [(128, 64, 4, 1), (64, 64, 2, 2)]
+    best, pick = -1, cands[0]
+    for c in cands:
+        blocks = -(-M // c[0]) * -(-N // c[1])
+        if blocks >= 512:
+            return c
+        if blocks > best:
+            best, pick = blocks, c
+    return pick
+
+
+def _launch(name, fl, by, fn, *args):
+    if _probe is None:
+        call(fn, *args)
+        return
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    call(fn, *args)
+    e1.record()
+    _probe.append((name, fl, by, e0, e1))
+
+
+def operand(data, ld, mode=OP_PLAIN, s=None, t=None, act=0, slope=0.0, z=None, ldz=0, mean=None, inv=None,
+            alpha=None, kb=None, arg=None, pool_k=0) -> Operand:
+    """pcs_operand for a tensor and its on-load transform (the tensors must outlive the launch)."""
+    return Operand(ptr(data), ld, mode, ptr(s), ptr(t), act, float(slope), ptr(z), ldz, ptr(mean), ptr(inv),
+                   ptr(alpha), ptr(kb), ptr(arg), pool_k)
+
+
+def _operand_bytes(op: Operand, M: int, K: int) -> int:
+    if op.mode == OP_POOLBWD:
+        return 4 * M * K                      # Z (the pooled gradient and argmax are M/pool_k rows)
+    return 4 * M * K * (2 if op.mode == OP_BNBWD else 1)
+
+
+def gemm_rows(a: Operand, M, K, W, ldw, bias, C, ldc, N, stats=None, epi: Operand | None = None, bstats=None,
+              st=None):
+    """C[M,N] = T(A)[M,K] . W^T (+bias) with optional BN-stat / BN-backward partials."""
+    bm, bn, wm, wn = _gemm_tile(M, N)
+    by = _operand_bytes(a, M, K) + 4 * M * N + (4 * M * N if bstats is not None else 0)
+    _launch(f'pcs::gemm_rows_kernel<{bm}, {bn}, {wm}, {wn}, {a.mode}>', 2 * M * K * N, by, 'pcs_gemm_rows',
+            a, M, K, ptr(W), ldw, ptr(bias), ptr(C), ldc, N, ptr(stats), epi, ptr(bstats), st)
+
+
+def wgrad(x: Operand, N, y: Operand, K, M, dW, db, st):
+    """dW[N,K] += T(X)^T . T(Y) over M rows, db += colsum(T(X))."""
+    name = f'pcs::wgrad_kernel<{128 if N > 64 else 64}, {128 if K > 64 else 64}, {x.mode}, {y.mode}>'
+    _launch(name, 2 * M * N * K, _operand_bytes(x, M, N) + _operand_bytes(y, M, K), 'pcs_wgrad',
+            x, N, y, K, M, ptr(dW), ptr(db), st)
+
+
 def _f64(shape, dev):
     return torch.empty(shape, dtype=torch.float64, device=dev)
 
@@ -93,14 +184,14 @@ class SharedMLPFn(torch.autograd.Function):
             if Cout % 4:
                 raise ValueError(f'engine: layer width {Cout} must be a multiple of 4')
             Z = _f32((M, Cout), dev)
+            a_op = operand(A, lda_cur) if s_prev is None else \
+                operand(A, lda_cur, OP_BNACT, s_prev, t_prev, a_code, slope)
             use_batch = bn.training or bn.running_mean is None
             s, t, mean, inv = (_f32((Cout,), dev) for _ in range(4))
             if use_batch:
-                nb = (M + BM - 1) // BM
+                nb = load().pcs_gemm_row_blocks(M, Cout)
                 part = _f64((nb, 2, Cout), dev)
-                call('pcs_gemm_rows', ptr(A), lda_cur, M, K_cur, ptr(s_prev), ptr(t_prev), a_code, slope,
-                     ptr(Wm), Wm.shape[1], ptr(b), ptr(Z), Cout, Cout, ptr(part),
-                     None, 0, None, None, None, None, 0, 0.0, None, st)
+                gemm_rows(a_op, M, K_cur, Wm, Wm.shape[1], b, Z, Cout, Cout, part, st=st)
                 momentum = 0.0
                 rm = rv = None
                 if bn.training and bn.track_running_stats and bn.running_mean is not None:
@@ -110,9 +201,7 @@ class SharedMLPFn(torch.autograd.Function):
                 call('pcs_bn_finalize', ptr(part), nb, Cout, M, ptr(g), ptr(be), float(bn.eps), float(momentum),
                      ptr(rm), ptr(rv), ptr(s), ptr(t), ptr(mean), ptr(inv), st)
             else:
-                call('pcs_gemm_rows', ptr(A), lda_cur, M, K_cur, ptr(s_prev), ptr(t_prev), a_code, slope,
-                     ptr(Wm), Wm.shape[1], ptr(b), ptr(Z), Cout, Cout, None,
-                     None, 0, None, None, None, None, 0, 0.0, None, st)
+                gemm_rows(a_op, M, K_cur, Wm, Wm.shape[1], b, Z, Cout, Cout, None, st=st)
                 with torch.no_grad():
                     inv.copy_(torch.rsqrt(bn.running_var + bn.eps))
                     mean.copy_(bn.running_mean)
@@ -174,19 +263,19 @@ class SharedMLPFn(torch.autograd.Function):
             part = _f64((nb, 2, CL), dev)
             call('pcs_bn_bwd_reduce', ptr(gout), CL, ptr(Zs[-1]), CL, M, CL, ptr(s), ptr(t), ptr(mean), ptr(inv),
                  a_code, slope, ptr(part), st)
-        kB, kC = _f32((CL,), dev), _f32((CL,), dev)
+        kB, alpha = _f32((CL,), dev), _f32((CL,), dev)
         gg, gb = grad_target(params[4 * (nl - 1) + 2]), grad_target(params[4 * (nl - 1) + 3])
-        call('pcs_bn_bwd_finalize', ptr(part), nb, CL, M, ptr(s), ptr(gg), ptr(gb), ptr(kB), ptr(kC), 1, st)
+        call('pcs_bn_bwd_finalize', ptr(part), nb, CL, M, ptr(s), ptr(inv), ptr(gg), ptr(gb), ptr(kB), ptr(alpha), 1,
+             st)
         if not use_batch[-1]:
             kB.zero_()
-            kC.zero_()
-        dZ = _f32((M, CL), dev)
+            alpha.zero_()
+        # dZ of the top layer is never materialised: its consumers rebuild it on load
         if pool_K:
-            call('pcs_pool_bwd_dz', ptr(gout), ptr(arg), ptr(Zs[-1]), CL, M // pool_K, pool_K, ptr(s), ptr(t),
-                 ptr(mean), ptr(inv), ptr(kB), ptr(kC), a_code, slope, ptr(dZ), st)
+            xop = operand(gout, CL, OP_POOLBWD, s, t, a_code, slope, Zs[-1], CL, mean, None, alpha, kB, arg, pool_K)
         else:
-            call('pcs_bn_bwd_dz', ptr(gout), CL, ptr(Zs[-1]), CL, M, CL, ptr(s), ptr(t), ptr(mean), ptr(inv),
-                 ptr(kB), ptr(kC), a_code, slope, ptr(dZ), st)
+            xop = operand(gout, CL, OP_BNBWD, s, t, a_code, slope, Zs[-1], CL, mean, None, alpha, kB)
+        keep = [gout, kB, alpha]
         dX = None
         for li in range(nl - 1, -1, -1):
             W, b = params[4 * li], params[4 * li + 1]
@@ -199,33 +288,29 @@ class SharedMLPFn(torch.autograd.Function):
             if dW is not None:
                 if li > 0:
                     sp, tp, mp, ip = stats[li - 1]
-                    call('pcs_wgrad', ptr(dZ), Cout, Cout, ptr(Zs[li - 1]), Cin, Cin, ptr(sp), ptr(tp), a_code, slope,
-                         M, ptr(dW), ptr(db), st)
+                    yop = operand(Zs[li - 1], Cin, OP_BNACT, sp, tp, a_code, slope)
+                    wgrad(xop, Cout, yop, Cin, M, dW, db, st)
                 else:
-                    call('pcs_wgrad', ptr(dZ), Cout, Cout, ptr(X), lda, Kin, None, None, 0, 0.0, M, ptr(dW), ptr(db),
-                         st)
+                    wgrad(xop, Cout, operand(X, lda), Kin, M, dW, db, st)
             if li > 0:
                 sp, tp, mp, ip = stats[li - 1]
                 dA = _f32((M, Cin), dev)
-                nbg = (M + BM - 1) // BM
+                nbg = lib.pcs_gemm_row_blocks(M, Cin)
                 bpart = _f64((nbg, 2, Cin), dev)
-                call('pcs_gemm_rows', ptr(dZ), Cout, M, Cout, None, None, 0, 0.0, ptr(Wt), Cout, None, ptr(dA), Cin,
-                     Cin, None, ptr(Zs[li - 1]), Cin, ptr(sp), ptr(tp), ptr(mp), ptr(ip), a_code, slope, ptr(bpart),
-                     st)
-                kB2, kC2 = _f32((Cin,), dev), _f32((Cin,), dev)
+                epi = operand(None, 0, OP_BNBWD, sp, tp, a_code, slope, Zs[li - 1], Cin, mp, ip)
+                gemm_rows(xop, M, Cout, Wt, Cout, None, dA, Cin, Cin, None, epi, bpart, st=st)
+                kB2, alpha2 = _f32((Cin,), dev), _f32((Cin,), dev)
                 g2, b2 = grad_target(params[4 * (li - 1) + 2]), grad_target(params[4 * (li - 1) + 3])
-                call('pcs_bn_bwd_finalize', ptr(bpart), nbg, Cin, M, ptr(sp), ptr(g2), ptr(b2), ptr(kB2), ptr(kC2), 1,
-                     st)
+                call('pcs_bn_bwd_finalize', ptr(bpart), nbg, Cin, M, ptr(sp), ptr(ip), ptr(g2), ptr(b2), ptr(kB2),
+                     ptr(alpha2), 1, st)
                 if not use_batch[li - 1]:
                     kB2.zero_()
-                    kC2.zero_()
-                dZ = _f32((M, Cin), dev)
-                call('pcs_bn_bwd_dz', ptr(dA), Cin, ptr(Zs[li - 1]), Cin, M, Cin, ptr(sp), ptr(tp), ptr(mp), ptr(ip),
-                     ptr(kB2), ptr(kC2), a_code, slope, ptr(dZ), st)
+                    alpha2.zero_()
+                xop = operand(dA, Cin, OP_BNBWD, sp, tp, a_code, slope, Zs[li - 1], Cin, mp, None, alpha2, kB2)
+                keep += [dA, kB2, alpha2]
             elif ctx.needs_input_grad[0]:
                 dX = torch.zeros((M, lda), dtype=torch.float32, device=dev) if lda != Kin else _f32((M, lda), dev)
-                call('pcs_gemm_rows', ptr(dZ), Cout, M, Cout, None, None, 0, 0.0, ptr(Wt), Cout, None, ptr(dX), lda,
-                     Kin, None, None, 0, None, None, None, None, 0, 0.0, None, st)
+                gemm_rows(xop, M, Cout, Wt, Cout, None, dX, lda, Kin, st=st)
         notify_grad_ready(params)
         return (dX, None, None, None, None, None, *grads)
 

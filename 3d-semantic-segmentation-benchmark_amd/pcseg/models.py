@@ -16,7 +16,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import ops
-from .common import SetAbstraction, FeaturePropagation, InvResMLP, UnitPointNet, sample_indices, _ball
+from .common import SetAbstraction, FeaturePropagation, InvResMLP, UnitPointNet, GeometryPlan, GeometryPrefetch
 from .mlp import conv_rows, bn_rows
 from .engine import shared_mlp, pad_rows
 from .replay import active as _replay
@@ -26,7 +26,7 @@ def _head_rows(x_rows: torch.Tensor, drop: nn.Module, conv: nn.Module) -> torch.
     return conv_rows(drop(x_rows), conv)
 
 
-class PointNetpp(nn.Module):
+class PointNetpp(GeometryPrefetch, nn.Module):
     """PointNet++ SSG semantic segmentation (reference PointNetpp.py:6-48)."""
 
     def __init__(self, part_classes: int):
@@ -42,22 +42,27 @@ class PointNetpp(nn.Module):
         self.drop = nn.Dropout(0.5)
         self.conv = nn.Conv1d(128, part_classes, 1)
 
+    def _plan_for(self, c0):
+        return GeometryPlan(c0, [(sa.C, [(sa.radius, sa.K, False)]) for sa in (self.sa1, self.sa2, self.sa3, self.sa4)])
+
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         B, N, _ = x.shape
-        c0 = x[:, :, :3].contiguous()
+        c0 = self._coords_of(x)
         f0 = x[:, :, 3:].contiguous()
-        c1, f1 = self.sa1(c0, f0)
-        c2, f2 = self.sa2(c1, f1)
-        c3, f3 = self.sa3(c2, f2)
-        c4, f4 = self.sa4(c3, f3)
-        f3 = self.fp4(c3, c4, f3, f4)
-        f2 = self.fp3(c2, c3, f2, f3)
-        f1 = self.fp2(c1, c2, f1, f2)
-        f0 = self.fp1(c0, c1, None, f1)
+        geo = self._geometry(x, c0)
+        c0 = geo.coords[0]
+        c1, f1 = self.sa1(c0, f0, geo=geo.sa(1))
+        c2, f2 = self.sa2(c1, f1, geo=geo.sa(2))
+        c3, f3 = self.sa3(c2, f2, geo=geo.sa(3))
+        c4, f4 = self.sa4(c3, f3, geo=geo.sa(4))
+        f3 = self.fp4(c3, c4, f3, f4, geo=geo.fp(3))
+        f2 = self.fp3(c2, c3, f2, f3, geo=geo.fp(2))
+        f1 = self.fp2(c1, c2, f1, f2, geo=geo.fp(1))
+        f0 = self.fp1(c0, c1, None, f1, geo=geo.fp(0))
         return _head_rows(f0.reshape(B * N, -1), self.drop, self.conv).view(B, N, -1)
 
 
-class PointNetppMSG(nn.Module):
+class PointNetppMSG(GeometryPrefetch, nn.Module):
     """PointNet++ MSG (multi-scale grouping) segmentation.
 
     Not in the reference (BASELINE.json config 4 names it); composed from the
@@ -91,32 +96,36 @@ class PointNetppMSG(nn.Module):
         self.drop = nn.Dropout(0.5)
         self.conv = nn.Conv1d(128, part_classes, 1)
 
-    def _sa_level(self, branches, coords, feats):
+    def _plan_for(self, c0):
+        return GeometryPlan(c0, [(br[0].C, [(sa.radius, sa.K, False) for sa in br]) for br in self.levels])
+
+    def _sa_level(self, branches, coords, feats, geo, level):
         C = branches[0].C
         B = coords.shape[0]
-        _, cent = sample_indices(coords, C)
         outs = []
-        for sa in branches:
-            idx = _ball(cent, coords, sa.radius, sa.K)
+        for q, sa in enumerate(branches):
+            cent, idx = geo.sa(level, q)
             rows = ops.group_rows(coords, feats, cent, idx, sa.radius, sa.grouping_norm)
             outs.append(sa.point_net.forward_rows(rows, 3 + feats.shape[2], pool_k=sa.K).view(B, C, -1))
         return cent, torch.cat(outs, dim=-1)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         B, N, _ = x.shape
-        cs, fs = [x[:, :, :3].contiguous()], [x[:, :, 3:].contiguous()]
-        for branches in self.levels:
-            c, f = self._sa_level(branches, cs[-1], fs[-1])
+        c0 = self._coords_of(x)
+        geo = self._geometry(x, c0)
+        cs, fs = [geo.coords[0]], [x[:, :, 3:].contiguous()]
+        for lv, branches in enumerate(self.levels, start=1):
+            c, f = self._sa_level(branches, cs[-1], fs[-1], geo, lv)
             cs.append(c)
             fs.append(f)
-        f3 = self.fp4(cs[3], cs[4], fs[3], fs[4])
-        f2 = self.fp3(cs[2], cs[3], fs[2], f3)
-        f1 = self.fp2(cs[1], cs[2], fs[1], f2)
-        f0 = self.fp1(cs[0], cs[1], None, f1)
+        f3 = self.fp4(cs[3], cs[4], fs[3], fs[4], geo=geo.fp(3))
+        f2 = self.fp3(cs[2], cs[3], fs[2], f3, geo=geo.fp(2))
+        f1 = self.fp2(cs[1], cs[2], fs[1], f2, geo=geo.fp(1))
+        f0 = self.fp1(cs[0], cs[1], None, f1, geo=geo.fp(0))
         return _head_rows(f0.reshape(B * N, -1), self.drop, self.conv).view(B, N, -1)
 
 
-class PointNeXt(nn.Module):
+class PointNeXt(GeometryPrefetch, nn.Module):
     """PointNeXt(-B-like) segmentation (reference PointNeXt.py:17-147)."""
 
     def __init__(self, part_classes: int, version: str = 'b'):
@@ -148,24 +157,35 @@ class PointNeXt(nn.Module):
         self.drop = nn.Dropout(0.5)
         self.conv = nn.Conv1d(fp1, part_classes, 1)
 
+    def _plan_for(self, c0):
+        def q(m, on_self):
+            return (m.radius, m.K, on_self)
+        return GeometryPlan(c0, [
+            (self.sa1.C, [q(self.sa1, False), q(self.irmlp1, True)]),
+            (self.sa2.C, [q(self.sa2, False), q(self.irmlp2, True), q(self.irmlp2_1, True)]),
+            (self.sa3.C, [q(self.sa3, False), q(self.irmlp3, True)]),
+            (self.sa4.C, [q(self.sa4, False), q(self.irmlp4, True)])])
+
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         B, N, Cin = x.shape
+        c0 = self._coords_of(x)
+        geo = self._geometry(x, c0)          # FPS etc. start on the side stream before the stem MLP
+        c0 = geo.coords[0]
         x = x.contiguous()
         f0 = self.mlp.forward_rows(pad_rows(x.view(B * N, Cin)), Cin).view(B, N, -1)
-        c0 = x[:, :, :3].contiguous()
-        c1, f1 = self.sa1(c0, f0)
-        c1, f1 = self.irmlp1(c1, c1, f1)
-        c2, f2 = self.sa2(c1, f1)
-        c2, f2 = self.irmlp2(c2, c2, f2)
-        c2, f2 = self.irmlp2_1(c2, c2, f2)
-        c3, f3 = self.sa3(c2, f2)
-        c3, f3 = self.irmlp3(c3, c3, f3)
-        c4, f4 = self.sa4(c3, f3)
-        c4, f4 = self.irmlp4(c4, c4, f4)
-        f3 = self.fp4(c3, c4, f3, f4)
-        f2 = self.fp3(c2, c3, f2, f3)
-        f1 = self.fp2(c1, c2, f1, f2)
-        f0 = self.fp1(c0, c1, f0, f1)
+        c1, f1 = self.sa1(c0, f0, geo=geo.sa(1, 0))
+        c1, f1 = self.irmlp1(c1, c1, f1, geo=geo.sa(1, 1)[1])
+        c2, f2 = self.sa2(c1, f1, geo=geo.sa(2, 0))
+        c2, f2 = self.irmlp2(c2, c2, f2, geo=geo.sa(2, 1)[1])
+        c2, f2 = self.irmlp2_1(c2, c2, f2, geo=geo.sa(2, 2)[1])
+        c3, f3 = self.sa3(c2, f2, geo=geo.sa(3, 0))
+        c3, f3 = self.irmlp3(c3, c3, f3, geo=geo.sa(3, 1)[1])
+        c4, f4 = self.sa4(c3, f3, geo=geo.sa(4, 0))
+        c4, f4 = self.irmlp4(c4, c4, f4, geo=geo.sa(4, 1)[1])
+        f3 = self.fp4(c3, c4, f3, f4, geo=geo.fp(3))
+        f2 = self.fp3(c2, c3, f2, f3, geo=geo.fp(2))
+        f1 = self.fp2(c1, c2, f1, f2, geo=geo.fp(1))
+        f0 = self.fp1(c0, c1, f0, f1, geo=geo.fp(0))
         return _head_rows(f0.reshape(B * N, -1), self.drop, self.conv).view(B, N, -1)
 
 

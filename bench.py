@@ -8,8 +8,9 @@ Multi-GPU: one process per GPU (torchrun), data-parallel, RCCL all-reduce of the
 flat gradient buffer, fixed per-GPU batch ("weak" scaling).
 
 Also reported on the same JSON line:
-  roofline      -- the dominant HIP kernel's algorithmic bytes / its average
-                   launch time (HIP events on its stream) vs 8 TB/s HBM;
+  roofline      -- the dominant HIP kernel (the engine GEMM variant with the
+                   largest time per step): its algorithmic flops / its launch
+                   time (HIP events on its stream) vs the fp32 MFMA peak;
   cpu_baseline  -- the CPU oracle (oracle/ref_ops.py, the reference algorithm
                    restated on PyTorch-CPU) on a bounded sample of the same
                    workload, in a subprocess with no GPU visible, rank 0 only.
@@ -37,6 +38,9 @@ MODELS = {
     'pointnet': ('PointNetSeg', lambda m: m.PointNetSeg(part_classes=14), 'points'),
 }
 HBM_PEAK_GBS = 8000.0           # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# reference-algorithm fwd+bwd GFLOP per sample (FlopCounterMode on the reference)
+ALGO_GFLOP_PER_SAMPLE = {('pointnetpp', 4096): 5.786, ('pointnext', 4096): 10.791, ('pointnext', 24576): 19.592,
+                         ('dgcnn', 4096): 53.468, ('pointnet', 4096): 24.635}
 FP32_PEAK_TFLOPS = 157.3
 
 
@@ -99,47 +103,40 @@ def run_cpu_baseline(args):
         return {'value': None, 'unit': 'points/s', 'cores': threads, 'kind': 'port', 'sample': f'failed: {e}'}
 
 
-# ----------------------------------------------------------------------------- roofline of one kernel
-def kernel_roofline(args, dev):
-    """Time the dominant HIP kernel alone, on the stream it is launched on (HIP events)."""
+# ----------------------------------------------------------------------------- roofline of the dominant kernel
+def kernel_roofline(step, dev):
+    """Run one more training step with every engine GEMM launch bracketed by HIP
+    events on its own stream (pcseg.engine.KernelProbe); the dominant kernel is
+    the variant with the largest summed time.  achieved = its algorithmic flops
+    (2*M*K*N per launch) / its summed launch time, vs the fp32 MFMA peak."""
     import torch
-    from pcseg import ops
-    from pcseg.synthetic import make_batch
-    B, N = args.batch, args.npoints
-    pts, _, _ = make_batch(B, N, seed=7)
-    xyz = pts[:, :, :3].contiguous().to(dev)
-    feats = pts[:, :, 3:].contiguous().to(dev)
-    start = torch.zeros(B, dtype=torch.int32, device=dev)
-    C, K, r = 1024, 32, 0.1
-    _, cent = ops.fps(xyz, C, start)
-    idx = ops.ball_query(cent, xyz, r, K)
-    D = feats.shape[2]
-    ld = (3 + D + 3) // 4 * 4
-    out = torch.empty((B * C * K, ld), device=dev)
-    from pcseg._lib import call, ptr, stream_ptr
-    s = stream_ptr(dev)
+    from pcseg.engine import KernelProbe
+    torch.cuda.synchronize(dev)
+    with KernelProbe() as kp:
+        step()
+    summ = kp.summary()
+    torch.cuda.synchronize(dev)
+    name, (n, fl, by, sec) = max(summ.items(), key=lambda kv: kv[1][3])
+    tf = fl / sec / 1e12
+    all_fl = sum(v[1] for v in summ.values())
+    all_sec = sum(v[3] for v in summ.values())
+    return {'kernel': name, 'bound': 'mfma', 'achieved': round(tf, 2), 'peak': FP32_PEAK_TFLOPS, 'unit': 'TFLOP/s',
+            'frac': round(tf / FP32_PEAK_TFLOPS, 4), 'traffic': None,
+            'launches_per_step': n, 'avg_launch_us': round(sec / n * 1e6, 2),
+            'algo_flops_per_launch': round(fl / n), 'algo_bytes_per_launch': round(by / n),
+            'achieved_hbm_gbs': round(by / sec / 1e9, 1),
+            'all_engine_gemms': {'tflops': round(all_fl / all_sec / 1e12, 2),
+                                 'ms_per_step': round(all_sec * 1e3, 3), 'launches': sum(v[0] for v in summ.values())}}
 
-    def launch():
-        call('pcs_group_fwd', ptr(xyz), ptr(feats), ptr(cent), ptr(idx), B, N, C, K, D, 0.1, 0, ptr(out), ld, s)
-    for _ in range(5):
-        launch()
-    st = torch.cuda.current_stream(dev)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    reps = 50
-    e0.record(st)
-    for _ in range(reps):
-        launch()
-    e1.record(st)
-    e1.synchronize()
-    ms = e0.elapsed_time(e1) / reps
-    # algorithmic bytes: write the grouped rows, read their indices, read the cloud
-    # (xyz+feats once) and the centroids once.
-    M = B * C * K
-    algo = M * ld * 4 + M * 4 + B * N * (3 + D) * 4 + B * C * 3 * 4
-    gbs = algo / (ms * 1e-3) / 1e9
-    return {'kernel': 'group_fwd_kernel (SA1 gather: B=%d C=%d K=%d D=%d)' % (B, C, K, D), 'bound': 'hbm',
-            'achieved': round(gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': round(gbs / HBM_PEAK_GBS, 4),
-            'traffic': None, 'avg_launch_us': round(ms * 1e3, 2), 'algo_bytes_per_launch': algo}
+
+def step_roofline(args, ms):
+    """Whole-step fraction of the fp32 MFMA roofline with the reference algorithm's flop count."""
+    gf = ALGO_GFLOP_PER_SAMPLE.get((args.model, args.npoints))
+    if gf is None:
+        return None
+    tf = gf * args.batch / (ms * 1e-3) / 1e3
+    return {'algo_gflop_per_sample': gf, 'achieved_tflops_per_gpu': round(tf, 2),
+            'frac_of_fp32_peak': round(tf / FP32_PEAK_TFLOPS, 4)}
 
 
 # ----------------------------------------------------------------------------- main bench
@@ -157,6 +154,8 @@ def main():
     ap.add_argument('--cpu-threads', type=int, default=0)
     ap.add_argument('--cpu-baseline-worker', action='store_true')
     ap.add_argument('--no-roofline', action='store_true')
+    ap.add_argument('--no-prefetch', action='store_true',
+                    help='do not enqueue the next step\'s FPS/ball-query/3-NN before this step\'s backward')
     args = ap.parse_args()
     if args.cpu_baseline_worker:
         cpu_baseline_worker(args)
@@ -179,10 +178,10 @@ def main():
     import pcseg
     from pcseg.ddp import FlatGradAllReduce, broadcast_model
     from pcseg.synthetic import make_batch
-    from oracle.ref_ops import seeded_init_
 
     name, ctor, kind = MODELS[args.model]
-    model = seeded_init_(ctor(pcseg), 0).to(dev).train()
+    torch.manual_seed(0)
+    model = ctor(pcseg).to(dev).train()     # PyTorch default init (random weights)
     broadcast_model(model)
     grads = FlatGradAllReduce(model)
     opt = torch.optim.Adam(model.parameters(), lr=1e-3)
@@ -191,9 +190,15 @@ def main():
     lab = (labels.float() if kind == 'chfirst6' else labels).to(dev)
     lengths = lengths.to(dev)
 
+    prefetch = hasattr(model, 'prefetch_geometry') and not args.no_prefetch
+
     def step():
         grads.zero_grad()
         loss = pcseg.masked_onehot_cross_entropy(logits_of(model(x)), lab, lengths)
+        if prefetch:
+            # pipelined input: the next batch's neighbour search (here the same resident
+            # blocks, fresh FPS starts) runs on the side stream under this backward
+            model.prefetch_geometry(x)
         loss.backward()
         grads.synchronize()
         opt.step()
@@ -218,8 +223,8 @@ def main():
     if not torch.isfinite(loss):
         raise RuntimeError('non-finite loss')
     roof = None
-    if rank == 0 and not args.no_roofline and args.model in ('pointnetpp', 'pointnetpp_msg', 'pointnext'):
-        roof = kernel_roofline(args, dev)
+    if not args.no_roofline:
+        roof = kernel_roofline(step, dev)     # every rank runs the step (collectives), rank 0 reports
     if rank == 0:
         ms = dt / args.steps * 1e3
         value = world * args.batch * args.npoints * args.steps / dt
@@ -232,8 +237,9 @@ def main():
             'config': {'workload': f'{name} seg, {args.npoints} pts, batch {args.batch}/GPU, fwd+CE+bwd'
                                    f'{"+allreduce" if world > 1 else ""}+Adam',
                        'model': name, 'global_batch': world * args.batch, 'npoints': args.npoints,
-                       'parallelism': f'dp{world}'},
+                       'parallelism': f'dp{world}', 'geometry_prefetch': prefetch},
             'roofline': roof,
+            'step_roofline': step_roofline(args, ms),
             'cpu_baseline': cpu_res,
         }
         print(json.dumps(res), flush=True)

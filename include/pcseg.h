@@ -28,6 +28,8 @@ extern "C" {
 
 const char* pcs_last_error(void);
 int pcs_abi_version(void);
+/* sizeof(pcs_operand), for bindings to check their struct layout */
+int pcs_operand_size(void);
 
 /* ---- neighbour search ------------------------------------------------- */
 
@@ -99,24 +101,38 @@ int pcs_edge_bwd(const float* grad_out, int ld_gout, const int32_t* idx, int B,
  * dgcnn.py:188-207.  act: 0 = ReLU, 1 = LeakyReLU(slope), 2 = identity.
  * BN partial-sum workspaces are fp64 [blocks][2][N]. */
 
+/* Operand of the engine GEMMs: row-major rows (row stride ld, multiple of 4)
+ * read through a per-channel transform applied on load, so BatchNorm-applied
+ * activations and BatchNorm-backward gradients never round-trip HBM:
+ *   PCS_OP_PLAIN   : data[r][c]
+ *   PCS_OP_BNACT   : act(data[r][c]*s[c] + t[c])              (forward BN + act)
+ *   PCS_OP_BNBWD   : s*dy - kb - alpha*(z - mean)              (BN backward, dZ)
+ *                    dy = data[r][c] * act'(z*s + t), z = Z[r][c] (row stride ldz)
+ *   PCS_OP_POOLBWD : as BNBWD with data[r][c] = arg[g][c] == k ? dpool[g][c] : 0,
+ *                    g = r / pool_k, k = r % pool_k (data/arg are G x ld)
+ * alpha = kC*invstd and kb = kB from pcs_bn_bwd_finalize; inv = invstd (epilogue). */
+enum { PCS_OP_PLAIN = 0, PCS_OP_BNACT = 1, PCS_OP_BNBWD = 2, PCS_OP_POOLBWD = 3 };
+typedef struct pcs_operand {
+    const float* data; int ld; int mode;
+    const float* s; const float* t; int act; float slope;
+    const float* z; int ldz;
+    const float* mean; const float* inv; const float* alpha; const float* kb;
+    const uint8_t* arg; int pool_k;
+} pcs_operand;
+
 /* row blocks of pcs_gemm_rows (sizes its stats/bstats workspace) */
 int pcs_gemm_row_blocks(int M, int N);
-/* C (M x N, ldc) = act_in(A*s_in + t_in) . W^T (+bias), W row-major N x K with
- * row stride ldw.  A rows have stride lda (multiple of 4).
+/* C (M x N, ldc) = T(A) . W^T (+bias), W row-major N x K with row stride ldw.
  * stats: partial (sum, sum^2) of C per channel.  bstats: fused BN-backward
- * partials (sum dy, sum dy*xhat) of the layer whose pre-BN output is zp
- * (dy = C * act'(zp*sp+tp), xhat = (zp-meanp)*invp). */
-int pcs_gemm_rows(const float* A, int lda, int M, int K, const float* s_in,
-                  const float* t_in, int act_in, float slope_in, const float* W,
-                  int ldw, const float* bias, float* C, int ldc,
-                  int N, double* stats, const float* zp, int ldzp,
-                  const float* sp, const float* tp, const float* meanp,
-                  const float* invp, int actp, float slopep, double* bstats,
-                  void* stream);
-/* dW (N x K) += X^T . act(Y*s+t) over M rows (s,t nullable = identity);
- * db (N, nullable) += column sums of X.   (accumulating) */
-int pcs_wgrad(const float* X, int ldx, int N, const float* Y, int ldy, int K,
-              const float* s, const float* t, int act, float slope, int M,
+ * partials (sum dy, sum dy*xhat) of the layer whose pre-BN output is epi->z
+ * (dy = C * act'(z*s+t), xhat = (z-mean)*inv; epi's s/t/mean/inv/act/slope). */
+int pcs_gemm_rows(const pcs_operand* a, int M, int K, const float* W, int ldw,
+                  const float* bias, float* C, int ldc, int N, double* stats,
+                  const pcs_operand* epi, double* bstats, void* stream);
+/* dW (N x K) += T(X)^T . T(Y) over M rows; db (N, nullable) += column sums of
+ * T(X).  X: PLAIN/BNBWD/POOLBWD (the layer's dZ), Y: PLAIN/BNACT (its input).
+ * (accumulating) */
+int pcs_wgrad(const pcs_operand* x, int N, const pcs_operand* y, int K, int M,
               float* dW, float* db, void* stream);
 /* BN forward finalize: partials -> scale s, shift t, mean, invstd; running
  * mean/var updated with `momentum` and the unbiased variance (nullable). */
@@ -125,20 +141,18 @@ int pcs_bn_finalize(const double* part, int nb, int N, long long M,
                     float momentum, float* run_mean, float* run_var, float* s,
                     float* t, float* mean, float* invstd, void* stream);
 /* BN backward finalize: partials -> dgamma, dbeta (written, or added when
- * accum != 0), kB = s*sum_dy/M, kC = s*sum(dy*xhat)/M
+ * accum != 0), kB = s*sum_dy/M, kC = s*sum(dy*xhat)/M (* invstd[c] when
+ * invstd is given: the `alpha` of PCS_OP_BNBWD)
  * (dZ = s*dy - kB - kC*xhat). */
 int pcs_bn_bwd_finalize(const double* part, int nb, int N, long long M,
-                        const float* s, float* dgamma, float* dbeta, float* kB,
-                        float* kC, int accum, void* stream);
+                        const float* s, const float* invstd, float* dgamma,
+                        float* dbeta, float* kB, float* kC, int accum,
+                        void* stream);
 int pcs_bn_bwd_reduce_blocks(int M);
 int pcs_bn_bwd_reduce(const float* dA, int ldd, const float* Z, int ldz, int M,
                       int N, const float* s, const float* t, const float* mean,
                       const float* inv, int act, float slope, double* part,
                       void* stream);
-int pcs_bn_bwd_dz(const float* dA, int ldd, const float* Z, int ldz, int M,
-                  int N, const float* s, const float* t, const float* mean,
-                  const float* inv, const float* kB, const float* kC, int act,
-                  float slope, float* dZ, void* stream);
 /* common.py:211-212 / dgcnn.py:76: pooled (G x N) = max_k act(Z*s+t), first
  * argmax (u8); Z rows are (g*K + k). */
 int pcs_pool_fwd(const float* Z, int N, long long G, int K, const float* s,
@@ -149,11 +163,6 @@ int pcs_pool_bwd_reduce(const float* dpool, const uint8_t* arg, const float* Z,
                         int N, long long G, int K, const float* s,
                         const float* t, const float* mean, const float* inv,
                         int act, float slope, double* part, void* stream);
-int pcs_pool_bwd_dz(const float* dpool, const uint8_t* arg, const float* Z,
-                    int N, long long G, int K, const float* s, const float* t,
-                    const float* mean, const float* inv, const float* kB,
-                    const float* kC, int act, float slope, float* dZ,
-                    void* stream);
 /* out (M x N, ldo) = act(Z*s + t) */
 int pcs_bn_act(const float* Z, int ldz, int M, int N, const float* s,
                const float* t, int act, float slope, float* out, int ldo,

@@ -6,7 +6,9 @@ sys.path[:0] = [os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                 os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                              '3d-semantic-segmentation-benchmark_amd')]
 import torch  # noqa: E402
-from pcseg._lib import call, ptr, stream_ptr  # noqa: E402
+from pcseg._lib import stream_ptr, OP_BNACT, OP_BNBWD  # noqa: E402
+from pcseg.engine import operand, gemm_rows, wgrad  # noqa: E402
+from pcseg._lib import load  # noqa: E402
 
 dev = 'cuda'
 SHAPES = [  # (name, M, K, N)
@@ -40,15 +42,19 @@ for name, M, K, N in SHAPES:
     t = torch.randn(K, device=dev) * 0.1
     b = torch.randn(N, device=dev)
     C = torch.empty(M, N, device=dev)
-    part = torch.empty((M + 127) // 128, 2, N, dtype=torch.float64, device=dev)
-    fwd = lambda: call('pcs_gemm_rows', ptr(A), lda, M, K, ptr(s), ptr(t), 0, 0.0, ptr(W), K, ptr(b), ptr(C), N, N,  # noqa
-                       ptr(part), None, 0, None, None, None, None, 0, 0.0, None, st)
+    part = torch.empty(load().pcs_gemm_row_blocks(M, N), 2, N, dtype=torch.float64, device=dev)
+    aop = operand(A, lda, OP_BNACT, s, t, 0, 0.0)
+    fwd = lambda: gemm_rows(aop, M, K, W, K, b, C, N, N, part, st=st)  # noqa
     ms = timeit(fwd)
     fl = 2.0 * M * K * N
     by = 4.0 * M * (lda + N)
     dW = torch.zeros(N, K, device=dev)
     db = torch.zeros(N, device=dev)
-    wg = lambda: call('pcs_wgrad', ptr(C), N, N, ptr(A), lda, K, ptr(s), ptr(t), 0, 0.0, M, ptr(dW), ptr(db), st)  # noqa
+    Z = torch.randn(M, N, device=dev)
+    sN, tN = torch.rand(N, device=dev) + 0.5, torch.randn(N, device=dev) * 0.1
+    mN, aN, kN = torch.randn(N, device=dev), torch.randn(N, device=dev) * 1e-3, torch.randn(N, device=dev) * 1e-3
+    xop = operand(C, N, OP_BNBWD, sN, tN, 0, 0.0, Z, N, mN, None, aN, kN)
+    wg = lambda: wgrad(xop, N, aop, K, M, dW, db, st)  # noqa
     ms2 = timeit(wg)
     print(f'{name:8s} M={M:8d} K={K:5d} N={N:5d}  fwd {ms*1e3:8.1f} us {fl/ms/1e9:6.1f} TF/s {by/ms/1e6:6.0f} GB/s'
           f' | wgrad {ms2*1e3:8.1f} us {fl/ms2/1e9:6.1f} TF/s', flush=True)

@@ -32,7 +32,17 @@ def test_library_exports_every_header_symbol():
         assert hasattr(lib, s), s
     # every typed binding corresponds to a header declaration and vice versa
     assert set(_lib.SIGNATURES) | {'pcs_last_error', 'pcs_abi_version'} == set(syms)
-    assert lib.pcs_abi_version() == 1
+    assert lib.pcs_abi_version() == 2
+    assert lib.pcs_operand_size() == ctypes.sizeof(_lib.Operand)
+
+
+def test_binding_arity_matches_header():
+    txt = re.sub(r'/\*.*?\*/', '', open(HEADER).read(), flags=re.S)
+    for name, params in re.findall(r'\b(pcs_[a-z0-9_]+)\s*\(([^)]*)\)\s*;', txt):
+        params = params.strip()
+        n = 0 if params in ('', 'void') else params.count(',') + 1
+        if name in _lib.SIGNATURES:
+            assert len(_lib.SIGNATURES[name]) == n, name
 
 
 def test_nm_exports_are_c_abi():

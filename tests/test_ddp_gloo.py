@@ -1,0 +1,169 @@
+"""Multi-process data-parallel path on the CPU (gloo, world size 2).
+
+SURVEY.md section 8(e): blocks are independent, the one exchange is the gradient
+all-reduce; BN statistics stay local per rank.  The check: after
+`FlatGradAllReduce.synchronize()` every rank holds the mean over ranks of the
+gradients each rank computes on its own shard with plain autograd (the
+reference algorithm, oracle model, local BN), and `broadcast_model` makes
+rank 1 start from rank 0's weights.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import REPO  # noqa: F401  (sets sys.path)
+from oracle import ref_ops as R
+from pcseg.ddp import FlatGradAllReduce, broadcast_model
+from pcseg.synthetic import make_batch
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def _dropout_off(m):
+    for mod in m.modules():
+        if isinstance(mod, torch.nn.Dropout):
+            mod.eval()
+
+
+def _step(model, x, lab, lengths, starts):
+    with R.replay(R.Replay(fps_starts=starts)):
+        loss = R.masked_onehot_cross_entropy(model(x), lab, lengths)
+    loss.backward()
+
+
+def _worker(rank, world, port, bucket_bytes, overlap, out):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    torch.set_num_threads(1)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        # rank-dependent init: broadcast_model must overwrite rank 1's weights
+        model = R.seeded_init_(R.PointNetpp(14), 10 + rank)
+        model.train()
+        _dropout_off(model)
+        broadcast_model(model)
+        ref = R.seeded_init_(R.PointNetpp(14), 10)
+        for (k, a), (_, b) in zip(model.state_dict().items(), ref.state_dict().items()):
+            assert torch.equal(a, b), k
+        pts, labels, lengths = make_batch(1, 1024, seed=500 + rank)
+        starts = [torch.tensor([3 * rank + i], dtype=torch.int32) for i in range(4)]
+
+        # local gradients with plain autograd on this rank's shard
+        ref.train()
+        _dropout_off(ref)
+        _step(ref, pts, labels, lengths, starts)
+        local = torch.cat([p.grad.reshape(-1) for p in ref.parameters()])
+        gathered = [torch.empty_like(local) for _ in range(world)]
+        dist.all_gather(gathered, local)
+        expect = torch.stack(gathered).mean(0)
+
+        # the data-parallel path: flat buffer, bucketed all-reduce from backward hooks
+        grads = FlatGradAllReduce(model, bucket_bytes=bucket_bytes, overlap=overlap)
+        for _ in range(2):                     # twice: zero_grad must reset the buckets
+            grads.zero_grad()
+            _step(model, pts, labels, lengths, starts)
+            grads.synchronize()
+            got = torch.cat([p.grad.reshape(-1) for p in model.parameters()])
+            err = float((got - expect).abs().max())
+            out[rank] = err
+            assert err <= 1e-6 * float(expect.abs().max()) + 1e-9, err
+            # the result is identical on both ranks
+            other = [torch.empty_like(got) for _ in range(world)]
+            dist.all_gather(other, got)
+            assert torch.equal(other[0], other[1])
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('bucket_bytes,overlap', [(256 << 10, True), (64 << 20, True), (1 << 20, False)])
+def test_flat_grad_allreduce_world2(bucket_bytes, overlap):
+    world = 2
+    ctx = mp.get_context('spawn')
+    out = ctx.Manager().dict()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, bucket_bytes, overlap, out)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    assert len(out) == world
+
+
+def test_bucket_layout_covers_every_parameter_once():
+    model = R.PointNetpp(14)
+    g = FlatGradAllReduce(model, bucket_bytes=128 << 10, overlap=False)
+    seen = [p for _, _, ps in g.buckets for p in ps]
+    assert len(seen) == len(g.params) and len({id(p) for p in seen}) == len(seen)
+    # buckets tile the flat buffer contiguously, last layers first
+    ends = [0] + [e for _, e, _ in g.buckets]
+    assert [s for s, _, _ in g.buckets] == ends[:-1] and ends[-1] == g.flat.numel()
+    assert g.buckets[0][2][0] is g.params[-1]
+    for p in g.params:
+        assert p.grad.data_ptr() >= g.flat.data_ptr()
+
+
+def _gpu_worker(rank, world, port, out):
+    """Product model on cuda:0 in both ranks, gloo over the GPU tensors: exercises the
+    engine's in-place gradient writes + `_pcs_grad_ready` bucket hooks."""
+    import pcseg
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        dev = torch.device('cuda', 0)
+        sd = R.seeded_init_(R.PointNetpp(14), 10).state_dict()
+        models = []
+        for _ in range(2):
+            m = pcseg.PointNetpp(14)
+            m.load_state_dict(sd)
+            m = m.to(dev).train()
+            _dropout_off(m)
+            models.append(m)
+        ref, model = models
+        pts, labels, lengths = make_batch(2, 4096, seed=700 + rank)
+        x, lab, ln = pts.to(dev), labels.to(dev), lengths.to(dev)
+
+        def step(m):
+            torch.manual_seed(rank)
+            loss = pcseg.masked_onehot_cross_entropy(m(x), lab, ln)
+            loss.backward()
+        step(ref)
+        local = torch.cat([p.grad.reshape(-1) for p in ref.parameters()])
+        gathered = [torch.empty_like(local) for _ in range(world)]
+        dist.all_gather(gathered, local)
+        expect = torch.stack(gathered).mean(0)
+        grads = FlatGradAllReduce(model, bucket_bytes=256 << 10, overlap=True)
+        grads.zero_grad()
+        step(model)
+        grads.synchronize()
+        got = torch.cat([p.grad.reshape(-1) for p in model.parameters()])
+        rel = float((got - expect).norm() / expect.norm())
+        out[rank] = rel
+        assert rel < 1e-5, rel                 # fp32 atomics make wgrad order run-dependent
+        assert all(h is not None for h in grads._handles) or not grads._handles
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_flat_grad_allreduce_world2_engine_on_gpu():
+    world = 2
+    ctx = mp.get_context('spawn')
+    out = ctx.Manager().dict()
+    port = _free_port()
+    procs = [ctx.Process(target=_gpu_worker, args=(r, world, port, out)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=600)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    assert len(out) == world

@@ -231,3 +231,27 @@ def test_msg_and_dgcnn_xyz_train_step():
         loss.backward()
         opt.step()
         assert torch.isfinite(loss)
+
+
+@pytest.mark.parametrize('ctor', [lambda: pcseg.PointNetpp(14), lambda: pcseg.PointNeXt(14),
+                                  lambda: pcseg.PointNetppMSG(14)])
+def test_prefetched_geometry_matches_inline(ctor):
+    """prefetch_geometry(x) on the side stream, then forward(x), must give the same
+    logits as computing the geometry inside forward with the same FPS start draws."""
+    torch.manual_seed(0)
+    model = ctor().to(DEV).train()
+    dropout_off(model)
+    pts, _, _ = make_batch(2, 4096, seed=31)
+    x = pts.to(DEV)
+    torch.manual_seed(5)
+    inline = model(x).detach().clone()
+    torch.manual_seed(5)
+    model.prefetch_geometry(x)
+    pre = model(x).detach()
+    assert torch.equal(inline, pre)
+    # a prefetched plan for a different tensor is not used
+    torch.manual_seed(6)
+    model.prefetch_geometry(x.clone())
+    torch.manual_seed(5)
+    again = model(x).detach()
+    assert torch.equal(inline, again)
