@@ -27,16 +27,14 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 enum { ACT_RELU = 0, ACT_LRELU = 1, ACT_NONE = 2 };
 
-__device__ __forceinline__ float act_f(float y, int act, float slope) {
-    if (act == ACT_RELU) return y > 0.f ? y : 0.f;
-    if (act == ACT_LRELU) return y > 0.f ? y : y * slope;
-    return y;
-}
+// The activation is folded into one slope at the ABI boundary (eff_slope): ReLU = 0,
+// LeakyReLU = its slope, identity = 1; both functions are branch-free selects.
 // derivative as autograd computes it: relu -> (result > 0); leaky_relu -> (input > 0 ? 1 : slope)
-__device__ __forceinline__ float dact_f(float y, int act, float slope) {
-    if (act == ACT_RELU) return y > 0.f ? 1.f : 0.f;
-    if (act == ACT_LRELU) return y > 0.f ? 1.f : slope;
-    return 1.f;
+__device__ __forceinline__ float act_f(float y, int, float slope) { return y > 0.f ? y : y * slope; }
+__device__ __forceinline__ float dact_f(float y, int, float slope) { return y > 0.f ? 1.f : slope; }
+
+static inline float eff_slope(int act, float slope) {
+    return act == ACT_RELU ? 0.f : act == ACT_LRELU ? slope : 1.f;
 }
 
 // Operand descriptor (layout-identical to pcs_operand in include/pcseg.h).  The
@@ -61,32 +59,31 @@ struct Quad {
     float4 s, t, mean, alpha, kb;
 };
 
+// transform modes require K % 4 == 0 (checked at the ABI), so a channel quad is all in or all
+// out.  Loads use clamped (always in-bounds) addresses and selects instead of branches, so
+// the compiler keeps the next slab's loads in flight under the current slab's MFMAs.
 template <int MODE>
 __device__ __forceinline__ void load_quad(const Operand& o, int c, int K, Quad& q) {
-    auto get = [&](const float* p, int j, float dflt) { return c + j < K ? p[c + j] : dflt; };
+    const int cc = c < K ? c : 0;          // the out-of-range quad is zeroed in xform4
     if (MODE >= OP_BNACT) {
-        q.s = make_float4(get(o.s, 0, 0.f), get(o.s, 1, 0.f), get(o.s, 2, 0.f), get(o.s, 3, 0.f));
-        q.t = make_float4(get(o.t, 0, 0.f), get(o.t, 1, 0.f), get(o.t, 2, 0.f), get(o.t, 3, 0.f));
+        q.s = *reinterpret_cast<const float4*>(o.s + cc);
+        q.t = *reinterpret_cast<const float4*>(o.t + cc);
     }
     if (MODE >= OP_BNBWD) {
-        q.mean = make_float4(get(o.mean, 0, 0.f), get(o.mean, 1, 0.f), get(o.mean, 2, 0.f), get(o.mean, 3, 0.f));
-        q.alpha = make_float4(get(o.alpha, 0, 0.f), get(o.alpha, 1, 0.f), get(o.alpha, 2, 0.f),
-                              get(o.alpha, 3, 0.f));
-        q.kb = make_float4(get(o.kb, 0, 0.f), get(o.kb, 1, 0.f), get(o.kb, 2, 0.f), get(o.kb, 3, 0.f));
+        q.mean = *reinterpret_cast<const float4*>(o.mean + cc);
+        q.alpha = *reinterpret_cast<const float4*>(o.alpha + cc);
+        q.kb = *reinterpret_cast<const float4*>(o.kb + cc);
     }
 }
 
-// raw global loads of one float4 (row r, channels c..c+3); z only for BNBWD/POOLBWD
+// raw global loads of one float4 at (row r, channels c..c+3); r and c must be in bounds
+// (callers clamp).  POOLBWD: v = dpool[g][c..], a = the 4 argmax bytes; z only for BNBWD/POOLBWD.
 template <int MODE>
-__device__ __forceinline__ void load_raw(const Operand& o, int r, int c, float4& v, float4& z) {
+__device__ __forceinline__ void load_raw(const Operand& o, int r, int c, float4& v, float4& z, unsigned& a) {
     if (MODE == OP_POOLBWD) {
-        const int g = r / o.pool_k, k = r - g * o.pool_k;
-        const float4 d = *reinterpret_cast<const float4*>(o.data + (size_t)g * o.ld + c);
-        const uchar4 a = *reinterpret_cast<const uchar4*>(o.arg + (size_t)g * o.ld + c);
-        v.x = a.x == k ? d.x : 0.f;
-        v.y = a.y == k ? d.y : 0.f;
-        v.z = a.z == k ? d.z : 0.f;
-        v.w = a.w == k ? d.w : 0.f;
+        const int g = r / o.pool_k;
+        v = *reinterpret_cast<const float4*>(o.data + (size_t)g * o.ld + c);
+        a = *reinterpret_cast<const unsigned*>(o.arg + (size_t)g * o.ld + c);
     } else {
         v = *reinterpret_cast<const float4*>(o.data + (size_t)r * o.ld + c);
     }
@@ -104,15 +101,32 @@ __device__ __forceinline__ float xform1(const Operand& o, float v, float z, floa
     return v;
 }
 
-// transformed float4; channels >= K give 0
+// transformed float4 of row r: channels at or beyond K give 0 (per element for PLAIN,
+// whose K need not be a multiple of 4); POOLBWD keeps dpool only where argmax == r % pool_k
 template <int MODE>
-__device__ __forceinline__ float4 xform4(const Operand& o, float4 v, float4 z, const Quad& q, int c, int K) {
-    float4 r;
-    r.x = c + 0 < K ? xform1<MODE>(o, v.x, z.x, q.s.x, q.t.x, q.mean.x, q.alpha.x, q.kb.x) : 0.f;
-    r.y = c + 1 < K ? xform1<MODE>(o, v.y, z.y, q.s.y, q.t.y, q.mean.y, q.alpha.y, q.kb.y) : 0.f;
-    r.z = c + 2 < K ? xform1<MODE>(o, v.z, z.z, q.s.z, q.t.z, q.mean.z, q.alpha.z, q.kb.z) : 0.f;
-    r.w = c + 3 < K ? xform1<MODE>(o, v.w, z.w, q.s.w, q.t.w, q.mean.w, q.alpha.w, q.kb.w) : 0.f;
-    return r;
+__device__ __forceinline__ float4 xform4(const Operand& o, float4 v, float4 z, unsigned a, int r, const Quad& q,
+                                         int c, int K) {
+    if (MODE == OP_PLAIN) {
+        v.x = c + 0 < K ? v.x : 0.f;
+        v.y = c + 1 < K ? v.y : 0.f;
+        v.z = c + 2 < K ? v.z : 0.f;
+        v.w = c + 3 < K ? v.w : 0.f;
+        return v;
+    }
+    if (MODE == OP_POOLBWD) {
+        const unsigned k = (unsigned)(r - (r / o.pool_k) * o.pool_k);
+        v.x = (a & 0xffu) == k ? v.x : 0.f;
+        v.y = ((a >> 8) & 0xffu) == k ? v.y : 0.f;
+        v.z = ((a >> 16) & 0xffu) == k ? v.z : 0.f;
+        v.w = (a >> 24) == k ? v.w : 0.f;
+    }
+    float4 out;
+    out.x = xform1<MODE>(o, v.x, z.x, q.s.x, q.t.x, q.mean.x, q.alpha.x, q.kb.x);
+    out.y = xform1<MODE>(o, v.y, z.y, q.s.y, q.t.y, q.mean.y, q.alpha.y, q.kb.y);
+    out.z = xform1<MODE>(o, v.z, z.z, q.s.z, q.t.z, q.mean.z, q.alpha.z, q.kb.z);
+    out.w = xform1<MODE>(o, v.w, z.w, q.s.w, q.t.w, q.mean.w, q.alpha.w, q.kb.w);
+    const bool in = c < K;
+    return in ? out : make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
 struct GemmArgs {
@@ -147,6 +161,7 @@ __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(GemmArgs g) {
     constexpr int TM = WTM / 32, TN = WTN / 32;
     constexpr int AV = BM * GBK / 4 / 256;
     constexpr int BV = (BN * GBK / 4 + 255) / 256;
+    constexpr bool kBFull = (BN * GBK / 4) % 256 == 0;     // every thread owns BV whole B quads
     static_assert(WM * WN == 4 && TM >= 1 && TN >= 1 && AV >= 1, "tile");
     __shared__ __attribute__((aligned(16))) float As[2][BM][GLDK];
     __shared__ __attribute__((aligned(16))) float Bs[2][BN][GLDK];
@@ -156,7 +171,6 @@ __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(GemmArgs g) {
     const int wm = wave / WN, wn = wave % WN;
     const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
     const int h = lane >> 5, l32 = lane & 31;
-    const bool wvec = (g.ldw & 3) == 0;
 
     f32x16 acc[TM][TN];
 #pragma unroll
@@ -167,38 +181,26 @@ __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(GemmArgs g) {
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
     float4 ra[AV], rz[AV], rb[BV];
+    unsigned rg[AV];
     // every A float4 of this thread sits at the same k offset 4*(tid&7) of a slab, so one
     // coefficient quad per slab serves all of them
     Quad q;
+    const int lda_last = g.a.ld - 4, ldw_last = g.ldw - 4;
     auto gload = [&](int k0) {
         const int gk = k0 + 4 * (tid & 7);
+        const int gkc = min(gk, lda_last);
         load_quad<AM>(g.a, gk, g.K, q);
 #pragma unroll
         for (int it = 0; it < AV; ++it) {
-            const int r = (it * 256 + tid) >> 3;
-            const int gr = m0 + r;
-            float4 v = make_float4(0.f, 0.f, 0.f, 0.f), z = v;
-            if (gr < g.M && gk < g.K) load_raw<AM>(g.a, gr, gk, v, z);
-            ra[it] = v;
-            rz[it] = z;
+            const int gr = min(m0 + ((it * 256 + tid) >> 3), g.M - 1);
+            load_raw<AM>(g.a, gr, gkc, ra[it], rz[it], rg[it]);
         }
 #pragma unroll
         for (int it = 0; it < BV; ++it) {
             const int e = it * 256 + tid;
-            const int n = e >> 3, c4 = e & 7;
-            const int gn = n0 + n, gk2 = k0 + 4 * c4;
-            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (e < BN * GBK / 4 && gn < g.N && gk2 < g.K) {
-                const float* w = g.W + (size_t)gn * g.ldw + gk2;
-                if (wvec && gk2 + 3 < g.K) v = *reinterpret_cast<const float4*>(w);
-                else {
-                    v.x = w[0];
-                    v.y = gk2 + 1 < g.K ? w[1] : 0.f;
-                    v.z = gk2 + 2 < g.K ? w[2] : 0.f;
-                    v.w = gk2 + 3 < g.K ? w[3] : 0.f;
-                }
-            }
-            rb[it] = v;
+            const int gn = min(n0 + (e >> 3), g.N - 1);
+            const int gk2 = min(k0 + 4 * (e & 7), ldw_last);
+            if (kBFull || e < BN * GBK / 4) rb[it] = *reinterpret_cast<const float4*>(g.W + (size_t)gn * g.ldw + gk2);
         }
     };
     auto sstore = [&](int buf, int k0) {
@@ -206,12 +208,19 @@ __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(GemmArgs g) {
 #pragma unroll
         for (int it = 0; it < AV; ++it) {
             const int r = (it * 256 + tid) >> 3;
-            *reinterpret_cast<float4*>(&As[buf][r][4 * (tid & 7)]) = xform4<AM>(g.a, ra[it], rz[it], q, gk, g.K);
+            *reinterpret_cast<float4*>(&As[buf][r][4 * (tid & 7)]) =
+                xform4<AM>(g.a, ra[it], rz[it], rg[it], m0 + r, q, gk, g.K);
         }
 #pragma unroll
         for (int it = 0; it < BV; ++it) {
             const int e = it * 256 + tid;
-            if (e < BN * GBK / 4) *reinterpret_cast<float4*>(&Bs[buf][e >> 3][4 * (e & 7)]) = rb[it];
+            const int gk2 = k0 + 4 * (e & 7);
+            float4 v = rb[it];
+            v.x = gk2 + 0 < g.K ? v.x : 0.f;
+            v.y = gk2 + 1 < g.K ? v.y : 0.f;
+            v.z = gk2 + 2 < g.K ? v.z : 0.f;
+            v.w = gk2 + 3 < g.K ? v.w : 0.f;
+            if (kBFull || e < BN * GBK / 4) *reinterpret_cast<float4*>(&Bs[buf][e >> 3][4 * (e & 7)]) = v;
         }
     };
 
@@ -221,7 +230,10 @@ __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(GemmArgs g) {
     __syncthreads();
     for (int ks = 0; ks < nk; ++ks) {
         const int buf = ks & 1;
-        if (ks + 1 < nk) gload((ks + 1) * GBK);
+        gload((ks + 1) * GBK);    // unconditional (clamped past the end): no phi copies of in-flight registers
+        // keep the next slab's loads in flight: nothing that consumes them may be
+        // scheduled above the MFMAs of this slab
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int qq = 0; qq < 4; ++qq) {
             float4 a[TM], b[TN];
@@ -241,6 +253,7 @@ __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(GemmArgs g) {
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].w, b[j].w, acc[i][j], 0, 0, 0);
                 }
         }
+        __builtin_amdgcn_sched_barrier(0);
         if (ks + 1 < nk) sstore(buf ^ 1, (ks + 1) * GBK);
         __syncthreads();
     }
@@ -350,30 +363,26 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(Operand xo, int N, Operan
             for (int r = 0; r < 16; ++r) { acc[i][j][r] = 0.f; tot[i][j][r] = 0.f; }
 
     float4 rx[XV], rxz[XV], ry[YV], ryz[YV];
+    unsigned rxa[XV], rya[YV];
+    const int gnc = min(gn, xo.ld - 4), gkc = min(gk, yo.ld - 4);
     auto gload = [&](int r0) {
 #pragma unroll
         for (int it = 0; it < XV; ++it) {
-            const int gr = r0 + (it * 256 + tid) / (BO / 4);
-            float4 v = make_float4(0.f, 0.f, 0.f, 0.f), z = v;
-            if (gr < re && gn < N) load_raw<XM>(xo, gr, gn, v, z);
-            rx[it] = v;
-            rxz[it] = z;
+            const int gr = min(r0 + (it * 256 + tid) / (BO / 4), M - 1);
+            load_raw<XM>(xo, gr, gnc, rx[it], rxz[it], rxa[it]);
         }
 #pragma unroll
         for (int it = 0; it < YV; ++it) {
-            const int gr = r0 + (it * 256 + tid) / (BI / 4);
-            float4 v = make_float4(0.f, 0.f, 0.f, 0.f), z = v;
-            if (gr < re && gk < K) load_raw<YM>(yo, gr, gk, v, z);
-            ry[it] = v;
-            ryz[it] = z;
+            const int gr = min(r0 + (it * 256 + tid) / (BI / 4), M - 1);
+            load_raw<YM>(yo, gr, gkc, ry[it], ryz[it], rya[it]);
         }
     };
     auto sstore = [&](int buf, int r0) {
 #pragma unroll
         for (int it = 0; it < XV; ++it) {
             const int r = (it * 256 + tid) / (BO / 4);
-            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (r0 + r < re) v = xform4<XM>(xo, rx[it], rxz[it], qx, gn, N);
+            float4 v = xform4<XM>(xo, rx[it], rxz[it], rxa[it], r0 + r, qx, gn, N);
+            if (r0 + r >= re) v = make_float4(0.f, 0.f, 0.f, 0.f);
             Xs[buf][4 * xc4 + 0][r] = v.x;
             Xs[buf][4 * xc4 + 1][r] = v.y;
             Xs[buf][4 * xc4 + 2][r] = v.z;
@@ -383,8 +392,8 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(Operand xo, int N, Operan
 #pragma unroll
         for (int it = 0; it < YV; ++it) {
             const int r = (it * 256 + tid) / (BI / 4);
-            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (r0 + r < re) v = xform4<YM>(yo, ry[it], ryz[it], qy, gk, K);
+            float4 v = xform4<YM>(yo, ry[it], ryz[it], rya[it], r0 + r, qy, gk, K);
+            if (r0 + r >= re) v = make_float4(0.f, 0.f, 0.f, 0.f);
             Ys[buf][4 * yc4 + 0][r] = v.x;
             Ys[buf][4 * yc4 + 1][r] = v.y;
             Ys[buf][4 * yc4 + 2][r] = v.z;
@@ -400,7 +409,8 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(Operand xo, int N, Operan
     __syncthreads();
     for (int sl = 0; sl < nslab; ++sl) {
         const int buf = sl & 1;
-        if (sl + 1 < nslab) gload(rb + (sl + 1) * BR);
+        gload(rb + (sl + 1) * BR);    // unconditional (clamped past the end), see gemm_rows_kernel
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             float4 a[TM], b[TN];
@@ -428,6 +438,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(Operand xo, int N, Operan
 #pragma unroll
                     for (int r = 0; r < 16; ++r) { tot[i][j][r] += acc[i][j][r]; acc[i][j][r] = 0.f; }
         }
+        __builtin_amdgcn_sched_barrier(0);
         if (sl + 1 < nslab) sstore(buf ^ 1, rb + (sl + 1) * BR);
         __syncthreads();
     }
@@ -763,7 +774,8 @@ static int check_operand(const pcs_operand* o, int K, const char* who, const cha
     PCS_CHECK_ARG(o->mode >= PCS_OP_PLAIN && o->mode <= PCS_OP_POOLBWD, "%s: %s mode %d", who, which, o->mode);
     PCS_CHECK_ARG(o->ld % 4 == 0 && o->ld >= K, "%s: %s ld=%d must be a multiple of 4 and >= %d", who, which, o->ld,
                   K);
-    PCS_CHECK_ARG(o->mode < PCS_OP_BNACT || (o->s && o->t), "%s: %s needs s/t", who, which);
+    PCS_CHECK_ARG(o->mode < PCS_OP_BNACT || (o->s && o->t && K % 4 == 0),
+                  "%s: %s needs s/t and K %% 4 == 0 (K=%d)", who, which, K);
     PCS_CHECK_ARG(o->mode < PCS_OP_BNBWD || (o->z && o->ldz % 4 == 0 && o->ldz >= K && o->mean && o->alpha && o->kb),
                   "%s: %s needs z/ldz/mean/alpha/kb", who, which);
     PCS_CHECK_ARG(o->mode != PCS_OP_POOLBWD || (o->arg && o->pool_k >= 1 && o->pool_k <= 256),
@@ -775,7 +787,7 @@ static Operand to_dev(const pcs_operand* o) {
     Operand r{};
     if (!o) return r;
     r.data = o->data; r.ld = o->ld; r.mode = o->mode;
-    r.s = o->s; r.t = o->t; r.act = o->act; r.slope = o->slope;
+    r.s = o->s; r.t = o->t; r.act = o->act; r.slope = eff_slope(o->act, o->slope);
     r.z = o->z; r.ldz = o->ldz;
     r.mean = o->mean; r.inv = o->inv; r.alpha = o->alpha; r.kb = o->kb;
     r.arg = o->arg; r.pool_k = o->pool_k;
@@ -794,7 +806,7 @@ PCS_API int pcs_gemm_rows(const pcs_operand* a, int M, int K, const float* W, in
     PCS_CHECK_ARG(!(stats && bstats), "pcs_gemm_rows: stats and bstats are exclusive");
     PCS_CHECK_ARG(!bstats || (epi && epi->z && epi->s && epi->t && epi->mean && epi->inv),
                   "pcs_gemm_rows: bstats needs epi z/s/t/mean/inv");
-    PCS_CHECK_ARG(ldw >= K, "pcs_gemm_rows: ldw=%d < K=%d", ldw, K);
+    PCS_CHECK_ARG(ldw >= K && ldw % 4 == 0, "pcs_gemm_rows: ldw=%d must be a multiple of 4 and >= K=%d", ldw, K);
     if (M == 0) return 0;
     GemmArgs g{to_dev(a), M, K, W, ldw, bias, C, ldc, N, stats, to_dev(epi), bstats};
     hipStream_t s = as_stream(stream);
@@ -867,7 +879,7 @@ PCS_API int pcs_bn_bwd_reduce(const float* dA, int ldd, const float* Z, int ldz,
     const int nq = N / 4;
     const dim3 grid((M + kRedRows - 1) / kRedRows, (nq + 255) / 256);
     hipLaunchKernelGGL(bn_bwd_reduce_kernel, grid, dim3(256), 2 * 256 * 4 * sizeof(double), as_stream(stream), dA, ldd,
-                       Z, ldz, M, N, s, t, mean, inv, act, slope, kRedRows, part);
+                       Z, ldz, M, N, s, t, mean, inv, act, eff_slope(act, slope), kRedRows, part);
     return launch_status("pcs_bn_bwd_reduce");
 }
 
@@ -878,7 +890,7 @@ PCS_API int pcs_pool_fwd(const float* Z, int N, long long G, int K, const float*
     PCS_CHECK_ARG(G * K * (long long)N < (1ll << 40) && total < (1ll << 31), "pcs_pool_fwd: too many elements");
     if (total == 0) return 0;
     hipLaunchKernelGGL(pool_fwd_kernel, dim3(ew_grid(total)), dim3(256), 0, as_stream(stream), Z, N / 4, (int)G, K, s,
-                       t, act, slope, out, arg);
+                       t, act, eff_slope(act, slope), out, arg);
     return launch_status("pcs_pool_fwd");
 }
 
@@ -891,7 +903,7 @@ PCS_API int pcs_pool_bwd_reduce(const float* dpool, const uint8_t* arg, const fl
     const int gpb = 64;
     const dim3 grid((unsigned)((G + gpb - 1) / gpb), (N + 63) / 64);
     hipLaunchKernelGGL(pool_bwd_reduce_kernel, grid, dim3(256), 0, as_stream(stream), dpool, arg, Z, N, (int)G, K, s,
-                       t, mean, inv, act, slope, gpb, part);
+                       t, mean, inv, act, eff_slope(act, slope), gpb, part);
     return launch_status("pcs_pool_bwd_reduce");
 }
 
@@ -902,6 +914,6 @@ PCS_API int pcs_bn_act(const float* Z, int ldz, int M, int N, const float* s, co
     PCS_CHECK_ARG(total < (1ll << 31), "pcs_bn_act: too many elements");
     if (total == 0) return 0;
     hipLaunchKernelGGL(bn_act_kernel, dim3(ew_grid(total)), dim3(256), 0, as_stream(stream), Z, ldz, (int)total, N / 4,
-                       s, t, act, slope, out, ldo);
+                       s, t, act, eff_slope(act, slope), out, ldo);
     return launch_status("pcs_bn_act");
 }

@@ -9,11 +9,11 @@ include/pcseg.h).
 from .common import (sample, group, reduce, interpolate, MiniPointNet, UnitPointNet, SetAbstraction,
                      FeaturePropagation, InvResMLP)
 from .models import (PointNetpp, PointNetppMSG, PointNeXt, EdgeConv, DGCNN, DGCNNWithColor, get_model, get_loss,
-                     TNet, PointNetEncoder, PointNetSeg)
+                     TNet, PointNetEncoder, PointNetSeg, knn, get_graph_feature)
 from .loss import masked_onehot_cross_entropy
 from .replay import Replay, replay
 
 __all__ = ['sample', 'group', 'reduce', 'interpolate', 'MiniPointNet', 'UnitPointNet', 'SetAbstraction',
            'FeaturePropagation', 'InvResMLP', 'PointNetpp', 'PointNetppMSG', 'PointNeXt', 'EdgeConv', 'DGCNN',
            'DGCNNWithColor', 'get_model', 'get_loss', 'TNet', 'PointNetEncoder', 'PointNetSeg',
-           'masked_onehot_cross_entropy', 'Replay', 'replay']
+           'masked_onehot_cross_entropy', 'Replay', 'replay', 'knn', 'get_graph_feature']

@@ -326,3 +326,61 @@ def shared_mlp(x_rows: torch.Tensor, kin: int, convs, bns, act: str = 'relu', sl
     for conv, bn in zip(convs, bns):
         params += [conv.weight, conv.bias, bn.weight, bn.bias]
     return SharedMLPFn.apply(x_rows, kin, pool_k, act, float(slope), list(bns), *params)
+
+
+class RowLinearFn(torch.autograd.Function):
+    """A bare 1x1 convolution (no BN) on rows, e.g. the segmentation heads
+    (PointNetpp.py:25,45 `self.conv`, dgcnn.py:210 `conv8`): out = X W^T + b on the
+    engine GEMM; backward = one dgrad GEMM + one wgrad."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        dev = x.device
+        M, K = x.shape
+        N = weight.shape[0]
+        Wm = weight.reshape(N, -1)
+        if Wm.shape[1] != K or K % 4:
+            raise ValueError(f'row linear: x has {K} channels, weight expects {Wm.shape[1]} (need a multiple of 4)')
+        Wm = Wm.contiguous()
+        out = _f32((M, N), dev)
+        gemm_rows(operand(x, K), M, K, Wm, K, bias, out, N, N, st=stream_ptr(dev))
+        ctx.save_for_backward(x, Wm)
+        ctx.has_bias = bias is not None
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        x, Wm = ctx.saved_tensors
+        dev = gout.device
+        st = stream_ptr(dev)
+        M, K = x.shape
+        N = Wm.shape[0]
+        N4 = ld4(N)
+        if N4 == N and gout.is_contiguous():
+            gp = gout
+        else:                                   # pad the class dimension to a 16-B row stride
+            gp = torch.zeros((M, N4), dtype=torch.float32, device=dev)
+            gp[:, :N] = gout
+        gop = operand(gp, N4)
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            Wt = torch.zeros((K, N4), dtype=torch.float32, device=dev)     # dgrad B[k=n][n=cin] = Wt[cin][n]
+            Wt[:, :N] = Wm.t()
+            dx = _f32((M, K), dev)
+            gemm_rows(gop, M, N, Wt, N4, None, dx, K, K, st=st)
+        if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
+            dwp = torch.zeros((N4, K), dtype=torch.float32, device=dev)
+            dbp = torch.zeros((N4,), dtype=torch.float32, device=dev) if ctx.has_bias else None
+            wgrad(gop, N4, operand(x, K), K, M, dwp, dbp, st)
+            dw = dwp[:N]
+            db = dbp[:N] if dbp is not None else None
+        return dx, dw, db
+
+
+def linear_rows(x: torch.Tensor, conv) -> torch.Tensor:
+    """x (M, Cin) -> (M, Cout) for a 1x1 Conv1d/Conv2d holder, on the engine GEMM."""
+    if not x.is_cuda:
+        raise RuntimeError('pcseg ops run only on the GPU (no CPU fallback); got a CPU tensor')
+    x = x.contiguous()
+    out = RowLinearFn.apply(x, conv.weight.reshape(conv.weight.shape[0], -1), conv.bias)
+    return out

@@ -18,12 +18,12 @@ import torch.nn.functional as F
 from . import ops
 from .common import SetAbstraction, FeaturePropagation, InvResMLP, UnitPointNet, GeometryPlan, GeometryPrefetch
 from .mlp import conv_rows, bn_rows
-from .engine import shared_mlp, pad_rows
+from .engine import shared_mlp, pad_rows, linear_rows
 from .replay import active as _replay
 
 
 def _head_rows(x_rows: torch.Tensor, drop: nn.Module, conv: nn.Module) -> torch.Tensor:
-    return conv_rows(drop(x_rows), conv)
+    return linear_rows(drop(x_rows), conv)
 
 
 class PointNetpp(GeometryPrefetch, nn.Module):
@@ -198,6 +198,29 @@ def _seq_rows(x_rows: torch.Tensor, seq: nn.Sequential, kin: int | None = None) 
     return y
 
 
+def knn(x: torch.Tensor, k: int) -> torch.Tensor:
+    """Reference `knn` (dgcnn.py:7-21): x (B, F, N) -> idx (B, N, k) int64, k largest of
+    -|xi|^2 + 2 xi.xj - |xj|^2 (self included).  HIP kernel: F in {3, 64}."""
+    return ops.knn(x.transpose(1, 2).contiguous(), k).long()
+
+
+def get_graph_feature(x: torch.Tensor, k: int = 20, idx: torch.Tensor | None = None,
+                      dim9: bool = False) -> torch.Tensor:
+    """Reference `get_graph_feature` (dgcnn.py:24-57): x (B, C, N) ->
+    (B, 2C, N, k) = [x_j - x_i, x_i] (dim9: [x_j - x_i, x_i, x_i], kNN on channels 6:)."""
+    B, N = x.size(0), x.size(2)
+    xp = x.reshape(B, -1, N).transpose(1, 2).contiguous()          # (B, N, C)
+    C = xp.shape[2]
+    if idx is None:
+        idx = ops.knn(xp[:, :, 6:].contiguous() if dim9 else xp, k)
+    k = idx.shape[2]
+    rows = ops.edge_rows(xp, idx.to(device=xp.device, dtype=torch.int32).contiguous())
+    feat = rows[:, :2 * C]
+    if dim9:
+        feat = torch.cat((feat, rows[:, C:2 * C]), dim=1)
+    return feat.reshape(B, N, k, -1).permute(0, 3, 1, 2).contiguous()
+
+
 class EdgeConv(nn.Module):
     """Reference dgcnn.py:60-77.  forward takes/returns the reference's (B, C, N) layout."""
 
@@ -234,7 +257,7 @@ def _dgcnn_head(self, parts: list[torch.Tensor], B: int, N: int):
     x5 = _seq_rows(xr, self.conv5)                      # (B*N, emb)
     x6 = _seq_rows(torch.cat((xr, x5), dim=1), self.conv6)
     x7 = _seq_rows(x6, self.conv7)
-    logits = conv_rows(x7, self.conv8).view(B, N, -1)
+    logits = linear_rows(x7, self.conv8).view(B, N, -1)
     # the reference returns x5 as a contiguous (B, emb, N); a transposed view of
     # the point-major tensor has the same shape and values without a 0.5 GB copy
     return logits, x5.view(B, N, -1).transpose(1, 2), None

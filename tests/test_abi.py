@@ -112,3 +112,12 @@ def test_loss_matches_oracle_on_cpu(golden):
 def test_reduce_rejects_unknown_pooling():
     with pytest.raises(ValueError):
         pcseg.reduce(torch.zeros(1, 2, 3, 4), 'sum')
+
+
+@pytest.mark.parametrize('name', ['sample', 'group', 'reduce', 'interpolate', 'knn', 'get_graph_feature',
+                                  'masked_onehot_cross_entropy'])
+def test_functional_signatures_match_reference(name):
+    a = inspect.signature(getattr(pcseg, name))
+    b = inspect.signature(getattr(R, name))
+    assert [(p.name, p.default) for p in a.parameters.values()] == \
+        [(p.name, p.default) for p in b.parameters.values()]

@@ -200,3 +200,23 @@ def test_dgcnn_knn_agrees_with_oracle(F_, seed):
     kth_got = d.gather(2, got).max(-1).values
     assert torch.allclose(kth_got, kth_ref, rtol=1e-4, atol=1e-5)
     assert (got[..., 0] == torch.arange(N)).float().mean() > 0.99   # self first
+
+
+@pytest.mark.parametrize('dim9', [False, True])
+def test_functional_get_graph_feature_and_knn(dim9):
+    """pcseg.get_graph_feature / pcseg.knn: the reference's functional API (dgcnn.py:7-57)."""
+    B, C, N, k = 2, 9 if dim9 else 3, 1024, 20
+    g = torch.Generator().manual_seed(21)
+    x = torch.randn(B, C, N, generator=g)
+    src = x[:, 6:] if dim9 else x
+    idx = R.knn(src, k)
+    ref = R.get_graph_feature(x, k=k, idx=idx, dim9=dim9)
+    got = pcseg.get_graph_feature(x.to(DEV), k=k, idx=idx.to(DEV), dim9=dim9)
+    assert got.shape == ref.shape and got.is_contiguous()
+    assert torch.equal(got.cpu(), ref)
+    kn = pcseg.knn(src.to(DEV), k)
+    assert kn.dtype == torch.int64 and kn.shape == (B, N, k)
+    same = (kn.cpu().sort(-1).values == idx.sort(-1).values).all(-1)
+    assert same.float().mean() > 0.99
+    # without idx: our own graph, same shape
+    assert pcseg.get_graph_feature(x.to(DEV), k=k, dim9=dim9).shape == ref.shape
