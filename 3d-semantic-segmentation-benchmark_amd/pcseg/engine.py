@@ -166,11 +166,10 @@ class SharedMLPFn(torch.autograd.Function):
     """rows X (M, ld) with Kin logical channels -> pooled (M/pool_K, C_L) or activation (M, C_L)."""
 
     @staticmethod
-    def forward(ctx, X, Kin, pool_K, act, slope, bns, *params):
+    def forward(ctx, X, Kin, pool_K, acts, bns, *params):
         dev = X.device
         st = stream_ptr(dev)
         M, lda = X.shape
-        a_code = ACT[act]
         A, lda_cur, K_cur, s_prev, t_prev = X, lda, Kin, None, None
         Zs, stats = [], []
         nl = len(bns)
@@ -179,13 +178,17 @@ class SharedMLPFn(torch.autograd.Function):
             bn = bns[li]
             Cout = W.shape[0]
             Wm = W.reshape(Cout, -1)
-            if not Wm.is_contiguous():
+            if Wm.shape[1] % 4:                 # 16-B weight rows (the pad columns are zero)
+                Wp = torch.zeros((Cout, ld4(Wm.shape[1])), dtype=torch.float32, device=dev)
+                Wp[:, :Wm.shape[1]] = Wm
+                Wm = Wp
+            elif not Wm.is_contiguous():
                 Wm = Wm.contiguous()
             if Cout % 4:
                 raise ValueError(f'engine: layer width {Cout} must be a multiple of 4')
             Z = _f32((M, Cout), dev)
             a_op = operand(A, lda_cur) if s_prev is None else \
-                operand(A, lda_cur, OP_BNACT, s_prev, t_prev, a_code, slope)
+                operand(A, lda_cur, OP_BNACT, s_prev, t_prev, *acts[li - 1])
             use_batch = bn.training or bn.running_mean is None
             s, t, mean, inv = (_f32((Cout,), dev) for _ in range(4))
             if use_batch:
@@ -216,21 +219,21 @@ class SharedMLPFn(torch.autograd.Function):
             G = M // pool_K
             out = _f32((G, CL), dev)
             arg = torch.empty((G, CL), dtype=torch.uint8, device=dev)
-            call('pcs_pool_fwd', ptr(Zs[-1]), CL, G, pool_K, ptr(s), ptr(t), a_code, slope, ptr(out), ptr(arg), st)
+            call('pcs_pool_fwd', ptr(Zs[-1]), CL, G, pool_K, ptr(s), ptr(t), *acts[-1], ptr(out), ptr(arg), st)
             ctx.mark_non_differentiable(arg)
         else:
             out = _f32((M, CL), dev)
             arg = None
-            call('pcs_bn_act', ptr(Zs[-1]), CL, M, CL, ptr(s), ptr(t), a_code, slope, ptr(out), CL, st)
+            call('pcs_bn_act', ptr(Zs[-1]), CL, M, CL, ptr(s), ptr(t), *acts[-1], ptr(out), CL, st)
         ctx.save_for_backward(X, *Zs, *[x for st_ in stats for x in st_[:4]], *(p for p in params if p is not None),
                               *([arg] if arg is not None else []))
-        ctx.meta = (Kin, pool_K, a_code, slope, nl, [st_[4] for st_ in stats],
+        ctx.meta = (Kin, pool_K, acts, nl, [st_[4] for st_ in stats],
                     [p is not None for p in params], arg is not None)
         return out
 
     @staticmethod
     def backward(ctx, gout):
-        Kin, pool_K, a_code, slope, nl, use_batch, present, has_arg = ctx.meta
+        Kin, pool_K, acts, nl, use_batch, present, has_arg = ctx.meta
         saved = list(ctx.saved_tensors)
         X = saved[0]
         Zs = saved[1:1 + nl]
@@ -257,12 +260,12 @@ class SharedMLPFn(torch.autograd.Function):
             nb = lib.pcs_pool_bwd_reduce_blocks(G)
             part = _f64((nb, 2, CL), dev)
             call('pcs_pool_bwd_reduce', ptr(gout), ptr(arg), ptr(Zs[-1]), CL, G, pool_K, ptr(s), ptr(t), ptr(mean),
-                 ptr(inv), a_code, slope, ptr(part), st)
+                 ptr(inv), *acts[-1], ptr(part), st)
         else:
             nb = lib.pcs_bn_bwd_reduce_blocks(M)
             part = _f64((nb, 2, CL), dev)
             call('pcs_bn_bwd_reduce', ptr(gout), CL, ptr(Zs[-1]), CL, M, CL, ptr(s), ptr(t), ptr(mean), ptr(inv),
-                 a_code, slope, ptr(part), st)
+                 *acts[-1], ptr(part), st)
         kB, alpha = _f32((CL,), dev), _f32((CL,), dev)
         gg, gb = grad_target(params[4 * (nl - 1) + 2]), grad_target(params[4 * (nl - 1) + 3])
         call('pcs_bn_bwd_finalize', ptr(part), nb, CL, M, ptr(s), ptr(inv), ptr(gg), ptr(gb), ptr(kB), ptr(alpha), 1,
@@ -272,9 +275,9 @@ class SharedMLPFn(torch.autograd.Function):
             alpha.zero_()
         # dZ of the top layer is never materialised: its consumers rebuild it on load
         if pool_K:
-            xop = operand(gout, CL, OP_POOLBWD, s, t, a_code, slope, Zs[-1], CL, mean, None, alpha, kB, arg, pool_K)
+            xop = operand(gout, CL, OP_POOLBWD, s, t, *acts[-1], Zs[-1], CL, mean, None, alpha, kB, arg, pool_K)
         else:
-            xop = operand(gout, CL, OP_BNBWD, s, t, a_code, slope, Zs[-1], CL, mean, None, alpha, kB)
+            xop = operand(gout, CL, OP_BNBWD, s, t, *acts[-1], Zs[-1], CL, mean, None, alpha, kB)
         keep = [gout, kB, alpha]
         dX = None
         for li in range(nl - 1, -1, -1):
@@ -288,7 +291,7 @@ class SharedMLPFn(torch.autograd.Function):
             if dW is not None:
                 if li > 0:
                     sp, tp, mp, ip = stats[li - 1]
-                    yop = operand(Zs[li - 1], Cin, OP_BNACT, sp, tp, a_code, slope)
+                    yop = operand(Zs[li - 1], Cin, OP_BNACT, sp, tp, *acts[li - 1])
                     wgrad(xop, Cout, yop, Cin, M, dW, db, st)
                 else:
                     wgrad(xop, Cout, operand(X, lda), Kin, M, dW, db, st)
@@ -297,7 +300,7 @@ class SharedMLPFn(torch.autograd.Function):
                 dA = _f32((M, Cin), dev)
                 nbg = lib.pcs_gemm_row_blocks(M, Cin)
                 bpart = _f64((nbg, 2, Cin), dev)
-                epi = operand(None, 0, OP_BNBWD, sp, tp, a_code, slope, Zs[li - 1], Cin, mp, ip)
+                epi = operand(None, 0, OP_BNBWD, sp, tp, *acts[li - 1], Zs[li - 1], Cin, mp, ip)
                 gemm_rows(xop, M, Cout, Wt, Cout, None, dA, Cin, Cin, None, epi, bpart, st=st)
                 kB2, alpha2 = _f32((Cin,), dev), _f32((Cin,), dev)
                 g2, b2 = grad_target(params[4 * (li - 1) + 2]), grad_target(params[4 * (li - 1) + 3])
@@ -306,26 +309,34 @@ class SharedMLPFn(torch.autograd.Function):
                 if not use_batch[li - 1]:
                     kB2.zero_()
                     alpha2.zero_()
-                xop = operand(dA, Cin, OP_BNBWD, sp, tp, a_code, slope, Zs[li - 1], Cin, mp, None, alpha2, kB2)
+                xop = operand(dA, Cin, OP_BNBWD, sp, tp, *acts[li - 1], Zs[li - 1], Cin, mp, None, alpha2, kB2)
                 keep += [dA, kB2, alpha2]
             elif ctx.needs_input_grad[0]:
                 dX = torch.zeros((M, lda), dtype=torch.float32, device=dev) if lda != Kin else _f32((M, lda), dev)
                 gemm_rows(xop, M, Cout, Wt, Cout, None, dX, lda, Kin, st=st)
         notify_grad_ready(params)
-        return (dX, None, None, None, None, None, *grads)
+        return (dX, None, None, None, None, *grads)
 
 
-def shared_mlp(x_rows: torch.Tensor, kin: int, convs, bns, act: str = 'relu', slope: float = 0.0,
+def shared_mlp(x_rows: torch.Tensor, kin: int, convs, bns, act='relu', slope=0.0,
                pool_k: int = 0) -> torch.Tensor:
-    """Run a conv/BN/act stack on rows.  x_rows (M, ld) with `kin` logical channels, ld % 4 == 0."""
+    """Run a conv/BN/act stack on rows.  x_rows (M, ld) with `kin` logical channels, ld % 4 == 0.
+    `act` / `slope` are one value for every layer or a sequence with one per layer
+    ('relu', 'lrelu', 'none')."""
     if not x_rows.is_cuda:
         raise RuntimeError('pcseg ops run only on the GPU (no CPU fallback); got a CPU tensor')
     if x_rows.shape[1] % 4 or not x_rows.is_contiguous():
         x_rows = pad_rows(x_rows[:, :kin])
+    nl = len(convs)
+    names = [act] * nl if isinstance(act, str) else list(act)
+    slopes = [slope] * nl if isinstance(slope, (int, float)) else list(slope)
+    if len(names) != nl or len(slopes) != nl:
+        raise ValueError('shared_mlp: one act/slope per layer')
+    acts = tuple((ACT[a], float(sl)) for a, sl in zip(names, slopes))
     params = []
     for conv, bn in zip(convs, bns):
         params += [conv.weight, conv.bias, bn.weight, bn.bias]
-    return SharedMLPFn.apply(x_rows, kin, pool_k, act, float(slope), list(bns), *params)
+    return SharedMLPFn.apply(x_rows, kin, pool_k, acts, list(bns), *params)
 
 
 class RowLinearFn(torch.autograd.Function):

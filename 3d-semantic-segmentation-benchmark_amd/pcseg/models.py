@@ -17,7 +17,6 @@ import torch.nn.functional as F
 
 from . import ops
 from .common import SetAbstraction, FeaturePropagation, InvResMLP, UnitPointNet, GeometryPlan, GeometryPrefetch
-from .mlp import conv_rows, bn_rows
 from .engine import shared_mlp, pad_rows, linear_rows
 from .replay import active as _replay
 
@@ -364,10 +363,8 @@ class TNet(nn.Module):
     def forward_points(self, xp):
         """xp (B, N, k) point-major."""
         B, N, _ = xp.shape
-        r = xp.reshape(B * N, -1)
-        r = F.relu(bn_rows(conv_rows(r, self.conv1), self.bn1))
-        r = F.relu(bn_rows(conv_rows(r, self.conv2), self.bn2))
-        r = F.relu(bn_rows(conv_rows(r, self.conv3), self.bn3))
+        r = pad_rows(xp.reshape(B * N, -1))
+        r = shared_mlp(r, self.k, [self.conv1, self.conv2, self.conv3], [self.bn1, self.bn2, self.bn3], 'relu')
         g = r.view(B, N, -1).max(dim=1)[0]
         g = F.relu(self.bn4(self.fc1(g)))
         g = F.relu(self.bn5(self.fc2(g)))
@@ -399,14 +396,14 @@ class PointNetEncoder(nn.Module):
         B, N, _ = xp.shape
         trans = self.stn.forward_points(xp)
         xp = torch.bmm(xp, trans)
-        r = F.relu(bn_rows(conv_rows(xp.reshape(B * N, -1), self.conv1), self.bn1))
+        r = shared_mlp(pad_rows(xp.reshape(B * N, -1)), xp.shape[2], [self.conv1], [self.bn1], 'relu')
         trans_feat = None
         if self.feature_transform:
             trans_feat = self.fstn.forward_points(r.view(B, N, -1))
             r = torch.bmm(r.view(B, N, -1), trans_feat).reshape(B * N, -1)
         pf = r.view(B, N, -1)
-        r = F.relu(bn_rows(conv_rows(r, self.conv2), self.bn2))
-        r = bn_rows(conv_rows(r, self.conv3), self.bn3)
+        # conv2 -> BN -> ReLU -> conv3 -> BN (no activation, PointNet.py:82-83) in one engine stack
+        r = shared_mlp(r, 64, [self.conv2, self.conv3], [self.bn2, self.bn3], ('relu', 'none'))
         g = r.view(B, N, -1).max(dim=1)[0]
         if self.global_feat:
             return g, trans, trans_feat
@@ -438,9 +435,7 @@ class PointNetSeg(nn.Module):
         B, N, _ = x.shape
         feat, _, _ = self.feat.forward_points(x)
         r = feat.reshape(B * N, -1)
-        r = F.relu(bn_rows(conv_rows(r, self.conv1), self.bn1))
-        r = F.relu(bn_rows(conv_rows(r, self.conv2), self.bn2))
-        r = F.relu(bn_rows(conv_rows(r, self.conv3), self.bn3))
-        r = conv_rows(r, self.conv4).view(B, N, -1)
+        r = shared_mlp(r, r.shape[1], [self.conv1, self.conv2, self.conv3], [self.bn1, self.bn2, self.bn3], 'relu')
+        r = linear_rows(r, self.conv4).view(B, N, -1)
         e = torch.exp(r)
         return e / torch.sum(e, keepdim=True, dim=-1)

@@ -104,7 +104,21 @@ def run_cpu_baseline(args):
 
 
 # ----------------------------------------------------------------------------- roofline of the dominant kernel
-def kernel_roofline(step, dev):
+def pmc_traffic(kernel, args):
+    """HBM bytes per launch of `kernel` from the committed PMC summary of this workload
+    (scripts/gpu_pmc.sh -> profiles/<round>_pmc_<model>.json; FETCH_SIZE x2 + WRITE_SIZE)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, 'profiles', f'*_pmc_{args.model}_b{args.batch}_n{args.npoints}.json')))
+    if not files:
+        return None, None
+    table = json.load(open(files[-1]))
+    for k, v in table.items():
+        if kernel in k:
+            return round(v['hbm_bytes_per_launch']), os.path.relpath(files[-1], REPO)
+    return None, None
+
+
+def kernel_roofline(step, dev, args):
     """Run one more training step with every engine GEMM launch bracketed by HIP
     events on its own stream (pcseg.engine.KernelProbe); the dominant kernel is
     the variant with the largest summed time.  achieved = its algorithmic flops
@@ -118,10 +132,12 @@ def kernel_roofline(step, dev):
     torch.cuda.synchronize(dev)
     name, (n, fl, by, sec) = max(summ.items(), key=lambda kv: kv[1][3])
     tf = fl / sec / 1e12
+    traffic, src = pmc_traffic(name, args)
     all_fl = sum(v[1] for v in summ.values())
     all_sec = sum(v[3] for v in summ.values())
     return {'kernel': name, 'bound': 'mfma', 'achieved': round(tf, 2), 'peak': FP32_PEAK_TFLOPS, 'unit': 'TFLOP/s',
-            'frac': round(tf / FP32_PEAK_TFLOPS, 4), 'traffic': None,
+            'frac': round(tf / FP32_PEAK_TFLOPS, 4), 'traffic': traffic, 'traffic_unit': 'bytes/launch',
+            'traffic_source': src,
             'launches_per_step': n, 'avg_launch_us': round(sec / n * 1e6, 2),
             'algo_flops_per_launch': round(fl / n), 'algo_bytes_per_launch': round(by / n),
             'achieved_hbm_gbs': round(by / sec / 1e9, 1),
@@ -212,6 +228,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step()
+    t_host = time.perf_counter() - t0          # host enqueue time (the step has no host sync)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -224,7 +241,7 @@ def main():
         raise RuntimeError('non-finite loss')
     roof = None
     if not args.no_roofline:
-        roof = kernel_roofline(step, dev)     # every rank runs the step (collectives), rank 0 reports
+        roof = kernel_roofline(step, dev, args)     # every rank runs the step (collectives), rank 0 reports
     if rank == 0:
         ms = dt / args.steps * 1e3
         value = world * args.batch * args.npoints * args.steps / dt
@@ -238,6 +255,7 @@ def main():
                                    f'{"+allreduce" if world > 1 else ""}+Adam',
                        'model': name, 'global_batch': world * args.batch, 'npoints': args.npoints,
                        'parallelism': f'dp{world}', 'geometry_prefetch': prefetch},
+            'host_enqueue_ms_per_step': round(t_host / args.steps * 1e3, 3),
             'roofline': roof,
             'step_roofline': step_roofline(args, ms),
             'cpu_baseline': cpu_res,

@@ -121,3 +121,26 @@ def test_functional_signatures_match_reference(name):
     b = inspect.signature(getattr(R, name))
     assert [(p.name, p.default) for p in a.parameters.values()] == \
         [(p.name, p.default) for p in b.parameters.values()]
+
+
+def test_engine_abi_argument_checks_without_gpu():
+    """The C ABI validates operands before any launch (host-only paths)."""
+    lib = _lib.load()
+    fake = 0x1000                       # never dereferenced: every call below fails its checks first
+    op = _lib.Operand(fake, 12, _lib.OP_PLAIN, None, None, 0, 0.0, None, 0, None, None, None, None, None, 0)
+    # weight rows must be 16-B aligned
+    assert lib.pcs_gemm_rows(op, 8, 9, fake, 9, None, fake, 32, 32, None, None, None, None) != 0
+    assert b'ldw' in lib.pcs_last_error()
+    # transform modes need K % 4 == 0 and their coefficient vectors
+    bad = _lib.Operand(fake, 12, _lib.OP_BNACT, None, None, 0, 0.0, None, 0, None, None, None, None, None, 0)
+    assert lib.pcs_gemm_rows(bad, 8, 8, fake, 8, None, fake, 32, 32, None, None, None, None) != 0
+    assert b'needs s/t' in lib.pcs_last_error()
+    bad = _lib.Operand(fake, 12, 7, None, None, 0, 0.0, None, 0, None, None, None, None, None, 0)
+    assert lib.pcs_gemm_rows(bad, 8, 8, fake, 8, None, fake, 32, 32, None, None, None, None) != 0
+    assert b'mode' in lib.pcs_last_error()
+    # pooled-backward operands need the argmax and 1 <= pool_k <= 256
+    pb = _lib.Operand(fake, 32, _lib.OP_POOLBWD, fake, fake, 0, 0.0, fake, 32, fake, None, fake, fake, None, 0)
+    assert lib.pcs_wgrad(pb, 32, op, 12, 64, fake, None, None) != 0
+    assert b'pool_k' in lib.pcs_last_error()
+    # the wgrad Y operand cannot be a backward transform
+    assert lib.pcs_wgrad(op, 32, pb, 32, 64, fake, None, None) != 0
