@@ -134,11 +134,11 @@ struct GemmArgs {
     const float* W; int ldw;                   // B[k][n] = W[n*ldw + k]
     const float* bias;                         // per n (or null)
     float* C; int ldc; int N;                  // output rows (M x N)
-    double* stats;                             // [gridDim.x][2][N]: sum, sum of squares of C (or null)
+    double* stats;                             // [2][N][gridDim.x]: sum, sum of squares of C (or null)
     // fused BN-backward reduce of the layer whose OUTPUT space C lives in (dgrad epilogue):
     // uses e.z (its pre-BN Z, M x N), e.s, e.t, e.mean, e.inv, e.act, e.slope
     Operand e;
-    double* bstats;                            // [gridDim.x][2][N]: sum dy, sum dy*xhat (or null)
+    double* bstats;                            // [2][N][gridDim.x]: sum dy, sum dy*xhat (or null)
 };
 
 // ------------------------------------------------------------------ row GEMM
@@ -310,8 +310,8 @@ __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(GemmArgs g) {
                 double a = 0.0, b = 0.0;
 #pragma unroll
                 for (int w = 0; w < WM; ++w) { a += red[0][w][c]; b += red[1][w][c]; }
-                out[((size_t)blockIdx.x * 2 + 0) * g.N + col] = a;
-                out[((size_t)blockIdx.x * 2 + 1) * g.N + col] = b;
+                out[(size_t)col * gridDim.x + blockIdx.x] = a;
+                out[((size_t)g.N + col) * gridDim.x + blockIdx.x] = b;
             }
         }
     }
@@ -481,8 +481,8 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const double* __restri
     const int n = blockIdx.x;
     double a = 0.0, b = 0.0;
     for (int i = threadIdx.x; i < nb; i += 256) {
-        a += part[((size_t)i * 2 + 0) * N + n];
-        b += part[((size_t)i * 2 + 1) * N + n];
+        a += part[(size_t)n * nb + i];
+        b += part[((size_t)N + n) * nb + i];
     }
     r1[threadIdx.x] = a;
     r2[threadIdx.x] = b;
@@ -527,8 +527,8 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const double* __re
     const int n = blockIdx.x;
     double a = 0.0, b = 0.0;
     for (int i = threadIdx.x; i < nb; i += 256) {
-        a += part[((size_t)i * 2 + 0) * N + n];
-        b += part[((size_t)i * 2 + 1) * N + n];
+        a += part[(size_t)n * nb + i];
+        b += part[((size_t)N + n) * nb + i];
     }
     r1[threadIdx.x] = a;
     r2[threadIdx.x] = b;
@@ -614,8 +614,8 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restr
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            part[((size_t)blockIdx.x * 2 + 0) * N + c + j] = a[j];
-            part[((size_t)blockIdx.x * 2 + 1) * N + c + j] = b[j];
+            part[(size_t)(c + j) * gridDim.x + blockIdx.x] = a[j];
+            part[((size_t)N + c + j) * gridDim.x + blockIdx.x] = b[j];
         }
     }
 }
@@ -685,8 +685,8 @@ __global__ __launch_bounds__(256) void pool_bwd_reduce_kernel(const float* __res
     r2[ph][lane] = b;
     __syncthreads();
     if (ph == 0 && col < N) {
-        part[((size_t)blockIdx.x * 2 + 0) * N + col] = r1[0][lane] + r1[1][lane] + r1[2][lane] + r1[3][lane];
-        part[((size_t)blockIdx.x * 2 + 1) * N + col] = r2[0][lane] + r2[1][lane] + r2[2][lane] + r2[3][lane];
+        part[(size_t)col * gridDim.x + blockIdx.x] = r1[0][lane] + r1[1][lane] + r1[2][lane] + r1[3][lane];
+        part[((size_t)N + col) * gridDim.x + blockIdx.x] = r2[0][lane] + r2[1][lane] + r2[2][lane] + r2[3][lane];
     }
 }
 
@@ -795,9 +795,9 @@ static Operand to_dev(const pcs_operand* o) {
 }
 
 // C = T(A) . W^T (+bias), W row-major N x K (row stride ldw).
-// stats (nullable): [row_blocks][2][N] fp64 partial (sum, sumsq) of C.
+// stats (nullable): [2][N][row_blocks] fp64 partial (sum, sumsq) of C.
 // bstats (nullable): fused BN-backward partials of the layer whose pre-BN output is epi->z (same shape as C):
-//   [row_blocks][2][N] of (sum dy, sum dy*xhat), dy = C * act'(z*s+t), xhat = (z-mean)*inv.
+//   [2][N][row_blocks] of (sum dy, sum dy*xhat), dy = C * act'(z*s+t), xhat = (z-mean)*inv.
 PCS_API int pcs_gemm_rows(const pcs_operand* a, int M, int K, const float* W, int ldw, const float* bias, float* C,
                           int ldc, int N, double* stats, const pcs_operand* epi, double* bstats, void* stream) {
     PCS_CHECK_ARG(M >= 0 && K >= 1 && N >= 1, "pcs_gemm_rows: bad sizes M=%d K=%d N=%d", M, K, N);
@@ -848,7 +848,7 @@ PCS_API int pcs_wgrad(const pcs_operand* x, int N, const pcs_operand* y, int K, 
     return launch_status("pcs_wgrad");
 }
 
-// BN forward finalize: part [nb][2][N] -> s, t, mean, invstd; running stats updated in place (nullable).
+// BN forward finalize: part [2][N][nb] -> s, t, mean, invstd; running stats updated in place (nullable).
 PCS_API int pcs_bn_finalize(const double* part, int nb, int N, long long M, const float* gamma, const float* beta,
                             float eps, float momentum, float* run_mean, float* run_var, float* s, float* t,
                             float* mean, float* invstd, void* stream) {
@@ -858,7 +858,7 @@ PCS_API int pcs_bn_finalize(const double* part, int nb, int N, long long M, cons
     return launch_status("pcs_bn_finalize");
 }
 
-// BN backward finalize: part [nb][2][N] of (sum dy, sum dy*xhat) -> dgamma, dbeta (+= when accum), kB, kC.
+// BN backward finalize: part [2][N][nb] of (sum dy, sum dy*xhat) -> dgamma, dbeta (+= when accum), kB, kC.
 PCS_API int pcs_bn_bwd_finalize(const double* part, int nb, int N, long long M, const float* s, const float* invstd,
                                 float* dgamma, float* dbeta, float* kB, float* kC, int accum, void* stream) {
     PCS_CHECK_ARG(nb >= 1 && N >= 1 && M >= 1, "pcs_bn_bwd_finalize: bad sizes");

@@ -193,7 +193,7 @@ class SharedMLPFn(torch.autograd.Function):
             s, t, mean, inv = (_f32((Cout,), dev) for _ in range(4))
             if use_batch:
                 nb = load().pcs_gemm_row_blocks(M, Cout)
-                part = _f64((nb, 2, Cout), dev)
+                part = _f64((2, Cout, nb), dev)
                 gemm_rows(a_op, M, K_cur, Wm, Wm.shape[1], b, Z, Cout, Cout, part, st=st)
                 momentum = 0.0
                 rm = rv = None
@@ -258,12 +258,12 @@ class SharedMLPFn(torch.autograd.Function):
         if pool_K:
             G = M // pool_K
             nb = lib.pcs_pool_bwd_reduce_blocks(G)
-            part = _f64((nb, 2, CL), dev)
+            part = _f64((2, CL, nb), dev)
             call('pcs_pool_bwd_reduce', ptr(gout), ptr(arg), ptr(Zs[-1]), CL, G, pool_K, ptr(s), ptr(t), ptr(mean),
                  ptr(inv), *acts[-1], ptr(part), st)
         else:
             nb = lib.pcs_bn_bwd_reduce_blocks(M)
-            part = _f64((nb, 2, CL), dev)
+            part = _f64((2, CL, nb), dev)
             call('pcs_bn_bwd_reduce', ptr(gout), CL, ptr(Zs[-1]), CL, M, CL, ptr(s), ptr(t), ptr(mean), ptr(inv),
                  *acts[-1], ptr(part), st)
         kB, alpha = _f32((CL,), dev), _f32((CL,), dev)
@@ -299,7 +299,7 @@ class SharedMLPFn(torch.autograd.Function):
                 sp, tp, mp, ip = stats[li - 1]
                 dA = _f32((M, Cin), dev)
                 nbg = lib.pcs_gemm_row_blocks(M, Cin)
-                bpart = _f64((nbg, 2, Cin), dev)
+                bpart = _f64((2, Cin, nbg), dev)
                 epi = operand(None, 0, OP_BNBWD, sp, tp, *acts[li - 1], Zs[li - 1], Cin, mp, ip)
                 gemm_rows(xop, M, Cout, Wt, Cout, None, dA, Cin, Cin, None, epi, bpart, st=st)
                 kB2, alpha2 = _f32((Cin,), dev), _f32((Cin,), dev)

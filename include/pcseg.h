@@ -99,7 +99,8 @@ int pcs_edge_bwd(const float* grad_out, int ld_gout, const int32_t* idx, int B,
 /* ---- shared-MLP engine: 1x1 conv + training-mode BN + ReLU/LeakyReLU ------
  * models/utils/common.py:125-178 (MiniPointNet/UnitPointNet), dgcnn.py:67-76,
  * dgcnn.py:188-207.  act: 0 = ReLU, 1 = LeakyReLU(slope), 2 = identity.
- * BN partial-sum workspaces are fp64 [blocks][2][N]. */
+ * BN partial-sum workspaces are fp64 [2][N][blocks] (each channel's partials
+ * contiguous, so the finalize kernels read them coalesced). */
 
 /* Operand of the engine GEMMs: row-major rows (row stride ld, multiple of 4)
  * read through a per-channel transform applied on load, so BatchNorm-applied

@@ -42,7 +42,7 @@ for name, M, K, N in SHAPES:
     t = torch.randn(K, device=dev) * 0.1
     b = torch.randn(N, device=dev)
     C = torch.empty(M, N, device=dev)
-    part = torch.empty(load().pcs_gemm_row_blocks(M, N), 2, N, dtype=torch.float64, device=dev)
+    part = torch.empty(2, N, load().pcs_gemm_row_blocks(M, N), dtype=torch.float64, device=dev)
     aop = operand(A, lda, OP_BNACT, s, t, 0, 0.0)
     fwd = lambda: gemm_rows(aop, M, K, W, K, b, C, N, N, part, st=st)  # noqa
     ms = timeit(fwd)
