@@ -169,6 +169,20 @@ int pcs_bn_act(const float* Z, int ldz, int M, int N, const float* s,
                const float* t, int act, float slope, float* out, int ldo,
                void* stream);
 
+/* ---- loss ---------------------------------------------------------------- */
+
+/* Training/train_model.py:15-57 `masked_onehot_cross_entropy`: logits (B,L,C)
+ * rows of stride ld, one-hot targets (u8 when target_kind = 0, f32 when 1) rows
+ * of stride ldt, lengths (B) int32; loss (1 float) = mean over positions
+ * l < lengths[b] of -sum_c onehot*log_softmax (0 if none).  grad (nullable,
+ * rows of stride ld) = d loss / d logits.  partial: fp64 workspace of
+ * pcs_masked_ce_blocks(B, L) entries.  C <= 64. */
+int pcs_masked_ce_blocks(int B, int L);
+int pcs_masked_ce(const float* logits, int ld, const void* targets,
+                  int target_kind, int ldt, const int32_t* lengths, int B,
+                  int L, int C, double* partial, float* loss, float* grad,
+                  void* stream);
+
 #ifdef __cplusplus
 }
 #endif

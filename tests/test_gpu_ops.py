@@ -220,3 +220,21 @@ def test_functional_get_graph_feature_and_knn(dim9):
     assert same.float().mean() > 0.99
     # without idx: our own graph, same shape
     assert pcseg.get_graph_feature(x.to(DEV), k=k, dim9=dim9).shape == ref.shape
+
+
+def test_masked_ce_matches_reference_golden(golden):
+    """Fused HIP cross entropy vs the reference's loss + gradient (tests/golden/loss.npz)."""
+    z = golden('loss.npz')
+    logits, onehot, lengths = (torch.from_numpy(np.array(z[k])) for k in ('logits', 'onehot', 'lengths'))
+    got = pcseg.masked_onehot_cross_entropy(logits.to(DEV), onehot.to(DEV), lengths.to(DEV))
+    assert torch.allclose(got.cpu(), torch.from_numpy(z['loss']), rtol=1e-6)
+    zero = pcseg.masked_onehot_cross_entropy(logits.to(DEV), onehot.to(DEV), torch.zeros(3, dtype=torch.int64,
+                                                                                         device=DEV))
+    assert float(zero) == 0.0
+    lf = logits.to(DEV).requires_grad_(True)
+    pcseg.masked_onehot_cross_entropy(lf, onehot.float().to(DEV), lengths.to(torch.int32).to(DEV)).backward()
+    assert torch.allclose(lf.grad.cpu(), torch.from_numpy(z['grad']), rtol=1e-5, atol=1e-8)
+    # scaled upstream gradient
+    lf.grad = None
+    (3.0 * pcseg.masked_onehot_cross_entropy(lf, onehot.to(DEV), lengths.to(DEV))).backward()
+    assert torch.allclose(lf.grad.cpu(), 3.0 * torch.from_numpy(z['grad']), rtol=1e-5, atol=1e-8)
