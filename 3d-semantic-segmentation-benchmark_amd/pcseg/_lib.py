@@ -60,6 +60,8 @@ SIGNATURES = {
     'pcs_pool_bwd_reduce_blocks': [I64],
     'pcs_pool_bwd_reduce': [P, P, P, I32, I64, I32, P, P, P, P, I32, F32, P, P],
     'pcs_bn_act': [P, I32, I32, I32, P, P, I32, F32, P, I32, P],
+    # block batches
+    'pcs_gather_blocks': [P, P, P, I64, P, P, P],
     # loss
     'pcs_masked_ce_blocks': [I32, I32],
     'pcs_masked_ce': [P, I32, P, I32, I32, P, I32, I32, I32, P, P, P, P],

@@ -1,0 +1,130 @@
+"""HBM-resident S3DIS block store -- the data path in front of the hot path
+(reference data_processing/block_datasets.py).
+
+The reference loads one `.pt` file per block per step in DataLoader workers,
+samples 4096 rows on the CPU and collates on the CPU (block_datasets.py:5-31,
+:118-128).  A whole S3DIS split is a few GB, so `DeviceBlockStore` loads every
+block of the split ONCE into two device arrays -- points (P, 9) f32 and
+one-hot labels (P, 14) u8, 50 B per point -- and assembles each batch on the
+GPU: the per-block row draw has the reference's distribution (a uniformly
+random ordered subset via `randperm(n)[:S]` when n > S, `randint(n, (S,))`
+otherwise), realised with one segmented sort of random keys, and the gather +
+zero padding is one HIP kernel (`pcs_gather_blocks`).  No host work per step
+beyond a few small launches.
+
+`collate_blocks`, the block-index builder and the file format follow the
+reference exactly (same names, errors and ordering).
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+from ._lib import call, check_cuda, ptr, stream_ptr
+
+
+def collate_blocks(batch):
+    """Reference `collate_blocks` (block_datasets.py:5-31): zero-pad a list of
+    (points (n, 9), labels (n, 14)) to (B, N, 9) / (B, N, 14), lengths uint64."""
+    B = len(batch)
+    N = max(x.shape[0] for x, _ in batch)
+    pts = torch.zeros((B, N, 9), dtype=torch.float32)
+    lab = torch.zeros((B, N, 14), dtype=torch.uint8)
+    for i, (p, l) in enumerate(batch):
+        pts[i, :p.shape[0]] = p
+        lab[i, :p.shape[0]] = l
+    return pts, lab, torch.tensor([x.shape[0] for x, _ in batch], dtype=torch.uint64)
+
+
+def block_index(data_dir: str, included_areas) -> torch.Tensor:
+    """(area, room, block) uint16 triples in the reference's order
+    (BlockS3DISDataset._create_block_index, block_datasets.py:63-93)."""
+    if not os.path.exists(data_dir):
+        raise FileNotFoundError(f'Data directory "{data_dir}" does not exist.')
+    if any(a < 1 or a > 6 for a in included_areas):
+        raise ValueError(f'Included areas can only contain values from the range [1, 6], got {included_areas}.')
+    blocks = []
+    for a in sorted(included_areas):
+        d = os.path.join(data_dir, f'area_{a}')
+        if not os.path.exists(d):
+            raise FileNotFoundError(f'Directory for area {a} does not exist.')
+        names = os.listdir(d)
+        if not names:
+            raise FileNotFoundError(f'Directory for area {a} does not contain any blocks.')
+        idx = [n.replace('room', '').replace('block', '').replace('.pt', '').split('_') for n in names]
+        blocks += sorted((a, int(r), int(b)) for r, b in idx)
+    return torch.tensor(blocks, dtype=torch.uint16)
+
+
+class DeviceBlockStore:
+    """Every block of a split resident in HBM; `batch(ids)` assembles a padded,
+    sampled batch on the device (see module docstring)."""
+
+    def __init__(self, data_dir: str, included_areas, sampling: int | None = 4096, device='cuda'):
+        self.blocks = block_index(data_dir, included_areas)
+        self.sampling = sampling
+        self.device = torch.device(device)
+        pts, lab, lens = [], [], []
+        for a, r, b in self.blocks.tolist():
+            p, l = torch.load(os.path.join(data_dir, f'area_{a}', f'room{r:02d}_block{b:03d}.pt'),
+                              weights_only=True)
+            if p.ndim != 2 or p.shape[1] != 9 or l.shape != (p.shape[0], 14):
+                raise ValueError(f'block area {a} room {r} block {b}: expected (n, 9) points and (n, 14) labels')
+            pts.append(p.to(torch.float32))
+            lab.append(l.to(torch.uint8))
+            lens.append(p.shape[0])
+        self.lengths = torch.tensor(lens, dtype=torch.int64)
+        self.offsets = torch.zeros(len(lens) + 1, dtype=torch.int64)
+        self.offsets[1:] = torch.cumsum(self.lengths, 0)
+        self.points = torch.cat(pts).to(self.device)
+        self.labels = torch.cat(lab).to(self.device)
+        self._offsets_dev = self.offsets.to(self.device)
+        self._lengths_dev = self.lengths.to(self.device)
+
+    def __len__(self) -> int:
+        return self.blocks.shape[0]
+
+    def _rows(self, ids_host: torch.Tensor, generator=None) -> tuple[torch.Tensor, int, torch.Tensor]:
+        """Store row per output row (B*N, -1 = padding), N, lengths (host ids: no device sync)."""
+        dev = self.device
+        ids = ids_host.to(dev, non_blocking=True)
+        n = self._lengths_dev[ids]                                   # (B,)
+        start = self._offsets_dev[ids]
+        B = ids.numel()
+        S = self.sampling
+        if S is None:                                                 # whole blocks, padded to the longest
+            N = int(self.lengths[ids_host].max())
+            pos = torch.arange(N, device=dev).unsqueeze(0)
+            rows = torch.where(pos < n.unsqueeze(1), start.unsqueeze(1) + pos, torch.full_like(pos, -1))
+            return rows.reshape(-1), N, n.to(torch.uint64)
+        # per block: n > S -> first S of a random permutation; else S draws with replacement
+        tot = int(self.lengths[ids_host].sum())
+        seg = torch.repeat_interleave(torch.arange(B, device=dev), n, output_size=tot)
+        local = torch.arange(tot, device=dev) - torch.repeat_interleave(torch.cumsum(n, 0) - n, n, output_size=tot)
+        key = torch.randint(0, 1 << 31, (tot,), device=dev, generator=generator, dtype=torch.int64)
+        order = torch.argsort(seg * (1 << 31) + key)                  # random order inside each block
+        first = (torch.cumsum(n, 0) - n)                               # segment starts in the sorted order
+        take = first.unsqueeze(1) + torch.arange(S, device=dev).unsqueeze(0)
+        perm_rows = local[order[take.clamp(max=tot - 1)]]             # (B, S) local row ids (valid where n > S)
+        draw = (torch.rand((B, S), device=dev, generator=generator) * n.unsqueeze(1)).long()
+        draw = torch.minimum(draw, (n - 1).unsqueeze(1))              # fp32 rounding can reach n
+        local_rows = torch.where((n > S).unsqueeze(1), perm_rows, draw)
+        rows = start.unsqueeze(1) + local_rows
+        return rows.reshape(-1), S, torch.full((B,), S, dtype=torch.uint64, device=dev)
+
+    def batch(self, ids, generator=None):
+        """ids: block indices (list or tensor) -> points (B, N, 9) f32, labels (B, N, 14) u8,
+        lengths (B,) uint64, all on the device (the reference's collate output)."""
+        ids = torch.as_tensor(ids, dtype=torch.int64).cpu()
+        rows, N, lengths = self._rows(ids, generator)
+        return self.gather(rows, ids.numel(), N) + (lengths,)
+
+    def gather(self, rows: torch.Tensor, B: int, N: int):
+        check_cuda(self.points, rows)
+        rows = rows.to(torch.int64).contiguous()
+        pts = torch.empty((B, N, 9), dtype=torch.float32, device=self.device)
+        lab = torch.empty((B, N, 14), dtype=torch.uint8, device=self.device)
+        call('pcs_gather_blocks', ptr(self.points), ptr(self.labels), ptr(rows), rows.numel(), ptr(pts), ptr(lab),
+             stream_ptr(self.device))
+        return pts, lab

@@ -169,6 +169,16 @@ int pcs_bn_act(const float* Z, int ldz, int M, int N, const float* s,
                const float* t, int act, float slope, float* out, int ldo,
                void* stream);
 
+/* ---- block batches --------------------------------------------------------- */
+
+/* data_processing/block_datasets.py:5-31,118-128: a padded batch gathered from an
+ * HBM-resident block store.  points (P,9) f32, labels (P,14) u8, src (rows)
+ * int64 store row per output row (< 0 = zero padding); out_points (rows,9),
+ * out_labels (rows,14). */
+int pcs_gather_blocks(const float* points, const uint8_t* labels,
+                      const long long* src, long long rows, float* out_points,
+                      uint8_t* out_labels, void* stream);
+
 /* ---- loss ---------------------------------------------------------------- */
 
 /* Training/train_model.py:15-57 `masked_onehot_cross_entropy`: logits (B,L,C)
