@@ -142,9 +142,12 @@ class GeometryPlan:
                 self.nn = nn_[::-1]                             # nn[lv] pairs level lv with lv + 1
                 self.nn_event = torch.cuda.Event()
                 self.nn_event.record(side)
-        coords.record_stream(side)
-        for t in made:
-            t.record_stream(main)
+        if not torch.cuda.is_current_stream_capturing():
+            # eager: tell the caching allocator about the cross-stream uses (under graph
+            # capture the graph's private pool keeps every block alive instead)
+            coords.record_stream(side)
+            for t in made:
+                t.record_stream(main)
 
     @staticmethod
     def _wait(ev):

@@ -170,6 +170,8 @@ def main():
     ap.add_argument('--cpu-threads', type=int, default=0)
     ap.add_argument('--cpu-baseline-worker', action='store_true')
     ap.add_argument('--no-roofline', action='store_true')
+    ap.add_argument('--graph', action='store_true',
+                    help='capture one training step in a HIP graph and time its replays (N=1, no prefetch)')
     ap.add_argument('--no-prefetch', action='store_true',
                     help='do not enqueue the next step\'s FPS/ball-query/3-NN before this step\'s backward')
     args = ap.parse_args()
@@ -200,13 +202,14 @@ def main():
     model = ctor(pcseg).to(dev).train()     # PyTorch default init (random weights)
     broadcast_model(model)
     grads = FlatGradAllReduce(model)
-    opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+    use_graph = args.graph and world == 1
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3, capturable=use_graph)
     pts, labels, lengths = make_batch(args.batch, args.npoints, seed=1000 * 2 + rank)
     x = model_input(pts.to(dev), kind)
     lab = (labels.float() if kind == 'chfirst6' else labels).to(dev)
     lengths = lengths.to(dev)
 
-    prefetch = hasattr(model, 'prefetch_geometry') and not args.no_prefetch
+    prefetch = hasattr(model, 'prefetch_geometry') and not args.no_prefetch and not use_graph
 
     def step():
         grads.zero_grad()
@@ -220,6 +223,22 @@ def main():
         opt.step()
         return loss
 
+    eager_step = step
+    if use_graph:
+        # warm up on a side stream (allocator + lazy init outside capture), then capture one step
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for _ in range(max(args.warmup, 2)):
+                step()
+        torch.cuda.current_stream(dev).wait_stream(side)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            static_loss = step()
+
+        def step():
+            graph.replay()
+            return static_loss
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
@@ -241,7 +260,7 @@ def main():
         raise RuntimeError('non-finite loss')
     roof = None
     if not args.no_roofline:
-        roof = kernel_roofline(step, dev, args)     # every rank runs the step (collectives), rank 0 reports
+        roof = kernel_roofline(eager_step, dev, args)     # every rank runs the step (collectives), rank 0 reports
     if rank == 0:
         ms = dt / args.steps * 1e3
         value = world * args.batch * args.npoints * args.steps / dt
@@ -254,7 +273,7 @@ def main():
             'config': {'workload': f'{name} seg, {args.npoints} pts, batch {args.batch}/GPU, fwd+CE+bwd'
                                    f'{"+allreduce" if world > 1 else ""}+Adam',
                        'model': name, 'global_batch': world * args.batch, 'npoints': args.npoints,
-                       'parallelism': f'dp{world}', 'geometry_prefetch': prefetch},
+                       'parallelism': f'dp{world}', 'geometry_prefetch': prefetch, 'hip_graph': use_graph},
             'host_enqueue_ms_per_step': round(t_host / args.steps * 1e3, 3),
             'roofline': roof,
             'step_roofline': step_roofline(args, ms),
