@@ -60,6 +60,11 @@ SIGNATURES = {
     'pcs_pool_bwd_reduce_blocks': [I64],
     'pcs_pool_bwd_reduce': [P, P, P, I32, I64, I32, P, P, P, P, I32, F32, P, P],
     'pcs_bn_act': [P, I32, I32, I32, P, P, I32, F32, P, I32, P],
+    # inverse neighbour maps
+    'pcs_inverse_index_workspace': [I64, I64, P],
+    'pcs_inverse_index': [P, I32, I32, I32, P, P, P, ctypes.c_size_t, P],
+    'pcs_group_bwd_csr': [P, I32, P, P, I32, I32, I32, P, P],
+    'pcs_interp_bwd_csr': [P, I32, I32, P, P, P, I32, I32, I32, P, P],
     # block batches
     'pcs_gather_blocks': [P, P, P, I64, P, P, P],
     # loss

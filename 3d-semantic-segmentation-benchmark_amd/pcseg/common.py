@@ -110,7 +110,7 @@ class GeometryPlan:
     reference's sequence.  Consumers wait on the per-level event before reading.
     """
 
-    def __init__(self, coords: torch.Tensor, levels, interp: bool = True):
+    def __init__(self, coords: torch.Tensor, levels, interp: bool = True, inverse: bool = True):
         dev = coords.device
         main = torch.cuda.current_stream(dev)
         side = side_stream(dev)
@@ -118,17 +118,25 @@ class GeometryPlan:
         self.coords = [coords]
         self.balls, self.events, self.nn = [], [], []
         made = []
+        self.inverse = inverse
         with torch.cuda.stream(side):
             prev = coords
             for C, queries in levels:
                 _, cent = sample_indices(prev, C)
-                bl = [_ball(cent, cent if on_self else prev, r, K) for r, K, on_self in queries]
+                bl = []
+                for r, K, on_self in queries:
+                    src = cent if on_self else prev
+                    idx = _ball(cent, src, r, K)
+                    # inverse map for the atomic-free backward of the feature gather
+                    inv = ops.inverse_index(idx, src.shape[1]) if inverse else None
+                    bl.append((idx, inv))
+                    made += [idx, *(inv or ())]
                 ev = torch.cuda.Event()
                 ev.record(side)
                 self.coords.append(cent)
                 self.balls.append(bl)
                 self.events.append(ev)
-                made += [cent, *bl]
+                made.append(cent)
                 prev = cent
             if interp:
                 nn_ = []
@@ -137,8 +145,9 @@ class GeometryPlan:
                     rp = _replay()
                     if rp is not None:
                         rp.rec_interp_idx.append(idx.detach().cpu())
-                    nn_.append((idx, dist))
-                    made += [idx, dist]
+                    inv = ops.inverse_index(idx, self.coords[lv + 1].shape[1]) if inverse else None
+                    nn_.append((idx, dist, inv))
+                    made += [idx, dist, *(inv or ())]
                 self.nn = nn_[::-1]                             # nn[lv] pairs level lv with lv + 1
                 self.nn_event = torch.cuda.Event()
                 self.nn_event.record(side)
@@ -154,12 +163,14 @@ class GeometryPlan:
         torch.cuda.current_stream().wait_event(ev)
 
     def sa(self, level: int, q: int = 0):
-        """(centroids, ball idx) of level >= 1 for its q-th query, after waiting for them."""
+        """(centroids, ball idx, inverse map or None) of level >= 1 for its q-th query,
+        after waiting for them."""
         self._wait(self.events[level - 1])
-        return self.coords[level], self.balls[level - 1][q]
+        idx, inv = self.balls[level - 1][q]
+        return self.coords[level], idx, inv
 
     def fp(self, level: int):
-        """(idx, dist) of the 3-NN from level `level` points into level `level + 1`."""
+        """(idx, dist, inverse map or None) of the 3-NN from level `level` into level `level + 1`."""
         self._wait(self.nn_event)
         return self.nn[level]
 
@@ -248,12 +259,14 @@ class SetAbstraction(nn.Module):
                 geo: tuple | None = None) -> tuple[torch.Tensor, torch.Tensor]:
         """geo = (centroids, ball idx) precomputed by a GeometryPlan, else computed here."""
         B = coords.shape[0]
+        inv = None
         if geo is None:
             _, cent = sample_indices(coords, self.C)
             idx = _ball(cent, coords, self.radius, self.K)
         else:
-            cent, idx = geo
-        rows = ops.group_rows(coords, features, cent, idx, self.radius, self.grouping_norm)
+            cent, idx = geo[0], geo[1]
+            inv = geo[2] if len(geo) > 2 else None
+        rows = ops.group_rows(coords, features, cent, idx, self.radius, self.grouping_norm, inv)
         kin = 3 + features.shape[2]
         if self.pooling_type == 'max':
             out = self.point_net.forward_rows(rows, kin, pool_k=self.K).view(B, self.C, -1)
@@ -274,14 +287,16 @@ class FeaturePropagation(nn.Module):
                 features_2: torch.Tensor, geo: tuple | None = None) -> torch.Tensor:
         """geo = (3-NN idx, squared dist) precomputed by a GeometryPlan, else computed here."""
         B, N, _ = coords_1.shape
+        inv = None
         if geo is None:
             idx, dist = ops.knn_select(coords_1, coords_2, 3)
             rp = _replay()
             if rp is not None:
                 rp.rec_interp_idx.append(idx.detach().cpu())
         else:
-            idx, dist = geo
-        rows = ops.interp_cat_rows(features_1, features_2, idx, dist)
+            idx, dist = geo[0], geo[1]
+            inv = geo[2] if len(geo) > 2 else None
+        rows = ops.interp_cat_rows(features_1, features_2, idx, dist, inv)
         return self.point_net.forward_rows(rows).view(B, N, -1)
 
 
@@ -297,11 +312,17 @@ class InvResMLP(nn.Module):
         self.point_features_mlp = UnitPointNet(mlp_size, [4 * mlp_size, mlp_size])
 
     def forward(self, centroid_coords: torch.Tensor, coords: torch.Tensor,
-                features: torch.Tensor, geo: torch.Tensor | None = None) -> tuple[torch.Tensor, torch.Tensor]:
-        """geo = ball idx precomputed by a GeometryPlan, else computed here."""
+                features: torch.Tensor, geo=None) -> tuple[torch.Tensor, torch.Tensor]:
+        """geo = ball idx (or (idx, inverse map)) precomputed by a GeometryPlan, else computed here."""
         B, C, _ = centroid_coords.shape
-        idx = _ball(centroid_coords, coords, self.radius, self.K) if geo is None else geo
-        rows = ops.group_rows(coords, features, centroid_coords, idx, self.radius, True)
+        inv = None
+        if geo is None:
+            idx = _ball(centroid_coords, coords, self.radius, self.K)
+        elif isinstance(geo, torch.Tensor):
+            idx = geo
+        else:
+            idx, inv = geo
+        rows = ops.group_rows(coords, features, centroid_coords, idx, self.radius, True, inv)
         kin = 3 + features.shape[2]
         if self.pooling_type == 'max':
             pooled = self.neighbour_features_mlp.forward_rows(rows, kin, pool_k=self.K)

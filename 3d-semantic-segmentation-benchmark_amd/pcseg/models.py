@@ -103,8 +103,8 @@ class PointNetppMSG(GeometryPrefetch, nn.Module):
         B = coords.shape[0]
         outs = []
         for q, sa in enumerate(branches):
-            cent, idx = geo.sa(level, q)
-            rows = ops.group_rows(coords, feats, cent, idx, sa.radius, sa.grouping_norm)
+            cent, idx, inv = geo.sa(level, q)
+            rows = ops.group_rows(coords, feats, cent, idx, sa.radius, sa.grouping_norm, inv)
             outs.append(sa.point_net.forward_rows(rows, 3 + feats.shape[2], pool_k=sa.K).view(B, C, -1))
         return cent, torch.cat(outs, dim=-1)
 
@@ -173,14 +173,14 @@ class PointNeXt(GeometryPrefetch, nn.Module):
         x = x.contiguous()
         f0 = self.mlp.forward_rows(pad_rows(x.view(B * N, Cin)), Cin).view(B, N, -1)
         c1, f1 = self.sa1(c0, f0, geo=geo.sa(1, 0))
-        c1, f1 = self.irmlp1(c1, c1, f1, geo=geo.sa(1, 1)[1])
+        c1, f1 = self.irmlp1(c1, c1, f1, geo=geo.sa(1, 1)[1:])
         c2, f2 = self.sa2(c1, f1, geo=geo.sa(2, 0))
-        c2, f2 = self.irmlp2(c2, c2, f2, geo=geo.sa(2, 1)[1])
-        c2, f2 = self.irmlp2_1(c2, c2, f2, geo=geo.sa(2, 2)[1])
+        c2, f2 = self.irmlp2(c2, c2, f2, geo=geo.sa(2, 1)[1:])
+        c2, f2 = self.irmlp2_1(c2, c2, f2, geo=geo.sa(2, 2)[1:])
         c3, f3 = self.sa3(c2, f2, geo=geo.sa(3, 0))
-        c3, f3 = self.irmlp3(c3, c3, f3, geo=geo.sa(3, 1)[1])
+        c3, f3 = self.irmlp3(c3, c3, f3, geo=geo.sa(3, 1)[1:])
         c4, f4 = self.sa4(c3, f3, geo=geo.sa(4, 0))
-        c4, f4 = self.irmlp4(c4, c4, f4, geo=geo.sa(4, 1)[1])
+        c4, f4 = self.irmlp4(c4, c4, f4, geo=geo.sa(4, 1)[1:])
         f3 = self.fp4(c3, c4, f3, f4, geo=geo.fp(3))
         f2 = self.fp3(c2, c3, f2, f3, geo=geo.fp(2))
         f1 = self.fp2(c1, c2, f1, f2, geo=geo.fp(1))

@@ -7,6 +7,8 @@ non-zero ABI status raises RuntimeError with the library's message.
 """
 from __future__ import annotations
 
+import ctypes
+
 import numpy as np
 import torch
 
@@ -72,6 +74,27 @@ def knn(x: torch.Tensor, k: int) -> torch.Tensor:
     return out
 
 
+def inverse_index(idx: torch.Tensor, targets: int):
+    """CSR inverse of a neighbour table idx (B, S, k) int32 with values in [0, targets):
+    (offsets (B*targets+1,), entries (B*S*k,)) int32 -- the slots reading each source point,
+    ascending (stable rocPRIM radix sort).  Feeds the atomic-free gather backward."""
+    check_cuda(idx)
+    idx = _c(idx.to(torch.int32))
+    B = idx.shape[0]
+    per = idx[0].numel()
+    lib = _lib.load()
+    need = ctypes.c_size_t(0)
+    rc = lib.pcs_inverse_index_workspace(B * per, B * targets, ctypes.byref(need))
+    if rc:
+        raise RuntimeError(lib.pcs_last_error().decode())
+    ws = torch.empty(max(int(need.value), 1), dtype=torch.uint8, device=idx.device)
+    offsets = torch.empty(B * targets + 1, dtype=torch.int32, device=idx.device)
+    entries = torch.empty(B * per, dtype=torch.int32, device=idx.device)
+    call('pcs_inverse_index', ptr(idx), B, per, targets, ptr(offsets), ptr(entries), ptr(ws), int(need.value),
+         stream_ptr(idx.device))
+    return offsets, entries
+
+
 # ------------------------------------------------------------------ differentiable gathers
 def ld4(n: int) -> int:
     return (n + 3) // 4 * 4
@@ -82,7 +105,7 @@ class GroupFn(torch.autograd.Function):
     grad flows to feats only (coords never require grad in the reference)."""
 
     @staticmethod
-    def forward(ctx, xyz, feats, cent, idx, r, normalize):
+    def forward(ctx, xyz, feats, cent, idx, r, normalize, inv=None):
         B, N, _ = xyz.shape
         C, K = idx.shape[1], idx.shape[2]
         D = feats.shape[2] if feats is not None else 0
@@ -90,28 +113,36 @@ class GroupFn(torch.autograd.Function):
         out = torch.empty((B * C * K, ld), dtype=torch.float32, device=xyz.device)
         call('pcs_group_fwd', ptr(xyz), ptr(feats), ptr(cent), ptr(idx), B, N, C, K, D, float(np.float32(r)),
              int(bool(normalize)), ptr(out), ld, stream_ptr(xyz.device))
-        ctx.save_for_backward(idx)
+        ctx.save_for_backward(idx, *(inv if inv is not None else ()))
         ctx.dims = (B, N, C, K, D, ld)
         ctx.has_feats = feats is not None
+        ctx.has_inv = inv is not None
         return out
 
     @staticmethod
     def backward(ctx, gout):
-        (idx,) = ctx.saved_tensors
+        saved = ctx.saved_tensors
+        idx = saved[0]
         B, N, C, K, D, ld = ctx.dims
         gfeats = None
         if ctx.has_feats and ctx.needs_input_grad[1]:
             gout = _c(gout)
-            gfeats = torch.zeros((B, N, D), dtype=torch.float32, device=gout.device)
-            call('pcs_group_bwd', ptr(gout), ld, ptr(idx), B, N, C, K, D, ptr(gfeats), stream_ptr(gout.device))
-        return None, gfeats, None, None, None, None
+            if ctx.has_inv:             # atomic-free gather over the inverse map
+                gfeats = torch.empty((B, N, D), dtype=torch.float32, device=gout.device)
+                call('pcs_group_bwd_csr', ptr(gout), ld, ptr(saved[1]), ptr(saved[2]), B, N, D, ptr(gfeats),
+                     stream_ptr(gout.device))
+            else:
+                gfeats = torch.zeros((B, N, D), dtype=torch.float32, device=gout.device)
+                call('pcs_group_bwd', ptr(gout), ld, ptr(idx), B, N, C, K, D, ptr(gfeats), stream_ptr(gout.device))
+        return None, gfeats, None, None, None, None, None
 
 
-def group_rows(xyz, feats, cent, idx, r, normalize):
+def group_rows(xyz, feats, cent, idx, r, normalize, inv=None):
+    """inv: optional inverse_index(idx, N) for the atomic-free backward."""
     check_cuda(xyz, cent, idx)
     xyz, cent = _c(xyz.float()), _c(cent.float())
     feats = _c(feats.float()) if feats is not None else None
-    return GroupFn.apply(xyz, feats, cent, _c(idx), r, normalize)
+    return GroupFn.apply(xyz, feats, cent, _c(idx), r, normalize, inv)
 
 
 class MaxKFn(torch.autograd.Function):
@@ -153,7 +184,7 @@ class InterpCatFn(torch.autograd.Function):
     """rows (B*N, D1+D2) = [f1, IDW-interpolate(f2)] (reference FeaturePropagation.forward)."""
 
     @staticmethod
-    def forward(ctx, f1, f2, idx, dist):
+    def forward(ctx, f1, f2, idx, dist, inv=None):
         B, M, D2 = f2.shape
         N = idx.shape[1]
         D1 = f1.shape[2] if f1 is not None else 0
@@ -162,30 +193,38 @@ class InterpCatFn(torch.autograd.Function):
         if f1 is not None:
             out.view(B, N, W)[:, :, :D1].copy_(f1)
         call('pcs_interp_fwd', ptr(f2), ptr(idx), ptr(dist), B, N, M, D2, ptr(out), W, D1, stream_ptr(f2.device))
-        ctx.save_for_backward(idx, dist)
+        ctx.save_for_backward(idx, dist, *(inv if inv is not None else ()))
         ctx.dims = (B, N, M, D1, D2)
         ctx.has_f1 = f1 is not None
+        ctx.has_inv = inv is not None
         return out
 
     @staticmethod
     def backward(ctx, gout):
-        idx, dist = ctx.saved_tensors
+        saved = ctx.saved_tensors
+        idx, dist = saved[0], saved[1]
         B, N, M, D1, D2 = ctx.dims
         gout = _c(gout)
         W = D1 + D2
         g1 = gout.view(B, N, W)[:, :, :D1] if (ctx.has_f1 and ctx.needs_input_grad[0]) else None
         g2 = None
         if ctx.needs_input_grad[1]:
-            g2 = torch.zeros((B, M, D2), dtype=torch.float32, device=gout.device)
-            call('pcs_interp_bwd', ptr(gout), ptr(idx), ptr(dist), B, N, M, D2, W, D1, ptr(g2),
-                 stream_ptr(gout.device))
-        return g1, g2, None, None
+            if ctx.has_inv:             # atomic-free gather over the inverse map
+                g2 = torch.empty((B, M, D2), dtype=torch.float32, device=gout.device)
+                call('pcs_interp_bwd_csr', ptr(gout), W, D1, ptr(dist), ptr(saved[2]), ptr(saved[3]), B, M, D2,
+                     ptr(g2), stream_ptr(gout.device))
+            else:
+                g2 = torch.zeros((B, M, D2), dtype=torch.float32, device=gout.device)
+                call('pcs_interp_bwd', ptr(gout), ptr(idx), ptr(dist), B, N, M, D2, W, D1, ptr(g2),
+                     stream_ptr(gout.device))
+        return g1, g2, None, None, None
 
 
-def interp_cat_rows(f1, f2, idx, dist):
+def interp_cat_rows(f1, f2, idx, dist, inv=None):
+    """inv: optional inverse_index(idx, M) for the atomic-free backward."""
     check_cuda(f2, idx, dist)
     f1 = _c(f1.float()) if f1 is not None else None
-    return InterpCatFn.apply(f1, _c(f2.float()), _c(idx), _c(dist))
+    return InterpCatFn.apply(f1, _c(f2.float()), _c(idx), _c(dist), inv)
 
 
 class EdgeFn(torch.autograd.Function):

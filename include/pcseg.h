@@ -169,6 +169,28 @@ int pcs_bn_act(const float* Z, int ldz, int M, int N, const float* s,
                const float* t, int act, float slope, float* out, int ldo,
                void* stream);
 
+/* ---- inverse neighbour maps (atomic-free gather backward) ------------------ */
+
+/* For a neighbour table idx (B x per_batch, values in [0, targets)), the CSR
+ * inverse: the slots reading source (b, p) are entries[offsets[b*targets+p] ..
+ * offsets[b*targets+p+1]), ascending.  offsets (B*targets + 1), entries
+ * (B*per_batch) int32; workspace of pcs_inverse_index_workspace bytes. */
+int pcs_inverse_index_workspace(long long n_slots, long long n_targets,
+                                size_t* bytes);
+int pcs_inverse_index(const int32_t* idx, int B, int per_batch, int targets,
+                      int32_t* offsets, int32_t* entries, void* workspace,
+                      size_t ws_bytes, void* stream);
+/* common.py:64-65 backward without atomics: grad_feats (B,N,D) = sum of
+ * grad_out[slot][3 + c] over the slots reading each point (overwrites). */
+int pcs_group_bwd_csr(const float* grad_out, int ld_gout, const int32_t* offsets,
+                      const int32_t* entries, int B, int N, int D,
+                      float* grad_feats, void* stream);
+/* common.py:115-122 backward without atomics: grad_pts (B,M,D) (overwrites). */
+int pcs_interp_bwd_csr(const float* grad_out, int ld_gout, int col_off,
+                       const float* dist, const int32_t* offsets,
+                       const int32_t* entries, int B, int M, int D,
+                       float* grad_pts, void* stream);
+
 /* ---- block batches --------------------------------------------------------- */
 
 /* data_processing/block_datasets.py:5-31,118-128: a padded batch gathered from an

@@ -238,3 +238,56 @@ def test_masked_ce_matches_reference_golden(golden):
     lf.grad = None
     (3.0 * pcseg.masked_onehot_cross_entropy(lf, onehot.to(DEV), lengths.to(DEV))).backward()
     assert torch.allclose(lf.grad.cpu(), 3.0 * torch.from_numpy(z['grad']), rtol=1e-5, atol=1e-8)
+
+
+# ----------------------------------------------------------------------------- inverse maps / CSR backward
+@pytest.mark.parametrize('B,N,C,K,r', [(3, 1024, 256, 32, 0.2), (2, 4096, 1024, 32, 0.1), (2, 256, 256, 16, 0.4)])
+def test_inverse_index_and_group_bwd_csr(B, N, C, K, r):
+    xyz = cloud(B, N, seed=41).to(DEV)
+    cent = xyz[:, :C].contiguous()
+    idx = ops.ball_query(cent, xyz, r, K)
+    off, ent = ops.inverse_index(idx, N)
+    # the CSR lists exactly the slots reading each point, ascending
+    flat = idx.reshape(B, -1).long().cpu()
+    key = (torch.arange(B).unsqueeze(1) * N + flat).reshape(-1)
+    order = torch.sort(key, stable=True).indices
+    assert torch.equal(ent.long().cpu(), order)
+    counts = torch.bincount(key, minlength=B * N)
+    assert torch.equal(off.long().cpu(), torch.cat([torch.zeros(1, dtype=torch.long), counts.cumsum(0)]))
+    # gather backward == atomic backward (same terms, fixed ascending order)
+    D = 19
+    feats = torch.randn(B, N, D, device=DEV)
+    fa = feats.clone().requires_grad_(True)
+    fb = feats.clone().requires_grad_(True)
+    ya = ops.group_rows(xyz, fa, cent, idx, r, False)
+    yb = ops.group_rows(xyz, fb, cent, idx, r, False, (off, ent))
+    assert torch.equal(ya, yb)
+    w = torch.randn_like(ya)
+    (ya * w).sum().backward()
+    (yb * w).sum().backward()
+    assert torch.allclose(fa.grad, fb.grad, rtol=1e-5, atol=1e-6)
+    # deterministic
+    fb.grad = None
+    (ops.group_rows(xyz, fb, cent, idx, r, False, (off, ent)) * w).sum().backward()
+    g1 = fb.grad.clone()
+    fb.grad = None
+    (ops.group_rows(xyz, fb, cent, idx, r, False, (off, ent)) * w).sum().backward()
+    assert torch.equal(g1, fb.grad)
+
+
+def test_interp_bwd_csr_matches_atomic():
+    B, N, M, D1, D2 = 2, 4096, 1024, 8, 64
+    c1 = cloud(B, N, seed=42).to(DEV)
+    c2 = c1[:, :M].contiguous()
+    idx, dist = ops.knn_select(c1, c2, 3)
+    inv = ops.inverse_index(idx, M)
+    f1 = torch.randn(B, N, D1, device=DEV)
+    f2a = torch.randn(B, M, D2, device=DEV).requires_grad_(True)
+    f2b = f2a.detach().clone().requires_grad_(True)
+    ya = ops.interp_cat_rows(f1, f2a, idx, dist)
+    yb = ops.interp_cat_rows(f1, f2b, idx, dist, inv)
+    assert torch.equal(ya, yb)
+    w = torch.randn_like(ya)
+    (ya * w).sum().backward()
+    (yb * w).sum().backward()
+    assert torch.allclose(f2a.grad, f2b.grad, rtol=1e-5, atol=1e-5)
