@@ -148,6 +148,14 @@ def _gpu_worker(rank, world, port, out):
         got = torch.cat([p.grad.reshape(-1) for p in model.parameters()])
         rel = float((got - expect).norm() / expect.norm())
         out[rank] = rel
+        if rel >= 1e-5 and rank == 0:
+            off = 0
+            for (name, p) in model.named_parameters():
+                n = p.numel()
+                e = float((got[off:off + n] - expect[off:off + n]).norm() / (expect[off:off + n].norm() + 1e-30))
+                loc = float((local[off:off + n] - expect[off:off + n]).norm() / (expect[off:off + n].norm() + 1e-30))
+                print(f'DDPDIAG {name} rel={e:.3e} local_vs_mean={loc:.3e}', flush=True)
+                off += n
         assert rel < 1e-5, rel                 # fp32 atomics make wgrad order run-dependent
         assert all(h is not None for h in grads._handles) or not grads._handles
     finally:
