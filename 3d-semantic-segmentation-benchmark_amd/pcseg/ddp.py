@@ -51,6 +51,8 @@ class FlatGradAllReduce:
             self.buckets.append((cur_start, off, cur))
         self._bucket_of = {p: i for i, (_, _, ps) in enumerate(self.buckets) for p in ps}
         self._pending = [len(ps) for _, _, ps in self.buckets]
+        self._launched = [False] * len(self.buckets)
+        self._seen: set[int] = set()
         self._handles: list = []
         self.overlap = overlap and self.world > 1
         self.attach()
@@ -66,17 +68,29 @@ class FlatGradAllReduce:
         for p in self.params:
             p.grad = self.views[p]
 
+    def _reset(self) -> None:
+        self._pending = [len(ps) for _, _, ps in self.buckets]
+        self._launched = [False] * len(self.buckets)
+        self._seen = set()
+        self._handles = []
+
     def zero_grad(self) -> None:
         self.flat.zero_()
         self.attach()
-        self._pending = [len(ps) for _, _, ps in self.buckets]
-        self._handles = []
+        self._reset()
 
     def _hook(self, p: torch.Tensor) -> None:
+        # A parameter may be announced twice: by the HIP engine (which writes .grad in place)
+        # and by autograd's post-accumulate hook, which still fires for it with an undefined
+        # gradient.  Count each parameter once per step.
+        if id(p) in self._seen:
+            return
+        self._seen.add(id(p))
         b = self._bucket_of[p]
         self._pending[b] -= 1
-        if self._pending[b] == 0:
+        if self._pending[b] == 0 and not self._launched[b]:
             s, e, _ = self.buckets[b]
+            self._launched[b] = True
             self._handles.append(dist.all_reduce(self.flat[s:e], op=dist.ReduceOp.SUM, async_op=True))
 
     def synchronize(self) -> None:
@@ -86,12 +100,11 @@ class FlatGradAllReduce:
         if self.overlap:
             for h in self._handles:
                 h.wait()
-            # any bucket whose hook did not fire (unused params) is reduced now
+            # any bucket not launched from backward (unused params) is reduced now
             for b, (s, e, _) in enumerate(self.buckets):
-                if self._pending[b] != 0:
+                if not self._launched[b]:
                     dist.all_reduce(self.flat[s:e], op=dist.ReduceOp.SUM)
         else:
             dist.all_reduce(self.flat, op=dist.ReduceOp.SUM)
         self.flat.div_(self.world)
-        self._handles = []
-        self._pending = [len(ps) for _, _, ps in self.buckets]
+        self._reset()
