@@ -37,18 +37,19 @@ st = stream_ptr(torch.device(dev))
 for name, M, K, N in SHAPES:
     lda = (K + 3) // 4 * 4
     A = torch.randn(M, lda, device=dev)
-    W = torch.randn(N, K, device=dev)
+    W = torch.zeros(N, lda, device=dev)
+    W[:, :K] = torch.randn(N, K, device=dev)
     s = torch.rand(K, device=dev) + 0.5
     t = torch.randn(K, device=dev) * 0.1
     b = torch.randn(N, device=dev)
     C = torch.empty(M, N, device=dev)
     part = torch.empty(2, N, load().pcs_gemm_row_blocks(M, N), dtype=torch.float64, device=dev)
     aop = operand(A, lda, OP_BNACT, s, t, 0, 0.0) if K % 4 == 0 else operand(A, lda)
-    fwd = lambda: gemm_rows(aop, M, K, W, K, b, C, N, N, part, st=st)  # noqa
+    fwd = lambda: gemm_rows(aop, M, K, W, lda, b, C, N, N, part, st=st)  # noqa
     ms = timeit(fwd)
     fl = 2.0 * M * K * N
     by = 4.0 * M * (lda + N)
-    dW = torch.zeros(N, K, device=dev)
+    dW = torch.zeros(N, K, device=dev)  # noqa
     db = torch.zeros(N, device=dev)
     Z = torch.randn(M, N, device=dev)
     sN, tN = torch.rand(N, device=dev) + 0.5, torch.randn(N, device=dev) * 0.1
