@@ -19,127 +19,11 @@
 //    (dW = dZ^T . T(A_prev)) split over rows with fp32 atomics; dZ is
 //    materialised once per layer by an elementwise kernel.
 // Statistics are accumulated in fp64 (as ATen's CPU batch norm does).
-#include "pcs_common.hpp"
+#include "mlp_common.hpp"
+
+#include <stdlib.h>
 
 namespace pcs {
-
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-
-enum { ACT_RELU = 0, ACT_LRELU = 1, ACT_NONE = 2 };
-
-// The activation is folded into one slope at the ABI boundary (eff_slope): ReLU = 0,
-// LeakyReLU = its slope, identity = 1; both functions are branch-free selects.
-// derivative as autograd computes it: relu -> (result > 0); leaky_relu -> (input > 0 ? 1 : slope)
-__device__ __forceinline__ float act_f(float y, int, float slope) { return y > 0.f ? y : y * slope; }
-__device__ __forceinline__ float dact_f(float y, int, float slope) { return y > 0.f ? 1.f : slope; }
-
-static inline float eff_slope(int act, float slope) {
-    return act == ACT_RELU ? 0.f : act == ACT_LRELU ? slope : 1.f;
-}
-
-// Operand descriptor (layout-identical to pcs_operand in include/pcseg.h).  The
-// value fed to the MFMA for channel c of row r is
-//   PLAIN   : data[r][c]
-//   BNACT   : act(data[r][c]*s[c] + t[c])                  (forward: previous layer's BN + act)
-//   BNBWD   : s*dy - kb - alpha*(z - mean),  dy = data[r][c]*act'(z*s+t), z = Z[r][c]
-//   POOLBWD : as BNBWD with data[r][c] = (arg[g][c] == k) ? dpool[g][c] : 0, g = r / pool_k, k = r % pool_k
-// i.e. BNBWD/POOLBWD rebuild the layer's dZ (BatchNorm backward) on the fly from its
-// output gradient and pre-BN Z, so dZ is never written to HBM.
-struct Operand {
-    const float* data; int ld; int mode;
-    const float* s; const float* t; int act; float slope;
-    const float* z; int ldz;
-    const float* mean; const float* inv; const float* alpha; const float* kb;
-    const unsigned char* arg; int pool_k;
-};
-enum { OP_PLAIN = 0, OP_BNACT = 1, OP_BNBWD = 2, OP_POOLBWD = 3 };
-
-// per-channel coefficients of a transform, for 4 consecutive channels
-struct Quad {
-    float4 s, t, mean, alpha, kb;
-};
-
-// transform modes require K % 4 == 0 (checked at the ABI), so a channel quad is all in or all
-// out.  Loads use clamped (always in-bounds) addresses and selects instead of branches, so
-// the compiler keeps the next slab's loads in flight under the current slab's MFMAs.
-template <int MODE>
-__device__ __forceinline__ void load_quad(const Operand& o, int c, int K, Quad& q) {
-    const int cc = c < K ? c : 0;          // the out-of-range quad is zeroed in xform4
-    if (MODE >= OP_BNACT) {
-        q.s = *reinterpret_cast<const float4*>(o.s + cc);
-        q.t = *reinterpret_cast<const float4*>(o.t + cc);
-    }
-    if (MODE >= OP_BNBWD) {
-        q.mean = *reinterpret_cast<const float4*>(o.mean + cc);
-        q.alpha = *reinterpret_cast<const float4*>(o.alpha + cc);
-        q.kb = *reinterpret_cast<const float4*>(o.kb + cc);
-    }
-}
-
-// raw global loads of one float4 at (row r, channels c..c+3); r and c must be in bounds
-// (callers clamp).  POOLBWD: v = dpool[g][c..], a = the 4 argmax bytes; z only for BNBWD/POOLBWD.
-template <int MODE>
-__device__ __forceinline__ void load_raw(const Operand& o, int r, int c, float4& v, float4& z, unsigned& a) {
-    if (MODE == OP_POOLBWD) {
-        const int g = r / o.pool_k;
-        v = *reinterpret_cast<const float4*>(o.data + (size_t)g * o.ld + c);
-        a = *reinterpret_cast<const unsigned*>(o.arg + (size_t)g * o.ld + c);
-    } else {
-        v = *reinterpret_cast<const float4*>(o.data + (size_t)r * o.ld + c);
-    }
-    if (MODE >= OP_BNBWD) z = *reinterpret_cast<const float4*>(o.z + (size_t)r * o.ldz + c);
-}
-
-template <int MODE>
-__device__ __forceinline__ float xform1(const Operand& o, float v, float z, float s, float t, float mean, float alpha,
-                                        float kb) {
-    if (MODE == OP_BNACT) return act_f(v * s + t, o.act, o.slope);
-    if (MODE >= OP_BNBWD) {
-        const float dy = v * dact_f(z * s + t, o.act, o.slope);
-        return s * dy - kb - alpha * (z - mean);
-    }
-    return v;
-}
-
-// transformed float4 of row r: channels at or beyond K give 0 (per element for PLAIN,
-// whose K need not be a multiple of 4); POOLBWD keeps dpool only where argmax == r % pool_k
-template <int MODE>
-__device__ __forceinline__ float4 xform4(const Operand& o, float4 v, float4 z, unsigned a, int r, const Quad& q,
-                                         int c, int K) {
-    if (MODE == OP_PLAIN) {
-        v.x = c + 0 < K ? v.x : 0.f;
-        v.y = c + 1 < K ? v.y : 0.f;
-        v.z = c + 2 < K ? v.z : 0.f;
-        v.w = c + 3 < K ? v.w : 0.f;
-        return v;
-    }
-    if (MODE == OP_POOLBWD) {
-        const unsigned k = (unsigned)(r - (r / o.pool_k) * o.pool_k);
-        v.x = (a & 0xffu) == k ? v.x : 0.f;
-        v.y = ((a >> 8) & 0xffu) == k ? v.y : 0.f;
-        v.z = ((a >> 16) & 0xffu) == k ? v.z : 0.f;
-        v.w = (a >> 24) == k ? v.w : 0.f;
-    }
-    float4 out;
-    out.x = xform1<MODE>(o, v.x, z.x, q.s.x, q.t.x, q.mean.x, q.alpha.x, q.kb.x);
-    out.y = xform1<MODE>(o, v.y, z.y, q.s.y, q.t.y, q.mean.y, q.alpha.y, q.kb.y);
-    out.z = xform1<MODE>(o, v.z, z.z, q.s.z, q.t.z, q.mean.z, q.alpha.z, q.kb.z);
-    out.w = xform1<MODE>(o, v.w, z.w, q.s.w, q.t.w, q.mean.w, q.alpha.w, q.kb.w);
-    const bool in = c < K;
-    return in ? out : make_float4(0.f, 0.f, 0.f, 0.f);
-}
-
-struct GemmArgs {
-    Operand a; int M; int K;                   // A rows (M x K) through its transform
-    const float* W; int ldw;                   // B[k][n] = W[n*ldw + k]
-    const float* bias;                         // per n (or null)
-    float* C; int ldc; int N;                  // output rows (M x N)
-    double* stats;                             // [2][N][gridDim.x]: sum, sum of squares of C (or null)
-    // fused BN-backward reduce of the layer whose OUTPUT space C lives in (dgrad epilogue):
-    // uses e.z (its pre-BN Z, M x N), e.s, e.t, e.mean, e.inv, e.act, e.slope
-    Operand e;
-    double* bstats;                            // [2][N][gridDim.x]: sum dy, sum dy*xhat (or null)
-};
 
 // ------------------------------------------------------------------ row GEMM
 // C[M x N] = T(A)[M x K] . B[K x N],  B[k][n] = W[n*ldw + k]  (W row-major N x K).
@@ -169,7 +53,7 @@ __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(GemmArgs g) {
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave / WN, wn = wave % WN;
-    const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+    const int n0 = blockIdx.y * BN;
     const int h = lane >> 5, l32 = lane & 31;
 
     f32x16 acc[TM][TN];
@@ -186,7 +70,7 @@ __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(GemmArgs g) {
     // coefficient quad per slab serves all of them
     Quad q;
     const int lda_last = g.a.ld - 4, ldw_last = g.ldw - 4;
-    auto gload = [&](int k0) {
+    auto gload = [&](int m0, int k0) {
         const int gk = k0 + 4 * (tid & 7);
         const int gkc = min(gk, lda_last);
         load_quad<AM>(g.a, gk, g.K, q);
@@ -203,13 +87,13 @@ __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(GemmArgs g) {
             if (kBFull || e < BN * GBK / 4) rb[it] = *reinterpret_cast<const float4*>(g.W + (size_t)gn * g.ldw + gk2);
         }
     };
-    auto sstore = [&](int buf, int k0) {
+    auto sstore = [&](int buf, int m0, int k0) {
         const int gk = k0 + 4 * (tid & 7);
 #pragma unroll
         for (int it = 0; it < AV; ++it) {
             const int r = (it * 256 + tid) >> 3;
             *reinterpret_cast<float4*>(&As[buf][r][4 * (tid & 7)]) =
-                xform4<AM>(g.a, ra[it], rz[it], rg[it], m0 + r, q, gk, g.K);
+                xform4<AM>(g.a, ra[it], rz[it], rg[it], min(m0 + r, g.M - 1), q, gk, g.K);
         }
 #pragma unroll
         for (int it = 0; it < BV; ++it) {
@@ -224,13 +108,30 @@ __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(GemmArgs g) {
         }
     };
 
+    // ---- persistent loop: this block owns row tiles blockIdx.x + t*gridDim.x; the (tile, slab)
+    // iterations are flattened so the NEXT tile's first slab is loading while this tile's
+    // epilogue stores C (no exposed prologue per tile)
+    const bool want_stats = g.stats != nullptr;
+    const bool want_b = g.bstats != nullptr;
+    double s1[TN], s2[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) { s1[j] = 0.0; s2[j] = 0.0; }
     const int nk = (g.K + GBK - 1) / GBK;
-    gload(0);
-    sstore(0, 0);
+    const int mtiles = (g.M + BM - 1) / BM;
+    const int my_tiles = blockIdx.x < mtiles ? (mtiles - 1 - blockIdx.x) / gridDim.x + 1 : 0;
+    const int total = my_tiles * nk;
+    if (total > 0) {
+        gload(blockIdx.x * BM, 0);
+        sstore(0, blockIdx.x * BM, 0);
+    }
     __syncthreads();
-    for (int ks = 0; ks < nk; ++ks) {
-        const int buf = ks & 1;
-        gload((ks + 1) * GBK);    // unconditional (clamped past the end): no phi copies of in-flight registers
+    for (int it = 0; it < total; ++it) {
+        const int buf = it & 1;
+        const int ti = it / nk, ks = it - ti * nk;
+        const int m0 = (blockIdx.x + ti * gridDim.x) * BM;
+        const int tn = (it + 1) / nk, kn = (it + 1) - tn * nk;
+        const int m0n = (blockIdx.x + tn * gridDim.x) * BM;      // past the end: clamped loads, unused
+        gload(m0n, kn * GBK);     // unconditional: no phi copies of in-flight registers
         // keep the next slab's loads in flight: nothing that consumes them may be
         // scheduled above the MFMAs of this slab
         __builtin_amdgcn_sched_barrier(0);
@@ -254,54 +155,55 @@ __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(GemmArgs g) {
                 }
         }
         __builtin_amdgcn_sched_barrier(0);
-        if (ks + 1 < nk) sstore(buf ^ 1, (ks + 1) * GBK);
-        __syncthreads();
-    }
-
-    // ---- epilogue: bias, store, per-channel partial reductions
-    const bool want_stats = g.stats != nullptr;
-    const bool want_b = g.bstats != nullptr;
+        if (ks == nk - 1) {
+            // ---- tile epilogue: bias, store, per-channel partial reductions
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-        const int lc = wn * WTN + j * 32 + l32;
-        const int col = n0 + lc;
-        const bool cok = col < g.N;
-        const float bv = (g.bias && cok) ? g.bias[col] : 0.f;
-        float sp = 0.f, tp = 0.f, mp = 0.f, ip = 0.f;
-        if (want_b && cok) { sp = g.e.s[col]; tp = g.e.t[col]; mp = g.e.mean[col]; ip = g.e.inv[col]; }
-        double s1 = 0.0, s2 = 0.0;
+            for (int j = 0; j < TN; ++j) {
+                const int col = n0 + wn * WTN + j * 32 + l32;
+                const bool cok = col < g.N;
+                const float bv = (g.bias && cok) ? g.bias[col] : 0.f;
+                float sp = 0.f, tp = 0.f, mp = 0.f, ip = 0.f;
+                if (want_b && cok) { sp = g.e.s[col]; tp = g.e.t[col]; mp = g.e.mean[col]; ip = g.e.inv[col]; }
 #pragma unroll
-        for (int i = 0; i < TM; ++i) {
+                for (int i = 0; i < TM; ++i) {
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int row = m0 + wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                if (row < g.M && cok) {
-                    const float v = acc[i][j][r] + bv;
-                    g.C[(size_t)row * g.ldc + col] = v;
-                    if (want_stats) {
-                        s1 += (double)v;
-                        s2 += (double)v * (double)v;
-                    }
-                    if (want_b) {
-                        const float z = g.e.z[(size_t)row * g.e.ldz + col];
-                        const float dy = v * dact_f(z * sp + tp, g.e.act, g.e.slope);
-                        const float xh = (z - mp) * ip;
-                        s1 += (double)dy;
-                        s2 += (double)dy * (double)xh;
+                    for (int r = 0; r < 16; ++r) {
+                        const int row = m0 + wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                        if (row < g.M && cok) {
+                            const float v = acc[i][j][r] + bv;
+                            g.C[(size_t)row * g.ldc + col] = v;
+                            if (want_stats) {
+                                s1[j] += (double)v;
+                                s2[j] += (double)v * (double)v;
+                            }
+                            if (want_b) {
+                                const float z = g.e.z[(size_t)row * g.e.ldz + col];
+                                const float dy = v * dact_f(z * sp + tp, g.e.act, g.e.slope);
+                                const float xh = (z - mp) * ip;
+                                s1[j] += (double)dy;
+                                s2[j] += (double)dy * (double)xh;
+                            }
+                        }
+                        acc[i][j][r] = 0.f;
                     }
                 }
             }
         }
-        if (want_stats || want_b) {
-            s1 += __shfl_xor(s1, 32);
-            s2 += __shfl_xor(s2, 32);
+        if (it + 1 < total) sstore(buf ^ 1, m0n, kn * GBK);
+        __syncthreads();
+    }
+
+    if (want_stats || want_b) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int lc = wn * WTN + j * 32 + l32;
+            double a = s1[j] + __shfl_xor(s1[j], 32);
+            double b = s2[j] + __shfl_xor(s2[j], 32);
             if (lane < 32) {
-                red[0][wm][lc] = s1;
-                red[1][wm][lc] = s2;
+                red[0][wm][lc] = a;
+                red[1][wm][lc] = b;
             }
         }
-    }
-    if (want_stats || want_b) {
         __syncthreads();
         double* out = want_stats ? g.stats : g.bstats;
         for (int c = tid; c < BN; c += 256) {
@@ -326,6 +228,9 @@ __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(GemmArgs g) {
 // stride) so each lane's fragment is 16 consecutive rows.  fp32 partial sums are
 // flushed every 8 slabs (256 rows) into a second accumulator to bound the
 // accumulation error, and blocks combine with fp32 atomics.
+// row swizzle of channel c's LDS row (multiples of 4: keeps 4-row groups 16-B contiguous)
+__device__ __forceinline__ int lds_swz(int c) { return ((c >> 3) & 7) << 2; }
+
 template <int BO, int BI, int XM, int YM>
 __global__ __launch_bounds__(256, 2) void wgrad_kernel(Operand xo, int N, Operand yo, int K, int M,
                                                        int rows_per_block, float* __restrict__ dW,
@@ -346,8 +251,15 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(Operand xo, int N, Operan
     const int re = min(M, rb + rows_per_block);
     const bool do_db = (db != nullptr) && (k0 == 0);
 
-    // this thread's fixed channel quads and their transform coefficients
-    const int xc4 = tid % (BO / 4), yc4 = tid % (BI / 4);
+    // Transposed LDS stores without bank conflicts: each 32-lane half stores 4 rows x 8
+    // channel quads, and the row index is XOR-swizzled in 4-row groups by the channel
+    // (lds_swz), so the 32 ds_write_b32 of a half hit 32 distinct banks; the fragment reads
+    // apply the same swizzle (4-row groups stay intact, so they remain ds_read_b128).
+    // this thread's fixed channel quads (and their transform coefficients) and rows
+    const int half = tid >> 5;
+    const int xc4 = (half % (BO / 32)) * 8 + ((tid >> 2) & 7), yc4 = (half % (BI / 32)) * 8 + ((tid >> 2) & 7);
+    const int xr = (half / (BO / 32)) * 4 + (tid & 3), yr = (half / (BI / 32)) * 4 + (tid & 3);
+    constexpr int XRPI = 1024 / BO, YRPI = 1024 / BI;     // rows per load iteration
     const int gn = n0 + 4 * xc4, gk = k0 + 4 * yc4;
     Quad qx, qy;
     load_quad<XM>(xo, gn, N, qx);
@@ -368,36 +280,38 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(Operand xo, int N, Operan
     auto gload = [&](int r0) {
 #pragma unroll
         for (int it = 0; it < XV; ++it) {
-            const int gr = min(r0 + (it * 256 + tid) / (BO / 4), M - 1);
+            const int gr = min(r0 + it * XRPI + xr, M - 1);
             load_raw<XM>(xo, gr, gnc, rx[it], rxz[it], rxa[it]);
         }
 #pragma unroll
         for (int it = 0; it < YV; ++it) {
-            const int gr = min(r0 + (it * 256 + tid) / (BI / 4), M - 1);
+            const int gr = min(r0 + it * YRPI + yr, M - 1);
             load_raw<YM>(yo, gr, gkc, ry[it], ryz[it], rya[it]);
         }
     };
     auto sstore = [&](int buf, int r0) {
 #pragma unroll
         for (int it = 0; it < XV; ++it) {
-            const int r = (it * 256 + tid) / (BO / 4);
+            const int r = it * XRPI + xr;
             float4 v = xform4<XM>(xo, rx[it], rxz[it], rxa[it], r0 + r, qx, gn, N);
             if (r0 + r >= re) v = make_float4(0.f, 0.f, 0.f, 0.f);
-            Xs[buf][4 * xc4 + 0][r] = v.x;
-            Xs[buf][4 * xc4 + 1][r] = v.y;
-            Xs[buf][4 * xc4 + 2][r] = v.z;
-            Xs[buf][4 * xc4 + 3][r] = v.w;
+            const int rs = r ^ lds_swz(4 * xc4);      // the 4 channels of a quad share the swizzle
+            Xs[buf][4 * xc4 + 0][rs] = v.x;
+            Xs[buf][4 * xc4 + 1][rs] = v.y;
+            Xs[buf][4 * xc4 + 2][rs] = v.z;
+            Xs[buf][4 * xc4 + 3][rs] = v.w;
             if (do_db) { dbv[0] += v.x; dbv[1] += v.y; dbv[2] += v.z; dbv[3] += v.w; }
         }
 #pragma unroll
         for (int it = 0; it < YV; ++it) {
-            const int r = (it * 256 + tid) / (BI / 4);
+            const int r = it * YRPI + yr;
             float4 v = xform4<YM>(yo, ry[it], ryz[it], rya[it], r0 + r, qy, gk, K);
             if (r0 + r >= re) v = make_float4(0.f, 0.f, 0.f, 0.f);
-            Ys[buf][4 * yc4 + 0][r] = v.x;
-            Ys[buf][4 * yc4 + 1][r] = v.y;
-            Ys[buf][4 * yc4 + 2][r] = v.z;
-            Ys[buf][4 * yc4 + 3][r] = v.w;
+            const int rs = r ^ lds_swz(4 * yc4);
+            Ys[buf][4 * yc4 + 0][rs] = v.x;
+            Ys[buf][4 * yc4 + 1][rs] = v.y;
+            Ys[buf][4 * yc4 + 2][rs] = v.z;
+            Ys[buf][4 * yc4 + 3][rs] = v.w;
         }
     };
 
@@ -416,10 +330,12 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(Operand xo, int N, Operan
             float4 a[TM], b[TN];
 #pragma unroll
             for (int i = 0; i < TM; ++i)
-                a[i] = *reinterpret_cast<const float4*>(&Xs[buf][wo * (BO / 2) + i * 32 + l32][16 * h + 4 * q]);
+                a[i] = *reinterpret_cast<const float4*>(
+                    &Xs[buf][wo * (BO / 2) + i * 32 + l32][(16 * h + 4 * q) ^ lds_swz(wo * (BO / 2) + i * 32 + l32)]);
 #pragma unroll
             for (int j = 0; j < TN; ++j)
-                b[j] = *reinterpret_cast<const float4*>(&Ys[buf][wi * (BI / 2) + j * 32 + l32][16 * h + 4 * q]);
+                b[j] = *reinterpret_cast<const float4*>(
+                    &Ys[buf][wi * (BI / 2) + j * 32 + l32][(16 * h + 4 * q) ^ lds_swz(wi * (BI / 2) + j * 32 + l32)]);
 #pragma unroll
             for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -454,11 +370,10 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(Operand xo, int N, Operan
             }
         }
     if (do_db) {
-        const int grp = tid / (BO / 4);
-        dbs[grp][4 * xc4 + 0] = dbv[0];
-        dbs[grp][4 * xc4 + 1] = dbv[1];
-        dbs[grp][4 * xc4 + 2] = dbv[2];
-        dbs[grp][4 * xc4 + 3] = dbv[3];
+        dbs[xr][4 * xc4 + 0] = dbv[0];
+        dbs[xr][4 * xc4 + 1] = dbv[1];
+        dbs[xr][4 * xc4 + 2] = dbv[2];
+        dbs[xr][4 * xc4 + 3] = dbv[3];
         __syncthreads();
         if (tid < BO && n0 + tid < N) {
             float a = 0.f;
@@ -712,8 +627,8 @@ static inline unsigned ew_grid(long long total) {
 }
 
 template <int BM, int BN, int WM, int WN>
-static void launch_gemm(const GemmArgs& g, hipStream_t s) {
-    const dim3 grid((g.M + BM - 1) / BM, (g.N + BN - 1) / BN);
+static void launch_gemm(const GemmArgs& g, int gx, hipStream_t s) {
+    const dim3 grid(gx, (g.N + BN - 1) / BN);
     switch (g.a.mode) {
     case OP_PLAIN: hipLaunchKernelGGL((gemm_rows_kernel<BM, BN, WM, WN, OP_PLAIN>), grid, dim3(256), 0, s, g); break;
     case OP_BNACT: hipLaunchKernelGGL((gemm_rows_kernel<BM, BN, WM, WN, OP_BNACT>), grid, dim3(256), 0, s, g); break;
@@ -762,11 +677,30 @@ static void gemm_tile(int M, int N, int* bm, int* bn) {
     }
 }
 
+// Persistent grid of the row GEMM: as many row blocks per column tile as fit on the chip
+// at once (LDS-limited blocks per CU x 256 CUs), each walking its row tiles with the next
+// tile's first slab prefetched under the current tile's epilogue.  PCS_GEMM_PERSIST=0
+// restores one block per tile (for A/B timing).
+static int gemm_grid_x(int M, int N, int bm, int bn) {
+    static const int persist = [] { const char* e = getenv("PCS_GEMM_PERSIST"); return e ? atoi(e) : 1; }();
+    const int mtiles = (M + bm - 1) / bm;
+    if (!persist) return mtiles;
+    const int lds = 4 * (bm + bn) * 2 * GLDK + 16 * bn;         // As + Bs + red (bytes)
+    int per_cu = (160 * 1024) / lds;
+    per_cu = per_cu < 1 ? 1 : (per_cu > 4 ? 4 : per_cu);
+    const int ntiles = (N + bn - 1) / bn;
+    const int slots = (256 * per_cu + ntiles - 1) / ntiles;
+    if (mtiles <= slots) return mtiles;
+    const int tpb = (mtiles + slots - 1) / slots;
+    return (mtiles + tpb - 1) / tpb;
+}
+
 // number of row blocks the row GEMM uses for M rows and N outputs (sizes the stats workspace)
 PCS_API int pcs_gemm_row_blocks(int M, int N) {
+    if (engine_impl() == 1) return direct_row_blocks(M, N);
     int bm, bn;
     gemm_tile(M, N, &bm, &bn);
-    return (M + bm - 1) / bm;
+    return gemm_grid_x(M, N, bm, bn);
 }
 
 static int check_operand(const pcs_operand* o, int K, const char* who, const char* which) {
@@ -810,14 +744,16 @@ PCS_API int pcs_gemm_rows(const pcs_operand* a, int M, int K, const float* W, in
     if (M == 0) return 0;
     GemmArgs g{to_dev(a), M, K, W, ldw, bias, C, ldc, N, stats, to_dev(epi), bstats};
     hipStream_t s = as_stream(stream);
+    if (engine_impl() == 1 && launch_gemm_direct(g, s)) return launch_status("pcs_gemm_rows");
     int bm, bn;
     gemm_tile(M, N, &bm, &bn);
-    if (bn == 32) launch_gemm<128, 32, 4, 1>(g, s);
-    else if (bm == 128 && bn == 64) launch_gemm<128, 64, 4, 1>(g, s);
-    else if (bm == 128) launch_gemm<128, 128, 2, 2>(g, s);
-    else if (bm == 64 && bn == 128) launch_gemm<64, 128, 2, 2>(g, s);
-    else if (bm == 64) launch_gemm<64, 64, 2, 2>(g, s);
-    else launch_gemm<32, 128, 1, 4>(g, s);
+    const int gx = gemm_grid_x(M, N, bm, bn);
+    if (bn == 32) launch_gemm<128, 32, 4, 1>(g, gx, s);
+    else if (bm == 128 && bn == 64) launch_gemm<128, 64, 4, 1>(g, gx, s);
+    else if (bm == 128) launch_gemm<128, 128, 2, 2>(g, gx, s);
+    else if (bm == 64 && bn == 128) launch_gemm<64, 128, 2, 2>(g, gx, s);
+    else if (bm == 64) launch_gemm<64, 64, 2, 2>(g, gx, s);
+    else launch_gemm<32, 128, 1, 4>(g, gx, s);
     return launch_status("pcs_gemm_rows");
 }
 
@@ -831,6 +767,9 @@ PCS_API int pcs_wgrad(const pcs_operand* x, int N, const pcs_operand* y, int K, 
     PCS_CHECK_ARG(y->mode <= PCS_OP_BNACT, "pcs_wgrad: Y operand must be PLAIN or BNACT");
     PCS_CHECK_ARG(dW && N % 4 == 0, "pcs_wgrad: dW null or N not a multiple of 4");
     if (M == 0) return 0;
+    if (engine_impl() == 1 &&
+        launch_wgrad_direct(to_dev(x), N, to_dev(y), K, M, dW, db, as_stream(stream)))
+        return launch_status("pcs_wgrad");
     const int BO = N > 64 ? 128 : 64, BI = K > 64 ? 128 : 64;
     const int tiles = ((N + BO - 1) / BO) * ((K + BI - 1) / BI);
     int splits = (1024 + tiles - 1) / tiles;

@@ -1,0 +1,134 @@
+// Shared definitions of the shared-MLP engine kernels (mlp.hip, gemm_direct.hip):
+// operand descriptors with their on-load transforms and the row-GEMM argument block.
+#pragma once
+
+#include "pcs_common.hpp"
+
+namespace pcs {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+enum { ACT_RELU = 0, ACT_LRELU = 1, ACT_NONE = 2 };
+
+// The activation is folded into one slope at the ABI boundary (eff_slope): ReLU = 0,
+// LeakyReLU = its slope, identity = 1; both functions are branch-free selects.
+// derivative as autograd computes it: relu -> (result > 0); leaky_relu -> (input > 0 ? 1 : slope)
+__device__ __forceinline__ float act_f(float y, int, float slope) { return y > 0.f ? y : y * slope; }
+__device__ __forceinline__ float dact_f(float y, int, float slope) { return y > 0.f ? 1.f : slope; }
+
+static inline float eff_slope(int act, float slope) {
+    return act == ACT_RELU ? 0.f : act == ACT_LRELU ? slope : 1.f;
+}
+
+// Operand descriptor (layout-identical to pcs_operand in include/pcseg.h).  The
+// value fed to the MFMA for channel c of row r is
+//   PLAIN   : data[r][c]
+//   BNACT   : act(data[r][c]*s[c] + t[c])                  (forward: previous layer's BN + act)
+//   BNBWD   : s*dy - kb - alpha*(z - mean),  dy = data[r][c]*act'(z*s+t), z = Z[r][c]
+//   POOLBWD : as BNBWD with data[r][c] = (arg[g][c] == k) ? dpool[g][c] : 0, g = r / pool_k, k = r % pool_k
+// i.e. BNBWD/POOLBWD rebuild the layer's dZ (BatchNorm backward) on the fly from its
+// output gradient and pre-BN Z, so dZ is never written to HBM.
+struct Operand {
+    const float* data; int ld; int mode;
+    const float* s; const float* t; int act; float slope;
+    const float* z; int ldz;
+    const float* mean; const float* inv; const float* alpha; const float* kb;
+    const unsigned char* arg; int pool_k;
+};
+enum { OP_PLAIN = 0, OP_BNACT = 1, OP_BNBWD = 2, OP_POOLBWD = 3 };
+
+// per-channel coefficients of a transform, for 4 consecutive channels
+struct Quad {
+    float4 s, t, mean, alpha, kb;
+};
+
+// transform modes require K % 4 == 0 (checked at the ABI), so a channel quad is all in or all
+// out.  Loads use clamped (always in-bounds) addresses and selects instead of branches, so
+// the compiler keeps the next slab's loads in flight under the current slab's MFMAs.
+template <int MODE>
+__device__ __forceinline__ void load_quad(const Operand& o, int c, int K, Quad& q) {
+    const int cc = c < K ? c : 0;          // the out-of-range quad is zeroed in xform4
+    if (MODE >= OP_BNACT) {
+        q.s = *reinterpret_cast<const float4*>(o.s + cc);
+        q.t = *reinterpret_cast<const float4*>(o.t + cc);
+    }
+    if (MODE >= OP_BNBWD) {
+        q.mean = *reinterpret_cast<const float4*>(o.mean + cc);
+        q.alpha = *reinterpret_cast<const float4*>(o.alpha + cc);
+        q.kb = *reinterpret_cast<const float4*>(o.kb + cc);
+    }
+}
+
+// raw global loads of one float4 at (row r, channels c..c+3); r and c must be in bounds
+// (callers clamp).  POOLBWD: v = dpool[g][c..], a = the 4 argmax bytes; z only for BNBWD/POOLBWD.
+template <int MODE>
+__device__ __forceinline__ void load_raw(const Operand& o, int r, int c, float4& v, float4& z, unsigned& a) {
+    if (MODE == OP_POOLBWD) {
+        const int g = r / o.pool_k;
+        v = *reinterpret_cast<const float4*>(o.data + (size_t)g * o.ld + c);
+        a = *reinterpret_cast<const unsigned*>(o.arg + (size_t)g * o.ld + c);
+    } else {
+        v = *reinterpret_cast<const float4*>(o.data + (size_t)r * o.ld + c);
+    }
+    if (MODE >= OP_BNBWD) z = *reinterpret_cast<const float4*>(o.z + (size_t)r * o.ldz + c);
+}
+
+template <int MODE>
+__device__ __forceinline__ float xform1(const Operand& o, float v, float z, float s, float t, float mean, float alpha,
+                                        float kb) {
+    if (MODE == OP_BNACT) return act_f(v * s + t, o.act, o.slope);
+    if (MODE >= OP_BNBWD) {
+        const float dy = v * dact_f(z * s + t, o.act, o.slope);
+        return s * dy - kb - alpha * (z - mean);
+    }
+    return v;
+}
+
+// transformed float4 of row r: channels at or beyond K give 0 (per element for PLAIN,
+// whose K need not be a multiple of 4); POOLBWD keeps dpool only where argmax == r % pool_k
+template <int MODE>
+__device__ __forceinline__ float4 xform4(const Operand& o, float4 v, float4 z, unsigned a, int r, const Quad& q,
+                                         int c, int K) {
+    if (MODE == OP_PLAIN) {
+        v.x = c + 0 < K ? v.x : 0.f;
+        v.y = c + 1 < K ? v.y : 0.f;
+        v.z = c + 2 < K ? v.z : 0.f;
+        v.w = c + 3 < K ? v.w : 0.f;
+        return v;
+    }
+    if (MODE == OP_POOLBWD) {
+        const unsigned k = (unsigned)(r - (r / o.pool_k) * o.pool_k);
+        v.x = (a & 0xffu) == k ? v.x : 0.f;
+        v.y = ((a >> 8) & 0xffu) == k ? v.y : 0.f;
+        v.z = ((a >> 16) & 0xffu) == k ? v.z : 0.f;
+        v.w = (a >> 24) == k ? v.w : 0.f;
+    }
+    float4 out;
+    out.x = xform1<MODE>(o, v.x, z.x, q.s.x, q.t.x, q.mean.x, q.alpha.x, q.kb.x);
+    out.y = xform1<MODE>(o, v.y, z.y, q.s.y, q.t.y, q.mean.y, q.alpha.y, q.kb.y);
+    out.z = xform1<MODE>(o, v.z, z.z, q.s.z, q.t.z, q.mean.z, q.alpha.z, q.kb.z);
+    out.w = xform1<MODE>(o, v.w, z.w, q.s.w, q.t.w, q.mean.w, q.alpha.w, q.kb.w);
+    const bool in = c < K;
+    return in ? out : make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+struct GemmArgs {
+    Operand a; int M; int K;                   // A rows (M x K) through its transform
+    const float* W; int ldw;                   // B[k][n] = W[n*ldw + k]
+    const float* bias;                         // per n (or null)
+    float* C; int ldc; int N;                  // output rows (M x N)
+    double* stats;                             // [2][N][gridDim.x]: sum, sum of squares of C (or null)
+    // fused BN-backward reduce of the layer whose OUTPUT space C lives in (dgrad epilogue):
+    // uses e.z (its pre-BN Z, M x N), e.s, e.t, e.mean, e.inv, e.act, e.slope
+    Operand e;
+    double* bstats;                            // [2][N][gridDim.x]: sum dy, sum dy*xhat (or null)
+};
+
+// LDS-free kernels (gemm_direct.hip); return false when the shape is not covered
+bool launch_gemm_direct(const GemmArgs& g, hipStream_t s);
+bool launch_wgrad_direct(const Operand& x, int N, const Operand& y, int K, int M, float* dW, float* db,
+                         hipStream_t s);
+int direct_row_blocks(int M, int N);
+int engine_impl();   // 0 = LDS-staged kernels, 1 = LDS-free (PCS_GEMM_IMPL)
+
+}  // namespace pcs

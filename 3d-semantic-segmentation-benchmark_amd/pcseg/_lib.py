@@ -49,6 +49,7 @@ SIGNATURES = {
     'pcs_edge_bwd': [P, I32, P, I32, I32, I32, I32, P, P],
     # shared-MLP engine
     'pcs_gemm_row_blocks': [I32, I32],
+    'pcs_engine_select': [I32],
     'pcs_operand_size': [],
     'pcs_gemm_rows': [OPP, I32, I32, P, I32, P, P, I32, I32, P, OPP, P, P],
     'pcs_wgrad': [OPP, I32, OPP, I32, I32, P, P, P],

@@ -121,6 +121,10 @@ typedef struct pcs_operand {
     const uint8_t* arg; int pool_k;
 } pcs_operand;
 
+/* engine GEMM kernels: 0 = LDS-staged persistent (default), 1 = LDS-free.
+ * Process-wide tuning/testing knob (also env PCS_GEMM_IMPL); call it only while
+ * no engine work is being enqueued.  pcs_gemm_row_blocks depends on it. */
+int pcs_engine_select(int impl);
 /* row blocks of pcs_gemm_rows (sizes its stats/bstats workspace) */
 int pcs_gemm_row_blocks(int M, int N);
 /* C (M x N, ldc) = T(A) . W^T (+bias), W row-major N x K with row stride ldw.

@@ -21,7 +21,10 @@ SHAPES = [  # (name, M, K, N)
 ]
 
 
-def timeit(fn, reps=10):
+REPS = int(os.environ.get('GEMM_REPS', '10'))
+
+
+def timeit(fn, reps=REPS):
     for _ in range(2):
         fn()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -57,5 +60,17 @@ for name, M, K, N in SHAPES:
     xop = operand(C, N, OP_BNBWD, sN, tN, 0, 0.0, Z, N, mN, None, aN, kN)
     wg = lambda: wgrad(xop, N, aop, K, M, dW, db, st)  # noqa
     ms2 = timeit(wg)
+    # dgrad: dA (M x K) = dZ(M x N, rebuilt from C and Z) . W, epilogue = previous layer's BN-backward sums
+    if K % 4 == 0:
+        Wt = W[:, :K].t().contiguous()
+        dA = torch.empty(M, K, device=dev)
+        ZK = torch.randn(M, K, device=dev)
+        bpart = torch.empty(2, K, load().pcs_gemm_row_blocks(M, K), dtype=torch.float64, device=dev)
+        epi = operand(None, 0, OP_BNBWD, s, t, 0, 0.0, ZK, K, torch.randn(K, device=dev), torch.rand(K, device=dev))
+        dg = lambda: gemm_rows(xop, M, N, Wt, N, None, dA, K, K, None, epi, bpart, st=st)  # noqa
+        ms3 = timeit(dg)
+        dgs = f'{ms3*1e3:8.1f} us {fl/ms3/1e9:6.1f} TF/s'
+    else:
+        dgs = '       -'
     print(f'{name:8s} M={M:8d} K={K:5d} N={N:5d}  fwd {ms*1e3:8.1f} us {fl/ms/1e9:6.1f} TF/s {by/ms/1e6:6.0f} GB/s'
-          f' | wgrad {ms2*1e3:8.1f} us {fl/ms2/1e9:6.1f} TF/s', flush=True)
+          f' | dgrad {dgs} | wgrad {ms2*1e3:8.1f} us {fl/ms2/1e9:6.1f} TF/s', flush=True)

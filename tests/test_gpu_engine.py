@@ -1,0 +1,156 @@
+"""Engine GEMMs (pcs_gemm_rows / pcs_wgrad) against a float64 torch reference of the
+same op, for every operand transform (PLAIN, BNACT, BNBWD, POOLBWD), the fused
+BN-statistics / BN-backward epilogues, ragged M / K / N, and both kernel families
+(0 = LDS-staged persistent, the default; 1 = LDS-free register-pipelined) selected through pcs_engine_select.
+
+Tolerance: fp32 MFMA accumulation vs the fp64 reference, norm-relative 2e-6 * sqrt(K)
+(plus 1e-5 absolute slack for the near-zero BN-backward sums)."""
+import math
+
+import pytest
+import torch
+
+from pcseg._lib import load, stream_ptr, OP_PLAIN, OP_BNACT, OP_BNBWD, OP_POOLBWD
+from pcseg.engine import operand, gemm_rows, wgrad, ld4
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda'
+
+
+@pytest.fixture(params=[1, 0], ids=['direct', 'lds'])
+def impl(request):
+    lib = load()
+    assert lib.pcs_engine_select(request.param) == 0
+    yield request.param
+    lib.pcs_engine_select(0)
+
+
+def act(v, slope):
+    return torch.where(v > 0, v, v * slope)
+
+
+def dact(v, slope):
+    return torch.where(v > 0, torch.ones_like(v), torch.full_like(v, slope))
+
+
+def rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+
+class Xform:
+    """Inputs of one operand transform and its float64 evaluation."""
+
+    def __init__(self, mode, M, K, ld, slope, pool_k=0, g=None):
+        self.mode, self.M, self.K, self.ld, self.slope, self.pool_k = mode, M, K, ld, slope, pool_k
+        rows = M // pool_k if mode == OP_POOLBWD else M
+        self.data = torch.randn(rows, ld, device=DEV, generator=g)
+        self.s = (torch.rand(K, device=DEV, generator=g) + 0.5)
+        self.t = torch.randn(K, device=DEV, generator=g) * 0.3
+        self.z = torch.randn(M, ld, device=DEV, generator=g)
+        self.mean = torch.randn(K, device=DEV, generator=g) * 0.1
+        self.alpha = torch.randn(K, device=DEV, generator=g) * 0.05
+        self.kb = torch.randn(K, device=DEV, generator=g) * 0.05
+        self.arg = torch.randint(0, max(pool_k, 1), (rows, ld), device=DEV, dtype=torch.uint8, generator=g)
+
+    def op(self):
+        if self.mode == OP_PLAIN:
+            return operand(self.data, self.ld)
+        if self.mode == OP_BNACT:
+            return operand(self.data, self.ld, OP_BNACT, self.s, self.t, 1, self.slope)
+        return operand(self.data, self.ld, self.mode, self.s, self.t, 1, self.slope, self.z, self.ld, self.mean,
+                       None, self.alpha, self.kb, self.arg if self.mode == OP_POOLBWD else None, self.pool_k)
+
+    def value(self):
+        K = self.K
+        d = self.data.double()[:, :K]
+        if self.mode == OP_PLAIN:
+            return d
+        s, t = self.s.double(), self.t.double()
+        if self.mode == OP_BNACT:
+            return act(d * s + t, self.slope)
+        if self.mode == OP_POOLBWD:
+            r = torch.arange(self.M, device=DEV)
+            gsel = r // self.pool_k
+            kk = (r % self.pool_k).to(torch.uint8)
+            d = torch.where(self.arg[gsel, :K] == kk[:, None], d[gsel], torch.zeros_like(d[gsel]))
+        z = self.z.double()[:, :K]
+        dy = d * dact(z * s + t, self.slope)
+        return s * dy - self.kb.double() - self.alpha.double() * (z - self.mean.double())
+
+
+SHAPES = [  # M, K, N
+    (1000, 9, 32), (4099, 32, 64), (2048, 67, 64), (3000, 128, 128), (515, 259, 256), (777, 384, 512),
+    (128, 1408, 96), (64, 20, 36), (131073, 32, 64), (70001, 128, 128), (300000, 12, 32),
+]
+
+
+@pytest.mark.parametrize('M,K,N', SHAPES)
+@pytest.mark.parametrize('mode', [OP_PLAIN, OP_BNACT, OP_BNBWD, OP_POOLBWD])
+def test_gemm_rows_vs_fp64(impl, M, K, N, mode):
+    if mode != OP_PLAIN and K % 4:
+        pytest.skip('transform modes need K % 4 == 0')
+    pool_k = 0
+    if mode == OP_POOLBWD:
+        pool_k = 16 if M % 16 == 0 else (4 if M % 4 == 0 else 1)
+    g = torch.Generator(device=DEV).manual_seed(M * 7 + K * 3 + N + mode)
+    lda = ld4(K)
+    x = Xform(mode, M, K, lda, 0.2, pool_k, g)
+    W = torch.zeros(N, lda, device=DEV)
+    W[:, :K] = torch.randn(N, K, device=DEV, generator=g) / math.sqrt(K)
+    bias = torch.randn(N, device=DEV, generator=g)
+    C = torch.full((M, N), float('nan'), device=DEV)
+    nb = load().pcs_gemm_row_blocks(M, N)
+    part = torch.empty(2, N, nb, dtype=torch.float64, device=DEV)
+    st = stream_ptr(torch.device(DEV))
+    gemm_rows(x.op(), M, K, W, lda, bias, C, N, N, part, st=st)
+    ref = x.value() @ W.double()[:, :K].t() + bias.double()
+    tol = 2e-6 * math.sqrt(K)
+    assert rel(C, ref) <= tol
+    sums = part.sum(-1)
+    assert rel(sums[0], ref.sum(0)) <= tol + 1e-6
+    assert rel(sums[1], (ref * ref).sum(0)) <= tol
+
+    # dgrad form: same A operand, BN-backward epilogue of a layer whose pre-BN output is ze
+    if N % 4 == 0:
+        ze = torch.randn(M, N, device=DEV, generator=g)
+        se, te = torch.rand(N, device=DEV, generator=g) + 0.5, torch.randn(N, device=DEV, generator=g) * 0.3
+        me, ie = torch.randn(N, device=DEV, generator=g) * 0.1, torch.rand(N, device=DEV, generator=g) + 0.5
+        epi = operand(None, 0, OP_BNBWD, se, te, 1, 0.2, ze, N, me, ie)
+        bpart = torch.empty(2, N, nb, dtype=torch.float64, device=DEV)
+        C2 = torch.empty(M, N, device=DEV)
+        gemm_rows(x.op(), M, K, W, lda, None, C2, N, N, None, epi, bpart, st=st)
+        ref2 = x.value() @ W.double()[:, :K].t()
+        assert rel(C2, ref2) <= tol
+        dy = ref2 * dact(ze.double() * se.double() + te.double(), 0.2)
+        xh = (ze.double() - me.double()) * ie.double()
+        bs = bpart.sum(-1)
+        assert rel(bs[0], dy.sum(0)) <= tol + 1e-5
+        assert rel(bs[1], (dy * xh).sum(0)) <= tol + 1e-5
+
+
+WSHAPES = [  # M rows, N (dZ channels), K (input channels)
+    (5000, 32, 9), (4099, 64, 32), (3000, 128, 67), (2100, 256, 128), (1030, 512, 259), (640, 96, 1408),
+    (100, 36, 20),
+]
+
+
+@pytest.mark.parametrize('M,N,K', WSHAPES)
+@pytest.mark.parametrize('xmode,ymode', [(OP_PLAIN, OP_PLAIN), (OP_BNBWD, OP_BNACT), (OP_POOLBWD, OP_BNACT),
+                                         (OP_BNBWD, OP_PLAIN)])
+def test_wgrad_vs_fp64(impl, M, N, K, xmode, ymode):
+    if ymode == OP_BNACT and K % 4:
+        pytest.skip('BNACT needs K % 4 == 0')
+    pool_k = 0
+    if xmode == OP_POOLBWD:
+        pool_k = 20 if M % 20 == 0 else (4 if M % 4 == 0 else 1)
+    g = torch.Generator(device=DEV).manual_seed(M + 11 * N + 5 * K + xmode * 3 + ymode)
+    x = Xform(xmode, M, N, ld4(N), 0.2, pool_k, g)
+    y = Xform(ymode, M, K, ld4(K), 0.0, 0, g)
+    dW = torch.zeros(N, K, device=DEV)
+    db = torch.zeros(N, device=DEV)
+    wgrad(x.op(), N, y.op(), K, M, dW, db, stream_ptr(torch.device(DEV)))
+    X, Y = x.value(), y.value()
+    tol = 2e-6 * math.sqrt(M)
+    assert rel(dW, X.t() @ Y) <= tol
+    assert rel(db, X.sum(0)) <= tol
