@@ -1,0 +1,307 @@
+// Native orchestration of a shared-MLP stack: one ABI call runs a whole
+// conv1x1 -> BatchNorm -> act [-> max over K] stack forward (or backward), so the
+// host pays one call per MiniPointNet / UnitPointNet / EdgeConv / DGCNN conv block
+// instead of one Python round trip per kernel.
+//
+// Reference semantics: MiniPointNet / UnitPointNet (models/utils/common.py:125-178)
+// followed by reduce(..., 'max') (common.py:211-212), EdgeConv (models/dgcnn/dgcnn.py:
+// 67-76), DGCNN conv5..conv7 (dgcnn.py:188-207); nn.BatchNorm train/eval semantics
+// (batch statistics + running-stat update with the unbiased variance, or running
+// statistics in eval mode).
+//
+// The kernels are the engine's (mlp.hip / gemm_direct.hip): forward per layer = one
+// row GEMM with the previous layer's BN+act applied on load and fp64 BN partials in
+// its epilogue + one finalize; backward per layer = one wgrad + one dgrad whose
+// epilogue already reduces the previous layer's BN-backward sums + one finalize.
+// Scratch comes from a caller-provided workspace (pcs_mlp_workspace bytes).
+#include "mlp_common.hpp"
+
+#include <algorithm>
+
+namespace pcs {
+
+// eval-mode BatchNorm: s = gamma * rsqrt(var + eps), t = beta - mean * s, from running stats
+__global__ __launch_bounds__(256) void bn_eval_coef_kernel(const float* __restrict__ rm, const float* __restrict__ rv,
+                                                           const float* __restrict__ gamma,
+                                                           const float* __restrict__ beta, float eps, int N,
+                                                           float* __restrict__ coef) {
+    const int n = blockIdx.x * 256 + threadIdx.x;
+    if (n >= N) return;
+    const float inv = 1.0f / sqrtf(rv[n] + eps);
+    const float m = rm[n];
+    const float sc = (gamma ? gamma[n] : 1.f) * inv;
+    coef[n] = sc;
+    coef[N + n] = (beta ? beta[n] : 0.f) - m * sc;
+    coef[2 * N + n] = m;
+    coef[3 * N + n] = inv;
+}
+
+// out (cols x rows) = in (rows x cols, row stride ld)^T ; out row stride = rows
+__global__ __launch_bounds__(256) void transpose_kernel(const float* __restrict__ in, int rows, int cols, int ld,
+                                                        float* __restrict__ out) {
+    __shared__ float tile[32][33];
+    const int r0 = blockIdx.y * 32, c0 = blockIdx.x * 32;
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+    for (int y = ty; y < 32; y += 8) {
+        const int r = r0 + y, c = c0 + tx;
+        tile[y][tx] = (r < rows && c < cols) ? in[(size_t)r * ld + c] : 0.f;
+    }
+    __syncthreads();
+    for (int y = ty; y < 32; y += 8) {
+        const int c = c0 + y, r = r0 + tx;
+        if (c < cols && r < rows) out[(size_t)c * rows + r] = tile[tx][y];
+    }
+}
+
+__global__ __launch_bounds__(256) void zero_kernel(float* __restrict__ p, long long n) {
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) p[i] = 0.f;
+}
+
+static void zero_f32(float* p, long long n, hipStream_t st) {
+    if (n <= 0) return;
+    long long g = (n + 255) / 256;
+    if (g > 4096) g = 4096;
+    hipLaunchKernelGGL(zero_kernel, dim3((unsigned)g), dim3(256), 0, st, p, n);
+}
+
+// ---------------------------------------------------------------- workspace carving
+struct Carve {
+    char* base;
+    size_t used, cap;
+    template <typename T>
+    T* take(size_t count) {
+        const size_t off = (used + 255) & ~size_t(255);
+        used = off + count * sizeof(T);
+        return base ? reinterpret_cast<T*>(base + off) : nullptr;
+    }
+};
+
+static int max_cout(const pcs_mlp_layer* L, int nl) {
+    int m = 4;
+    for (int l = 0; l < nl; ++l) m = (int)L[l].cout > m ? (int)L[l].cout : m;
+    return m;
+}
+
+// partial-sum entries (doubles) the finalize of every stage needs, maximum over stages
+static size_t max_partials(int M, int kin, const pcs_mlp_layer* L, int nl, int pool_k, bool backward) {
+    size_t m = 0;
+    for (int l = 0; l < nl; ++l) {
+        const size_t c = (size_t)L[l].cout;
+        m = std::max(m, 2 * c * (size_t)pcs_gemm_row_blocks(M, (int)c));
+    }
+    if (backward) {
+        const size_t c = (size_t)L[nl - 1].cout;
+        const size_t nb = pool_k ? (size_t)pcs_pool_bwd_reduce_blocks(M / pool_k) : (size_t)pcs_bn_bwd_reduce_blocks(M);
+        m = std::max(m, 2 * c * nb);
+    }
+    (void)kin;
+    return m;
+}
+
+struct BwdScratch {
+    double* part;
+    float* kb[2];
+    float* alpha[2];
+    float* wt;
+    float* dA[2];
+};
+
+static size_t carve_backward(Carve& cv, int M, int kin, int ldx, const pcs_mlp_layer* L, int nl, int pool_k,
+                             BwdScratch* out) {
+    const int mc = std::max(max_cout(L, nl), ldx);
+    BwdScratch s{};
+    s.part = cv.take<double>(max_partials(M, kin, L, nl, pool_k, true));
+    for (int i = 0; i < 2; ++i) { s.kb[i] = cv.take<float>(mc); s.alpha[i] = cv.take<float>(mc); }
+    size_t wt = 0, da = 0;
+    for (int l = 0; l < nl; ++l) {
+        wt = std::max(wt, (size_t)L[l].cout * (size_t)L[l].ldw);
+        if (l > 0) da = std::max(da, (size_t)M * (size_t)L[l].cin);
+    }
+    s.wt = cv.take<float>(wt);
+    s.dA[0] = cv.take<float>(da);
+    s.dA[1] = cv.take<float>(da);
+    if (out) *out = s;
+    return cv.used;
+}
+
+static pcs_operand plain_op(const float* data, int ld) {
+    pcs_operand o{};
+    o.data = data; o.ld = ld; o.mode = PCS_OP_PLAIN;
+    return o;
+}
+
+static pcs_operand bnact_op(const float* data, int ld, const pcs_mlp_layer& P) {
+    pcs_operand o = plain_op(data, ld);
+    o.mode = PCS_OP_BNACT;
+    o.s = P.coef; o.t = P.coef + P.cout; o.act = (int)P.act; o.slope = (float)P.slope;
+    return o;
+}
+
+// BN-backward operand of layer P (its dZ rebuilt from output gradient `dy` and P.Z)
+static pcs_operand bnbwd_op(const float* dy, int ld, const pcs_mlp_layer& P, const float* alpha, const float* kb) {
+    pcs_operand o = bnact_op(dy, ld, P);
+    o.mode = PCS_OP_BNBWD;
+    o.z = P.Z; o.ldz = (int)P.cout;
+    o.mean = P.coef + 2 * P.cout; o.inv = P.coef + 3 * P.cout;
+    o.alpha = alpha; o.kb = kb;
+    return o;
+}
+
+static int check_layers(int M, int kin, int ldx, const pcs_mlp_layer* L, int nl, int pool_k, const char* who) {
+    PCS_CHECK_ARG(M >= 0 && kin >= 1 && ldx >= kin && ldx % 4 == 0 && L && nl >= 1,
+                  "%s: bad sizes M=%d kin=%d ldx=%d nl=%d", who, M, kin, ldx, nl);
+    PCS_CHECK_ARG(pool_k == 0 || (pool_k >= 1 && pool_k <= 256 && M % pool_k == 0),
+                  "%s: pool_k=%d must divide M=%d and be <= 256", who, pool_k, M);
+    int cin = kin;
+    for (int l = 0; l < nl; ++l) {
+        PCS_CHECK_ARG(L[l].W && L[l].Z && L[l].coef, "%s: layer %d: W/Z/coef missing", who, l);
+        PCS_CHECK_ARG(L[l].cin == cin, "%s: layer %d: cin=%lld, expected %d", who, l, (long long)L[l].cin, cin);
+        PCS_CHECK_ARG(L[l].cout >= 4 && L[l].cout % 4 == 0, "%s: layer %d: cout=%lld must be a multiple of 4", who,
+                      l, (long long)L[l].cout);
+        PCS_CHECK_ARG(L[l].ldw >= L[l].cin && L[l].ldw % 4 == 0, "%s: layer %d: ldw=%lld", who, l,
+                      (long long)L[l].ldw);
+        PCS_CHECK_ARG(L[l].use_batch || (L[l].run_mean && L[l].run_var),
+                      "%s: layer %d: eval-mode BatchNorm needs running statistics", who, l);
+        PCS_CHECK_ARG(L[l].act >= 0 && L[l].act <= 2, "%s: layer %d: act=%lld", who, l, (long long)L[l].act);
+        cin = (int)L[l].cout;
+    }
+    return 0;
+}
+
+}  // namespace pcs
+
+using namespace pcs;
+
+PCS_API int pcs_mlp_workspace(int M, int kin, int ldx, const pcs_mlp_layer* layers, int nl, int pool_k, int backward,
+                              size_t* bytes) {
+    if (int e = check_layers(M, kin, ldx, layers, nl, pool_k, "pcs_mlp_workspace")) return e;
+    PCS_CHECK_ARG(bytes, "pcs_mlp_workspace: null bytes");
+    Carve cv{nullptr, 0, 0};
+    if (backward) carve_backward(cv, M, kin, ldx, layers, nl, pool_k, nullptr);
+    else cv.take<double>(max_partials(M, kin, layers, nl, pool_k, false));
+    *bytes = cv.used + 256;
+    return 0;
+}
+
+PCS_API int pcs_mlp_forward(const float* X, int ldx, int kin, int M, pcs_mlp_layer* layers, int nl, int pool_k,
+                            float* out, uint8_t* arg, void* ws, size_t ws_bytes, void* stream) {
+    if (int e = check_layers(M, kin, ldx, layers, nl, pool_k, "pcs_mlp_forward")) return e;
+    PCS_CHECK_ARG(X && out && (!pool_k || arg), "pcs_mlp_forward: null pointer");
+    if (M == 0) return 0;
+    hipStream_t st = as_stream(stream);
+    Carve cv{static_cast<char*>(ws), 0, ws_bytes};
+    double* part = cv.take<double>(max_partials(M, kin, layers, nl, pool_k, false));
+    PCS_CHECK_ARG(ws && cv.used <= ws_bytes, "pcs_mlp_forward: workspace too small (%zu < %zu)", ws_bytes, cv.used);
+
+    const float* A = X;
+    int lda = ldx, K = kin;
+    for (int l = 0; l < nl; ++l) {
+        pcs_mlp_layer& P = layers[l];
+        const int C = (int)P.cout;
+        const pcs_operand a = l == 0 ? plain_op(A, lda) : bnact_op(A, lda, layers[l - 1]);
+        float* s = P.coef;
+        if (P.use_batch) {
+            const int nb = pcs_gemm_row_blocks(M, C);
+            if (int e = pcs_gemm_rows(&a, M, K, P.W, (int)P.ldw, P.bias, P.Z, C, C, part, nullptr, nullptr, stream))
+                return e;
+            const bool track = P.run_mean != nullptr;
+            bn_finalize_launch(part, nb, C, M, P.gamma, P.beta, (float)P.eps, track ? (float)P.momentum : 0.f,
+                               P.run_mean, P.run_var, s, s + C, s + 2 * C, s + 3 * C,
+                               reinterpret_cast<long long*>(P.num_batches), st);
+        } else {
+            if (int e = pcs_gemm_rows(&a, M, K, P.W, (int)P.ldw, P.bias, P.Z, C, C, nullptr, nullptr, nullptr, stream))
+                return e;
+            hipLaunchKernelGGL(bn_eval_coef_kernel, dim3((C + 255) / 256), dim3(256), 0, st, P.run_mean, P.run_var,
+                               P.gamma, P.beta, (float)P.eps, C, s);
+        }
+        A = P.Z; lda = C; K = C;
+    }
+    const pcs_mlp_layer& T = layers[nl - 1];
+    const int C = (int)T.cout;
+    if (pool_k)
+        return pcs_pool_fwd(T.Z, C, M / pool_k, pool_k, T.coef, T.coef + C, (int)T.act, (float)T.slope, out, arg,
+                            stream);
+    return pcs_bn_act(T.Z, C, M, C, T.coef, T.coef + C, (int)T.act, (float)T.slope, out, C, stream);
+}
+
+PCS_API int pcs_mlp_backward(const float* X, int ldx, int kin, int M, const pcs_mlp_layer* layers, int nl,
+                             int pool_k, const uint8_t* arg, const float* gout, float* dX, void* ws, size_t ws_bytes,
+                             void* stream) {
+    if (int e = check_layers(M, kin, ldx, layers, nl, pool_k, "pcs_mlp_backward")) return e;
+    PCS_CHECK_ARG(X && gout && (!pool_k || arg), "pcs_mlp_backward: null pointer");
+    if (M == 0) return 0;
+    hipStream_t st = as_stream(stream);
+    Carve cv{static_cast<char*>(ws), 0, ws_bytes};
+    BwdScratch S;
+    carve_backward(cv, M, kin, ldx, layers, nl, pool_k, &S);
+    PCS_CHECK_ARG(ws && cv.used <= ws_bytes, "pcs_mlp_backward: workspace too small (%zu < %zu)", ws_bytes, cv.used);
+
+    // ---- top layer: BN-backward sums of its output gradient
+    const pcs_mlp_layer& T = layers[nl - 1];
+    const int CL = (int)T.cout;
+    const float* sT = T.coef;
+    int nb;
+    if (pool_k) {
+        const long long G = M / pool_k;
+        nb = pcs_pool_bwd_reduce_blocks(G);
+        if (int e = pcs_pool_bwd_reduce(gout, arg, T.Z, CL, G, pool_k, sT, sT + CL, sT + 2 * CL, sT + 3 * CL,
+                                        (int)T.act, (float)T.slope, S.part, stream))
+            return e;
+    } else {
+        nb = pcs_bn_bwd_reduce_blocks(M);
+        if (int e = pcs_bn_bwd_reduce(gout, CL, T.Z, CL, M, CL, sT, sT + CL, sT + 2 * CL, sT + 3 * CL, (int)T.act,
+                                      (float)T.slope, S.part, stream))
+            return e;
+    }
+    int pp = 0;
+    if (int e = pcs_bn_bwd_finalize(S.part, nb, CL, M, sT, sT + 3 * CL, T.dgamma, T.dbeta, S.kb[pp], S.alpha[pp], 1,
+                                    stream))
+        return e;
+    if (!T.use_batch) { zero_f32(S.kb[pp], CL, st); zero_f32(S.alpha[pp], CL, st); }
+    // the top layer's dZ is never materialised: both consumers rebuild it on load
+    pcs_operand xop = bnbwd_op(gout, CL, T, S.alpha[pp], S.kb[pp]);
+    if (pool_k) { xop.mode = PCS_OP_POOLBWD; xop.arg = arg; xop.pool_k = pool_k; }
+
+    int da = 0;
+    for (int l = nl - 1; l >= 0; --l) {
+        const pcs_mlp_layer& P = layers[l];
+        const int C = (int)P.cout, Cin = (int)P.cin;
+        if (P.dW) {
+            if (l > 0) {
+                const pcs_mlp_layer& Q = layers[l - 1];
+                const pcs_operand y = bnact_op(Q.Z, Cin, Q);
+                if (int e = pcs_wgrad(&xop, C, &y, Cin, M, P.dW, P.db, stream)) return e;
+            } else {
+                const pcs_operand y = plain_op(X, ldx);
+                if (int e = pcs_wgrad(&xop, C, &y, kin, M, P.dW, P.db, stream)) return e;
+            }
+        }
+        if (l == 0 && !dX) break;
+        // dgrad B operand: B[k = cout][n = cin] = Wt[n][k], Wt = W^T (cin x cout)
+        {
+            const dim3 g((Cin + 31) / 32, (C + 31) / 32);
+            hipLaunchKernelGGL(transpose_kernel, g, dim3(256), 0, st, P.W, C, Cin, (int)P.ldw, S.wt);
+        }
+        if (l > 0) {
+            const pcs_mlp_layer& Q = layers[l - 1];
+            float* dA = S.dA[da];
+            const int nbg = pcs_gemm_row_blocks(M, Cin);
+            pcs_operand epi = bnbwd_op(nullptr, 0, Q, nullptr, nullptr);
+            if (int e = pcs_gemm_rows(&xop, M, C, S.wt, C, nullptr, dA, Cin, Cin, nullptr, &epi, S.part, stream))
+                return e;
+            pp ^= 1;
+            const float* sq = Q.coef;
+            if (int e = pcs_bn_bwd_finalize(S.part, nbg, Cin, M, sq, sq + 3 * Cin, Q.dgamma, Q.dbeta, S.kb[pp],
+                                            S.alpha[pp], 1, stream))
+                return e;
+            if (!Q.use_batch) { zero_f32(S.kb[pp], Cin, st); zero_f32(S.alpha[pp], Cin, st); }
+            xop = bnbwd_op(dA, Cin, Q, S.alpha[pp], S.kb[pp]);
+            da ^= 1;
+        } else {
+            if (ldx != kin) zero_f32(dX, (long long)M * ldx, st);
+            if (int e = pcs_gemm_rows(&xop, M, C, S.wt, C, nullptr, dX, ldx, kin, nullptr, nullptr, nullptr, stream))
+                return e;
+        }
+    }
+    return launch_status("pcs_mlp_backward");
+}

@@ -377,6 +377,15 @@ static DirectTile direct_tile(int M, int N) {
     return DirectTile{tm, tn, wn};
 }
 
+void direct_gemm_name(int M, int N, int mode, char* buf, int cap) {
+    const DirectTile t = direct_tile(M, N);
+    snprintf(buf, cap, "pcs::gemm_direct_kernel<%d, %d, %d, %d>", t.tm, t.tn, t.wn, mode);
+}
+
+void direct_wgrad_name(int N, int K, int xm, int ym, char* buf, int cap) {
+    snprintf(buf, cap, "pcs::wgrad_direct_kernel<%d, %d, %d, %d>", N <= 32 ? 1 : 2, K <= 32 ? 1 : 2, xm, ym);
+}
+
 int direct_row_blocks(int M, int N) {
     const DirectTile t = direct_tile(M, N);
     const int bm = (4 / t.wn) * 32 * t.tm;

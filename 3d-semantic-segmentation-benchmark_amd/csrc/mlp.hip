@@ -156,33 +156,45 @@ __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(GemmArgs g) {
         }
         __builtin_amdgcn_sched_barrier(0);
         if (ks == nk - 1) {
-            // ---- tile epilogue: bias, store, per-channel partial reductions
+            // ---- tile epilogue: bias, store, per-channel partial reductions.  The fused
+            // BN-backward epilogue's Z loads are issued for a whole column strip first
+            // (clamped addresses, no branches) so their latency is paid once, not per element.
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
                 const int col = n0 + wn * WTN + j * 32 + l32;
                 const bool cok = col < g.N;
+                const int colc = cok ? col : g.N - 1;
                 const float bv = (g.bias && cok) ? g.bias[col] : 0.f;
                 float sp = 0.f, tp = 0.f, mp = 0.f, ip = 0.f;
-                if (want_b && cok) { sp = g.e.s[col]; tp = g.e.t[col]; mp = g.e.mean[col]; ip = g.e.inv[col]; }
+                if (want_b) { sp = g.e.s[colc]; tp = g.e.t[colc]; mp = g.e.mean[colc]; ip = g.e.inv[colc]; }
 #pragma unroll
                 for (int i = 0; i < TM; ++i) {
+                    float zt[16];
+                    if (want_b) {
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) {
+                            const int row = min(m0 + wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h, g.M - 1);
+                            zt[r] = g.e.z[(size_t)row * g.e.ldz + colc];
+                        }
+                    }
 #pragma unroll
                     for (int r = 0; r < 16; ++r) {
                         const int row = m0 + wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                        if (row < g.M && cok) {
-                            const float v = acc[i][j][r] + bv;
-                            g.C[(size_t)row * g.ldc + col] = v;
-                            if (want_stats) {
-                                s1[j] += (double)v;
-                                s2[j] += (double)v * (double)v;
-                            }
-                            if (want_b) {
-                                const float z = g.e.z[(size_t)row * g.e.ldz + col];
-                                const float dy = v * dact_f(z * sp + tp, g.e.act, g.e.slope);
-                                const float xh = (z - mp) * ip;
-                                s1[j] += (double)dy;
-                                s2[j] += (double)dy * (double)xh;
-                            }
+                        const bool ok = row < g.M && cok;
+                        const float v = acc[i][j][r] + bv;
+                        if (ok) g.C[(size_t)row * g.ldc + col] = v;
+                        if (want_stats) {
+                            const double d = ok ? (double)v : 0.0;
+                            s1[j] += d;
+                            s2[j] += d * d;
+                        }
+                        if (want_b) {
+                            const float z = zt[r];
+                            const float dy = v * dact_f(z * sp + tp, g.e.act, g.e.slope);
+                            const float xh = (z - mp) * ip;
+                            const double dd = ok ? (double)dy : 0.0;
+                            s1[j] += dd;
+                            s2[j] += dd * (double)xh;
                         }
                         acc[i][j][r] = 0.f;
                     }
@@ -391,7 +403,8 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const double* __restri
                                                           const float* __restrict__ beta, float eps, float momentum,
                                                           float* __restrict__ run_mean, float* __restrict__ run_var,
                                                           float* __restrict__ s, float* __restrict__ t,
-                                                          float* __restrict__ mean_out, float* __restrict__ inv_out) {
+                                                          float* __restrict__ mean_out, float* __restrict__ inv_out,
+                                                          long long* __restrict__ nbt) {
     __shared__ double r1[256], r2[256];
     const int n = blockIdx.x;
     double a = 0.0, b = 0.0;
@@ -410,6 +423,7 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const double* __restri
         __syncthreads();
     }
     if (threadIdx.x == 0) {
+        if (nbt && n == 0) nbt[0] += 1;         // BatchNorm.num_batches_tracked
         const double mean = r1[0] / (double)M;
         double var = r2[0] / (double)M - mean * mean;
         if (var < 0.0) var = 0.0;
@@ -620,6 +634,13 @@ __global__ __launch_bounds__(256) void bn_act_kernel(const float* __restrict__ Z
     }
 }
 
+void bn_finalize_launch(const double* part, int nb, int N, long long M, const float* gamma, const float* beta,
+                        float eps, float momentum, float* run_mean, float* run_var, float* s, float* t, float* mean,
+                        float* invstd, long long* nbt, hipStream_t st) {
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3(N), dim3(256), 0, st, part, nb, N, M, gamma, beta, eps, momentum,
+                       run_mean, run_var, s, t, mean, invstd, nbt);
+}
+
 static inline unsigned ew_grid(long long total) {
     long long g = (total + 255) / 256;
     if (g > 8192) g = 8192;
@@ -695,6 +716,19 @@ static int gemm_grid_x(int M, int N, int bm, int bn) {
     return (mtiles + tpb - 1) / tpb;
 }
 
+// wave grid of a row-GEMM tile (mirrors the launch table in pcs_gemm_rows)
+static void gemm_waves(int bm, int bn, int* wm, int* wn) {
+    if (bn == 32 || (bm == 128 && bn == 64)) { *wm = 4; *wn = 1; }
+    else if (bm == 32) { *wm = 1; *wn = 4; }
+    else { *wm = 2; *wn = 2; }
+}
+
+// algorithmic HBM bytes of reading operand o over M rows x K channels (SURVEY.md 8(d) model)
+static double operand_bytes(const pcs_operand& o, int M, int K) {
+    if (o.mode == PCS_OP_POOLBWD) return 4.0 * M * K + 5.0 * (double)(M / o.pool_k) * K;   // z + dpool + argmax
+    return 4.0 * M * K * (o.mode == PCS_OP_BNBWD ? 2 : 1);
+}
+
 // number of row blocks the row GEMM uses for M rows and N outputs (sizes the stats workspace)
 PCS_API int pcs_gemm_row_blocks(int M, int N) {
     if (engine_impl() == 1) return direct_row_blocks(M, N);
@@ -744,7 +778,24 @@ PCS_API int pcs_gemm_rows(const pcs_operand* a, int M, int K, const float* W, in
     if (M == 0) return 0;
     GemmArgs g{to_dev(a), M, K, W, ldw, bias, C, ldc, N, stats, to_dev(epi), bstats};
     hipStream_t s = as_stream(stream);
-    if (engine_impl() == 1 && launch_gemm_direct(g, s)) return launch_status("pcs_gemm_rows");
+    int probe = -1;
+    if (probe_enabled()) {
+        char nm[96];
+        if (engine_impl() == 1) {
+            direct_gemm_name(M, N, a->mode, nm, sizeof nm);
+        } else {
+            int bm, bn, wm, wn;
+            gemm_tile(M, N, &bm, &bn);
+            gemm_waves(bm, bn, &wm, &wn);
+            snprintf(nm, sizeof nm, "pcs::gemm_rows_kernel<%d, %d, %d, %d, %d>", bm, bn, wm, wn, a->mode);
+        }
+        const double bytes = operand_bytes(*a, M, K) + 4.0 * M * N * (bstats ? 2 : 1);
+        probe = probe_start(nm, 2.0 * M * K * N, bytes, s);
+    }
+    if (engine_impl() == 1 && launch_gemm_direct(g, s)) {
+        probe_stop(probe, s);
+        return launch_status("pcs_gemm_rows");
+    }
     int bm, bn;
     gemm_tile(M, N, &bm, &bn);
     const int gx = gemm_grid_x(M, N, bm, bn);
@@ -754,6 +805,7 @@ PCS_API int pcs_gemm_rows(const pcs_operand* a, int M, int K, const float* W, in
     else if (bm == 64 && bn == 128) launch_gemm<64, 128, 2, 2>(g, gx, s);
     else if (bm == 64) launch_gemm<64, 64, 2, 2>(g, gx, s);
     else launch_gemm<32, 128, 1, 4>(g, gx, s);
+    probe_stop(probe, s);
     return launch_status("pcs_gemm_rows");
 }
 
@@ -767,10 +819,20 @@ PCS_API int pcs_wgrad(const pcs_operand* x, int N, const pcs_operand* y, int K, 
     PCS_CHECK_ARG(y->mode <= PCS_OP_BNACT, "pcs_wgrad: Y operand must be PLAIN or BNACT");
     PCS_CHECK_ARG(dW && N % 4 == 0, "pcs_wgrad: dW null or N not a multiple of 4");
     if (M == 0) return 0;
-    if (engine_impl() == 1 &&
-        launch_wgrad_direct(to_dev(x), N, to_dev(y), K, M, dW, db, as_stream(stream)))
-        return launch_status("pcs_wgrad");
     const int BO = N > 64 ? 128 : 64, BI = K > 64 ? 128 : 64;
+    int probe = -1;
+    if (probe_enabled()) {
+        char nm[96];
+        if (engine_impl() == 1) direct_wgrad_name(N, K, x->mode, y->mode, nm, sizeof nm);
+        else snprintf(nm, sizeof nm, "pcs::wgrad_kernel<%d, %d, %d, %d>", BO, BI, x->mode, y->mode);
+        probe = probe_start(nm, 2.0 * M * N * K, operand_bytes(*x, M, N) + operand_bytes(*y, M, K),
+                            as_stream(stream));
+    }
+    if (engine_impl() == 1 &&
+        launch_wgrad_direct(to_dev(x), N, to_dev(y), K, M, dW, db, as_stream(stream))) {
+        probe_stop(probe, as_stream(stream));
+        return launch_status("pcs_wgrad");
+    }
     const int tiles = ((N + BO - 1) / BO) * ((K + BI - 1) / BI);
     int splits = (1024 + tiles - 1) / tiles;
     int rows = (M + splits - 1) / splits;
@@ -784,6 +846,7 @@ PCS_API int pcs_wgrad(const pcs_operand* x, int N, const pcs_operand* y, int K, 
     else if (BO == 128) launch_wgrad<128, 64>(grid, st, xd, N, yd, K, M, rows, dW, db);
     else if (BI == 128) launch_wgrad<64, 128>(grid, st, xd, N, yd, K, M, rows, dW, db);
     else launch_wgrad<64, 64>(grid, st, xd, N, yd, K, M, rows, dW, db);
+    probe_stop(probe, st);
     return launch_status("pcs_wgrad");
 }
 
@@ -793,7 +856,7 @@ PCS_API int pcs_bn_finalize(const double* part, int nb, int N, long long M, cons
                             float* mean, float* invstd, void* stream) {
     PCS_CHECK_ARG(nb >= 1 && N >= 1 && M >= 1, "pcs_bn_finalize: bad sizes");
     hipLaunchKernelGGL(bn_finalize_kernel, dim3(N), dim3(256), 0, as_stream(stream), part, nb, N, M, gamma, beta, eps,
-                       momentum, run_mean, run_var, s, t, mean, invstd);
+                       momentum, run_mean, run_var, s, t, mean, invstd, (long long*)nullptr);
     return launch_status("pcs_bn_finalize");
 }
 

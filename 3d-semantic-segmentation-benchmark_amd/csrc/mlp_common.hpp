@@ -129,6 +129,17 @@ bool launch_gemm_direct(const GemmArgs& g, hipStream_t s);
 bool launch_wgrad_direct(const Operand& x, int N, const Operand& y, int K, int M, float* dW, float* db,
                          hipStream_t s);
 int direct_row_blocks(int M, int N);
-int engine_impl();   // 0 = LDS-staged kernels, 1 = LDS-free (PCS_GEMM_IMPL)
+// bn_finalize_kernel launch that also bumps BatchNorm.num_batches_tracked (nbt, nullable)
+void bn_finalize_launch(const double* part, int nb, int N, long long M, const float* gamma, const float* beta,
+                        float eps, float momentum, float* run_mean, float* run_var, float* s, float* t, float* mean,
+                        float* invstd, long long* nbt, hipStream_t st);
+int engine_impl();
+// kernel names of the LDS-free family (as rocprofv3 reports them) for the launch probe
+void direct_gemm_name(int M, int N, int mode, char* buf, int cap);
+void direct_wgrad_name(int N, int K, int xm, int ym, char* buf, int cap);
+// engine launch probe (probe.cpp)
+bool probe_enabled();
+int probe_start(const char* name, double flops, double bytes, hipStream_t s);
+void probe_stop(int idx, hipStream_t s);   // 0 = LDS-staged kernels, 1 = LDS-free (PCS_GEMM_IMPL)
 
 }  // namespace pcs

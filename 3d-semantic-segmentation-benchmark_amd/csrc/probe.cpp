@@ -1,0 +1,101 @@
+// Launch probe of the engine GEMMs: while enabled (pcs_probe_begin .. pcs_probe_end),
+// every pcs_gemm_rows / pcs_wgrad launch -- including those issued by pcs_mlp_forward /
+// pcs_mlp_backward -- is bracketed by two HIP events recorded on the launch's own stream,
+// together with the kernel name as rocprofv3 reports it and its algorithmic flops /
+// bytes.  bench.py uses it for the live roofline of the dominant kernel.  Thread-safe:
+// the autograd backward thread launches too.
+#include <hip/hip_runtime.h>
+
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "pcs_common.hpp"
+
+namespace pcs {
+
+struct ProbeRec {
+    std::string name;
+    double flops, bytes;
+    hipEvent_t e0, e1;
+};
+
+static std::mutex g_probe_mu;
+static bool g_probe_on = false;
+static std::vector<ProbeRec> g_probe;
+
+bool probe_enabled() { return g_probe_on; }
+
+// returns the record index, or -1 (probe off / event failure); call before the launch
+int probe_start(const char* name, double flops, double bytes, hipStream_t s) {
+    if (!g_probe_on) return -1;
+    ProbeRec r{name, flops, bytes, nullptr, nullptr};
+    if (hipEventCreate(&r.e0) != hipSuccess || hipEventCreate(&r.e1) != hipSuccess) return -1;
+    (void)hipEventRecord(r.e0, s);
+    std::lock_guard<std::mutex> g(g_probe_mu);
+    g_probe.push_back(r);
+    return (int)g_probe.size() - 1;
+}
+
+void probe_stop(int idx, hipStream_t s) {
+    if (idx < 0) return;
+    hipEvent_t e;
+    {
+        std::lock_guard<std::mutex> g(g_probe_mu);
+        e = g_probe[idx].e1;
+    }
+    (void)hipEventRecord(e, s);
+}
+
+static void probe_clear() {
+    for (auto& r : g_probe) {
+        (void)hipEventDestroy(r.e0);
+        (void)hipEventDestroy(r.e1);
+    }
+    g_probe.clear();
+}
+
+}  // namespace pcs
+
+using namespace pcs;
+
+PCS_API int pcs_probe_begin(void) {
+    std::lock_guard<std::mutex> g(g_probe_mu);
+    probe_clear();
+    g_probe_on = true;
+    return 0;
+}
+
+PCS_API int pcs_probe_end(void) {
+    std::lock_guard<std::mutex> g(g_probe_mu);
+    g_probe_on = false;
+    return (int)g_probe.size();
+}
+
+// record i: kernel name (NUL-terminated, truncated to cap), algorithmic flops and bytes,
+// elapsed milliseconds (waits for the stop event)
+PCS_API int pcs_probe_get(int i, char* name, int cap, double* flops, double* bytes, float* ms) {
+    hipEvent_t e0, e1;
+    {
+        std::lock_guard<std::mutex> g(g_probe_mu);
+        PCS_CHECK_ARG(i >= 0 && i < (int)g_probe.size(), "pcs_probe_get: index %d of %zu", i, g_probe.size());
+        const ProbeRec& r = g_probe[i];
+        if (name && cap > 0) {
+            strncpy(name, r.name.c_str(), cap - 1);
+            name[cap - 1] = 0;
+        }
+        if (flops) *flops = r.flops;
+        if (bytes) *bytes = r.bytes;
+        e0 = r.e0;
+        e1 = r.e1;
+    }
+    if (hipEventSynchronize(e1) != hipSuccess) return (int)hipErrorUnknown;
+    float t = 0.f;
+    const hipError_t err = hipEventElapsedTime(&t, e0, e1);
+    if (err != hipSuccess) {
+        set_error("pcs_probe_get: %s", hipGetErrorString(err));
+        return (int)err;
+    }
+    if (ms) *ms = t;
+    return 0;
+}

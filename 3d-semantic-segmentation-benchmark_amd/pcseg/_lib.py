@@ -50,6 +50,12 @@ SIGNATURES = {
     # shared-MLP engine
     'pcs_gemm_row_blocks': [I32, I32],
     'pcs_engine_select': [I32],
+    'pcs_probe_begin': [],
+    'pcs_probe_end': [],
+    'pcs_probe_get': [I32, ctypes.c_char_p, I32, P, P, P],
+    'pcs_mlp_workspace': [I32, I32, I32, ctypes.c_char_p, I32, I32, I32, P],
+    'pcs_mlp_forward': [P, I32, I32, I32, ctypes.c_char_p, I32, I32, P, P, P, ctypes.c_size_t, P],
+    'pcs_mlp_backward': [P, I32, I32, I32, ctypes.c_char_p, I32, I32, P, P, P, P, ctypes.c_size_t, P],
     'pcs_operand_size': [],
     'pcs_gemm_rows': [OPP, I32, I32, P, I32, P, P, I32, I32, P, OPP, P, P],
     'pcs_wgrad': [OPP, I32, OPP, I32, I32, P, P, P],

@@ -15,7 +15,9 @@ gradient GEMMs) from the output gradient and Z, so it is never stored either.
 """
 from __future__ import annotations
 
+import ctypes
 import math
+import struct
 
 import torch
 
@@ -66,63 +68,42 @@ def notify_grad_ready(params) -> None:
 
 
 # --------------------------------------------------------------------------- launch probe
-_probe: list | None = None
-
-
 class KernelProbe:
     """Bracket every engine GEMM launch with HIP events on the stream it runs on.
 
-    Inside `with KernelProbe() as kp:` each pcs_gemm_rows / pcs_wgrad launch is
-    recorded as (kernel name as rocprof reports it, algorithmic flops,
-    algorithmic bytes, start event, end event).  Used by bench.py's roofline.
+    Inside `with KernelProbe() as kp:` each pcs_gemm_rows / pcs_wgrad launch -- also
+    those issued natively inside pcs_mlp_forward / pcs_mlp_backward -- is recorded by
+    the library's launch probe (csrc/probe.cpp) as (kernel name as rocprof reports it,
+    algorithmic flops, algorithmic bytes, elapsed time).  Used by bench.py's roofline.
     """
 
     def __enter__(self):
-        global _probe
-        self.records = []
-        _probe = self.records
+        call('pcs_probe_begin')
+        self.n = 0
         return self
 
     def __exit__(self, *exc):
-        global _probe
-        _probe = None
+        self.n = load().pcs_probe_end()
         return False
+
+    def records(self):
+        """[(name, flops, bytes, seconds)] (waits for the launches)."""
+        lib = load()
+        out = []
+        buf = ctypes.create_string_buffer(128)
+        fl, by, ms = ctypes.c_double(), ctypes.c_double(), ctypes.c_float()
+        for i in range(self.n):
+            call('pcs_probe_get', i, buf, 128, ctypes.byref(fl), ctypes.byref(by), ctypes.byref(ms))
+            out.append((buf.value.decode(), fl.value, by.value, ms.value * 1e-3))
+        return out
 
     def summary(self):
         """{kernel: (launches, flops, bytes, seconds)} (synchronises)."""
         out = {}
-        for name, fl, by, e0, e1 in self.records:
-            e1.synchronize()
+        for name, fl, by, sec in self.records():
             n, f, b, t = out.get(name, (0, 0, 0, 0.0))
-            out[name] = (n + 1, f + fl, b + by, t + e0.elapsed_time(e1) * 1e-3)
+            out[name] = (n + 1, f + fl, b + by, t + sec)
         return out
-
-
-def _gemm_tile(M: int, N: int) -> tuple[int, int, int, int]:
-    """(BM, BN, WM, WN) of the row GEMM -- mirrors gemm_tile() in csrc/mlp.hip (used for naming only)."""
-    if N <= 32:
-        return 128, 32, 4, 1
-    cands = [(128, 128, 2, 2), (64, 128, 2, 2), (64, 64, 2, 2), (32, 128, 1, 4)] if N > 64 else \
-        [(128, 64, 4, 1), (64, 64, 2, 2)]
-    best, pick = -1, cands[0]
-    for c in cands:
-        blocks = -(-M // c[0]) * -(-N // c[1])
-        if blocks >= 512:
-            return c
-        if blocks > best:
-            best, pick = blocks, c
-    return pick
-
-
-def _launch(name, fl, by, fn, *args):
-    if _probe is None:
-        call(fn, *args)
-        return
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    call(fn, *args)
-    e1.record()
-    _probe.append((name, fl, by, e0, e1))
 
 
 def operand(data, ld, mode=OP_PLAIN, s=None, t=None, act=0, slope=0.0, z=None, ldz=0, mean=None, inv=None,
@@ -132,26 +113,15 @@ def operand(data, ld, mode=OP_PLAIN, s=None, t=None, act=0, slope=0.0, z=None, l
                    ptr(alpha), ptr(kb), ptr(arg), pool_k)
 
 
-def _operand_bytes(op: Operand, M: int, K: int) -> int:
-    if op.mode == OP_POOLBWD:
-        return 4 * M * K                      # Z (the pooled gradient and argmax are M/pool_k rows)
-    return 4 * M * K * (2 if op.mode == OP_BNBWD else 1)
-
-
 def gemm_rows(a: Operand, M, K, W, ldw, bias, C, ldc, N, stats=None, epi: Operand | None = None, bstats=None,
               st=None):
     """C[M,N] = T(A)[M,K] . W^T (+bias) with optional BN-stat / BN-backward partials."""
-    bm, bn, wm, wn = _gemm_tile(M, N)
-    by = _operand_bytes(a, M, K) + 4 * M * N + (4 * M * N if bstats is not None else 0)
-    _launch(f'pcs::gemm_rows_kernel<{bm}, {bn}, {wm}, {wn}, {a.mode}>', 2 * M * K * N, by, 'pcs_gemm_rows',
-            a, M, K, ptr(W), ldw, ptr(bias), ptr(C), ldc, N, ptr(stats), epi, ptr(bstats), st)
+    call('pcs_gemm_rows', a, M, K, ptr(W), ldw, ptr(bias), ptr(C), ldc, N, ptr(stats), epi, ptr(bstats), st)
 
 
 def wgrad(x: Operand, N, y: Operand, K, M, dW, db, st):
     """dW[N,K] += T(X)^T . T(Y) over M rows, db += colsum(T(X))."""
-    name = f'pcs::wgrad_kernel<{128 if N > 64 else 64}, {128 if K > 64 else 64}, {x.mode}, {y.mode}>'
-    _launch(name, 2 * M * N * K, _operand_bytes(x, M, N) + _operand_bytes(y, M, K), 'pcs_wgrad',
-            x, N, y, K, M, ptr(dW), ptr(db), st)
+    call('pcs_wgrad', x, N, y, K, M, ptr(dW), ptr(db), st)
 
 
 def _f64(shape, dev):
@@ -162,160 +132,132 @@ def _f32(shape, dev):
     return torch.empty(shape, dtype=torch.float32, device=dev)
 
 
+# pcs_mlp_layer (include/pcseg.h): 24 little-endian 8-byte slots
+_REC = struct.Struct('<QqqqQQQQQQddqqdQQQQQQqqq')
+_ws_cache: dict = {}
+
+
+def _workspace(lib, key, M, kin, ldx, recs, nl, pool_k, backward):
+    n = _ws_cache.get(key)
+    if n is None:
+        out = ctypes.c_size_t(0)
+        rc = lib.pcs_mlp_workspace(M, kin, ldx, recs, nl, pool_k, backward, ctypes.byref(out))
+        if rc:
+            raise RuntimeError(f'pcs_mlp_workspace failed ({rc}): {lib.pcs_last_error().decode()}')
+        n = int(out.value)
+        _ws_cache[key] = n
+    return n
+
+
+def _nz(p) -> int:
+    return 0 if p is None else p.data_ptr()
+
+
 class SharedMLPFn(torch.autograd.Function):
-    """rows X (M, ld) with Kin logical channels -> pooled (M/pool_K, C_L) or activation (M, C_L)."""
+    """rows X (M, ld) with Kin logical channels -> pooled (M/pool_K, C_L) or activation (M, C_L).
+
+    The whole stack runs in ONE native call each way (pcs_mlp_forward / pcs_mlp_backward,
+    csrc/engine.hip); Python only allocates the outputs and packs one pcs_mlp_layer
+    record per layer."""
 
     @staticmethod
     def forward(ctx, X, Kin, pool_K, acts, bns, *params):
         dev = X.device
         st = stream_ptr(dev)
-        M, lda = X.shape
-        A, lda_cur, K_cur, s_prev, t_prev = X, lda, Kin, None, None
-        Zs, stats = [], []
+        lib = load()
+        M, ldx = X.shape
         nl = len(bns)
+        couts = [params[4 * li].shape[0] for li in range(nl)]
+        tot = sum(couts)
+        Zbuf = _f32((M * tot,), dev)
+        coef = _f32((4 * tot,), dev)
+        Wms, fixed = [], []
+        off, cin = 0, Kin
         for li in range(nl):
             W, b, g, be = params[4 * li:4 * li + 4]
             bn = bns[li]
-            Cout = W.shape[0]
-            Wm = W.reshape(Cout, -1)
+            C = couts[li]
+            if C % 4:
+                raise ValueError(f'engine: layer width {C} must be a multiple of 4')
+            Wm = W.reshape(C, -1)
             if Wm.shape[1] % 4:                 # 16-B weight rows (the pad columns are zero)
-                Wp = torch.zeros((Cout, ld4(Wm.shape[1])), dtype=torch.float32, device=dev)
+                Wp = torch.zeros((C, ld4(Wm.shape[1])), dtype=torch.float32, device=dev)
                 Wp[:, :Wm.shape[1]] = Wm
                 Wm = Wp
             elif not Wm.is_contiguous():
                 Wm = Wm.contiguous()
-            if Cout % 4:
-                raise ValueError(f'engine: layer width {Cout} must be a multiple of 4')
-            Z = _f32((M, Cout), dev)
-            a_op = operand(A, lda_cur) if s_prev is None else \
-                operand(A, lda_cur, OP_BNACT, s_prev, t_prev, *acts[li - 1])
+            Wms.append(Wm)
             use_batch = bn.training or bn.running_mean is None
-            s, t, mean, inv = (_f32((Cout,), dev) for _ in range(4))
-            if use_batch:
-                nb = load().pcs_gemm_row_blocks(M, Cout)
-                part = _f64((2, Cout, nb), dev)
-                gemm_rows(a_op, M, K_cur, Wm, Wm.shape[1], b, Z, Cout, Cout, part, st=st)
-                momentum = 0.0
-                rm = rv = None
-                if bn.training and bn.track_running_stats and bn.running_mean is not None:
-                    bn.num_batches_tracked.add_(1)
-                    momentum = bn.momentum if bn.momentum is not None else 1.0 / float(bn.num_batches_tracked)
-                    rm, rv = bn.running_mean, bn.running_var
-                call('pcs_bn_finalize', ptr(part), nb, Cout, M, ptr(g), ptr(be), float(bn.eps), float(momentum),
-                     ptr(rm), ptr(rv), ptr(s), ptr(t), ptr(mean), ptr(inv), st)
-            else:
-                gemm_rows(a_op, M, K_cur, Wm, Wm.shape[1], b, Z, Cout, Cout, None, st=st)
-                with torch.no_grad():
-                    inv.copy_(torch.rsqrt(bn.running_var + bn.eps))
-                    mean.copy_(bn.running_mean)
-                    s.copy_((g if g is not None else 1.0) * inv)
-                    t.copy_((be if be is not None else 0.0) - mean * s)
-            Zs.append(Z)
-            stats.append((s, t, mean, inv, use_batch))
-            A, lda_cur, K_cur, s_prev, t_prev = Z, Cout, Cout, s, t
-        CL = Zs[-1].shape[1]
-        s, t = stats[-1][0], stats[-1][1]
+            track = use_batch and bn.training and bn.track_running_stats and bn.running_mean is not None
+            momentum = 0.0
+            if track:
+                momentum = bn.momentum if bn.momentum is not None else 1.0 / float(bn.num_batches_tracked + 1)
+            rm = bn.running_mean if (track or not use_batch) else None
+            rv = bn.running_var if (track or not use_batch) else None
+            nbt = bn.num_batches_tracked if track else None
+            act, slope = acts[li]
+            fixed.append((Wm.data_ptr(), Wm.shape[1], cin, C, _nz(b), _nz(g), _nz(be), _nz(rm), _nz(rv), _nz(nbt),
+                          float(momentum), float(bn.eps), int(use_batch), act, slope,
+                          Zbuf.data_ptr() + 4 * M * off, coef.data_ptr() + 16 * off))
+            off += C
+            cin = C
+        recs = b''.join(_REC.pack(*f, 0, 0, 0, 0, 0, 0, 0) for f in fixed)
+        CL = couts[-1]
         if pool_K:
             G = M // pool_K
             out = _f32((G, CL), dev)
             arg = torch.empty((G, CL), dtype=torch.uint8, device=dev)
-            call('pcs_pool_fwd', ptr(Zs[-1]), CL, G, pool_K, ptr(s), ptr(t), *acts[-1], ptr(out), ptr(arg), st)
             ctx.mark_non_differentiable(arg)
         else:
             out = _f32((M, CL), dev)
             arg = None
-            call('pcs_bn_act', ptr(Zs[-1]), CL, M, CL, ptr(s), ptr(t), *acts[-1], ptr(out), CL, st)
-        ctx.save_for_backward(X, *Zs, *[x for st_ in stats for x in st_[:4]], *(p for p in params if p is not None),
-                              *([arg] if arg is not None else []))
-        ctx.meta = (Kin, pool_K, acts, nl, [st_[4] for st_ in stats],
-                    [p is not None for p in params], arg is not None)
+        key = (M, Kin, ldx, tuple(couts), pool_K, 0, _impl())
+        nws = _workspace(lib, key, M, Kin, ldx, recs, nl, pool_K, 0)
+        ws = torch.empty((nws,), dtype=torch.uint8, device=dev)
+        call('pcs_mlp_forward', ptr(X), ldx, Kin, M, recs, nl, pool_K, ptr(out), ptr(arg), ptr(ws), nws, st)
+        ctx.save_for_backward(X, Zbuf, coef, *Wms, *([arg] if arg is not None else []))
+        ctx.meta = (Kin, pool_K, nl, fixed, couts, arg is not None)
+        ctx.params = params
         return out
 
     @staticmethod
     def backward(ctx, gout):
-        Kin, pool_K, acts, nl, use_batch, present, has_arg = ctx.meta
-        saved = list(ctx.saved_tensors)
+        Kin, pool_K, nl, fixed, couts, has_arg = ctx.meta
+        saved = ctx.saved_tensors
         X = saved[0]
-        Zs = saved[1:1 + nl]
-        flat = saved[1 + nl:1 + nl + 4 * nl]
-        stats = [tuple(flat[4 * i:4 * i + 4]) for i in range(nl)]
-        rest = saved[1 + nl + 4 * nl:]
-        params = []
-        it = iter(rest)
-        for pr in present:
-            params.append(next(it) if pr else None)
-        arg = next(it) if has_arg else None
+        arg = saved[3 + nl] if has_arg else None
+        params = ctx.params
         dev = gout.device
         st = stream_ptr(dev)
         lib = load()
-        M, lda = X.shape
+        M, ldx = X.shape
         gout = gout.contiguous()
-        CL = Zs[-1].shape[1]
-        s, t, mean, inv = stats[-1]
-        grads = [None] * len(params)
-
-        # ---- top layer: BN-backward sums and dZ
-        if pool_K:
-            G = M // pool_K
-            nb = lib.pcs_pool_bwd_reduce_blocks(G)
-            part = _f64((2, CL, nb), dev)
-            call('pcs_pool_bwd_reduce', ptr(gout), ptr(arg), ptr(Zs[-1]), CL, G, pool_K, ptr(s), ptr(t), ptr(mean),
-                 ptr(inv), *acts[-1], ptr(part), st)
-        else:
-            nb = lib.pcs_bn_bwd_reduce_blocks(M)
-            part = _f64((2, CL, nb), dev)
-            call('pcs_bn_bwd_reduce', ptr(gout), CL, ptr(Zs[-1]), CL, M, CL, ptr(s), ptr(t), ptr(mean), ptr(inv),
-                 *acts[-1], ptr(part), st)
-        kB, alpha = _f32((CL,), dev), _f32((CL,), dev)
-        gg, gb = grad_target(params[4 * (nl - 1) + 2]), grad_target(params[4 * (nl - 1) + 3])
-        call('pcs_bn_bwd_finalize', ptr(part), nb, CL, M, ptr(s), ptr(inv), ptr(gg), ptr(gb), ptr(kB), ptr(alpha), 1,
-             st)
-        if not use_batch[-1]:
-            kB.zero_()
-            alpha.zero_()
-        # dZ of the top layer is never materialised: its consumers rebuild it on load
-        if pool_K:
-            xop = operand(gout, CL, OP_POOLBWD, s, t, *acts[-1], Zs[-1], CL, mean, None, alpha, kB, arg, pool_K)
-        else:
-            xop = operand(gout, CL, OP_BNBWD, s, t, *acts[-1], Zs[-1], CL, mean, None, alpha, kB)
-        keep = [gout, kB, alpha]
+        recs = b''.join(_REC.pack(*f, _nz(grad_target(params[4 * li])), _nz(grad_target(params[4 * li + 1])),
+                                  _nz(grad_target(params[4 * li + 2])), _nz(grad_target(params[4 * li + 3])), 0, 0, 0)
+                        for li, f in enumerate(fixed))
         dX = None
-        for li in range(nl - 1, -1, -1):
-            W, b = params[4 * li], params[4 * li + 1]
-            Cout = W.shape[0]
-            Wm = W.reshape(Cout, -1)
-            Cin = Wm.shape[1]
-            Wt = Wm.t().contiguous()          # (Cin x Cout): dgrad B[k=cout][n=cin] = Wt[n][k]
-            dW = grad_target(W)
-            db = grad_target(b)
-            if dW is not None:
-                if li > 0:
-                    sp, tp, mp, ip = stats[li - 1]
-                    yop = operand(Zs[li - 1], Cin, OP_BNACT, sp, tp, *acts[li - 1])
-                    wgrad(xop, Cout, yop, Cin, M, dW, db, st)
-                else:
-                    wgrad(xop, Cout, operand(X, lda), Kin, M, dW, db, st)
-            if li > 0:
-                sp, tp, mp, ip = stats[li - 1]
-                dA = _f32((M, Cin), dev)
-                nbg = lib.pcs_gemm_row_blocks(M, Cin)
-                bpart = _f64((2, Cin, nbg), dev)
-                epi = operand(None, 0, OP_BNBWD, sp, tp, *acts[li - 1], Zs[li - 1], Cin, mp, ip)
-                gemm_rows(xop, M, Cout, Wt, Cout, None, dA, Cin, Cin, None, epi, bpart, st=st)
-                kB2, alpha2 = _f32((Cin,), dev), _f32((Cin,), dev)
-                g2, b2 = grad_target(params[4 * (li - 1) + 2]), grad_target(params[4 * (li - 1) + 3])
-                call('pcs_bn_bwd_finalize', ptr(bpart), nbg, Cin, M, ptr(sp), ptr(ip), ptr(g2), ptr(b2), ptr(kB2),
-                     ptr(alpha2), 1, st)
-                if not use_batch[li - 1]:
-                    kB2.zero_()
-                    alpha2.zero_()
-                xop = operand(dA, Cin, OP_BNBWD, sp, tp, *acts[li - 1], Zs[li - 1], Cin, mp, None, alpha2, kB2)
-                keep += [dA, kB2, alpha2]
-            elif ctx.needs_input_grad[0]:
-                dX = torch.zeros((M, lda), dtype=torch.float32, device=dev) if lda != Kin else _f32((M, lda), dev)
-                gemm_rows(xop, M, Cout, Wt, Cout, None, dX, lda, Kin, st=st)
+        if ctx.needs_input_grad[0]:
+            dX = _f32((M, ldx), dev)
+        key = (M, Kin, ldx, tuple(couts), pool_K, 1, _impl())
+        nws = _workspace(lib, key, M, Kin, ldx, recs, nl, pool_K, 1)
+        ws = torch.empty((nws,), dtype=torch.uint8, device=dev)
+        call('pcs_mlp_backward', ptr(X), ldx, Kin, M, recs, nl, pool_K, ptr(arg), ptr(gout), ptr(dX), ptr(ws), nws, st)
         notify_grad_ready(params)
-        return (dX, None, None, None, None, *grads)
+        return (dX, None, None, None, None, *([None] * len(params)))
+
+
+def _impl() -> int:
+    """The engine GEMM family in use (its row-block count sizes the workspaces)."""
+    return _ENGINE_IMPL[0]
+
+
+_ENGINE_IMPL = [0]
+
+
+def select_engine(impl: int) -> None:
+    """0 = LDS-staged persistent GEMMs (default), 1 = LDS-free (pcs_engine_select)."""
+    call('pcs_engine_select', int(impl))
+    _ENGINE_IMPL[0] = int(impl)
 
 
 def shared_mlp(x_rows: torch.Tensor, kin: int, convs, bns, act='relu', slope=0.0,

@@ -173,6 +173,56 @@ int pcs_bn_act(const float* Z, int ldz, int M, int N, const float* s,
                const float* t, int act, float slope, float* out, int ldo,
                void* stream);
 
+/* ---- shared-MLP stack in one call -------------------------------------------
+ * A stack of nl layers conv1x1 (W, bias) -> BatchNorm (gamma, beta; batch statistics
+ * with running-stat update, or running statistics when use_batch = 0) -> act, on
+ * point-major rows, optionally max-pooled over consecutive groups of pool_k rows
+ * (reference: common.py:125-178 + reduce 'max' common.py:211-212, dgcnn.py:67-76,
+ * dgcnn.py:188-207).  Every field is 8 bytes, so bindings can pack a record as 24
+ * little-endian u64/i64/f64 slots.
+ *   W (cout x ldw) row-major, columns >= cin zero;  cin of layer 0 = kin, of layer
+ *   l = cout of layer l-1;  cout % 4 == 0.  num_batches (nullable) += 1 per forward
+ *   that updates running statistics.  act: 0 ReLU, 1 LeakyReLU(slope), 2 identity.
+ *   Z (M x cout) and coef (4 x cout: scale, shift, mean, invstd) are written by the
+ *   forward and read by the backward.  dW (cout x cin), db, dgamma, dbeta: gradients,
+ *   accumulating (nullable = not wanted). */
+typedef struct pcs_mlp_layer {
+    const float* W; int64_t ldw, cin, cout;
+    const float* bias; const float* gamma; const float* beta;
+    float* run_mean; float* run_var; int64_t* num_batches;
+    double momentum, eps;
+    int64_t use_batch, act; double slope;
+    float* Z; float* coef;
+    float* dW; float* db; float* dgamma; float* dbeta;
+    int64_t reserved[3];
+} pcs_mlp_layer;
+
+/* workspace bytes of pcs_mlp_forward (backward = 0) or pcs_mlp_backward (1) */
+int pcs_mlp_workspace(int M, int kin, int ldx, const pcs_mlp_layer* layers, int nl,
+                      int pool_k, int backward, size_t* bytes);
+/* X (M x ldx rows, kin channels) -> out = pooled (M/pool_k x cout_L) + argmax u8
+ * (pool_k > 0), or the activation (M x cout_L). */
+int pcs_mlp_forward(const float* X, int ldx, int kin, int M, pcs_mlp_layer* layers,
+                    int nl, int pool_k, float* out, uint8_t* arg, void* workspace,
+                    size_t ws_bytes, void* stream);
+/* gout = d loss / d out (same shape as out, contiguous); accumulates every layer's
+ * dW/db/dgamma/dbeta; dX (M x ldx, nullable) = d loss / d X (pad columns zeroed). */
+int pcs_mlp_backward(const float* X, int ldx, int kin, int M,
+                     const pcs_mlp_layer* layers, int nl, int pool_k,
+                     const uint8_t* arg, const float* gout, float* dX,
+                     void* workspace, size_t ws_bytes, void* stream);
+
+/* ---- launch probe (measurement) -----------------------------------------------
+ * While enabled, every engine GEMM launch (pcs_gemm_rows / pcs_wgrad, also those
+ * issued inside pcs_mlp_forward/backward) is bracketed by HIP events recorded on its
+ * own stream.  pcs_probe_end returns the record count; pcs_probe_get(i) returns the
+ * kernel name (as rocprofv3 reports it), algorithmic flops / HBM bytes and the
+ * measured milliseconds (waits for the launch). */
+int pcs_probe_begin(void);
+int pcs_probe_end(void);
+int pcs_probe_get(int i, char* name, int cap, double* flops, double* bytes,
+                  float* ms);
+
 /* ---- inverse neighbour maps (atomic-free gather backward) ------------------ */
 
 /* For a neighbour table idx (B x per_batch, values in [0, targets)), the CSR

@@ -66,12 +66,15 @@ def three_way(prod_ctor, ref_ctor, B, N, seed, uniform=False, pad=0, dev='cuda',
     pcseg.masked_onehot_cross_entropy(lg, lab.to(dev), lengths.to(dev)).backward()
 
     # neighbour choices of the GPU run must equal the reference's (index-exact work)
-    for a, b in zip(rg.rec_group_idx, rp.rec_group_idx):
-        assert torch.equal(a.long().sort(-1).values, b.sort(-1).values), 'ball-query set mismatch'
+    for lv, (a, b) in enumerate(zip(rg.rec_fps_idx, rp.rec_fps_idx)):
+        assert torch.equal(a, b), f'FPS index mismatch at level {lv}'
+    for q, (a, b) in enumerate(zip(rg.rec_group_idx, rp.rec_group_idx)):
+        sa, sb = a.long().sort(-1).values, b.sort(-1).values
+        bad = (sa != sb).any(-1).nonzero()
+        assert bad.numel() == 0, (f'ball-query set mismatch in query {q}: {bad.shape[0]} rows, first {bad[0].tolist()}: '
+                                  f'gpu {sa[tuple(bad[0])].tolist()} ref {sb[tuple(bad[0])].tolist()}')
     for a, b in zip(rg.rec_interp_idx, rp.rec_interp_idx):
         assert torch.equal(a.long().sort(-1).values, b.sort(-1).values), '3-NN set mismatch'
-    for a, b in zip(rg.rec_fps_idx, rp.rec_fps_idx):
-        assert torch.equal(a, b), 'FPS index mismatch'
 
     rows = []
 
