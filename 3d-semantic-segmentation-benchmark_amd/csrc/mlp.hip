@@ -243,7 +243,7 @@ __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(GemmArgs g) {
 // row swizzle of channel c's LDS row (multiples of 4: keeps 4-row groups 16-B contiguous)
 __device__ __forceinline__ int lds_swz(int c) { return ((c >> 3) & 7) << 2; }
 
-template <int BO, int BI, int XM, int YM>
+template <int BO, int BI, int XM, int YM, bool PF2>
 __global__ __launch_bounds__(256, 2) void wgrad_kernel(Operand xo, int N, Operand yo, int K, int M,
                                                        int rows_per_block, float* __restrict__ dW,
                                                        float* __restrict__ db) {
@@ -286,26 +286,29 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(Operand xo, int N, Operan
 #pragma unroll
             for (int r = 0; r < 16; ++r) { acc[i][j][r] = 0.f; tot[i][j][r] = 0.f; }
 
-    float4 rx[XV], rxz[XV], ry[YV], ryz[YV];
-    unsigned rxa[XV], rya[YV];
+    // PF2: two register stages, so each slab's loads are issued two slabs ahead of their
+    // LDS store (thin tiles, where one slab of MFMAs is too short to cover HBM latency)
+    constexpr int NS = PF2 ? 2 : 1;
+    float4 rx[NS][XV], rxz[NS][XV], ry[NS][YV], ryz[NS][YV];
+    unsigned rxa[NS][XV], rya[NS][YV];
     const int gnc = min(gn, xo.ld - 4), gkc = min(gk, yo.ld - 4);
-    auto gload = [&](int r0) {
+    auto gload = [&](int st, int r0) {
 #pragma unroll
         for (int it = 0; it < XV; ++it) {
             const int gr = min(r0 + it * XRPI + xr, M - 1);
-            load_raw<XM>(xo, gr, gnc, rx[it], rxz[it], rxa[it]);
+            load_raw<XM>(xo, gr, gnc, rx[st][it], rxz[st][it], rxa[st][it]);
         }
 #pragma unroll
         for (int it = 0; it < YV; ++it) {
             const int gr = min(r0 + it * YRPI + yr, M - 1);
-            load_raw<YM>(yo, gr, gkc, ry[it], ryz[it], rya[it]);
+            load_raw<YM>(yo, gr, gkc, ry[st][it], ryz[st][it], rya[st][it]);
         }
     };
-    auto sstore = [&](int buf, int r0) {
+    auto sstore = [&](int st, int buf, int r0) {
 #pragma unroll
         for (int it = 0; it < XV; ++it) {
             const int r = it * XRPI + xr;
-            float4 v = xform4<XM>(xo, rx[it], rxz[it], rxa[it], r0 + r, qx, gn, N);
+            float4 v = xform4<XM>(xo, rx[st][it], rxz[st][it], rxa[st][it], r0 + r, qx, gn, N);
             if (r0 + r >= re) v = make_float4(0.f, 0.f, 0.f, 0.f);
             const int rs = r ^ lds_swz(4 * xc4);      // the 4 channels of a quad share the swizzle
             Xs[buf][4 * xc4 + 0][rs] = v.x;
@@ -317,7 +320,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(Operand xo, int N, Operan
 #pragma unroll
         for (int it = 0; it < YV; ++it) {
             const int r = it * YRPI + yr;
-            float4 v = xform4<YM>(yo, ry[it], ryz[it], rya[it], r0 + r, qy, gk, K);
+            float4 v = xform4<YM>(yo, ry[st][it], ryz[st][it], rya[st][it], r0 + r, qy, gk, K);
             if (r0 + r >= re) v = make_float4(0.f, 0.f, 0.f, 0.f);
             const int rs = r ^ lds_swz(4 * yc4);
             Ys[buf][4 * yc4 + 0][rs] = v.x;
@@ -329,13 +332,16 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(Operand xo, int N, Operan
 
     const int nslab = (re - rb + BR - 1) / BR;
     if (nslab > 0) {
-        gload(rb);
-        sstore(0, rb);
+        gload(0, rb);
+        if (PF2) gload(NS - 1, rb + BR);
+        sstore(0, 0, rb);
     }
     __syncthreads();
-    for (int sl = 0; sl < nslab; ++sl) {
+    // one slab: issue the loads of slab sl+NS into stage `lst` (unconditional, clamped past the
+    // end), MFMAs on LDS buffer sl&1, then slab sl+1 from stage `sst` into the other buffer
+    auto body = [&](int sl, int lst, int sst) {
         const int buf = sl & 1;
-        gload(rb + (sl + 1) * BR);    // unconditional (clamped past the end), see gemm_rows_kernel
+        gload(lst, rb + (sl + NS) * BR);
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -367,8 +373,17 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(Operand xo, int N, Operan
                     for (int r = 0; r < 16; ++r) { tot[i][j][r] += acc[i][j][r]; acc[i][j][r] = 0.f; }
         }
         __builtin_amdgcn_sched_barrier(0);
-        if (sl + 1 < nslab) sstore(buf ^ 1, rb + (sl + 1) * BR);
+        if (sl + 1 < nslab) sstore(sst, buf ^ 1, rb + (sl + 1) * BR);
         __syncthreads();
+    };
+    if constexpr (PF2) {
+        for (int sl = 0; sl < nslab; sl += 2) {
+            body(sl, 0, 1);           // slab sl+2 -> stage 0, slab sl+1 from stage 1
+            if (sl + 1 >= nslab) break;
+            body(sl + 1, 1, 0);
+        }
+    } else {
+        for (int sl = 0; sl < nslab; ++sl) body(sl, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -661,10 +676,13 @@ static void launch_gemm(const GemmArgs& g, int gx, hipStream_t s) {
 template <int BO, int BI, int XM>
 static void launch_wgrad_y(dim3 grid, hipStream_t st, const Operand& x, int N, const Operand& y, int K, int M,
                            int rows, float* dW, float* db) {
+    constexpr bool PF2 = BO == 64 && BI == 64;      // thin tiles: two slabs of loads in flight
     if (y.mode == OP_BNACT)
-        hipLaunchKernelGGL((wgrad_kernel<BO, BI, XM, OP_BNACT>), grid, dim3(256), 0, st, x, N, y, K, M, rows, dW, db);
+        hipLaunchKernelGGL((wgrad_kernel<BO, BI, XM, OP_BNACT, PF2>), grid, dim3(256), 0, st, x, N, y, K, M, rows, dW,
+                           db);
     else
-        hipLaunchKernelGGL((wgrad_kernel<BO, BI, XM, OP_PLAIN>), grid, dim3(256), 0, st, x, N, y, K, M, rows, dW, db);
+        hipLaunchKernelGGL((wgrad_kernel<BO, BI, XM, OP_PLAIN, PF2>), grid, dim3(256), 0, st, x, N, y, K, M, rows, dW,
+                           db);
 }
 
 template <int BO, int BI>
