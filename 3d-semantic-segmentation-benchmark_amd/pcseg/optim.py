@@ -1,0 +1,51 @@
+"""Adam on flat buffers: one HIP launch per step for the whole model (pcs_adam).
+
+The gradients already live in one flat fp32 buffer (pcseg.ddp.FlatGradAllReduce);
+FlatAdam moves the parameters into a second flat buffer with the same layout (every
+`param.data` becomes a view into it) and keeps the two moment estimates likewise, so
+an optimizer step is a single memory-bound kernel instead of torch.optim.Adam's
+~10 foreach launches per parameter group.  Same update and fp32 operation order as
+torch.optim.Adam's default path (the reference trains with Adam, lr 1e-3:
+Training/train_model.py:263, models/dgcnn/train.py:79).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from ._lib import call, ptr, stream_ptr
+
+
+class FlatAdam:
+    def __init__(self, grads, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
+                 weight_decay: float = 0.0):
+        """grads: a pcseg.ddp.FlatGradAllReduce over the model's trainable parameters."""
+        self.grads = grads
+        self.lr, self.betas, self.eps, self.weight_decay = float(lr), tuple(betas), float(eps), float(weight_decay)
+        flat_g = grads.flat
+        self.flat = torch.empty_like(flat_g)
+        base = flat_g.storage_offset()
+        with torch.no_grad():
+            for p in grads.params:
+                off = grads.views[p].storage_offset() - base
+                n = p.numel()
+                self.flat[off:off + n].copy_(p.detach().reshape(-1))
+                p.data = self.flat[off:off + n].view_as(p)
+        self.exp_avg = torch.zeros_like(self.flat)
+        self.exp_avg_sq = torch.zeros_like(self.flat)
+        self.t = 0
+
+    def zero_grad(self, set_to_none: bool = False) -> None:
+        self.grads.zero_grad()
+
+    @torch.no_grad()
+    def step(self) -> None:
+        self.t += 1
+        b1, b2 = self.betas
+        bc1 = 1 - b1 ** self.t
+        step = -(self.lr / bc1)
+        bc2_sqrt = math.sqrt(1 - b2 ** self.t)
+        call('pcs_adam', ptr(self.flat), ptr(self.grads.flat), ptr(self.exp_avg), ptr(self.exp_avg_sq),
+             self.flat.numel(), 1 - b1, b2, step, bc2_sqrt, self.eps, self.weight_decay,
+             stream_ptr(self.flat.device))

@@ -195,6 +195,7 @@ def main():
 
     import pcseg
     from pcseg.ddp import FlatGradAllReduce, broadcast_model
+    from pcseg.optim import FlatAdam
     from pcseg.synthetic import make_batch
 
     name, ctor, kind = MODELS[args.model]
@@ -203,7 +204,10 @@ def main():
     broadcast_model(model)
     grads = FlatGradAllReduce(model)
     use_graph = args.graph and world == 1
-    opt = torch.optim.Adam(model.parameters(), lr=1e-3, capturable=use_graph)
+    if use_graph:      # graph replays need device-side step counters
+        opt = torch.optim.Adam(model.parameters(), lr=1e-3, capturable=True)
+    else:              # one HIP launch over the flat parameter / gradient buffers
+        opt = FlatAdam(grads, lr=1e-3)
     pts, labels, lengths = make_batch(args.batch, args.npoints, seed=1000 * 2 + rank)
     x = model_input(pts.to(dev), kind)
     lab = (labels.float() if kind == 'chfirst6' else labels).to(dev)

@@ -255,6 +255,16 @@ int pcs_gather_blocks(const float* points, const uint8_t* labels,
                       const long long* src, long long rows, float* out_points,
                       uint8_t* out_labels, void* stream);
 
+/* ---- optimizer -------------------------------------------------------------- */
+
+/* torch.optim.Adam step (amsgrad=False; the reference trains with Adam lr 1e-3,
+ * Training/train_model.py:263) over flat fp32 arrays of n parameters: p, g, m
+ * (exp_avg), v (exp_avg_sq); beta1_w = 1 - beta1, step = -lr / (1 - beta1^t),
+ * bc2_sqrt = sqrt(1 - beta2^t).  16-byte aligned buffers. */
+int pcs_adam(float* p, const float* g, float* m, float* v, long long n, float beta1_w,
+             float beta2, float step, float bc2_sqrt, float eps, float weight_decay,
+             void* stream);
+
 /* ---- loss ---------------------------------------------------------------- */
 
 /* Training/train_model.py:15-57 `masked_onehot_cross_entropy`: logits (B,L,C)
