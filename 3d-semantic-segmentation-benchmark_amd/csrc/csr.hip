@@ -2,45 +2,97 @@
 //
 // The backward of a neighbour gather (models/utils/common.py:64-65 `group`,
 // :120-122 `interpolate`) is a scatter-add into the source points.  Instead of
-// fp32 atomics (one per gathered element, order-nondeterministic), the geometry
-// stage -- which depends on coordinates only and runs on the side stream, off the
-// critical path -- also builds the INVERSE map of each neighbour table: for every
-// source point, the ascending list of gather slots that read it (CSR: offsets +
-// entries, from a stable rocPRIM radix sort of (target, slot) pairs).  The
-// backward then gathers: one thread per (source point, channel) sums its slots'
-// gradients in ascending slot order -- deterministic, no atomics, no zero fill.
+// fp32 atomics (one per gathered element), the geometry stage -- which depends on
+// coordinates only and runs on the side stream, off the critical path -- also
+// builds the INVERSE map of each neighbour table: for every source point, the
+// list of gather slots that read it (CSR: offsets + entries).  The backward then
+// gathers: one thread per (source point, channel) sums its slots' gradients.
+//
+// Build: one workgroup per cloud, one launch per map.  Every slot of cloud b
+// reads a point of cloud b, so cloud b's entries are exactly positions
+// [b*per_batch, (b+1)*per_batch) and the clouds are independent: LDS histogram of
+// the cloud's targets -> in-LDS exclusive scan -> LDS-atomic scatter of the slots.
+// The order of slots inside one point's list is therefore unspecified; the
+// consumers accumulate in fp64, where the sum of a point's fp32 terms is exact
+// (or rounds at 2^-53) whatever the order, so the fp32 result is reproducible.
 #include "pcs_common.hpp"
-
-#include <rocprim/rocprim.hpp>
 
 namespace pcs {
 
-__global__ __launch_bounds__(256) void inv_keys_kernel(const int32_t* __restrict__ idx, long long n, int per_batch,
-                                                       int targets, uint32_t* __restrict__ keys,
-                                                       int32_t* __restrict__ vals) {
-    const long long s = (long long)blockIdx.x * 256 + threadIdx.x;
-    if (s < n) {
-        const int b = (int)(s / per_batch);
-        keys[s] = (uint32_t)b * (uint32_t)targets + (uint32_t)idx[s];
-        vals[s] = (int32_t)s;
+constexpr int kInvThreads = 1024;
+constexpr int kInvLdsTargets = 32768;   // 128 KB of LDS counters; larger clouds count in global memory
+
+// block-wide exclusive scan of cnt[0, n) in place (kInvThreads threads); returns the total
+__device__ int block_exclusive_scan(int* cnt, int n, int* wsum) {
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int per = (n + kInvThreads - 1) / kInvThreads;
+    const int a = tid * per, z = min(a + per, n);
+    int local = 0;
+    for (int i = a; i < z; ++i) local += cnt[i];
+    int incl = local;   // inclusive wave scan
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int v = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += v;
+    }
+    if (lane == 63) wsum[wv] = incl;
+    __syncthreads();
+    if (tid < 64) {
+        int w = tid < kInvThreads / 64 ? wsum[tid] : 0;
+        int wi = w;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int v = __shfl_up(wi, d, 64);
+            if (tid >= d) wi += v;
+        }
+        if (tid < kInvThreads / 64) wsum[tid] = wi - w;     // exclusive wave offsets
+        if (tid == kInvThreads / 64 - 1) wsum[kInvThreads / 64] = wi;
+    }
+    __syncthreads();
+    int run = wsum[wv] + incl - local;
+    for (int i = a; i < z; ++i) {
+        const int c = cnt[i];
+        cnt[i] = run;
+        run += c;
+    }
+    const int total = wsum[kInvThreads / 64];
+    __syncthreads();
+    return total;
+}
+
+template <bool kLds>
+__global__ __launch_bounds__(kInvThreads) void inverse_index_kernel(const int32_t* __restrict__ idx, int per_batch,
+                                                                    int targets, int nbatch,
+                                                                    int32_t* __restrict__ offsets,
+                                                                    int32_t* __restrict__ entries, int* gcnt) {
+    extern __shared__ int smem[];
+    int* wsum = smem;                                   // kInvThreads/64 + 1
+    int* cnt = kLds ? smem + 32 : gcnt + (size_t)blockIdx.x * targets;
+    const int b = blockIdx.x, tid = threadIdx.x;
+    const int32_t* id = idx + (size_t)b * per_batch;
+    const long long base = (long long)b * per_batch;
+    for (int t = tid; t < targets; t += kInvThreads) cnt[t] = 0;
+    __syncthreads();
+    for (int s = tid; s < per_batch; s += kInvThreads) {
+        const unsigned t = (unsigned)id[s];
+        if (t < (unsigned)targets) atomicAdd(&cnt[t], 1);
+    }
+    __syncthreads();
+    block_exclusive_scan(cnt, targets, wsum);
+    int32_t* off = offsets + (size_t)b * targets;
+    for (int t = tid; t < targets; t += kInvThreads) off[t] = (int32_t)(base + cnt[t]);
+    if (b == nbatch - 1 && tid == 0) offsets[(size_t)nbatch * targets] = (int32_t)(base + per_batch);
+    __syncthreads();
+    for (int s = tid; s < per_batch; s += kInvThreads) {
+        const unsigned t = (unsigned)id[s];
+        if (t < (unsigned)targets) {
+            const int pos = atomicAdd(&cnt[t], 1);
+            entries[base + pos] = (int32_t)(base + s);
+        }
     }
 }
 
-// offsets[t] = first position of key t in the sorted keys (lower bound), t in [0, T]
-__global__ __launch_bounds__(256) void inv_offsets_kernel(const uint32_t* __restrict__ sorted, long long n,
-                                                          long long T, int32_t* __restrict__ offsets) {
-    const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
-    if (t > T) return;
-    long long lo = 0, hi = n;
-    while (lo < hi) {
-        const long long mid = (lo + hi) >> 1;
-        if ((long long)sorted[mid] < t) lo = mid + 1;
-        else hi = mid;
-    }
-    offsets[t] = (int32_t)lo;
-}
-
-// grad_feats[(b, p), c] = sum over slots s reading p (ascending) of gout[s][3 + c]
+// grad_feats[(b, p), c] = sum over slots s reading p of gout[s][3 + c]  (fp64 accumulation)
 __global__ __launch_bounds__(256) void group_bwd_csr_kernel(const float* __restrict__ gout, int ld,
                                                             const int32_t* __restrict__ off,
                                                             const int32_t* __restrict__ ent, int total, int D,
@@ -48,13 +100,13 @@ __global__ __launch_bounds__(256) void group_bwd_csr_kernel(const float* __restr
     const int e = blockIdx.x * 256 + threadIdx.x;
     if (e >= total) return;
     const int t = e / D, c = e - t * D;
-    float acc = 0.f;
+    double acc = 0.0;
     const int a = off[t], z = off[t + 1];
-    for (int i = a; i < z; ++i) acc += gout[(size_t)ent[i] * ld + 3 + c];
-    gfeats[e] = acc;
+    for (int i = a; i < z; ++i) acc += (double)gout[(size_t)ent[i] * ld + 3 + c];
+    gfeats[e] = (float)acc;
 }
 
-// grad_pts[(b, m), c] = sum over slots s = 3*row + j reading m (ascending) of
+// grad_pts[(b, m), c] = sum over slots s = 3*row + j reading m (fp64 accumulation) of
 //   (gout[row][col_off + c] / norm_row) * w_j      -- the autograd rounding of
 // interpolate's (p*w)/norm (common.py:119-122), as the atomic kernel computes it
 __global__ __launch_bounds__(256) void interp_bwd_csr_kernel(const float* __restrict__ gout, int ld, int col_off,
@@ -65,7 +117,7 @@ __global__ __launch_bounds__(256) void interp_bwd_csr_kernel(const float* __rest
     const int e = blockIdx.x * 256 + threadIdx.x;
     if (e >= total) return;
     const int t = e / D, c = e - t * D;
-    float acc = 0.f;
+    double acc = 0.0;
     const int a = off[t], z = off[t + 1];
     for (int i = a; i < z; ++i) {
         const int s = ent[i];
@@ -75,69 +127,46 @@ __global__ __launch_bounds__(256) void interp_bwd_csr_kernel(const float* __rest
         const float w2 = 1.0f / (dist[(size_t)row * 3 + 2] + 1e-9f);
         const float nrm = (w0 + w1) + w2;
         const float wj = j == 0 ? w0 : (j == 1 ? w1 : w2);
-        acc += (gout[(size_t)row * ld + col_off + c] / nrm) * wj;
+        acc += (double)((gout[(size_t)row * ld + col_off + c] / nrm) * wj);
     }
-    gpts[e] = acc;
-}
-
-static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
-
-static int key_bits(long long T) {
-    int bits = 1;
-    while (bits < 32 && (1ll << bits) < T) ++bits;
-    return bits;
+    gpts[e] = (float)acc;
 }
 
 }  // namespace pcs
 
 using namespace pcs;
 
-// workspace bytes of pcs_inverse_index for n_slots gather slots into n_targets (= B*T) sources
+// workspace bytes of pcs_inverse_index: none while one cloud's targets fit the LDS counters
 PCS_API int pcs_inverse_index_workspace(long long n_slots, long long n_targets, size_t* bytes) {
     PCS_CHECK_ARG(n_slots >= 1 && n_slots < (1ll << 31) && n_targets >= 1 && n_targets < (1ll << 31) && bytes,
                   "pcs_inverse_index_workspace: bad sizes");
-    size_t tmp = 0;
-    const hipError_t e = rocprim::radix_sort_pairs((void*)nullptr, tmp, (const uint32_t*)nullptr, (uint32_t*)nullptr,
-                                                   (const int32_t*)nullptr, (int32_t*)nullptr, (size_t)n_slots, 0,
-                                                   key_bits(n_targets));
-    if (e != hipSuccess) {
-        set_error("pcs_inverse_index_workspace: %s", hipGetErrorString(e));
-        return (int)e;
-    }
-    *bytes = align256(tmp) + 3 * align256((size_t)n_slots * 4);
+    *bytes = (size_t)n_targets * 4;   // upper bound (global counters), also valid for the LDS path
     return 0;
 }
 
 // idx: (B * per_batch) int32 neighbour table, values in [0, targets); offsets (B*targets + 1),
 // entries (B * per_batch): slots reading source (b, p) are entries[offsets[b*targets+p] ..
-// offsets[b*targets+p+1]) in ascending order.
+// offsets[b*targets+p+1]) (order within a list unspecified).
 PCS_API int pcs_inverse_index(const int32_t* idx, int B, int per_batch, int targets, int32_t* offsets,
                               int32_t* entries, void* workspace, size_t ws_bytes, void* stream) {
     PCS_CHECK_ARG(B >= 1 && per_batch >= 1 && targets >= 1, "pcs_inverse_index: bad sizes");
     const long long n = (long long)B * per_batch, T = (long long)B * targets;
     PCS_CHECK_ARG(n < (1ll << 31) && T < (1ll << 31), "pcs_inverse_index: too many slots/targets");
-    PCS_CHECK_ARG(idx && offsets && entries && workspace, "pcs_inverse_index: null pointer");
-    size_t need = 0;
-    if (int e = pcs_inverse_index_workspace(n, T, &need)) return e;
-    PCS_CHECK_ARG(ws_bytes >= need, "pcs_inverse_index: workspace %zu < %zu bytes", ws_bytes, need);
-    char* w = (char*)workspace;
-    const size_t slot_bytes = align256((size_t)n * 4);
-    uint32_t* keys_in = (uint32_t*)w;
-    uint32_t* keys_out = (uint32_t*)(w + slot_bytes);
-    int32_t* vals_in = (int32_t*)(w + 2 * slot_bytes);
-    void* tmp = w + 3 * slot_bytes;
-    size_t tmp_bytes = need - 3 * slot_bytes;
+    PCS_CHECK_ARG(idx && offsets && entries, "pcs_inverse_index: null pointer");
     hipStream_t s = as_stream(stream);
-    hipLaunchKernelGGL(inv_keys_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, idx, n, per_batch,
-                       targets, keys_in, vals_in);
-    const hipError_t e = rocprim::radix_sort_pairs(tmp, tmp_bytes, keys_in, keys_out, vals_in, entries, (size_t)n, 0,
-                                                   key_bits(T), s);
-    if (e != hipSuccess) {
-        set_error("pcs_inverse_index: radix sort: %s", hipGetErrorString(e));
-        return (int)e;
+    if (targets <= kInvLdsTargets) {
+        static const hipError_t attr = hipFuncSetAttribute(
+            reinterpret_cast<const void*>(&inverse_index_kernel<true>), hipFuncAttributeMaxDynamicSharedMemorySize,
+            (32 + kInvLdsTargets) * (int)sizeof(int));
+        (void)attr;
+        hipLaunchKernelGGL(inverse_index_kernel<true>, dim3(B), dim3(kInvThreads), (32 + targets) * sizeof(int), s,
+                           idx, per_batch, targets, B, offsets, entries, (int*)nullptr);
+    } else {
+        PCS_CHECK_ARG(workspace && ws_bytes >= (size_t)T * 4, "pcs_inverse_index: workspace %zu < %lld bytes",
+                      ws_bytes, T * 4);
+        hipLaunchKernelGGL(inverse_index_kernel<false>, dim3(B), dim3(kInvThreads), 32 * sizeof(int), s, idx,
+                           per_batch, targets, B, offsets, entries, (int*)workspace);
     }
-    hipLaunchKernelGGL(inv_offsets_kernel, dim3((unsigned)((T + 1 + 255) / 256)), dim3(256), 0, s, keys_out, n, T,
-                       offsets);
     return launch_status("pcs_inverse_index");
 }
 

@@ -808,7 +808,11 @@ PCS_API int pcs_gemm_rows(const pcs_operand* a, int M, int K, const float* W, in
             snprintf(nm, sizeof nm, "pcs::gemm_rows_kernel<%d, %d, %d, %d, %d>", bm, bn, wm, wn, a->mode);
         }
         const double bytes = operand_bytes(*a, M, K) + 4.0 * M * N * (bstats ? 2 : 1);
-        probe = probe_start(nm, 2.0 * M * K * N, bytes, s);
+        const pcs_operand ac = *a, ec = epi ? *epi : pcs_operand{};
+        const bool he = epi != nullptr;
+        probe = probe_start(nm, 2.0 * M * K * N, bytes, s, [=]() {
+            pcs_gemm_rows(&ac, M, K, W, ldw, bias, C, ldc, N, stats, he ? &ec : nullptr, bstats, stream);
+        });
     }
     if (engine_impl() == 1 && launch_gemm_direct(g, s)) {
         probe_stop(probe, s);
@@ -843,8 +847,9 @@ PCS_API int pcs_wgrad(const pcs_operand* x, int N, const pcs_operand* y, int K, 
         char nm[96];
         if (engine_impl() == 1) direct_wgrad_name(N, K, x->mode, y->mode, nm, sizeof nm);
         else snprintf(nm, sizeof nm, "pcs::wgrad_kernel<%d, %d, %d, %d>", BO, BI, x->mode, y->mode);
+        const pcs_operand xc = *x, yc = *y;
         probe = probe_start(nm, 2.0 * M * N * K, operand_bytes(*x, M, N) + operand_bytes(*y, M, K),
-                            as_stream(stream));
+                            as_stream(stream), [=]() { pcs_wgrad(&xc, N, &yc, K, M, dW, db, stream); });
     }
     if (engine_impl() == 1 &&
         launch_wgrad_direct(to_dev(x), N, to_dev(y), K, M, dW, db, as_stream(stream))) {

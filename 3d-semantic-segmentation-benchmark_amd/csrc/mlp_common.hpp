@@ -2,6 +2,8 @@
 // operand descriptors with their on-load transforms and the row-GEMM argument block.
 #pragma once
 
+#include <functional>
+
 #include "pcs_common.hpp"
 
 namespace pcs {
@@ -139,7 +141,7 @@ void direct_gemm_name(int M, int N, int mode, char* buf, int cap);
 void direct_wgrad_name(int N, int K, int xm, int ym, char* buf, int cap);
 // engine launch probe (probe.cpp)
 bool probe_enabled();
-int probe_start(const char* name, double flops, double bytes, hipStream_t s);
+int probe_start(const char* name, double flops, double bytes, hipStream_t s, std::function<void()> relaunch);
 void probe_stop(int idx, hipStream_t s);   // 0 = LDS-staged kernels, 1 = LDS-free (PCS_GEMM_IMPL)
 
 }  // namespace pcs

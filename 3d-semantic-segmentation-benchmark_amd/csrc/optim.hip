@@ -51,10 +51,11 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
 
 using namespace pcs;
 
-// one Adam step over n parameters; beta1_w = 1 - beta1 (the lerp weight), step = -lr/(1-beta1^t),
+// one Adam step over n parameters; beta1_w = 1 - beta1 (the lerp weight), beta2_w = 1 - beta2 (both
+// rounded from double, as torch passes python floats), step = -lr/(1-beta1^t),
 // bc2_sqrt = sqrt(1 - beta2^t).  p, g, m, v: 16-byte aligned device arrays of n floats.
 PCS_API int pcs_adam(float* p, const float* g, float* m, float* v, long long n, float beta1_w, float beta2,
-                     float step, float bc2_sqrt, float eps, float weight_decay, void* stream) {
+                     float beta2_w, float step, float bc2_sqrt, float eps, float weight_decay, void* stream) {
     PCS_CHECK_ARG(n >= 0 && p && g && m && v, "pcs_adam: bad arguments");
     PCS_CHECK_ARG(((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) % 16 == 0,
                   "pcs_adam: buffers must be 16-byte aligned");
@@ -62,6 +63,6 @@ PCS_API int pcs_adam(float* p, const float* g, float* m, float* v, long long n, 
     long long blocks = (n / 4 + 255) / 256;
     blocks = blocks < 1 ? 1 : (blocks > 2048 ? 2048 : blocks);
     hipLaunchKernelGGL(adam_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), p, g, m, v, n, beta1_w,
-                       beta2, 1.f - beta2, step, bc2_sqrt, eps, weight_decay);
+                       beta2, beta2_w, step, bc2_sqrt, eps, weight_decay);
     return launch_status("pcs_adam");
 }

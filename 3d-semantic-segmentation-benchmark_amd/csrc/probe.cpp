@@ -6,6 +6,7 @@
 // the autograd backward thread launches too.
 #include <hip/hip_runtime.h>
 
+#include <functional>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -18,6 +19,8 @@ struct ProbeRec {
     std::string name;
     double flops, bytes;
     hipEvent_t e0, e1;
+    hipStream_t stream;
+    std::function<void()> relaunch;   // the identical launch again (pcs_probe_replay)
 };
 
 static std::mutex g_probe_mu;
@@ -27,9 +30,9 @@ static std::vector<ProbeRec> g_probe;
 bool probe_enabled() { return g_probe_on; }
 
 // returns the record index, or -1 (probe off / event failure); call before the launch
-int probe_start(const char* name, double flops, double bytes, hipStream_t s) {
+int probe_start(const char* name, double flops, double bytes, hipStream_t s, std::function<void()> relaunch) {
     if (!g_probe_on) return -1;
-    ProbeRec r{name, flops, bytes, nullptr, nullptr};
+    ProbeRec r{name, flops, bytes, nullptr, nullptr, s, std::move(relaunch)};
     if (hipEventCreate(&r.e0) != hipSuccess || hipEventCreate(&r.e1) != hipSuccess) return -1;
     (void)hipEventRecord(r.e0, s);
     std::lock_guard<std::mutex> g(g_probe_mu);
@@ -97,5 +100,43 @@ PCS_API int pcs_probe_get(int i, char* name, int cap, double* flops, double* byt
         return (int)err;
     }
     if (ms) *ms = t;
+    return 0;
+}
+
+// Re-issue every recorded launch of kernel `name` back to back, `reps` times (after one
+// untimed pass), between two events on their stream: the average duration of one launch
+// with the queue kept full, the figure rocprofv3 --stats reports as AverageNs for that
+// kernel (the per-launch event brackets of a step also include launch gaps).  The
+// launches rewrite their outputs (and accumulate into dW again): call after the timed run.
+PCS_API int pcs_probe_replay(const char* name, int reps, float* us_per_launch, int* launches) {
+    std::vector<ProbeRec> sel;
+    {
+        std::lock_guard<std::mutex> g(g_probe_mu);
+        PCS_CHECK_ARG(!g_probe_on, "pcs_probe_replay: call after pcs_probe_end");
+        for (const auto& r : g_probe)
+            if (r.name == name && r.relaunch) sel.push_back(r);
+    }
+    PCS_CHECK_ARG(name && reps >= 1 && us_per_launch && !sel.empty(), "pcs_probe_replay: no launches of '%s'",
+                  name ? name : "(null)");
+    const hipStream_t s = sel[0].stream;
+    for (const auto& r : sel) PCS_CHECK_ARG(r.stream == s, "pcs_probe_replay: launches of '%s' on different streams", name);
+    for (const auto& r : sel) r.relaunch();
+    hipEvent_t e0, e1;
+    if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) return (int)hipErrorUnknown;
+    (void)hipEventRecord(e0, s);
+    for (int i = 0; i < reps; ++i)
+        for (const auto& r : sel) r.relaunch();
+    (void)hipEventRecord(e1, s);
+    hipError_t err = hipEventSynchronize(e1);
+    float ms = 0.f;
+    if (err == hipSuccess) err = hipEventElapsedTime(&ms, e0, e1);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    if (err != hipSuccess) {
+        set_error("pcs_probe_replay: %s", hipGetErrorString(err));
+        return (int)err;
+    }
+    *us_per_launch = ms * 1e3f / (float)(reps * (int)sel.size());
+    if (launches) *launches = (int)sel.size();
     return 0;
 }

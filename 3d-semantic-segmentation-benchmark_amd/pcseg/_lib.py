@@ -53,6 +53,7 @@ SIGNATURES = {
     'pcs_probe_begin': [],
     'pcs_probe_end': [],
     'pcs_probe_get': [I32, ctypes.c_char_p, I32, P, P, P],
+    'pcs_probe_replay': [ctypes.c_char_p, I32, P, P],
     'pcs_mlp_workspace': [I32, I32, I32, ctypes.c_char_p, I32, I32, I32, P],
     'pcs_mlp_forward': [P, I32, I32, I32, ctypes.c_char_p, I32, I32, P, P, P, ctypes.c_size_t, P],
     'pcs_mlp_backward': [P, I32, I32, I32, ctypes.c_char_p, I32, I32, P, P, P, P, ctypes.c_size_t, P],
@@ -75,7 +76,7 @@ SIGNATURES = {
     # block batches
     'pcs_gather_blocks': [P, P, P, I64, P, P, P],
     # optimizer
-    'pcs_adam': [P, P, P, P, I64, F32, F32, F32, F32, F32, F32, P],
+    'pcs_adam': [P, P, P, P, I64, F32, F32, F32, F32, F32, F32, F32, P],
     # loss
     'pcs_masked_ce_blocks': [I32, I32],
     'pcs_masked_ce': [P, I32, P, I32, I32, P, I32, I32, I32, P, P, P, P],

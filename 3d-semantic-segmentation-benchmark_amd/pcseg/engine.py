@@ -97,6 +97,13 @@ class KernelProbe:
             out.append((buf.value.decode(), fl.value, by.value, ms.value * 1e-3))
         return out
 
+    def replay(self, name: str, reps: int = 20) -> float:
+        """Average seconds per launch of kernel `name`, its recorded launches re-issued
+        back to back (pcs_probe_replay; comparable with rocprofv3's AverageNs)."""
+        us, n = ctypes.c_float(), ctypes.c_int()
+        call('pcs_probe_replay', name.encode(), reps, ctypes.byref(us), ctypes.byref(n))
+        return us.value * 1e-6
+
     def summary(self):
         """{kernel: (launches, flops, bytes, seconds)} (synchronises)."""
         out = {}

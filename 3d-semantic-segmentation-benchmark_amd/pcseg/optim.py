@@ -47,5 +47,5 @@ class FlatAdam:
         step = -(self.lr / bc1)
         bc2_sqrt = math.sqrt(1 - b2 ** self.t)
         call('pcs_adam', ptr(self.flat), ptr(self.grads.flat), ptr(self.exp_avg), ptr(self.exp_avg_sq),
-             self.flat.numel(), 1 - b1, b2, step, bc2_sqrt, self.eps, self.weight_decay,
+             self.flat.numel(), 1 - b1, b2, 1 - b2, step, bc2_sqrt, self.eps, self.weight_decay,
              stream_ptr(self.flat.device))

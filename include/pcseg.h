@@ -222,6 +222,11 @@ int pcs_probe_begin(void);
 int pcs_probe_end(void);
 int pcs_probe_get(int i, char* name, int cap, double* flops, double* bytes,
                   float* ms);
+/* After pcs_probe_end: re-issue every recorded launch of kernel `name` back to back
+ * `reps` times (after one untimed pass) between two events on their stream; returns
+ * the average microseconds per launch -- comparable with rocprofv3's AverageNs for
+ * that kernel.  The launches rewrite their outputs. */
+int pcs_probe_replay(const char* name, int reps, float* us_per_launch, int* launches);
 
 /* ---- inverse neighbour maps (atomic-free gather backward) ------------------ */
 
@@ -259,11 +264,12 @@ int pcs_gather_blocks(const float* points, const uint8_t* labels,
 
 /* torch.optim.Adam step (amsgrad=False; the reference trains with Adam lr 1e-3,
  * Training/train_model.py:263) over flat fp32 arrays of n parameters: p, g, m
- * (exp_avg), v (exp_avg_sq); beta1_w = 1 - beta1, step = -lr / (1 - beta1^t),
+ * (exp_avg), v (exp_avg_sq); beta1_w = 1 - beta1, beta2_w = 1 - beta2 (computed in
+ * double, as torch does with python floats), step = -lr / (1 - beta1^t),
  * bc2_sqrt = sqrt(1 - beta2^t).  16-byte aligned buffers. */
 int pcs_adam(float* p, const float* g, float* m, float* v, long long n, float beta1_w,
-             float beta2, float step, float bc2_sqrt, float eps, float weight_decay,
-             void* stream);
+             float beta2, float beta2_w, float step, float bc2_sqrt, float eps,
+             float weight_decay, void* stream);
 
 /* ---- loss ---------------------------------------------------------------- */
 

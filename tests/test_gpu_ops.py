@@ -247,14 +247,18 @@ def test_inverse_index_and_group_bwd_csr(B, N, C, K, r):
     cent = xyz[:, :C].contiguous()
     idx = ops.ball_query(cent, xyz, r, K)
     off, ent = ops.inverse_index(idx, N)
-    # the CSR lists exactly the slots reading each point, ascending
+    # the CSR lists exactly the slots reading each point (order within a list unspecified)
     flat = idx.reshape(B, -1).long().cpu()
     key = (torch.arange(B).unsqueeze(1) * N + flat).reshape(-1)
     order = torch.sort(key, stable=True).indices
-    assert torch.equal(ent.long().cpu(), order)
     counts = torch.bincount(key, minlength=B * N)
-    assert torch.equal(off.long().cpu(), torch.cat([torch.zeros(1, dtype=torch.long), counts.cumsum(0)]))
-    # gather backward == atomic backward (same terms, fixed ascending order)
+    offs = torch.cat([torch.zeros(1, dtype=torch.long), counts.cumsum(0)])
+    assert torch.equal(off.long().cpu(), offs)
+    seg = torch.repeat_interleave(torch.arange(B * N), counts)
+    got = ent.long().cpu()
+    # sort each list by slot: (segment, slot) lexicographic == the stable order
+    assert torch.equal(got[torch.argsort(seg * (B * C * K) + got)], order)
+    # gather backward == atomic backward (same terms; CSR sums in fp64)
     D = 19
     feats = torch.randn(B, N, D, device=DEV)
     fa = feats.clone().requires_grad_(True)
@@ -265,7 +269,7 @@ def test_inverse_index_and_group_bwd_csr(B, N, C, K, r):
     w = torch.randn_like(ya)
     (ya * w).sum().backward()
     (yb * w).sum().backward()
-    # same terms, different fp32 summation order (atomics vs ascending slots): sums of up
+    # same terms, different summation (fp32 atomics vs fp64 gather): sums of up
     # to ~K*C/N*... randn terms, so compare with an absolute floor at the fp32 ulp of the terms
     assert torch.allclose(fa.grad, fb.grad, rtol=1e-5, atol=1e-4), float((fa.grad - fb.grad).abs().max())
     # deterministic
@@ -293,3 +297,23 @@ def test_interp_bwd_csr_matches_atomic():
     (ya * w).sum().backward()
     (yb * w).sum().backward()
     assert torch.allclose(f2a.grad, f2b.grad, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize('B,S,k,targets,kind', [(3, 500, 7, 1000, 'random'), (2, 1024, 32, 4096, 'same'),
+                                                  (2, 3000, 3, 40000, 'random'), (1, 2048, 32, 50000, 'same'),
+                                                  (2, 1, 1, 1, 'random')])
+def test_inverse_index_random_tables(B, S, k, targets, kind):
+    """CSR of arbitrary tables: LDS-counter path (targets <= 32768) and global-counter path,
+    including the degenerate table where every slot reads the same point."""
+    g = torch.Generator().manual_seed(7)
+    if kind == 'same':
+        idx = torch.full((B, S, k), targets // 3, dtype=torch.int32)
+    else:
+        idx = torch.randint(0, targets, (B, S, k), generator=g, dtype=torch.int32)
+    off, ent = ops.inverse_index(idx.to(DEV), targets)
+    key = (torch.arange(B).unsqueeze(1) * targets + idx.reshape(B, -1).long()).reshape(-1)
+    counts = torch.bincount(key, minlength=B * targets)
+    assert torch.equal(off.long().cpu(), torch.cat([torch.zeros(1, dtype=torch.long), counts.cumsum(0)]))
+    seg = torch.repeat_interleave(torch.arange(B * targets), counts)
+    got = ent.long().cpu()
+    assert torch.equal(got[torch.argsort(seg * (B * S * k) + got)], torch.sort(key, stable=True).indices)
