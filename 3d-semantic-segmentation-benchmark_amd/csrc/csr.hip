@@ -92,18 +92,43 @@ __global__ __launch_bounds__(kInvThreads) void inverse_index_kernel(const int32_
     }
 }
 
+// Gather backward over the inverse maps: ONE WAVE PER SOURCE POINT, lanes over channels,
+// so every slot's gradient row is read as contiguous channel runs (coalesced).  The slot
+// list is fetched 64 entries at a time, one per lane (with the entry's per-slot
+// coefficients computed once, lane-parallel), then walked with v_readlane, 4 row loads
+// in flight per lane.
+
 // grad_feats[(b, p), c] = sum over slots s reading p of gout[s][3 + c]  (fp64 accumulation)
 __global__ __launch_bounds__(256) void group_bwd_csr_kernel(const float* __restrict__ gout, int ld,
                                                             const int32_t* __restrict__ off,
-                                                            const int32_t* __restrict__ ent, int total, int D,
+                                                            const int32_t* __restrict__ ent, int targets, int D,
                                                             float* __restrict__ gfeats) {
-    const int e = blockIdx.x * 256 + threadIdx.x;
-    if (e >= total) return;
-    const int t = e / D, c = e - t * D;
-    double acc = 0.0;
+    const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (t >= targets) return;
     const int a = off[t], z = off[t + 1];
-    for (int i = a; i < z; ++i) acc += (double)gout[(size_t)ent[i] * ld + 3 + c];
-    gfeats[e] = (float)acc;
+    for (int c0 = 0; c0 < D; c0 += 64) {
+        const int c = c0 + lane;
+        const int cc = 3 + (c < D ? c : D - 1);
+        double acc = 0.0;
+        for (int base = a; base < z; base += 64) {
+            const int n = min(64, z - base);
+            const int mine = lane < n ? ent[base + lane] : 0;
+            int e = 0;
+            for (; e + 4 <= n; e += 4) {
+                const float v0 = gout[(size_t)__builtin_amdgcn_readlane(mine, e) * ld + cc];
+                const float v1 = gout[(size_t)__builtin_amdgcn_readlane(mine, e + 1) * ld + cc];
+                const float v2 = gout[(size_t)__builtin_amdgcn_readlane(mine, e + 2) * ld + cc];
+                const float v3 = gout[(size_t)__builtin_amdgcn_readlane(mine, e + 3) * ld + cc];
+                acc += (double)v0;
+                acc += (double)v1;
+                acc += (double)v2;
+                acc += (double)v3;
+            }
+            for (; e < n; ++e) acc += (double)gout[(size_t)__builtin_amdgcn_readlane(mine, e) * ld + cc];
+        }
+        if (c < D) gfeats[(size_t)t * D + c] = (float)acc;
+    }
 }
 
 // grad_pts[(b, m), c] = sum over slots s = 3*row + j reading m (fp64 accumulation) of
@@ -112,24 +137,49 @@ __global__ __launch_bounds__(256) void group_bwd_csr_kernel(const float* __restr
 __global__ __launch_bounds__(256) void interp_bwd_csr_kernel(const float* __restrict__ gout, int ld, int col_off,
                                                              const float* __restrict__ dist,
                                                              const int32_t* __restrict__ off,
-                                                             const int32_t* __restrict__ ent, int total, int D,
+                                                             const int32_t* __restrict__ ent, int targets, int D,
                                                              float* __restrict__ gpts) {
-    const int e = blockIdx.x * 256 + threadIdx.x;
-    if (e >= total) return;
-    const int t = e / D, c = e - t * D;
-    double acc = 0.0;
+    const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (t >= targets) return;
     const int a = off[t], z = off[t + 1];
-    for (int i = a; i < z; ++i) {
-        const int s = ent[i];
-        const int row = s / 3, j = s - 3 * row;
-        const float w0 = 1.0f / (dist[(size_t)row * 3 + 0] + 1e-9f);
-        const float w1 = 1.0f / (dist[(size_t)row * 3 + 1] + 1e-9f);
-        const float w2 = 1.0f / (dist[(size_t)row * 3 + 2] + 1e-9f);
-        const float nrm = (w0 + w1) + w2;
-        const float wj = j == 0 ? w0 : (j == 1 ? w1 : w2);
-        acc += (double)((gout[(size_t)row * ld + col_off + c] / nrm) * wj);
+    for (int c0 = 0; c0 < D; c0 += 64) {
+        const int c = c0 + lane;
+        const int cc = col_off + (c < D ? c : D - 1);
+        double acc = 0.0;
+        for (int base = a; base < z; base += 64) {
+            const int n = min(64, z - base);
+            // this lane's entry: its row and IDW coefficients (nrm, w_j)
+            int row = 0;
+            float nrm = 1.f, wj = 0.f;
+            if (lane < n) {
+                const int s = ent[base + lane];
+                row = s / 3;
+                const int j = s - 3 * row;
+                const float w0 = 1.0f / (dist[(size_t)row * 3 + 0] + 1e-9f);
+                const float w1 = 1.0f / (dist[(size_t)row * 3 + 1] + 1e-9f);
+                const float w2 = 1.0f / (dist[(size_t)row * 3 + 2] + 1e-9f);
+                nrm = (w0 + w1) + w2;
+                wj = j == 0 ? w0 : (j == 1 ? w1 : w2);
+            }
+            auto term = [&](int e) {
+                const int r = __builtin_amdgcn_readlane(row, e);
+                const float nv = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(nrm), e));
+                const float wv = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wj), e));
+                return (gout[(size_t)r * ld + cc] / nv) * wv;
+            };
+            int e = 0;
+            for (; e + 4 <= n; e += 4) {
+                const float v0 = term(e), v1 = term(e + 1), v2 = term(e + 2), v3 = term(e + 3);
+                acc += (double)v0;
+                acc += (double)v1;
+                acc += (double)v2;
+                acc += (double)v3;
+            }
+            for (; e < n; ++e) acc += (double)term(e);
+        }
+        if (c < D) gpts[(size_t)t * D + c] = (float)acc;
     }
-    gpts[e] = (float)acc;
 }
 
 }  // namespace pcs
@@ -174,11 +224,11 @@ PCS_API int pcs_inverse_index(const int32_t* idx, int B, int per_batch, int targ
 PCS_API int pcs_group_bwd_csr(const float* grad_out, int ld_gout, const int32_t* offsets, const int32_t* entries,
                               int B, int N, int D, float* grad_feats, void* stream) {
     PCS_CHECK_ARG(B >= 1 && N >= 1 && D >= 1 && ld_gout >= 3 + D, "pcs_group_bwd_csr: bad sizes");
-    const long long total = (long long)B * N * D;
+    const long long total = (long long)B * N * D, targets = (long long)B * N;
     PCS_CHECK_ARG(total < (1ll << 31), "pcs_group_bwd_csr: too many elements");
     PCS_CHECK_ARG(grad_out && offsets && entries && grad_feats, "pcs_group_bwd_csr: null pointer");
-    hipLaunchKernelGGL(group_bwd_csr_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, as_stream(stream),
-                       grad_out, ld_gout, offsets, entries, (int)total, D, grad_feats);
+    hipLaunchKernelGGL(group_bwd_csr_kernel, dim3((unsigned)((targets + 3) / 4)), dim3(256), 0, as_stream(stream),
+                       grad_out, ld_gout, offsets, entries, (int)targets, D, grad_feats);
     return launch_status("pcs_group_bwd_csr");
 }
 
@@ -187,10 +237,10 @@ PCS_API int pcs_interp_bwd_csr(const float* grad_out, int ld_gout, int col_off, 
                                const int32_t* offsets, const int32_t* entries, int B, int M, int D, float* grad_pts,
                                void* stream) {
     PCS_CHECK_ARG(B >= 1 && M >= 1 && D >= 1 && ld_gout >= col_off + D && col_off >= 0, "pcs_interp_bwd_csr: bad sizes");
-    const long long total = (long long)B * M * D;
+    const long long total = (long long)B * M * D, targets = (long long)B * M;
     PCS_CHECK_ARG(total < (1ll << 31), "pcs_interp_bwd_csr: too many elements");
     PCS_CHECK_ARG(grad_out && dist && offsets && entries && grad_pts, "pcs_interp_bwd_csr: null pointer");
-    hipLaunchKernelGGL(interp_bwd_csr_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, as_stream(stream),
-                       grad_out, ld_gout, col_off, dist, offsets, entries, (int)total, D, grad_pts);
+    hipLaunchKernelGGL(interp_bwd_csr_kernel, dim3((unsigned)((targets + 3) / 4)), dim3(256), 0, as_stream(stream),
+                       grad_out, ld_gout, col_off, dist, offsets, entries, (int)targets, D, grad_pts);
     return launch_status("pcs_interp_bwd_csr");
 }

@@ -45,6 +45,38 @@ __global__ void group_fwd_kernel(const float* __restrict__ xyz, const float* __r
     }
 }
 
+// one thread per (row, 4 output channels): same per-element arithmetic, one 16-B store
+// (ld % 4 == 0; rows are 16-B aligned)
+__global__ __launch_bounds__(256) void group_fwd_q_kernel(const float* __restrict__ xyz,
+                                                          const float* __restrict__ feats,
+                                                          const float* __restrict__ cent, const int* __restrict__ idx,
+                                                          int C, int N, int K, int D, float r, int normalize,
+                                                          float* __restrict__ out, int nq, long long total) {
+    for (long long t = gtid(); t < total; t += gstride()) {
+        const long long row = t / nq;
+        const int q = (int)(t - row * nq);
+        const long long g = row / K;          // centroid row b*C + c
+        const int b = (int)(g / C);
+        const long long pb = (long long)b * N + idx[row];
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int ch = 4 * q + e;
+            float x;
+            if (ch < 3) {
+                x = xyz[pb * 3 + ch] - cent[g * 3 + ch];
+                if (normalize) x = x / r;
+            } else if (ch < 3 + D) {
+                x = feats[pb * D + (ch - 3)];
+            } else {
+                x = 0.f;
+            }
+            v[e] = x;
+        }
+        reinterpret_cast<float4*>(out)[t] = make_float4(v[0], v[1], v[2], v[3]);
+    }
+}
+
 __global__ void group_bwd_kernel(const float* __restrict__ gout, const int* __restrict__ idx, int C, int N, int K,
                                  int D, int W, float* __restrict__ gfeats, long long total) {
     for (long long t = gtid(); t < total; t += gstride()) {
@@ -104,6 +136,41 @@ __global__ void interp_fwd_kernel(const float* __restrict__ pts, const int* __re
         const float t1 = (P[(long long)idx[row * 3 + 1] * D] * w1) / nrm;
         const float t2 = (P[(long long)idx[row * 3 + 2] * D] * w2) / nrm;
         out[row * ld_out + col_off + ch] = (t0 + t1) + t2;
+    }
+}
+
+// [f1 | IDW-interpolate(pts)] rows in one pass, one thread per (row, 4 channels): the
+// skip features are copied, the interpolated quad uses float4 gathers of the three
+// neighbours with the scalar kernel's per-element arithmetic.  D1, D2, ld_out % 4 == 0.
+__global__ __launch_bounds__(256) void interp_cat_q_kernel(const float* __restrict__ f1, int D1,
+                                                           const float* __restrict__ pts,
+                                                           const int* __restrict__ idx,
+                                                           const float* __restrict__ dist, int N, int M, int D2,
+                                                           float* __restrict__ out, int ldq, long long total) {
+    const int q1 = D1 / 4, nq = q1 + D2 / 4;
+    for (long long t = gtid(); t < total; t += gstride()) {
+        const long long row = t / nq;           // b*N + n
+        const int q = (int)(t - row * nq);
+        float4 o;
+        if (q < q1) {
+            o = reinterpret_cast<const float4*>(f1)[row * q1 + q];
+        } else {
+            const int b = (int)(row / N);
+            const float w0 = 1.0f / (dist[row * 3 + 0] + 1e-9f);
+            const float w1 = 1.0f / (dist[row * 3 + 1] + 1e-9f);
+            const float w2 = 1.0f / (dist[row * 3 + 2] + 1e-9f);
+            const float nrm = (w0 + w1) + w2;
+            const float4* P = reinterpret_cast<const float4*>(pts + (long long)b * M * D2) + (q - q1);
+            const int dq = D2 / 4;
+            const float4 a = P[(long long)idx[row * 3 + 0] * dq];
+            const float4 c = P[(long long)idx[row * 3 + 1] * dq];
+            const float4 d = P[(long long)idx[row * 3 + 2] * dq];
+            o.x = ((a.x * w0) / nrm + (c.x * w1) / nrm) + (d.x * w2) / nrm;
+            o.y = ((a.y * w0) / nrm + (c.y * w1) / nrm) + (d.y * w2) / nrm;
+            o.z = ((a.z * w0) / nrm + (c.z * w1) / nrm) + (d.z * w2) / nrm;
+            o.w = ((a.w * w0) / nrm + (c.w * w1) / nrm) + (d.w * w2) / nrm;
+        }
+        reinterpret_cast<float4*>(out)[row * ldq + q] = o;
     }
 }
 
@@ -177,6 +244,11 @@ PCS_API int pcs_group_fwd(const float* xyz, const float* feats, const float* cen
     PCS_CHECK_ARG(xyz && centroids && idx && out && (D == 0 || feats), "pcs_group_fwd: null pointer");
     const long long total = (long long)B * C * K * ld_out;
     if (total == 0) return 0;
+    if (ld_out % 4 == 0 && (uintptr_t)out % 16 == 0) {
+        hipLaunchKernelGGL(group_fwd_q_kernel, grid_for(total / 4), dim3(256), 0, as_stream(stream), xyz, feats,
+                           centroids, idx, C, N, K, D, r, normalize, out, ld_out / 4, total / 4);
+        return launch_status("pcs_group_fwd");
+    }
     hipLaunchKernelGGL(group_fwd_kernel, grid_for(total), dim3(256), 0, as_stream(stream), xyz, feats, centroids,
                        idx, C, N, K, D, r, normalize, out, ld_out, total);
     return launch_status("pcs_group_fwd");
@@ -226,6 +298,14 @@ PCS_API int pcs_interp_fwd(const float* pts, const int32_t* idx, const float* di
     const long long total = (long long)B * N * D;
     if (total == 0) return 0;
     PCS_CHECK_ARG(pts && idx && dist && out, "pcs_interp_fwd: null pointer");
+    if (D % 4 == 0 && col_off % 4 == 0 && ld_out % 4 == 0 && ((uintptr_t)out | (uintptr_t)pts) % 16 == 0) {
+        // the interpolated columns as the f1-less case of the fused kernel, shifted by col_off
+        const long long rows = (long long)B * N;
+        hipLaunchKernelGGL(interp_cat_q_kernel, grid_for(rows * (D / 4)), dim3(256), 0, as_stream(stream),
+                           (const float*)nullptr, 0, pts, idx, dist, N, M, D, out + col_off, ld_out / 4,
+                           rows * (D / 4));
+        return launch_status("pcs_interp_fwd");
+    }
     hipLaunchKernelGGL(interp_fwd_kernel, grid_for(total), dim3(256), 0, as_stream(stream), pts, idx, dist, N, M, D,
                        out, ld_out, col_off, total);
     return launch_status("pcs_interp_fwd");
@@ -266,4 +346,20 @@ PCS_API int pcs_edge_bwd(const float* grad_out, int ld_gout, const int32_t* idx,
     hipLaunchKernelGGL(edge_bwd_kernel, grid_for(total), dim3(256), 0, as_stream(stream), grad_out, idx, N, k, D,
                        ld_gout, grad_x, total);
     return launch_status("pcs_edge_bwd");
+}
+
+// Reference FeaturePropagation (common.py:115-122, 238-240): rows (B*N, ld_out) =
+// [f1 (B, N, D1) | interpolate(pts (B, M, D2))] in one pass; D1, D2, ld_out multiples of 4
+// with ld_out >= D1 + D2 (the pad columns are not written).  f1 may be null when D1 == 0.
+PCS_API int pcs_interp_cat_fwd(const float* f1, int D1, const float* pts, const int32_t* idx, const float* dist,
+                               int B, int N, int M, int D2, float* out, int ld_out, void* stream) {
+    PCS_CHECK_ARG(B >= 0 && N >= 0 && M >= 3 && D2 >= 4 && D1 >= 0 && ld_out >= D1 + D2, "pcs_interp_cat_fwd: bad sizes");
+    PCS_CHECK_ARG(D1 % 4 == 0 && D2 % 4 == 0 && ld_out % 4 == 0, "pcs_interp_cat_fwd: D1, D2, ld_out must be multiples of 4");
+    PCS_CHECK_ARG(pts && idx && dist && out && (D1 == 0 || f1), "pcs_interp_cat_fwd: null pointer");
+    PCS_CHECK_ARG(((uintptr_t)out | (uintptr_t)pts | (uintptr_t)f1) % 16 == 0, "pcs_interp_cat_fwd: 16-B alignment");
+    const long long total = (long long)B * N * ((D1 + D2) / 4);
+    if (total == 0) return 0;
+    hipLaunchKernelGGL(interp_cat_q_kernel, grid_for(total), dim3(256), 0, as_stream(stream), f1, D1, pts, idx, dist,
+                       N, M, D2, out, ld_out / 4, total);
+    return launch_status("pcs_interp_cat_fwd");
 }

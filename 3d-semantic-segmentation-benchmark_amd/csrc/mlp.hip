@@ -168,17 +168,21 @@ __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(GemmArgs g) {
                 float sp = 0.f, tp = 0.f, mp = 0.f, ip = 0.f;
                 if (want_b) { sp = g.e.s[colc]; tp = g.e.t[colc]; mp = g.e.mean[colc]; ip = g.e.inv[colc]; }
 #pragma unroll
-                for (int i = 0; i < TM; ++i) {
-                    float zt[16];
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int hb = 0; hb < 2; ++hb) {     // Z loads batched 8 at a time (register budget)
+                    float zt[8];
                     if (want_b) {
 #pragma unroll
-                        for (int r = 0; r < 16; ++r) {
+                        for (int rr = 0; rr < 8; ++rr) {
+                            const int r = 8 * hb + rr;
                             const int row = min(m0 + wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h, g.M - 1);
-                            zt[r] = g.e.z[(size_t)row * g.e.ldz + colc];
+                            zt[rr] = g.e.z[(size_t)row * g.e.ldz + colc];
                         }
                     }
 #pragma unroll
-                    for (int r = 0; r < 16; ++r) {
+                    for (int rr = 0; rr < 8; ++rr) {
+                        const int r = 8 * hb + rr;
                         const int row = m0 + wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
                         const bool ok = row < g.M && cok;
                         const float v = acc[i][j][r] + bv;
@@ -189,7 +193,7 @@ __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(GemmArgs g) {
                             s2[j] += d * d;
                         }
                         if (want_b) {
-                            const float z = zt[r];
+                            const float z = zt[rr];
                             const float dy = v * dact_f(z * sp + tp, g.e.act, g.e.slope);
                             const float xh = (z - mp) * ip;
                             const double dd = ok ? (double)dy : 0.0;
@@ -237,24 +241,30 @@ __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(GemmArgs g) {
 // gradient and Z on load), Y = the layer's input (through the previous layer's BNACT).
 // Same LDS/fragment scheme as the row GEMM with the ROW index as the reduction
 // axis: X and Y slabs of 32 rows are stored transposed ([channel][row], 144-B
-// stride) so each lane's fragment is 16 consecutive rows.  fp32 partial sums are
-// flushed every 8 slabs (256 rows) into a second accumulator to bound the
-// accumulation error, and blocks combine with fp32 atomics.
+// stride) so each lane's fragment is 16 consecutive rows.  Each block accumulates its
+// row range in the MFMA's fp32 accumulators and blocks combine with fp32 atomics.
 // row swizzle of channel c's LDS row (multiples of 4: keeps 4-row groups 16-B contiguous)
 __device__ __forceinline__ int lds_swz(int c) { return ((c >> 3) & 7) << 2; }
 
-template <int BO, int BI, int XM, int YM, bool PF2>
+//
+// Wave grid: WGO x WGI waves split the BO x BI tile and WR = 4 / (WGO * WGI) waves split
+// each slab's 32 rows (thin tiles: a 32-wide side has one wave, the spare waves take
+// disjoint row quarters/halves of the slab and add their partial tiles separately).
+template <int BO, int BI, int XM, int YM, int NS>
 __global__ __launch_bounds__(256, 2) void wgrad_kernel(Operand xo, int N, Operand yo, int K, int M,
                                                        int rows_per_block, float* __restrict__ dW,
                                                        float* __restrict__ db) {
     constexpr int BR = 32, LDR = BR + 4;
-    constexpr int TM = BO / 64, TN = BI / 64;
+    constexpr int WGO = BO >= 64 ? 2 : 1, WGI = BI >= 64 ? 2 : 1, WR = 4 / (WGO * WGI);
+    constexpr int QPW = 4 / WR;                       // 4-row fragment groups (q) per wave per half-slab
+    constexpr int TM = BO / WGO / 32, TN = BI / WGI / 32;
     constexpr int XV = BR * BO / 4 / 256, YV = BR * BI / 4 / 256;
+    static_assert(TM >= 1 && TN >= 1 && XV >= 1 && YV >= 1, "wgrad tile");
     __shared__ __attribute__((aligned(16))) float Xs[2][BO][LDR];
     __shared__ __attribute__((aligned(16))) float Ys[2][BI][LDR];
     __shared__ float dbs[256 / (BO / 4)][BO];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wo = wave >> 1, wi = wave & 1;
+    const int wi = wave % WGI, wo = (wave / WGI) % WGO, wr = wave / (WGI * WGO);
     const int h = lane >> 5, l32 = lane & 31;
     const int tiles_i = (K + BI - 1) / BI;
     const int n0 = (blockIdx.y / tiles_i) * BO;
@@ -278,17 +288,19 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(Operand xo, int N, Operan
     load_quad<YM>(yo, gk, K, qy);
     float dbv[4] = {0.f, 0.f, 0.f, 0.f};
 
-    f32x16 acc[TM][TN], tot[TM][TN];
+    // the MFMA accumulates the block's rows (<= a few thousand) directly in fp32: a second
+    // flush accumulator would cost TM*TN*16 more VGPRs and push the wide tiles into scratch
+    f32x16 acc[TM][TN];
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) { acc[i][j][r] = 0.f; tot[i][j][r] = 0.f; }
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-    // PF2: two register stages, so each slab's loads are issued two slabs ahead of their
-    // LDS store (thin tiles, where one slab of MFMAs is too short to cover HBM latency)
-    constexpr int NS = PF2 ? 2 : 1;
+    // NS register stages: each slab's loads are issued NS slabs ahead of their LDS store
+    // (thin tiles, where one slab of MFMAs is too short to cover HBM latency)
+    static_assert(NS >= 1 && NS <= 4, "stages");
     float4 rx[NS][XV], rxz[NS][XV], ry[NS][YV], ryz[NS][YV];
     unsigned rxa[NS][XV], rya[NS][YV];
     const int gnc = min(gn, xo.ld - 4), gkc = min(gk, yo.ld - 4);
@@ -332,8 +344,8 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(Operand xo, int N, Operan
 
     const int nslab = (re - rb + BR - 1) / BR;
     if (nslab > 0) {
-        gload(0, rb);
-        if (PF2) gload(NS - 1, rb + BR);
+#pragma unroll
+        for (int u = 0; u < NS; ++u) gload(u, rb + u * BR);
         sstore(0, 0, rb);
     }
     __syncthreads();
@@ -344,16 +356,17 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(Operand xo, int N, Operan
         gload(lst, rb + (sl + NS) * BR);
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
+        for (int qi = 0; qi < QPW; ++qi) {
+            const int q = wr * QPW + qi;
             float4 a[TM], b[TN];
 #pragma unroll
             for (int i = 0; i < TM; ++i)
                 a[i] = *reinterpret_cast<const float4*>(
-                    &Xs[buf][wo * (BO / 2) + i * 32 + l32][(16 * h + 4 * q) ^ lds_swz(wo * (BO / 2) + i * 32 + l32)]);
+                    &Xs[buf][wo * (BO / WGO) + i * 32 + l32][(16 * h + 4 * q) ^ lds_swz(wo * (BO / WGO) + i * 32 + l32)]);
 #pragma unroll
             for (int j = 0; j < TN; ++j)
                 b[j] = *reinterpret_cast<const float4*>(
-                    &Ys[buf][wi * (BI / 2) + j * 32 + l32][(16 * h + 4 * q) ^ lds_swz(wi * (BI / 2) + j * 32 + l32)]);
+                    &Ys[buf][wi * (BI / WGI) + j * 32 + l32][(16 * h + 4 * q) ^ lds_swz(wi * (BI / WGI) + j * 32 + l32)]);
 #pragma unroll
             for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -364,36 +377,27 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(Operand xo, int N, Operan
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].w, b[j].w, acc[i][j], 0, 0, 0);
                 }
         }
-        if ((sl & 7) == 7) {
-#pragma unroll
-            for (int i = 0; i < TM; ++i)
-#pragma unroll
-                for (int j = 0; j < TN; ++j)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) { tot[i][j][r] += acc[i][j][r]; acc[i][j][r] = 0.f; }
-        }
         __builtin_amdgcn_sched_barrier(0);
         if (sl + 1 < nslab) sstore(sst, buf ^ 1, rb + (sl + 1) * BR);
         __syncthreads();
     };
-    if constexpr (PF2) {
-        for (int sl = 0; sl < nslab; sl += 2) {
-            body(sl, 0, 1);           // slab sl+2 -> stage 0, slab sl+1 from stage 1
-            if (sl + 1 >= nslab) break;
-            body(sl + 1, 1, 0);
+    // slab sl's registers live in stage sl % NS: freed once stored, refilled with slab sl + NS
+    for (int sl = 0; sl < nslab; sl += NS) {
+#pragma unroll
+        for (int u = 0; u < NS; ++u) {
+            if (sl + u >= nslab) break;
+            body(sl + u, u, (u + 1) % NS);
         }
-    } else {
-        for (int sl = 0; sl < nslab; ++sl) body(sl, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
-            const int kcol = k0 + wi * (BI / 2) + j * 32 + l32;
+            const int kcol = k0 + wi * (BI / WGI) + j * 32 + l32;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const int n = n0 + wo * (BO / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                if (n < N && kcol < K) atomicAdd(&dW[(size_t)n * K + kcol], tot[i][j][r] + acc[i][j][r]);
+                const int n = n0 + wo * (BO / WGO) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (n < N && kcol < K) atomicAdd(&dW[(size_t)n * K + kcol], acc[i][j][r]);
             }
         }
     if (do_db) {
@@ -673,15 +677,38 @@ static void launch_gemm(const GemmArgs& g, int gx, hipStream_t s) {
     }
 }
 
+// register stages of thin wgrad tiles (PCS_WGRAD_STAGES: 2 or 4) and whether 32-wide
+// wgrad tiles are used for <= 32 channels (PCS_WGRAD_THIN32)
+static int wgrad_stages() {
+    static const int v = [] { const char* e = getenv("PCS_WGRAD_STAGES"); return e && atoi(e) == 4 ? 4 : 2; }();
+    return v;
+}
+static int wgrad_thin32() {
+    static const int v = [] { const char* e = getenv("PCS_WGRAD_THIN32"); return e ? atoi(e) : 0; }();
+    return v;
+}
+
 template <int BO, int BI, int XM>
 static void launch_wgrad_y(dim3 grid, hipStream_t st, const Operand& x, int N, const Operand& y, int K, int M,
                            int rows, float* dW, float* db) {
-    constexpr bool PF2 = BO == 64 && BI == 64;      // thin tiles: two slabs of loads in flight
+    // thin tiles keep wgrad_stages() slabs of loads in flight, wide tiles one
+    if constexpr (BO <= 64 && BI <= 64) {
+        if (wgrad_stages() == 4) {
+            if (y.mode == OP_BNACT)
+                hipLaunchKernelGGL((wgrad_kernel<BO, BI, XM, OP_BNACT, 4>), grid, dim3(256), 0, st, x, N, y, K, M, rows,
+                                   dW, db);
+            else
+                hipLaunchKernelGGL((wgrad_kernel<BO, BI, XM, OP_PLAIN, 4>), grid, dim3(256), 0, st, x, N, y, K, M, rows,
+                                   dW, db);
+            return;
+        }
+    }
+    constexpr int NS = BO <= 64 && BI <= 64 ? 2 : 1;
     if (y.mode == OP_BNACT)
-        hipLaunchKernelGGL((wgrad_kernel<BO, BI, XM, OP_BNACT, PF2>), grid, dim3(256), 0, st, x, N, y, K, M, rows, dW,
+        hipLaunchKernelGGL((wgrad_kernel<BO, BI, XM, OP_BNACT, NS>), grid, dim3(256), 0, st, x, N, y, K, M, rows, dW,
                            db);
     else
-        hipLaunchKernelGGL((wgrad_kernel<BO, BI, XM, OP_PLAIN, PF2>), grid, dim3(256), 0, st, x, N, y, K, M, rows, dW,
+        hipLaunchKernelGGL((wgrad_kernel<BO, BI, XM, OP_PLAIN, NS>), grid, dim3(256), 0, st, x, N, y, K, M, rows, dW,
                            db);
 }
 
@@ -841,12 +868,14 @@ PCS_API int pcs_wgrad(const pcs_operand* x, int N, const pcs_operand* y, int K, 
     PCS_CHECK_ARG(y->mode <= PCS_OP_BNACT, "pcs_wgrad: Y operand must be PLAIN or BNACT");
     PCS_CHECK_ARG(dW && N % 4 == 0, "pcs_wgrad: dW null or N not a multiple of 4");
     if (M == 0) return 0;
-    const int BO = N > 64 ? 128 : 64, BI = K > 64 ? 128 : 64;
+    const int lo = wgrad_thin32() ? 32 : 64;
+    const int BO = N > 64 ? 128 : (N > lo ? 64 : lo), BI = K > 64 ? 128 : (K > lo ? 64 : lo);
     int probe = -1;
     if (probe_enabled()) {
         char nm[96];
         if (engine_impl() == 1) direct_wgrad_name(N, K, x->mode, y->mode, nm, sizeof nm);
-        else snprintf(nm, sizeof nm, "pcs::wgrad_kernel<%d, %d, %d, %d>", BO, BI, x->mode, y->mode);
+        else snprintf(nm, sizeof nm, "pcs::wgrad_kernel<%d, %d, %d, %d, %d>", BO, BI, x->mode, y->mode,
+                      BO <= 64 && BI <= 64 ? wgrad_stages() : 1);
         const pcs_operand xc = *x, yc = *y;
         probe = probe_start(nm, 2.0 * M * N * K, operand_bytes(*x, M, N) + operand_bytes(*y, M, K),
                             as_stream(stream), [=]() { pcs_wgrad(&xc, N, &yc, K, M, dW, db, stream); });
@@ -857,7 +886,8 @@ PCS_API int pcs_wgrad(const pcs_operand* x, int N, const pcs_operand* y, int K, 
         return launch_status("pcs_wgrad");
     }
     const int tiles = ((N + BO - 1) / BO) * ((K + BI - 1) / BI);
-    int splits = (1024 + tiles - 1) / tiles;
+    static const int target = [] { const char* e = getenv("PCS_WGRAD_BLOCKS"); return e ? atoi(e) : 1024; }();
+    int splits = (target + tiles - 1) / tiles;
     int rows = (M + splits - 1) / splits;
     rows = ((rows + 255) / 256) * 256;
     if (rows < 256) rows = 256;
@@ -865,10 +895,11 @@ PCS_API int pcs_wgrad(const pcs_operand* x, int N, const pcs_operand* y, int K, 
     const dim3 grid(splits, tiles);
     hipStream_t st = as_stream(stream);
     const Operand xd = to_dev(x), yd = to_dev(y);
-    if (BO == 128 && BI == 128) launch_wgrad<128, 128>(grid, st, xd, N, yd, K, M, rows, dW, db);
-    else if (BO == 128) launch_wgrad<128, 64>(grid, st, xd, N, yd, K, M, rows, dW, db);
-    else if (BI == 128) launch_wgrad<64, 128>(grid, st, xd, N, yd, K, M, rows, dW, db);
-    else launch_wgrad<64, 64>(grid, st, xd, N, yd, K, M, rows, dW, db);
+#define PCS_WG(o, i) \
+    if (BO == o && BI == i) { launch_wgrad<o, i>(grid, st, xd, N, yd, K, M, rows, dW, db); }
+    PCS_WG(128, 128) else PCS_WG(128, 64) else PCS_WG(128, 32) else PCS_WG(64, 128) else PCS_WG(64, 64)
+    else PCS_WG(64, 32) else PCS_WG(32, 128) else PCS_WG(32, 64) else PCS_WG(32, 32)
+#undef PCS_WG
     probe_stop(probe, st);
     return launch_status("pcs_wgrad");
 }

@@ -44,6 +44,7 @@ SIGNATURES = {
     'pcs_maxk_fwd': [P, I64, I32, I32, P, P, P],
     'pcs_maxk_bwd': [P, P, I64, I32, I32, P, P],
     'pcs_interp_fwd': [P, P, P, I32, I32, I32, I32, P, I32, I32, P],
+    'pcs_interp_cat_fwd': [P, I32, P, P, P, I32, I32, I32, I32, P, I32, P],
     'pcs_interp_bwd': [P, P, P, I32, I32, I32, I32, I32, I32, P, P],
     'pcs_edge_fwd': [P, P, I32, I32, I32, I32, P, I32, P],
     'pcs_edge_bwd': [P, I32, P, I32, I32, I32, I32, P, P],

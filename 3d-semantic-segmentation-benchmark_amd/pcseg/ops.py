@@ -190,9 +190,13 @@ class InterpCatFn(torch.autograd.Function):
         D1 = f1.shape[2] if f1 is not None else 0
         W = D1 + D2
         out = torch.empty((B * N, W), dtype=torch.float32, device=f2.device)
-        if f1 is not None:
-            out.view(B, N, W)[:, :, :D1].copy_(f1)
-        call('pcs_interp_fwd', ptr(f2), ptr(idx), ptr(dist), B, N, M, D2, ptr(out), W, D1, stream_ptr(f2.device))
+        if D1 % 4 == 0 and D2 % 4 == 0:        # skip copy + interpolation in one pass
+            call('pcs_interp_cat_fwd', ptr(f1), D1, ptr(f2), ptr(idx), ptr(dist), B, N, M, D2, ptr(out), W,
+                 stream_ptr(f2.device))
+        else:
+            if f1 is not None:
+                out.view(B, N, W)[:, :, :D1].copy_(f1)
+            call('pcs_interp_fwd', ptr(f2), ptr(idx), ptr(dist), B, N, M, D2, ptr(out), W, D1, stream_ptr(f2.device))
         ctx.save_for_backward(idx, dist, *(inv if inv is not None else ()))
         ctx.dims = (B, N, M, D1, D2)
         ctx.has_f1 = f1 is not None

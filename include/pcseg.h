@@ -83,6 +83,12 @@ int pcs_maxk_bwd(const float* grad_out, const uint8_t* argmax, long long G,
 int pcs_interp_fwd(const float* pts, const int32_t* idx, const float* dist,
                    int B, int N, int M, int D, float* out, int ld_out,
                    int col_off, void* stream);
+/* FeaturePropagation rows (common.py:238-240): out (B*N, ld_out) = [f1 (B,N,D1) |
+ * interpolate(pts (B,M,D2))] in one pass; D1, D2, ld_out multiples of 4, 16-B aligned
+ * buffers, f1 may be null when D1 == 0. */
+int pcs_interp_cat_fwd(const float* f1, int D1, const float* pts, const int32_t* idx,
+                       const float* dist, int B, int N, int M, int D2, float* out,
+                       int ld_out, void* stream);
 /* grad_pts (B,M,D) += weighted scatter   (accumulating) */
 int pcs_interp_bwd(const float* grad_out, const int32_t* idx, const float* dist,
                    int B, int N, int M, int D, int ld_gout, int col_off,

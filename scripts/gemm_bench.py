@@ -22,6 +22,9 @@ SHAPES = [  # (name, M, K, N)
 
 
 REPS = int(os.environ.get('GEMM_REPS', '10'))
+_only = os.environ.get('GEMM_SHAPES')
+if _only:
+    SHAPES = [sh for sh in SHAPES if any(sh[0].startswith(p) for p in _only.split(','))]
 
 
 def timeit(fn, reps=REPS):

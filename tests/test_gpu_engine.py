@@ -131,7 +131,7 @@ def test_gemm_rows_vs_fp64(impl, M, K, N, mode):
 
 WSHAPES = [  # M rows, N (dZ channels), K (input channels)
     (5000, 32, 9), (4099, 64, 32), (3000, 128, 67), (2100, 256, 128), (1030, 512, 259), (640, 96, 1408),
-    (100, 36, 20),
+    (100, 36, 20), (70001, 32, 32), (300000, 32, 12), (9000, 96, 32), (4100, 32, 96), (4100, 40, 24),
 ]
 
 

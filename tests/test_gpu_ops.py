@@ -317,3 +317,25 @@ def test_inverse_index_random_tables(B, S, k, targets, kind):
     seg = torch.repeat_interleave(torch.arange(B * targets), counts)
     got = ent.long().cpu()
     assert torch.equal(got[torch.argsort(seg * (B * S * k) + got)], torch.sort(key, stable=True).indices)
+
+
+@pytest.mark.parametrize('D1,D2', [(0, 128), (64, 256), (12, 8)])
+def test_interp_cat_fused_bit_exact(D1, D2):
+    """pcs_interp_cat_fwd (float4, skip copy fused) == the scalar pcs_interp_fwd + copy, bitwise."""
+    from pcseg._lib import call, ptr, stream_ptr
+    B, N, M = 2, 2048, 512
+    c1 = cloud(B, N, seed=43).to(DEV)
+    c2 = c1[:, :M].contiguous()
+    idx, dist = ops.knn_select(c1, c2, 3)
+    f1 = torch.randn(B, N, D1, device=DEV) if D1 else None
+    f2 = torch.randn(B, M, D2, device=DEV)
+    W = D1 + D2
+    fused = torch.full((B * N, W), float('nan'), device=DEV)
+    call('pcs_interp_cat_fwd', ptr(f1), D1, ptr(f2), ptr(idx), ptr(dist), B, N, M, D2, ptr(fused), W,
+         stream_ptr(f2.device))
+    # scalar kernel: an odd row stride forces the per-element path
+    ref = torch.zeros((B * N, W + 1), device=DEV)
+    if f1 is not None:
+        ref.view(B, N, W + 1)[:, :, :D1] = f1
+    call('pcs_interp_fwd', ptr(f2), ptr(idx), ptr(dist), B, N, M, D2, ptr(ref), W + 1, D1, stream_ptr(f2.device))
+    assert torch.equal(fused, ref[:, :W])
