@@ -277,17 +277,23 @@ PCS_API int pcs_mlp_backward(const float* X, int ldx, int kin, int M, const pcs_
             }
         }
         if (l == 0 && !dX) break;
-        // dgrad B operand: B[k = cout][n = cin] = Wt[n][k], Wt = W^T (cin x cout)
-        {
+        // dgrad B operand: B[k = cout][n = cin] = W[k][n] -- read k-major straight from W by the
+        // LDS engine (bt = 1); the LDS-free family takes the transpose Wt (cin x cout)
+        const bool bt = engine_impl() == 0;
+        const float* Bw = P.W;
+        int ldb = (int)P.ldw;
+        if (!bt) {
             const dim3 g((Cin + 31) / 32, (C + 31) / 32);
             hipLaunchKernelGGL(transpose_kernel, g, dim3(256), 0, st, P.W, C, Cin, (int)P.ldw, S.wt);
+            Bw = S.wt;
+            ldb = C;
         }
         if (l > 0) {
             const pcs_mlp_layer& Q = layers[l - 1];
             float* dA = S.dA[da];
             const int nbg = pcs_gemm_row_blocks(M, Cin);
             pcs_operand epi = bnbwd_op(nullptr, 0, Q, nullptr, nullptr);
-            if (int e = pcs_gemm_rows(&xop, M, C, S.wt, C, nullptr, dA, Cin, Cin, nullptr, &epi, S.part, stream))
+            if (int e = gemm_rows_ex(&xop, M, C, Bw, ldb, bt, nullptr, dA, Cin, Cin, nullptr, &epi, S.part, stream))
                 return e;
             pp ^= 1;
             const float* sq = Q.coef;
@@ -299,7 +305,7 @@ PCS_API int pcs_mlp_backward(const float* X, int ldx, int kin, int M, const pcs_
             da ^= 1;
         } else {
             if (ldx != kin) zero_f32(dX, (long long)M * ldx, st);
-            if (int e = pcs_gemm_rows(&xop, M, C, S.wt, C, nullptr, dX, ldx, kin, nullptr, nullptr, nullptr, stream))
+            if (int e = gemm_rows_ex(&xop, M, C, Bw, ldb, bt, nullptr, dX, ldx, kin, nullptr, nullptr, nullptr, stream))
                 return e;
         }
     }

@@ -39,7 +39,14 @@ namespace pcs {
 constexpr int GBK = 32;
 constexpr int GLDK = GBK + 4;
 
-template <int BM, int BN, int WM, int WN, int AM>
+// row swizzle of channel c's LDS row (multiples of 4: keeps 4-row groups 16-B contiguous)
+__device__ __forceinline__ int lds_swz(int c) { return ((c >> 3) & 7) << 2; }
+
+//
+// BT: B is stored k-major, B[k][n] = W[k*ldw + n] (the data-gradient GEMM reads the layer's
+// own weight matrix, no transpose): quads are loaded along n and written transposed into
+// Bs with the lds_swz row swizzle (the fragment reads apply the same swizzle).
+template <int BM, int BN, int WM, int WN, int AM, bool BT>
 __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(GemmArgs g) {
     constexpr int WTM = BM / WM, WTN = BN / WN;
     constexpr int TM = WTM / 32, TN = WTN / 32;
@@ -82,9 +89,17 @@ __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(GemmArgs g) {
 #pragma unroll
         for (int it = 0; it < BV; ++it) {
             const int e = it * 256 + tid;
-            const int gn = min(n0 + (e >> 3), g.N - 1);
-            const int gk2 = min(k0 + 4 * (e & 7), ldw_last);
-            if (kBFull || e < BN * GBK / 4) rb[it] = *reinterpret_cast<const float4*>(g.W + (size_t)gn * g.ldw + gk2);
+            if constexpr (BT) {
+                const int gk = min(k0 + e / (BN / 4), g.K - 1);
+                const int gn = min(n0 + 4 * (e % (BN / 4)), ldw_last);
+                if (kBFull || e < BN * GBK / 4)
+                    rb[it] = *reinterpret_cast<const float4*>(g.W + (size_t)gk * g.ldw + gn);
+            } else {
+                const int gn = min(n0 + (e >> 3), g.N - 1);
+                const int gk2 = min(k0 + 4 * (e & 7), ldw_last);
+                if (kBFull || e < BN * GBK / 4)
+                    rb[it] = *reinterpret_cast<const float4*>(g.W + (size_t)gn * g.ldw + gk2);
+            }
         }
     };
     auto sstore = [&](int buf, int m0, int k0) {
@@ -98,13 +113,24 @@ __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(GemmArgs g) {
 #pragma unroll
         for (int it = 0; it < BV; ++it) {
             const int e = it * 256 + tid;
-            const int gk2 = k0 + 4 * (e & 7);
-            float4 v = rb[it];
-            v.x = gk2 + 0 < g.K ? v.x : 0.f;
-            v.y = gk2 + 1 < g.K ? v.y : 0.f;
-            v.z = gk2 + 2 < g.K ? v.z : 0.f;
-            v.w = gk2 + 3 < g.K ? v.w : 0.f;
-            if (kBFull || e < BN * GBK / 4) *reinterpret_cast<float4*>(&Bs[buf][e >> 3][4 * (e & 7)]) = v;
+            if constexpr (BT) {
+                const int kk = e / (BN / 4), n = 4 * (e % (BN / 4));
+                const float4 v = k0 + kk < g.K ? rb[it] : make_float4(0.f, 0.f, 0.f, 0.f);
+                if (kBFull || e < BN * GBK / 4) {
+                    Bs[buf][n + 0][kk ^ lds_swz(n + 0)] = v.x;
+                    Bs[buf][n + 1][kk ^ lds_swz(n + 1)] = v.y;
+                    Bs[buf][n + 2][kk ^ lds_swz(n + 2)] = v.z;
+                    Bs[buf][n + 3][kk ^ lds_swz(n + 3)] = v.w;
+                }
+            } else {
+                const int gk2 = k0 + 4 * (e & 7);
+                float4 v = rb[it];
+                v.x = gk2 + 0 < g.K ? v.x : 0.f;
+                v.y = gk2 + 1 < g.K ? v.y : 0.f;
+                v.z = gk2 + 2 < g.K ? v.z : 0.f;
+                v.w = gk2 + 3 < g.K ? v.w : 0.f;
+                if (kBFull || e < BN * GBK / 4) *reinterpret_cast<float4*>(&Bs[buf][e >> 3][4 * (e & 7)]) = v;
+            }
         }
     };
 
@@ -142,8 +168,10 @@ __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(GemmArgs g) {
             for (int i = 0; i < TM; ++i)
                 a[i] = *reinterpret_cast<const float4*>(&As[buf][wm * WTM + i * 32 + l32][16 * h + 4 * qq]);
 #pragma unroll
-            for (int j = 0; j < TN; ++j)
-                b[j] = *reinterpret_cast<const float4*>(&Bs[buf][wn * WTN + j * 32 + l32][16 * h + 4 * qq]);
+            for (int j = 0; j < TN; ++j) {
+                const int n = wn * WTN + j * 32 + l32;
+                b[j] = *reinterpret_cast<const float4*>(&Bs[buf][n][(16 * h + 4 * qq) ^ (BT ? lds_swz(n) : 0)]);
+            }
 #pragma unroll
             for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -243,8 +271,6 @@ __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(GemmArgs g) {
 // axis: X and Y slabs of 32 rows are stored transposed ([channel][row], 144-B
 // stride) so each lane's fragment is 16 consecutive rows.  Each block accumulates its
 // row range in the MFMA's fp32 accumulators and blocks combine with fp32 atomics.
-// row swizzle of channel c's LDS row (multiples of 4: keeps 4-row groups 16-B contiguous)
-__device__ __forceinline__ int lds_swz(int c) { return ((c >> 3) & 7) << 2; }
 
 //
 // Wave grid: WGO x WGI waves split the BO x BI tile and WR = 4 / (WGO * WGI) waves split
@@ -667,13 +693,21 @@ static inline unsigned ew_grid(long long total) {
 }
 
 template <int BM, int BN, int WM, int WN>
-static void launch_gemm(const GemmArgs& g, int gx, hipStream_t s) {
+static void launch_gemm(const GemmArgs& g, int gx, bool bt, hipStream_t s) {
     const dim3 grid(gx, (g.N + BN - 1) / BN);
+    if (bt) {   // data-gradient GEMMs: dZ operand (rebuilt on load) or a plain gradient
+        switch (g.a.mode) {
+        case OP_PLAIN: hipLaunchKernelGGL((gemm_rows_kernel<BM, BN, WM, WN, OP_PLAIN, true>), grid, dim3(256), 0, s, g); break;
+        case OP_BNBWD: hipLaunchKernelGGL((gemm_rows_kernel<BM, BN, WM, WN, OP_BNBWD, true>), grid, dim3(256), 0, s, g); break;
+        default: hipLaunchKernelGGL((gemm_rows_kernel<BM, BN, WM, WN, OP_POOLBWD, true>), grid, dim3(256), 0, s, g); break;
+        }
+        return;
+    }
     switch (g.a.mode) {
-    case OP_PLAIN: hipLaunchKernelGGL((gemm_rows_kernel<BM, BN, WM, WN, OP_PLAIN>), grid, dim3(256), 0, s, g); break;
-    case OP_BNACT: hipLaunchKernelGGL((gemm_rows_kernel<BM, BN, WM, WN, OP_BNACT>), grid, dim3(256), 0, s, g); break;
-    case OP_BNBWD: hipLaunchKernelGGL((gemm_rows_kernel<BM, BN, WM, WN, OP_BNBWD>), grid, dim3(256), 0, s, g); break;
-    default: hipLaunchKernelGGL((gemm_rows_kernel<BM, BN, WM, WN, OP_POOLBWD>), grid, dim3(256), 0, s, g); break;
+    case OP_PLAIN: hipLaunchKernelGGL((gemm_rows_kernel<BM, BN, WM, WN, OP_PLAIN, false>), grid, dim3(256), 0, s, g); break;
+    case OP_BNACT: hipLaunchKernelGGL((gemm_rows_kernel<BM, BN, WM, WN, OP_BNACT, false>), grid, dim3(256), 0, s, g); break;
+    case OP_BNBWD: hipLaunchKernelGGL((gemm_rows_kernel<BM, BN, WM, WN, OP_BNBWD, false>), grid, dim3(256), 0, s, g); break;
+    default: hipLaunchKernelGGL((gemm_rows_kernel<BM, BN, WM, WN, OP_POOLBWD, false>), grid, dim3(256), 0, s, g); break;
     }
 }
 
@@ -811,15 +845,19 @@ static Operand to_dev(const pcs_operand* o) {
 // stats (nullable): [2][N][row_blocks] fp64 partial (sum, sumsq) of C.
 // bstats (nullable): fused BN-backward partials of the layer whose pre-BN output is epi->z (same shape as C):
 //   [2][N][row_blocks] of (sum dy, sum dy*xhat), dy = C * act'(z*s+t), xhat = (z-mean)*inv.
-PCS_API int pcs_gemm_rows(const pcs_operand* a, int M, int K, const float* W, int ldw, const float* bias, float* C,
-                          int ldc, int N, double* stats, const pcs_operand* epi, double* bstats, void* stream) {
+// bt = 0: W row-major N x K (B[k][n] = W[n*ldw + k]); bt = 1: W row-major K x N
+// (B[k][n] = W[k*ldw + n], ldw >= N) -- the data-gradient GEMM on the layer's own weights.
+int pcs::gemm_rows_ex(const pcs_operand* a, int M, int K, const float* W, int ldw, int bt, const float* bias, float* C,
+                 int ldc, int N, double* stats, const pcs_operand* epi, double* bstats, void* stream) {
     PCS_CHECK_ARG(M >= 0 && K >= 1 && N >= 1, "pcs_gemm_rows: bad sizes M=%d K=%d N=%d", M, K, N);
     if (int e = check_operand(a, K, "pcs_gemm_rows", "A")) return e;
     PCS_CHECK_ARG(W && C, "pcs_gemm_rows: null pointer");
     PCS_CHECK_ARG(!(stats && bstats), "pcs_gemm_rows: stats and bstats are exclusive");
     PCS_CHECK_ARG(!bstats || (epi && epi->z && epi->s && epi->t && epi->mean && epi->inv),
                   "pcs_gemm_rows: bstats needs epi z/s/t/mean/inv");
-    PCS_CHECK_ARG(ldw >= K && ldw % 4 == 0, "pcs_gemm_rows: ldw=%d must be a multiple of 4 and >= K=%d", ldw, K);
+    PCS_CHECK_ARG(ldw % 4 == 0 && ldw >= (bt ? N : K), "pcs_gemm_rows: ldw=%d must be a multiple of 4 and >= %d",
+                  ldw, bt ? N : K);
+    PCS_CHECK_ARG(!bt || (engine_impl() == 0 && a->mode != PCS_OP_BNACT), "pcs_gemm_rows: k-major W needs the LDS engine and a PLAIN/BNBWD/POOLBWD A");
     if (M == 0) return 0;
     GemmArgs g{to_dev(a), M, K, W, ldw, bias, C, ldc, N, stats, to_dev(epi), bstats};
     hipStream_t s = as_stream(stream);
@@ -832,13 +870,14 @@ PCS_API int pcs_gemm_rows(const pcs_operand* a, int M, int K, const float* W, in
             int bm, bn, wm, wn;
             gemm_tile(M, N, &bm, &bn);
             gemm_waves(bm, bn, &wm, &wn);
-            snprintf(nm, sizeof nm, "pcs::gemm_rows_kernel<%d, %d, %d, %d, %d>", bm, bn, wm, wn, a->mode);
+            snprintf(nm, sizeof nm, "pcs::gemm_rows_kernel<%d, %d, %d, %d, %d, %s>", bm, bn, wm, wn, a->mode,
+                     bt ? "true" : "false");
         }
         const double bytes = operand_bytes(*a, M, K) + 4.0 * M * N * (bstats ? 2 : 1);
         const pcs_operand ac = *a, ec = epi ? *epi : pcs_operand{};
         const bool he = epi != nullptr;
         probe = probe_start(nm, 2.0 * M * K * N, bytes, s, [=]() {
-            pcs_gemm_rows(&ac, M, K, W, ldw, bias, C, ldc, N, stats, he ? &ec : nullptr, bstats, stream);
+            gemm_rows_ex(&ac, M, K, W, ldw, bt, bias, C, ldc, N, stats, he ? &ec : nullptr, bstats, stream);
         });
     }
     if (engine_impl() == 1 && launch_gemm_direct(g, s)) {
@@ -848,14 +887,25 @@ PCS_API int pcs_gemm_rows(const pcs_operand* a, int M, int K, const float* W, in
     int bm, bn;
     gemm_tile(M, N, &bm, &bn);
     const int gx = gemm_grid_x(M, N, bm, bn);
-    if (bn == 32) launch_gemm<128, 32, 4, 1>(g, gx, s);
-    else if (bm == 128 && bn == 64) launch_gemm<128, 64, 4, 1>(g, gx, s);
-    else if (bm == 128) launch_gemm<128, 128, 2, 2>(g, gx, s);
-    else if (bm == 64 && bn == 128) launch_gemm<64, 128, 2, 2>(g, gx, s);
-    else if (bm == 64) launch_gemm<64, 64, 2, 2>(g, gx, s);
-    else launch_gemm<32, 128, 1, 4>(g, gx, s);
+    const bool b = bt != 0;
+    if (bn == 32) launch_gemm<128, 32, 4, 1>(g, gx, b, s);
+    else if (bm == 128 && bn == 64) launch_gemm<128, 64, 4, 1>(g, gx, b, s);
+    else if (bm == 128) launch_gemm<128, 128, 2, 2>(g, gx, b, s);
+    else if (bm == 64 && bn == 128) launch_gemm<64, 128, 2, 2>(g, gx, b, s);
+    else if (bm == 64) launch_gemm<64, 64, 2, 2>(g, gx, b, s);
+    else launch_gemm<32, 128, 1, 4>(g, gx, b, s);
     probe_stop(probe, s);
     return launch_status("pcs_gemm_rows");
+}
+
+PCS_API int pcs_gemm_rows(const pcs_operand* a, int M, int K, const float* W, int ldw, const float* bias, float* C,
+                          int ldc, int N, double* stats, const pcs_operand* epi, double* bstats, void* stream) {
+    return gemm_rows_ex(a, M, K, W, ldw, 0, bias, C, ldc, N, stats, epi, bstats, stream);
+}
+
+PCS_API int pcs_gemm_rows_kmajor(const pcs_operand* a, int M, int K, const float* W, int ldw, float* C, int ldc,
+                                 int N, const pcs_operand* epi, double* bstats, void* stream) {
+    return gemm_rows_ex(a, M, K, W, ldw, 1, nullptr, C, ldc, N, nullptr, epi, bstats, stream);
 }
 
 // dW (N x K) += T(X)^T . T(Y) over M rows; db (N) += column sums of T(X). dW/db zeroed by caller.

@@ -136,6 +136,9 @@ void bn_finalize_launch(const double* part, int nb, int N, long long M, const fl
                         float eps, float momentum, float* run_mean, float* run_var, float* s, float* t, float* mean,
                         float* invstd, long long* nbt, hipStream_t st);
 int engine_impl();
+// row GEMM with W row-major N x K (bt = 0, = pcs_gemm_rows) or K x N (bt = 1, LDS engine only)
+int gemm_rows_ex(const pcs_operand* a, int M, int K, const float* W, int ldw, int bt, const float* bias, float* C,
+                 int ldc, int N, double* stats, const pcs_operand* epi, double* bstats, void* stream);
 // kernel names of the LDS-free family (as rocprofv3 reports them) for the launch probe
 void direct_gemm_name(int M, int N, int mode, char* buf, int cap);
 void direct_wgrad_name(int N, int K, int xm, int ym, char* buf, int cap);

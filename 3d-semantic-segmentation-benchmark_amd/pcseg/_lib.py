@@ -60,6 +60,7 @@ SIGNATURES = {
     'pcs_mlp_backward': [P, I32, I32, I32, ctypes.c_char_p, I32, I32, P, P, P, P, ctypes.c_size_t, P],
     'pcs_operand_size': [],
     'pcs_gemm_rows': [OPP, I32, I32, P, I32, P, P, I32, I32, P, OPP, P, P],
+    'pcs_gemm_rows_kmajor': [OPP, I32, I32, P, I32, P, I32, I32, OPP, P, P],
     'pcs_wgrad': [OPP, I32, OPP, I32, I32, P, P, P],
     'pcs_bn_finalize': [P, I32, I32, I64, P, P, F32, F32, P, P, P, P, P, P, P],
     'pcs_bn_bwd_finalize': [P, I32, I32, I64, P, P, P, P, P, P, I32, P],

@@ -126,6 +126,11 @@ def gemm_rows(a: Operand, M, K, W, ldw, bias, C, ldc, N, stats=None, epi: Operan
     call('pcs_gemm_rows', a, M, K, ptr(W), ldw, ptr(bias), ptr(C), ldc, N, ptr(stats), epi, ptr(bstats), st)
 
 
+def gemm_rows_kmajor(a: Operand, M, K, W, ldw, C, ldc, N, epi: Operand | None = None, bstats=None, st=None):
+    """C[M,N] = T(A)[M,K] . W with W row-major K x N (the data-gradient GEMM, no transpose)."""
+    call('pcs_gemm_rows_kmajor', a, M, K, ptr(W), ldw, ptr(C), ldc, N, epi, ptr(bstats), st)
+
+
 def wgrad(x: Operand, N, y: Operand, K, M, dW, db, st):
     """dW[N,K] += T(X)^T . T(Y) over M rows, db += colsum(T(X))."""
     call('pcs_wgrad', x, N, y, K, M, ptr(dW), ptr(db), st)
@@ -324,10 +329,13 @@ class RowLinearFn(torch.autograd.Function):
         gop = operand(gp, N4)
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            Wt = torch.zeros((K, N4), dtype=torch.float32, device=dev)     # dgrad B[k=n][n=cin] = Wt[cin][n]
-            Wt[:, :N] = Wm.t()
             dx = _f32((M, K), dev)
-            gemm_rows(gop, M, N, Wt, N4, None, dx, K, K, st=st)
+            if _impl() == 0:                    # dgrad B[k=class][n=cin] = Wm[class][cin], read k-major
+                gemm_rows_kmajor(gop, M, N, Wm, K, dx, K, K, st=st)
+            else:
+                Wt = torch.zeros((K, N4), dtype=torch.float32, device=dev)
+                Wt[:, :N] = Wm.t()
+                gemm_rows(gop, M, N, Wt, N4, None, dx, K, K, st=st)
         if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
             dwp = torch.zeros((N4, K), dtype=torch.float32, device=dev)
             dbp = torch.zeros((N4,), dtype=torch.float32, device=dev) if ctx.has_bias else None

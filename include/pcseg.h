@@ -140,6 +140,12 @@ int pcs_gemm_row_blocks(int M, int N);
 int pcs_gemm_rows(const pcs_operand* a, int M, int K, const float* W, int ldw,
                   const float* bias, float* C, int ldc, int N, double* stats,
                   const pcs_operand* epi, double* bstats, void* stream);
+/* Data-gradient form of pcs_gemm_rows: W row-major K x N (B[k][n] = W[k*ldw + n],
+ * ldw >= N, a multiple of 4) -- dA = dZ . W on the layer's own weight matrix, no
+ * transpose.  LDS engine only; A must be PLAIN, BNBWD or POOLBWD. */
+int pcs_gemm_rows_kmajor(const pcs_operand* a, int M, int K, const float* W, int ldw,
+                         float* C, int ldc, int N, const pcs_operand* epi,
+                         double* bstats, void* stream);
 /* dW (N x K) += T(X)^T . T(Y) over M rows; db (N, nullable) += column sums of
  * T(X).  X: PLAIN/BNBWD/POOLBWD (the layer's dZ), Y: PLAIN/BNACT (its input).
  * (accumulating) */

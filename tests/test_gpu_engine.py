@@ -11,7 +11,7 @@ import pytest
 import torch
 
 from pcseg._lib import load, stream_ptr, OP_PLAIN, OP_BNACT, OP_BNBWD, OP_POOLBWD
-from pcseg.engine import operand, gemm_rows, wgrad, ld4
+from pcseg.engine import operand, gemm_rows, gemm_rows_kmajor, wgrad, ld4
 
 pytestmark = pytest.mark.gpu
 DEV = 'cuda'
@@ -122,7 +122,50 @@ def test_gemm_rows_vs_fp64(impl, M, K, N, mode):
         gemm_rows(x.op(), M, K, W, lda, None, C2, N, N, None, epi, bpart, st=st)
         ref2 = x.value() @ W.double()[:, :K].t()
         assert rel(C2, ref2) <= tol
-        dy = ref2 * dact(ze.double() * se.double() + te.double(), 0.2)
+        dy = ref2 * dact((ze * se + te).double(), 0.2)     # the kernel's fp32 gate
+        xh = (ze.double() - me.double()) * ie.double()
+        bs = bpart.sum(-1)
+        assert rel(bs[0], dy.sum(0)) <= tol + 1e-5
+        assert rel(bs[1], (dy * xh).sum(0)) <= tol + 1e-5
+
+
+KSHAPES = [  # M, K (= cout of the layer), N (= its cin): the data-gradient GEMM on k-major W
+    (1000, 32, 12), (4099, 64, 32), (3000, 128, 128), (515, 256, 260), (777, 512, 384), (64, 36, 20),
+    (70001, 128, 128), (2000, 13, 128), (300000, 32, 12),
+]
+
+
+@pytest.mark.parametrize('M,K,N', KSHAPES)
+@pytest.mark.parametrize('mode', [OP_PLAIN, OP_BNBWD, OP_POOLBWD])
+def test_gemm_rows_kmajor_vs_fp64(M, K, N, mode):
+    """pcs_gemm_rows_kmajor: B[k][n] = W[k*ldw + n] (W read in place, no transpose), with the
+    fused BN-backward epilogue; LDS engine only."""
+    if mode != OP_PLAIN and K % 4:
+        pytest.skip('transform modes need K % 4 == 0')
+    pool_k = 0
+    if mode == OP_POOLBWD:
+        pool_k = 16 if M % 16 == 0 else (4 if M % 4 == 0 else 1)
+    g = torch.Generator(device=DEV).manual_seed(M * 5 + K * 3 + N + mode)
+    lda, ldw = ld4(K), ld4(N)
+    x = Xform(mode, M, K, lda, 0.2, pool_k, g)
+    W = torch.randn(K, ldw, device=DEV, generator=g) / math.sqrt(K)    # pad columns hold junk: never read into C
+    C = torch.full((M, N), float('nan'), device=DEV)
+    st = stream_ptr(torch.device(DEV))
+    tol = 2e-6 * math.sqrt(K)
+    if N % 4 == 0:
+        nb = load().pcs_gemm_row_blocks(M, N)
+        ze = torch.randn(M, N, device=DEV, generator=g)
+        se, te = torch.rand(N, device=DEV, generator=g) + 0.5, torch.randn(N, device=DEV, generator=g) * 0.3
+        me, ie = torch.randn(N, device=DEV, generator=g) * 0.1, torch.rand(N, device=DEV, generator=g) + 0.5
+        epi = operand(None, 0, OP_BNBWD, se, te, 1, 0.2, ze, N, me, ie)
+        bpart = torch.empty(2, N, nb, dtype=torch.float64, device=DEV)
+        gemm_rows_kmajor(x.op(), M, K, W, ldw, C, N, N, epi, bpart, st=st)
+    else:
+        gemm_rows_kmajor(x.op(), M, K, W, ldw, C, N, N, st=st)
+    ref = x.value() @ W.double()[:, :N]
+    assert rel(C, ref) <= tol
+    if N % 4 == 0:
+        dy = ref * dact((ze * se + te).double(), 0.2)      # the kernel's fp32 gate
         xh = (ze.double() - me.double()) * ie.double()
         bs = bpart.sum(-1)
         assert rel(bs[0], dy.sum(0)) <= tol + 1e-5
