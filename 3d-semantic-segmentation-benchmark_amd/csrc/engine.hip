@@ -158,7 +158,8 @@ static int check_layers(int M, int kin, int ldx, const pcs_mlp_layer* L, int nl,
         PCS_CHECK_ARG(L[l].cin == cin, "%s: layer %d: cin=%lld, expected %d", who, l, (long long)L[l].cin, cin);
         PCS_CHECK_ARG(L[l].cout >= 4 && L[l].cout % 4 == 0, "%s: layer %d: cout=%lld must be a multiple of 4", who,
                       l, (long long)L[l].cout);
-        PCS_CHECK_ARG(L[l].ldw >= L[l].cin && L[l].ldw % 4 == 0, "%s: layer %d: ldw=%lld", who, l,
+        PCS_CHECK_ARG(L[l].ldw >= L[l].cin && (L[l].ldw % 4 == 0 || (l == 0 && engine_impl() == 0)),
+                      "%s: layer %d: ldw=%lld (a multiple of 4 except for the first layer on the LDS engine)", who, l,
                       (long long)L[l].ldw);
         PCS_CHECK_ARG(L[l].use_batch || (L[l].run_mean && L[l].run_var),
                       "%s: layer %d: eval-mode BatchNorm needs running statistics", who, l);
@@ -279,7 +280,7 @@ PCS_API int pcs_mlp_backward(const float* X, int ldx, int kin, int M, const pcs_
         if (l == 0 && !dX) break;
         // dgrad B operand: B[k = cout][n = cin] = W[k][n] -- read k-major straight from W by the
         // LDS engine (bt = 1); the LDS-free family takes the transpose Wt (cin x cout)
-        const bool bt = engine_impl() == 0;
+        const bool bt = engine_impl() == 0 && P.ldw % 4 == 0;
         const float* Bw = P.W;
         int ldb = (int)P.ldw;
         if (!bt) {

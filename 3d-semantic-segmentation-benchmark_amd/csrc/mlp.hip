@@ -96,9 +96,17 @@ __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(GemmArgs g) {
                     rb[it] = *reinterpret_cast<const float4*>(g.W + (size_t)gk * g.ldw + gn);
             } else {
                 const int gn = min(n0 + (e >> 3), g.N - 1);
-                const int gk2 = min(k0 + 4 * (e & 7), ldw_last);
-                if (kBFull || e < BN * GBK / 4)
-                    rb[it] = *reinterpret_cast<const float4*>(g.W + (size_t)gn * g.ldw + gk2);
+                if (g.ldw & 3) {      // unpadded weight rows (a stack's first layer, K = 3 + D): scalar loads
+                    const float* wr = g.W + (size_t)gn * g.ldw;
+                    const int gk = k0 + 4 * (e & 7), kl = g.ldw - 1;
+                    if (kBFull || e < BN * GBK / 4)
+                        rb[it] = make_float4(wr[min(gk, kl)], wr[min(gk + 1, kl)], wr[min(gk + 2, kl)],
+                                             wr[min(gk + 3, kl)]);
+                } else {
+                    const int gk2 = min(k0 + 4 * (e & 7), ldw_last);
+                    if (kBFull || e < BN * GBK / 4)
+                        rb[it] = *reinterpret_cast<const float4*>(g.W + (size_t)gn * g.ldw + gk2);
+                }
             }
         }
     };
@@ -855,7 +863,8 @@ int pcs::gemm_rows_ex(const pcs_operand* a, int M, int K, const float* W, int ld
     PCS_CHECK_ARG(!(stats && bstats), "pcs_gemm_rows: stats and bstats are exclusive");
     PCS_CHECK_ARG(!bstats || (epi && epi->z && epi->s && epi->t && epi->mean && epi->inv),
                   "pcs_gemm_rows: bstats needs epi z/s/t/mean/inv");
-    PCS_CHECK_ARG(ldw % 4 == 0 && ldw >= (bt ? N : K), "pcs_gemm_rows: ldw=%d must be a multiple of 4 and >= %d",
+    PCS_CHECK_ARG((ldw % 4 == 0 || (!bt && engine_impl() == 0)) && ldw >= (bt ? N : K),
+                  "pcs_gemm_rows: ldw=%d must be >= %d (and a multiple of 4 for k-major W or the LDS-free engine)",
                   ldw, bt ? N : K);
     PCS_CHECK_ARG(!bt || (engine_impl() == 0 && a->mode != PCS_OP_BNACT), "pcs_gemm_rows: k-major W needs the LDS engine and a PLAIN/BNBWD/POOLBWD A");
     if (M == 0) return 0;

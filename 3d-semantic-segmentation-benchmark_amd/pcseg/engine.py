@@ -192,11 +192,11 @@ class SharedMLPFn(torch.autograd.Function):
             if C % 4:
                 raise ValueError(f'engine: layer width {C} must be a multiple of 4')
             Wm = W.reshape(C, -1)
-            if Wm.shape[1] % 4:                 # 16-B weight rows (the pad columns are zero)
+            if Wm.shape[1] % 4 and (li > 0 or _impl() != 0):    # 16-B weight rows (the pad columns are zero)
                 Wp = torch.zeros((C, ld4(Wm.shape[1])), dtype=torch.float32, device=dev)
                 Wp[:, :Wm.shape[1]] = Wm
                 Wm = Wp
-            elif not Wm.is_contiguous():
+            elif not Wm.is_contiguous():        # (the LDS engine reads an unpadded first layer as is)
                 Wm = Wm.contiguous()
             Wms.append(Wm)
             use_batch = bn.training or bn.running_mean is None
