@@ -124,6 +124,30 @@ static size_t carve_backward(Carve& cv, int M, int kin, int ldx, const pcs_mlp_l
     return cv.used;
 }
 
+// the top layer's pooling is fused into its GEMM epilogue (z-space max/min + pool_finalize)
+static bool fused_pool(int pool_k) {
+    static const bool on = [] { const char* e = getenv("PCS_FUSED_POOL"); return !e || atoi(e) != 0; }();
+    return on && (pool_k == 16 || pool_k == 32) && engine_impl() == 0;
+}
+
+struct FwdScratch {
+    double* part;
+    float* pz;
+    unsigned char* pa;
+};
+
+static size_t carve_forward(Carve& cv, int M, int kin, const pcs_mlp_layer* L, int nl, int pool_k, FwdScratch* out) {
+    FwdScratch s{};
+    s.part = cv.take<double>(max_partials(M, kin, L, nl, pool_k, false));
+    if (fused_pool(pool_k)) {
+        const size_t gn = (size_t)(M / pool_k) * (size_t)L[nl - 1].cout;
+        s.pz = cv.take<float>(2 * gn);
+        s.pa = cv.take<unsigned char>(2 * gn);
+    }
+    if (out) *out = s;
+    return cv.used;
+}
+
 static pcs_operand plain_op(const float* data, int ld) {
     pcs_operand o{};
     o.data = data; o.ld = ld; o.mode = PCS_OP_PLAIN;
@@ -179,7 +203,7 @@ PCS_API int pcs_mlp_workspace(int M, int kin, int ldx, const pcs_mlp_layer* laye
     PCS_CHECK_ARG(bytes, "pcs_mlp_workspace: null bytes");
     Carve cv{nullptr, 0, 0};
     if (backward) carve_backward(cv, M, kin, ldx, layers, nl, pool_k, nullptr);
-    else cv.take<double>(max_partials(M, kin, layers, nl, pool_k, false));
+    else carve_forward(cv, M, kin, layers, nl, pool_k, nullptr);
     *bytes = cv.used + 256;
     return 0;
 }
@@ -191,8 +215,11 @@ PCS_API int pcs_mlp_forward(const float* X, int ldx, int kin, int M, pcs_mlp_lay
     if (M == 0) return 0;
     hipStream_t st = as_stream(stream);
     Carve cv{static_cast<char*>(ws), 0, ws_bytes};
-    double* part = cv.take<double>(max_partials(M, kin, layers, nl, pool_k, false));
+    FwdScratch S;
+    carve_forward(cv, M, kin, layers, nl, pool_k, &S);
+    double* part = S.part;
     PCS_CHECK_ARG(ws && cv.used <= ws_bytes, "pcs_mlp_forward: workspace too small (%zu < %zu)", ws_bytes, cv.used);
+    const bool fuse = fused_pool(pool_k);
 
     const float* A = X;
     int lda = ldx, K = kin;
@@ -201,16 +228,22 @@ PCS_API int pcs_mlp_forward(const float* X, int ldx, int kin, int M, pcs_mlp_lay
         const int C = (int)P.cout;
         const pcs_operand a = l == 0 ? plain_op(A, lda) : bnact_op(A, lda, layers[l - 1]);
         float* s = P.coef;
+        const bool top_pool = fuse && l == nl - 1;
+        float* pz = top_pool ? S.pz : nullptr;
+        unsigned char* pa = top_pool ? S.pa : nullptr;
+        const int pk = top_pool ? pool_k : 0;
         if (P.use_batch) {
             const int nb = pcs_gemm_row_blocks(M, C);
-            if (int e = pcs_gemm_rows(&a, M, K, P.W, (int)P.ldw, P.bias, P.Z, C, C, part, nullptr, nullptr, stream))
+            if (int e = gemm_rows_ex(&a, M, K, P.W, (int)P.ldw, 0, P.bias, P.Z, C, C, part, nullptr, nullptr, stream,
+                                     pz, pa, pk))
                 return e;
             const bool track = P.run_mean != nullptr;
             bn_finalize_launch(part, nb, C, M, P.gamma, P.beta, (float)P.eps, track ? (float)P.momentum : 0.f,
                                P.run_mean, P.run_var, s, s + C, s + 2 * C, s + 3 * C,
                                reinterpret_cast<long long*>(P.num_batches), st);
         } else {
-            if (int e = pcs_gemm_rows(&a, M, K, P.W, (int)P.ldw, P.bias, P.Z, C, C, nullptr, nullptr, nullptr, stream))
+            if (int e = gemm_rows_ex(&a, M, K, P.W, (int)P.ldw, 0, P.bias, P.Z, C, C, nullptr, nullptr, nullptr, stream,
+                                     pz, pa, pk))
                 return e;
             hipLaunchKernelGGL(bn_eval_coef_kernel, dim3((C + 255) / 256), dim3(256), 0, st, P.run_mean, P.run_var,
                                P.gamma, P.beta, (float)P.eps, C, s);
@@ -219,6 +252,8 @@ PCS_API int pcs_mlp_forward(const float* X, int ldx, int kin, int M, pcs_mlp_lay
     }
     const pcs_mlp_layer& T = layers[nl - 1];
     const int C = (int)T.cout;
+    if (fuse)
+        return pool_finalize(S.pz, S.pa, M / pool_k, C, T.coef, T.coef + C, (int)T.act, (float)T.slope, out, arg, st);
     if (pool_k)
         return pcs_pool_fwd(T.Z, C, M / pool_k, pool_k, T.coef, T.coef + C, (int)T.act, (float)T.slope, out, arg,
                             stream);

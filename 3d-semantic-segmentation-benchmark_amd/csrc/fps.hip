@@ -155,15 +155,15 @@ __global__ __launch_bounds__(BLOCK) void fps_kernel(const float* __restrict__ xy
         if (wk != 0) {
             const unsigned mb = wk - 1u;
             const float Mw = __uint_as_float(mb);
-            const float S = __fsqrt_rn(Mw);
+            const float S = sqrt_cr(Mw);
             // at most 3 floats below Mw share its sqrt (sqrt halves relative spacing):
             // test them in parallel instead of a dependent chain of sqrts
             const float p1 = mb >= 1u ? __uint_as_float(mb - 1u) : -1.f;
             const float p2 = mb >= 2u ? __uint_as_float(mb - 2u) : -1.f;
             const float p3 = mb >= 3u ? __uint_as_float(mb - 3u) : -1.f;
-            const bool e1 = p1 >= 0.f && __fsqrt_rn(p1) == S;
-            const bool e2 = p2 >= 0.f && __fsqrt_rn(p2) == S;
-            const bool e3 = p3 >= 0.f && __fsqrt_rn(p3) == S;
+            const bool e1 = p1 >= 0.f && sqrt_cr(p1) == S;
+            const bool e2 = p2 >= 0.f && sqrt_cr(p2) == S;
+            const bool e3 = p3 >= 0.f && sqrt_cr(p3) == S;
             const float lo = e1 ? (e2 ? (e3 ? p3 : p2) : p1) : Mw;
             unsigned cand = 0xFFFFFFFFu;
 #pragma unroll

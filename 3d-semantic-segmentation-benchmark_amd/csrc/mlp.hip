@@ -204,9 +204,14 @@ __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(GemmArgs g) {
                 float sp = 0.f, tp = 0.f, mp = 0.f, ip = 0.f;
                 if (want_b) { sp = g.e.s[colc]; tp = g.e.t[colc]; mp = g.e.mean[colc]; ip = g.e.inv[colc]; }
 #pragma unroll
-                for (int i = 0; i < TM; ++i)
+                for (int i = 0; i < TM; ++i) {
+                // fused pooling state of this lane's rows of the 32-row block (a group of 32, or
+                // one group of 16 per hb): running max/min of C and the first row reaching it
+                float pmx = -INFINITY, pmn = INFINITY;
+                int imx = 4 * h, imn = 4 * h;
 #pragma unroll
                 for (int hb = 0; hb < 2; ++hb) {     // Z loads batched 8 at a time (register budget)
+                    if (g.pool_k == 16 && hb == 1) { pmx = -INFINITY; pmn = INFINITY; imx = imn = 16 + 4 * h; }
                     float zt[8];
                     if (want_b) {
 #pragma unroll
@@ -223,6 +228,11 @@ __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(GemmArgs g) {
                         const bool ok = row < g.M && cok;
                         const float v = acc[i][j][r] + bv;
                         if (ok) g.C[(size_t)row * g.ldc + col] = v;
+                        if (g.pool_k) {
+                            const int rib = (r & 3) + 8 * (r >> 2) + 4 * h;   // increasing in r: first wins
+                            if (v > pmx) { pmx = v; imx = rib; }
+                            if (v < pmn) { pmn = v; imn = rib; }
+                        }
                         if (want_stats) {
                             const double d = ok ? (double)v : 0.0;
                             s1[j] += d;
@@ -238,6 +248,23 @@ __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(GemmArgs g) {
                         }
                         acc[i][j][r] = 0.f;
                     }
+                    if (g.pool_k && (g.pool_k == 16 || hb == 1)) {
+                        // merge with the other lane half (same column, the other rows), first row on ties
+                        const float ox = __shfl_xor(pmx, 32), on = __shfl_xor(pmn, 32);
+                        const int oix = __shfl_xor(imx, 32), oin = __shfl_xor(imn, 32);
+                        if (ox > pmx || (ox == pmx && oix < imx)) { pmx = ox; imx = oix; }
+                        if (on < pmn || (on == pmn && oin < imn)) { pmn = on; imn = oin; }
+                        const int r0 = m0 + wm * WTM + i * 32 + (g.pool_k == 16 ? 16 * hb : 0);
+                        if (h == 0 && cok && r0 < g.M) {
+                            const size_t G = (size_t)(g.M / g.pool_k), gi = (size_t)(r0 / g.pool_k);
+                            const int base = g.pool_k == 16 ? 16 * hb : 0;
+                            g.pz[gi * g.N + col] = pmx;
+                            g.pz[(G + gi) * g.N + col] = pmn;
+                            g.pa[gi * g.N + col] = (unsigned char)(imx - base);
+                            g.pa[(G + gi) * g.N + col] = (unsigned char)(imn - base);
+                        }
+                    }
+                }
                 }
             }
         }
@@ -604,6 +631,21 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restr
 
 // ------------------------------------------------------------------ pooling over K with BN + act
 // pooled[g][c] = max_k act(z*s+t) (first max), argmax u8
+__global__ __launch_bounds__(256) void pool_finalize_kernel(const float* __restrict__ pz,
+                                                            const unsigned char* __restrict__ pa, long long GN, int N,
+                                                            const float* __restrict__ s, const float* __restrict__ t,
+                                                            float slope, float* __restrict__ out,
+                                                            unsigned char* __restrict__ arg) {
+    for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < GN; e += (long long)gridDim.x * 256) {
+        const int c = (int)(e % N);
+        const float sc = s[c], tc = t[c];
+        const bool neg = sc < 0.f;
+        const float z = pz[neg ? GN + e : e];
+        out[e] = act_f(z * sc + tc, 0, slope);
+        arg[e] = sc == 0.f ? (unsigned char)0 : pa[neg ? GN + e : e];
+    }
+}
+
 __global__ __launch_bounds__(256) void pool_fwd_kernel(const float* __restrict__ Z, int nq, int G, int K,
                                                        const float* __restrict__ s, const float* __restrict__ t,
                                                        int act, float slope, float* __restrict__ out,
@@ -856,7 +898,11 @@ static Operand to_dev(const pcs_operand* o) {
 // bt = 0: W row-major N x K (B[k][n] = W[n*ldw + k]); bt = 1: W row-major K x N
 // (B[k][n] = W[k*ldw + n], ldw >= N) -- the data-gradient GEMM on the layer's own weights.
 int pcs::gemm_rows_ex(const pcs_operand* a, int M, int K, const float* W, int ldw, int bt, const float* bias, float* C,
-                 int ldc, int N, double* stats, const pcs_operand* epi, double* bstats, void* stream) {
+                 int ldc, int N, double* stats, const pcs_operand* epi, double* bstats, void* stream, float* pz,
+                 unsigned char* pa, int pool_k) {
+    PCS_CHECK_ARG(pool_k == 0 || ((pool_k == 16 || pool_k == 32) && M % pool_k == 0 && pz && pa && !bt &&
+                                  engine_impl() == 0),
+                  "pcs_gemm_rows: fused pooling needs pool_k 16|32 dividing M, pz/pa, the LDS engine");
     PCS_CHECK_ARG(M >= 0 && K >= 1 && N >= 1, "pcs_gemm_rows: bad sizes M=%d K=%d N=%d", M, K, N);
     if (int e = check_operand(a, K, "pcs_gemm_rows", "A")) return e;
     PCS_CHECK_ARG(W && C, "pcs_gemm_rows: null pointer");
@@ -868,7 +914,7 @@ int pcs::gemm_rows_ex(const pcs_operand* a, int M, int K, const float* W, int ld
                   ldw, bt ? N : K);
     PCS_CHECK_ARG(!bt || (engine_impl() == 0 && a->mode != PCS_OP_BNACT), "pcs_gemm_rows: k-major W needs the LDS engine and a PLAIN/BNBWD/POOLBWD A");
     if (M == 0) return 0;
-    GemmArgs g{to_dev(a), M, K, W, ldw, bias, C, ldc, N, stats, to_dev(epi), bstats};
+    GemmArgs g{to_dev(a), M, K, W, ldw, bias, C, ldc, N, stats, to_dev(epi), bstats, pz, pa, pool_k};
     hipStream_t s = as_stream(stream);
     int probe = -1;
     if (probe_enabled()) {
@@ -1007,6 +1053,17 @@ PCS_API int pcs_pool_fwd(const float* Z, int N, long long G, int K, const float*
     hipLaunchKernelGGL(pool_fwd_kernel, dim3(ew_grid(total)), dim3(256), 0, as_stream(stream), Z, N / 4, (int)G, K, s,
                        t, act, eff_slope(act, slope), out, arg);
     return launch_status("pcs_pool_fwd");
+}
+
+int pcs::pool_finalize(const float* pz, const unsigned char* pa, long long G, int N, const float* s, const float* t,
+                       int act, float slope, float* out, unsigned char* arg, hipStream_t st) {
+    const long long GN = G * N;
+    if (GN == 0) return 0;
+    long long blocks = (GN + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(pool_finalize_kernel, dim3((unsigned)blocks), dim3(256), 0, st, pz, pa, GN, N, s, t,
+                       eff_slope(act, slope), out, arg);
+    return launch_status("pool_finalize");
 }
 
 PCS_API int pcs_pool_bwd_reduce_blocks(long long G) { return (int)((G + 63) / 64); }

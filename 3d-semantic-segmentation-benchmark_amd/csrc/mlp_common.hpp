@@ -124,6 +124,9 @@ struct GemmArgs {
     // uses e.z (its pre-BN Z, M x N), e.s, e.t, e.mean, e.inv, e.act, e.slope
     Operand e;
     double* bstats;                            // [2][N][gridDim.x]: sum dy, sum dy*xhat (or null)
+    // fused max/min pooling of C over groups of pool_k consecutive rows (pool_k = 16 or 32; 0 = off):
+    // pz [2][M/pool_k][N] (max, min of C), pa [2][M/pool_k][N] (their first row within the group)
+    float* pz; unsigned char* pa; int pool_k;
 };
 
 // LDS-free kernels (gemm_direct.hip); return false when the shape is not covered
@@ -138,7 +141,13 @@ void bn_finalize_launch(const double* part, int nb, int N, long long M, const fl
 int engine_impl();
 // row GEMM with W row-major N x K (bt = 0, = pcs_gemm_rows) or K x N (bt = 1, LDS engine only)
 int gemm_rows_ex(const pcs_operand* a, int M, int K, const float* W, int ldw, int bt, const float* bias, float* C,
-                 int ldc, int N, double* stats, const pcs_operand* epi, double* bstats, void* stream);
+                 int ldc, int N, double* stats, const pcs_operand* epi, double* bstats, void* stream,
+                 float* pz = nullptr, unsigned char* pa = nullptr, int pool_k = 0);
+// pooled output of a stack from the GEMM's fused z-space max/min (pz/pa of gemm_rows_ex):
+// out = act(s*z + t) with z = max (s > 0), min (s < 0) or any (s == 0, arg 0) -- act(s*z+t) is
+// monotone in z, so this is max_k act(s*z_k + t) with its first argmax
+int pool_finalize(const float* pz, const unsigned char* pa, long long G, int N, const float* s, const float* t,
+                  int act, float slope, float* out, unsigned char* arg, hipStream_t st);
 // kernel names of the LDS-free family (as rocprofv3 reports them) for the launch probe
 void direct_gemm_name(int M, int N, int mode, char* buf, int cap);
 void direct_wgrad_name(int N, int K, int xm, int ym, char* buf, int cap);

@@ -61,6 +61,23 @@ __device__ __forceinline__ float readlane_f(float v, int l) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
 
+// IEEE correctly rounded single-precision sqrt of x >= 0 (the CPU's sqrtf).  On gfx950
+// __fsqrt_rn / sqrtf lower to v_sqrt_f32, which is only faithful (1 ulp): the hardware
+// value t is fixed up against the exact midpoints to its float neighbours -- t and a
+// neighbour average to a 25-bit value and its square to 50 bits, both exact in double.
+__device__ __forceinline__ float sqrt_cr(float x) {
+    float t = __builtin_sqrtf(x);
+    if (!(t < __builtin_inff())) return t;            // inf / NaN pass through
+    const double xd = (double)x;
+    const float tu = __uint_as_float(__float_as_uint(t) + 1u);          // next float up (t >= 0)
+    const double mu = 0.5 * ((double)t + (double)tu);
+    if (mu * mu < xd) t = tu;
+    const float td = t > 0.f ? __uint_as_float(__float_as_uint(t) - 1u) : 0.f;   // next float down
+    const double md = 0.5 * ((double)t + (double)td);
+    if (md * md > xd) t = td;
+    return t;
+}
+
 // bit pattern of a non-negative float (incl. +inf) orders like the float
 __device__ __forceinline__ unsigned fbits(float x) { return __float_as_uint(x); }
 

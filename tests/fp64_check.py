@@ -67,7 +67,12 @@ def three_way(prod_ctor, ref_ctor, B, N, seed, uniform=False, pad=0, dev='cuda',
 
     # neighbour choices of the GPU run must equal the reference's (index-exact work)
     for lv, (a, b) in enumerate(zip(rg.rec_fps_idx, rp.rec_fps_idx)):
-        assert torch.equal(a, b), f'FPS index mismatch at level {lv}'
+        if not torch.equal(a, b):
+            bad = (a.long() != b.long()).nonzero()
+            bb, ii = bad[0].tolist()
+            raise AssertionError(f'FPS index mismatch at level {lv}: {bad.shape[0]} entries, first (batch {bb}, '
+                                 f'step {ii}): gpu {a[bb, max(ii - 2, 0):ii + 3].tolist()} '
+                                 f'ref {b[bb, max(ii - 2, 0):ii + 3].tolist()} starts {rp.rec_fps_starts[lv].tolist()}')
     for q, (a, b) in enumerate(zip(rg.rec_group_idx, rp.rec_group_idx)):
         sa, sb = a.long().sort(-1).values, b.sort(-1).values
         bad = (sa != sb).any(-1).nonzero()

@@ -203,3 +203,44 @@ def test_wgrad_vs_fp64(impl, M, N, K, xmode, ymode):
     tol = 2e-6 * math.sqrt(M)
     assert rel(dW, X.t() @ Y) <= tol
     assert rel(db, X.sum(0)) <= tol
+
+
+@pytest.mark.parametrize('K,act', [(32, 'relu'), (16, 'lrelu'), (20, 'relu'), (32, 'lrelu')])
+def test_stack_pooling_matches_max_of_activation(K, act):
+    """A pooled stack (SA / EdgeConv: conv -> BN -> act -> max over K) against the same stack
+    unpooled followed by torch's max over K.  K = 16 / 32 take the GEMM-epilogue z-space
+    max/min + pool_finalize path; K = 20 the separate pooling kernel.  Negative and zero BN
+    scales exercise the min / first-index branches."""
+    from pcseg.engine import shared_mlp
+    torch.manual_seed(K)
+    G, kin, widths = 777, 9, [32, 48]
+
+    def stack():
+        convs = torch.nn.ModuleList([torch.nn.Conv2d(kin, widths[0], 1), torch.nn.Conv2d(widths[0], widths[1], 1)])
+        bns = torch.nn.ModuleList([torch.nn.BatchNorm2d(w) for w in widths])
+        with torch.no_grad():
+            bns[1].weight[::3] = -0.7
+            bns[1].weight[1] = 0.0
+        return convs.to(DEV), bns.to(DEV).train()
+    c1, b1 = stack()
+    c2, b2 = stack()
+    c2.load_state_dict(c1.state_dict())
+    b2.load_state_dict(b1.state_dict())
+    x = torch.randn(G * K, 12, device=DEV)
+    x[:, 9:] = 0
+    x.view(G, K, 12)[:, 5] = x.view(G, K, 12)[:, 2]            # duplicated rows: exact ties in z
+    slope = 0.2 if act == 'lrelu' else 0.0
+    xa = x.clone().requires_grad_(True)
+    xb = x.clone().requires_grad_(True)
+    pooled = shared_mlp(xa, kin, list(c1), list(b1), act, slope, pool_k=K)
+    full = shared_mlp(xb, kin, list(c2), list(b2), act, slope, pool_k=0)
+    ref = full.view(G, K, -1).max(dim=1).values
+    assert torch.equal(pooled, ref)
+    w = torch.randn_like(pooled)
+    (pooled * w).sum().backward()
+    (ref * w).sum().backward()
+    assert rel(xa.grad, xb.grad) <= 1e-5
+    # (pre-BN conv biases have an analytically zero gradient: compare on the scale of the stack's gradients)
+    scale = max(float(q.grad.abs().max()) for q in list(c2.parameters()) + list(b2.parameters()))
+    for p, q in zip(list(c1.parameters()) + list(b1.parameters()), list(c2.parameters()) + list(b2.parameters())):
+        assert float((p.grad - q.grad).abs().max()) <= 1e-5 * scale

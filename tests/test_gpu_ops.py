@@ -339,3 +339,15 @@ def test_interp_cat_fused_bit_exact(D1, D2):
         ref.view(B, N, W + 1)[:, :, :D1] = f1
     call('pcs_interp_fwd', ptr(f2), ptr(idx), ptr(dist), B, N, M, D2, ptr(ref), W + 1, D1, stream_ptr(f2.device))
     assert torch.equal(fused, ref[:, :W])
+
+
+def test_fps_sqrt_tie_is_correctly_rounded():
+    """Regression: two points whose running distances differ by 2 ulps in the square but share
+    one correctly rounded sqrt (a tie the reference breaks on the lower index).  gfx950's
+    v_sqrt_f32 is only faithful; FPS uses a correctly rounded sqrt (pcs_common.hpp sqrt_cr)."""
+    pts, _, _ = make_batch(2, 4096, seed=102, uniform=True)
+    xyz = pts[:, :, :3].contiguous()
+    start = torch.tensor([3910, 920], dtype=torch.int32)
+    ref = R.fps_indices(xyz, 1024, start)
+    got, _ = ops.fps(xyz.to(DEV), 1024, start.to(DEV))
+    assert torch.equal(got.cpu(), ref)
