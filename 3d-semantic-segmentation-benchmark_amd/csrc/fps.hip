@@ -156,15 +156,17 @@ __global__ __launch_bounds__(BLOCK) void fps_kernel(const float* __restrict__ xy
             const unsigned mb = wk - 1u;
             const float Mw = __uint_as_float(mb);
             const float S = sqrt_cr(Mw);
-            // at most 3 floats below Mw share its sqrt (sqrt halves relative spacing):
-            // test them in parallel instead of a dependent chain of sqrts
-            const float p1 = mb >= 1u ? __uint_as_float(mb - 1u) : -1.f;
-            const float p2 = mb >= 2u ? __uint_as_float(mb - 2u) : -1.f;
-            const float p3 = mb >= 3u ? __uint_as_float(mb - 3u) : -1.f;
-            const bool e1 = p1 >= 0.f && sqrt_cr(p1) == S;
-            const bool e2 = p2 >= 0.f && sqrt_cr(p2) == S;
-            const bool e3 = p3 >= 0.f && sqrt_cr(p3) == S;
-            const float lo = e1 ? (e2 ? (e3 ? p3 : p2) : p1) : Mw;
+            // lo = the smallest float whose correctly rounded sqrt is S: the first float above
+            // the square of the midpoint between S and its lower neighbour (exact in double;
+            // a float's sqrt is never exactly a midpoint)
+            float lo = 0.f;
+            if (S > 0.f) {
+                const double mid = 0.5 * ((double)S + (double)__uint_as_float(__float_as_uint(S) - 1u));
+                const double m2 = mid * mid;
+                float f = (float)m2;
+                if ((double)f <= m2) f = __uint_as_float(__float_as_uint(f) + 1u);
+                lo = f;
+            }
             unsigned cand = 0xFFFFFFFFu;
 #pragma unroll
             for (int j = PPT - 1; j >= 0; --j)
