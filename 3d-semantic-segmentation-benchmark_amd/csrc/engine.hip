@@ -88,6 +88,7 @@ static size_t max_partials(int M, int kin, const pcs_mlp_layer* L, int nl, int p
     for (int l = 0; l < nl; ++l) {
         const size_t c = (size_t)L[l].cout;
         m = std::max(m, 2 * c * (size_t)pcs_gemm_row_blocks(M, (int)c));
+        if (backward) m = std::max(m, 2 * c * (size_t)pcs_gemm_row_blocks_dgrad(M, (int)c));
     }
     if (backward) {
         const size_t c = (size_t)L[nl - 1].cout;
@@ -327,7 +328,7 @@ PCS_API int pcs_mlp_backward(const float* X, int ldx, int kin, int M, const pcs_
         if (l > 0) {
             const pcs_mlp_layer& Q = layers[l - 1];
             float* dA = S.dA[da];
-            const int nbg = pcs_gemm_row_blocks(M, Cin);
+            const int nbg = pcs_gemm_row_blocks_dgrad(M, Cin);
             pcs_operand epi = bnbwd_op(nullptr, 0, Q, nullptr, nullptr);
             if (int e = gemm_rows_ex(&xop, M, C, Bw, ldb, bt, nullptr, dA, Cin, Cin, nullptr, &epi, S.part, stream))
                 return e;

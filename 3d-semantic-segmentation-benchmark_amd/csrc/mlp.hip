@@ -812,12 +812,24 @@ using namespace pcs;
 
 // row-GEMM tile (BM x BN) for M rows and N outputs: the largest tile that still
 // gives >= 2 blocks per CU (256 CUs), else the one with the most blocks
-static void gemm_tile(int M, int N, int* bm, int* bn) {
+// bwd: the A operand is a rebuilt dZ (BNBWD / POOLBWD, the data-gradient GEMM): its heavier
+// operand transform and BN-backward epilogue run out of registers on 128 x 128 tiles, so it
+// uses the <= 64-wide tile list for every N
+static void gemm_tile(int M, int N, bool bwd, int* bm, int* bn) {
+    // PCS_GEMM_TILE=bm,bn forces one tile shape (tuning sweeps; must be a built variant)
+    static const int forced = [] {
+        const char* e = getenv("PCS_GEMM_TILE");
+        int a = 0, b = 0;
+        return (e && sscanf(e, "%d,%d", &a, &b) == 2) ? a * 1000 + b : 0;
+    }();
+    if (forced) { *bm = forced / 1000; *bn = forced % 1000; return; }
     struct T { int bm, bn; };
     static const T big[] = {{128, 128}, {64, 128}, {64, 64}, {32, 128}};
     static const T mid[] = {{128, 64}, {64, 64}};
-    const T* c = N > 64 ? big : mid;
-    const int nc = N > 64 ? 4 : 2;
+    static const bool dgrad_wide = [] { const char* e = getenv("PCS_DGRAD_WIDE"); return e && atoi(e); }();
+    const bool wide = N > 64 && (!bwd || dgrad_wide);      // PCS_DGRAD_WIDE=1: A/B against wide dgrad tiles
+    const T* c = wide ? big : mid;
+    const int nc = wide ? 4 : 2;
     if (N <= 32) { *bm = 128; *bn = 32; return; }
     long long best = -1;
     for (int i = 0; i < nc; ++i) {
@@ -859,12 +871,16 @@ static double operand_bytes(const pcs_operand& o, int M, int K) {
 }
 
 // number of row blocks the row GEMM uses for M rows and N outputs (sizes the stats workspace)
-PCS_API int pcs_gemm_row_blocks(int M, int N) {
+static int row_blocks(int M, int N, bool bwd) {
     if (engine_impl() == 1) return direct_row_blocks(M, N);
     int bm, bn;
-    gemm_tile(M, N, &bm, &bn);
+    gemm_tile(M, N, bwd, &bm, &bn);
     return gemm_grid_x(M, N, bm, bn);
 }
+
+PCS_API int pcs_gemm_row_blocks(int M, int N) { return row_blocks(M, N, false); }
+
+PCS_API int pcs_gemm_row_blocks_dgrad(int M, int N) { return row_blocks(M, N, true); }
 
 static int check_operand(const pcs_operand* o, int K, const char* who, const char* which) {
     PCS_CHECK_ARG(o && o->data, "%s: %s operand missing", who, which);
@@ -923,7 +939,7 @@ int pcs::gemm_rows_ex(const pcs_operand* a, int M, int K, const float* W, int ld
             direct_gemm_name(M, N, a->mode, nm, sizeof nm);
         } else {
             int bm, bn, wm, wn;
-            gemm_tile(M, N, &bm, &bn);
+            gemm_tile(M, N, a->mode >= PCS_OP_BNBWD, &bm, &bn);
             gemm_waves(bm, bn, &wm, &wn);
             snprintf(nm, sizeof nm, "pcs::gemm_rows_kernel<%d, %d, %d, %d, %d, %s>", bm, bn, wm, wn, a->mode,
                      bt ? "true" : "false");
@@ -940,7 +956,7 @@ int pcs::gemm_rows_ex(const pcs_operand* a, int M, int K, const float* W, int ld
         return launch_status("pcs_gemm_rows");
     }
     int bm, bn;
-    gemm_tile(M, N, &bm, &bn);
+    gemm_tile(M, N, a->mode >= PCS_OP_BNBWD, &bm, &bn);
     const int gx = gemm_grid_x(M, N, bm, bn);
     const bool b = bt != 0;
     if (bn == 32) launch_gemm<128, 32, 4, 1>(g, gx, b, s);

@@ -50,6 +50,7 @@ SIGNATURES = {
     'pcs_edge_bwd': [P, I32, P, I32, I32, I32, I32, P, P],
     # shared-MLP engine
     'pcs_gemm_row_blocks': [I32, I32],
+    'pcs_gemm_row_blocks_dgrad': [I32, I32],
     'pcs_engine_select': [I32],
     'pcs_probe_begin': [],
     'pcs_probe_end': [],

@@ -131,8 +131,11 @@ typedef struct pcs_operand {
  * Process-wide tuning/testing knob (also env PCS_GEMM_IMPL); call it only while
  * no engine work is being enqueued.  pcs_gemm_row_blocks depends on it. */
 int pcs_engine_select(int impl);
-/* row blocks of pcs_gemm_rows (sizes its stats/bstats workspace) */
+/* row blocks of pcs_gemm_rows with a PLAIN / BNACT A (sizes its stats/bstats workspace) */
 int pcs_gemm_row_blocks(int M, int N);
+/* row blocks of pcs_gemm_rows / pcs_gemm_rows_kmajor when A is BNBWD or POOLBWD (the
+ * data-gradient form; sizes its bstats workspace) */
+int pcs_gemm_row_blocks_dgrad(int M, int N);
 /* C (M x N, ldc) = T(A) . W^T (+bias), W row-major N x K with row stride ldw.
  * stats: partial (sum, sum^2) of C per channel.  bstats: fused BN-backward
  * partials (sum dy, sum dy*xhat) of the layer whose pre-BN output is epi->z

@@ -68,7 +68,7 @@ for name, M, K, N in SHAPES:
         Wt = W[:, :K].t().contiguous()
         dA = torch.empty(M, K, device=dev)
         ZK = torch.randn(M, K, device=dev)
-        bpart = torch.empty(2, K, load().pcs_gemm_row_blocks(M, K), dtype=torch.float64, device=dev)
+        bpart = torch.empty(2, K, load().pcs_gemm_row_blocks_dgrad(M, K), dtype=torch.float64, device=dev)
         epi = operand(None, 0, OP_BNBWD, s, t, 0, 0.0, ZK, K, torch.randn(K, device=dev), torch.rand(K, device=dev))
         dg = lambda: gemm_rows(xop, M, N, Wt, N, None, dA, K, K, None, epi, bpart, st=st)  # noqa
         ms3 = timeit(dg)

@@ -100,7 +100,7 @@ def test_gemm_rows_vs_fp64(impl, M, K, N, mode):
     W[:, :K] = torch.randn(N, K, device=DEV, generator=g) / math.sqrt(K)
     bias = torch.randn(N, device=DEV, generator=g)
     C = torch.full((M, N), float('nan'), device=DEV)
-    nb = load().pcs_gemm_row_blocks(M, N)
+    nb = (load().pcs_gemm_row_blocks_dgrad if mode >= OP_BNBWD else load().pcs_gemm_row_blocks)(M, N)
     part = torch.empty(2, N, nb, dtype=torch.float64, device=DEV)
     st = stream_ptr(torch.device(DEV))
     gemm_rows(x.op(), M, K, W, lda, bias, C, N, N, part, st=st)
@@ -159,7 +159,7 @@ def test_gemm_rows_kmajor_vs_fp64(M, K, N, mode):
     st = stream_ptr(torch.device(DEV))
     tol = 2e-6 * math.sqrt(K)
     if N % 4 == 0:
-        nb = load().pcs_gemm_row_blocks(M, N)
+        nb = (load().pcs_gemm_row_blocks_dgrad if mode >= OP_BNBWD else load().pcs_gemm_row_blocks)(M, N)
         ze = torch.randn(M, N, device=DEV, generator=g)
         se, te = torch.rand(N, device=DEV, generator=g) + 0.5, torch.randn(N, device=DEV, generator=g) * 0.3
         me, ie = torch.randn(N, device=DEV, generator=g) * 0.1, torch.rand(N, device=DEV, generator=g) + 0.5
