@@ -17,6 +17,7 @@
 #include "mlp_common.hpp"
 
 #include <algorithm>
+#include <mutex>
 
 namespace pcs {
 
@@ -147,6 +148,42 @@ static size_t carve_forward(Carve& cv, int M, int kin, const pcs_mlp_layer* L, i
     }
     if (out) *out = s;
     return cv.used;
+}
+
+// ---------------------------------------------------------------- wgrad on a second stream
+// In a stack's backward, layer l's weight gradient and data gradient both only READ the
+// layer's rebuilt dZ; they are independent GEMMs.  The wgrad runs on a per-device side
+// stream (forked from the caller's stream by an event), so it overlaps the dgrad and the
+// BN-backward finalize of the same layer; the caller's stream joins it before the next
+// layer's dgrad, whose outputs (the dA buffer and the BN-backward coefficients) recycle
+// the buffers this wgrad reads.  PCS_WGRAD_OVERLAP=0 keeps everything on one stream.
+struct WgradLane {
+    hipStream_t side = nullptr;
+    hipEvent_t ev[8] = {};
+    int next = 0;
+};
+
+static WgradLane* wgrad_lane() {
+    static const bool on = [] { const char* e = getenv("PCS_WGRAD_OVERLAP"); return !e || atoi(e) != 0; }();
+    if (!on) return nullptr;
+    static WgradLane lanes[16];
+    static std::mutex mu;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return nullptr;
+    std::lock_guard<std::mutex> g(mu);
+    WgradLane& L = lanes[dev];
+    if (!L.side) {
+        if (hipStreamCreateWithFlags(&L.side, hipStreamNonBlocking) != hipSuccess) { L.side = nullptr; return nullptr; }
+        for (auto& e : L.ev)
+            if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+    }
+    return &L;
+}
+
+static hipEvent_t lane_event(WgradLane* L) {
+    hipEvent_t e = L->ev[L->next];
+    L->next = (L->next + 1) & 7;
+    return e;
 }
 
 static pcs_operand plain_op(const float* data, int ld) {
@@ -300,18 +337,43 @@ PCS_API int pcs_mlp_backward(const float* X, int ldx, int kin, int M, const pcs_
     if (pool_k) { xop.mode = PCS_OP_POOLBWD; xop.arg = arg; xop.pool_k = pool_k; }
 
     int da = 0;
+    WgradLane* lane = wgrad_lane();
+    hipEvent_t pending = nullptr;          // the last wgrad launched on the side stream
+    hipEvent_t prev = nullptr;             // the wgrad of the layer above (joined before this dgrad)
+    auto join = [&]() {
+        if (pending) {
+            (void)hipStreamWaitEvent(st, pending, 0);
+            pending = nullptr;
+        }
+    };
     for (int l = nl - 1; l >= 0; --l) {
         const pcs_mlp_layer& P = layers[l];
         const int C = (int)P.cout, Cin = (int)P.cin;
         if (P.dW) {
+            void* ws_stream = stream;
+            if (lane) {                    // fork: the side stream waits for dZ's inputs
+                hipEvent_t ready = lane_event(lane);
+                (void)hipEventRecord(ready, st);
+                (void)hipStreamWaitEvent(lane->side, ready, 0);
+                ws_stream = lane->side;
+            }
             if (l > 0) {
                 const pcs_mlp_layer& Q = layers[l - 1];
                 const pcs_operand y = bnact_op(Q.Z, Cin, Q);
-                if (int e = pcs_wgrad(&xop, C, &y, Cin, M, P.dW, P.db, stream)) return e;
+                if (int e = pcs_wgrad(&xop, C, &y, Cin, M, P.dW, P.db, ws_stream)) { join(); return e; }
             } else {
                 const pcs_operand y = plain_op(X, ldx);
-                if (int e = pcs_wgrad(&xop, C, &y, kin, M, P.dW, P.db, stream)) return e;
+                if (int e = pcs_wgrad(&xop, C, &y, kin, M, P.dW, P.db, ws_stream)) { join(); return e; }
             }
+            if (lane) {
+                prev = pending;
+                pending = lane_event(lane);
+                (void)hipEventRecord(pending, lane->side);
+            }
+        }
+        if (prev) {                        // the layer above's wgrad read the buffers this dgrad recycles
+            (void)hipStreamWaitEvent(st, prev, 0);
+            prev = nullptr;
         }
         if (l == 0 && !dX) break;
         // dgrad B operand: B[k = cout][n = cin] = W[k][n] -- read k-major straight from W by the
@@ -346,5 +408,6 @@ PCS_API int pcs_mlp_backward(const float* X, int ldx, int kin, int M, const pcs_
                 return e;
         }
     }
+    join();
     return launch_status("pcs_mlp_backward");
 }
