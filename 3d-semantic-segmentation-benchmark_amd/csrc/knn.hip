@@ -6,10 +6,18 @@
 // device; parity for DGCNN uses neighbour-index replay and this
 // kernel is checked by set agreement + distance-margin tests.
 //
-// One thread per query row keeps its feature vector and a sorted top-K list in
-// registers; candidate points stream through LDS in 64-point tiles that every
-// lane reads by broadcast, so the (B, N, N) distance matrix of the reference is
-// never materialised.  Ties resolve to the lower index (strict > insertion).
+// knn_tile_kernel (k <= 20): a workgroup owns 128 query rows (32 per wave) and streams
+// the cloud through LDS in 32-point candidate tiles.  Each wave computes its 32 x 32
+// block of inner products with v_mfma_f32_32x32x2_f32 (F % 4 == 0; the k-slice of lane
+// half h is features h*F/2 .. h*F/2+F/2-1, so every lane reads one contiguous run) or
+// with VALU fma chains (F = 3), then filters it against each row's running threshold
+// (the current k-th best): the compare IS the wave ballot, so a candidate costs a few
+// VALU ops and only survivors (about k ln(N/k) per row) are appended to the row's LDS
+// list.  When a row's list could overflow it is merged: one item per lane, rank =
+// number of items that beat it (larger pd, ties to the lower index), items of rank < k
+// kept in rank order and the threshold reset to the k-th.  The scan starts at the
+// workgroup's own tile, so spatially ordered clouds tighten the thresholds early.
+// knn_kernel (k = 40): one thread per query row with a sorted register list.
 #include "pcs_common.hpp"
 
 namespace pcs {
@@ -105,8 +113,367 @@ __global__ __launch_bounds__(256) void knn_kernel(const float* __restrict__ x, i
     }
 }
 
+
+// ----------------------------------------------------------------------------- tiled kNN
+constexpr int KNN_TC = 32;      // candidates per tile
+constexpr int KNN_WAVES = 4;
+constexpr int KNN_QROWS = 32 * KNN_WAVES;
+constexpr int KNN_NMAX = 60;    // LDS items per row: top-k list + one survivor segment per lane half
+constexpr int KNN_RS = KNN_NMAX;       // row stride in items
+
+// accumulator register i of lane half h holds candidate acc_row(i, h) of the tile
+// (v_mfma_f32_32x32x2_f32 C/D layout: row = (i & 3) + 8 (i >> 2) + 4 h, column = lane & 31)
+__device__ __forceinline__ constexpr int acc_row(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
+
+#ifdef PCS_KNN_STATS
+__device__ unsigned long long g_knn_stats[2];   // merges, dropped-and-re-appended survivors (diagnostic build)
+#endif
+
+// Merge row r of this wave (r uniform): its top-k list (nl items) and the two lane-half
+// survivor segments (c0, c1 items) -- n <= 64 items, one per lane.  rank = number of items
+// that beat it (larger pd; ties to the lower index); ranks < k are written back to the list
+// in order (and to `out` if non-null).  Returns the new threshold: the k-th best value, or
+// -inf while the row has fewer than k candidates.
+template <int K, int SEG>
+__device__ __forceinline__ float knn_merge_row(float2* L, int nl, int c0, int c1, int l, int* out) {
+    const int n = nl + c0 + c1;
+    const bool have = l < n;
+    int src = l < nl ? l : (l < nl + c0 ? K + (l - nl) : K + SEG + (l - nl - c0));
+    src = have ? src : 0;
+    const float2 it = L[src];
+    const float v = have ? it.x : -INFINITY;
+    const int id = have ? __float_as_int(it.y) : 0x7fffffff;
+    int rank = 0;
+    for (int j = 0; j < n; ++j) {
+        const float vj = readlane_f(v, j);
+        const int ij = (int)readlane_u((unsigned)id, j);
+        rank += (vj > v || (vj == v && ij < id)) ? 1 : 0;
+    }
+    if (have && rank < K) {
+        L[rank] = make_float2(v, __int_as_float(id));
+        if (out) out[rank] = id;
+    }
+    if (n < K) return -INFINITY;
+    return readlane_f(v, ffs64(ballot(have && rank == K - 1)));
+}
+
+
+// order-preserving uint key of a float (-0 folded into +0, so key ties == float ties)
+__device__ __forceinline__ unsigned knn_key(float v) {
+    const unsigned u = __float_as_uint(v + 0.f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float knn_unkey(unsigned k) {
+    return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
+
+// Running merge of row r (r uniform): keep the k best of its list and both survivor
+// segments (n <= 64 items, one per lane) WITHOUT sorting them: the k-th best key T is
+// found by a 32-step bitwise search (count of keys >= candidate via one ballot each),
+// items above T are kept, items equal to T by lowest index, and the kept ones are
+// compacted into the list.  Returns the new threshold (-inf while fewer than k).
+template <int K, int SEG>
+__device__ __forceinline__ float knn_select_row(float2* L, int nl, int c0, int c1, int l) {
+    const int n = nl + c0 + c1;
+    const bool have = l < n;
+    int src = l < nl ? l : (l < nl + c0 ? K + (l - nl) : K + SEG + (l - nl - c0));
+    src = have ? src : 0;
+    const float2 it = L[src];
+    const unsigned long long hm = ballot(have);
+    unsigned long long keep = hm;
+    float tnew = -INFINITY;
+    if (n > K) {
+        const unsigned key = knn_key(it.x);
+        unsigned T = 0;
+        for (int bit = 31; bit >= 0; --bit) {
+            const unsigned c = T | (1u << bit);
+            if (popc64(ballot(key >= c) & hm) >= K) T = c;
+        }
+        keep = ballot(key > T) & hm;
+        unsigned long long eq = ballot(key == T) & hm;
+        int need = K - popc64(keep);
+        if (popc64(eq) == need) {
+            keep |= eq;
+        } else {               // ties on the k-th value: the lowest indices
+            const int id = __float_as_int(it.y);
+            for (; need > 0; --need) {
+                int best = -1, bid = 0x7fffffff;
+                for (unsigned long long r2 = eq; r2; r2 &= r2 - 1) {
+                    const int ln = ffs64(r2);
+                    const int il = (int)readlane_u((unsigned)id, ln);
+                    if (il < bid) { bid = il; best = ln; }
+                }
+                keep |= 1ull << best;
+                eq &= ~(1ull << best);
+            }
+        }
+        tnew = knn_unkey(T);
+    } else if (n == K) {
+        unsigned mn = 0xffffffffu;
+        const unsigned key = have ? knn_key(it.x) : 0xffffffffu;
+        for (int j = 0; j < n; ++j) mn = min(mn, readlane_u(key, j));
+        tnew = knn_unkey(mn);
+    }
+    if ((keep >> l) & 1ull) L[popc64(keep & lanemask_lt())] = it;
+    return tnew;
+}
+
+// One workgroup = 128 query rows (32 per wave, row = lane & 31 of both lane halves).  The
+// MFMA computes the transposed block (candidates x queries), so each lane holds 16
+// candidates of ONE row: filtering is per lane, branch-free: every candidate is written
+// to the lane's LDS segment at its fill count (a rejected one is overwritten by the next),
+// and the count advances only for survivors.  A full segment flags the survivor as
+// dropped; after the wave merges the flagged rows the dropped survivors are re-appended.
+template <int F, int K>
+__global__ __launch_bounds__(256, 2) void knn_tile_kernel(const float* __restrict__ x, int N,
+                                                          int* __restrict__ out_idx) {
+    constexpr bool MF = (F % 4 == 0);
+    constexpr int FP = MF ? F + 4 : F;       // LDS row stride: conflict-free b128 reads
+    constexpr int FH = MF ? F / 2 : 1;       // features per lane half (MFMA k-slice)
+    constexpr int SEG = (KNN_NMAX - K) / 2;  // CAP usable slots + 1 dump slot per lane half
+    constexpr int CAP = SEG - 1;
+    static_assert(CAP >= 16, "a segment must take one tile's 16 candidates after a merge");
+    __shared__ __attribute__((aligned(16))) float s_c[2][KNN_TC * FP];   // double-buffered tile
+    __shared__ float s_cxx[2][KNN_WAVES][KNN_TC];
+    __shared__ float2 s_it[KNN_QROWS * KNN_RS];
+
+    const int b = blockIdx.y;
+    const int q0 = blockIdx.x * KNN_QROWS;
+    const int tid = threadIdx.x;
+    const int w = tid >> 6, l = tid & 63, h = l >> 5, l32 = l & 31;
+    const float* X = x + (size_t)b * N * F;
+    const int wrow0 = w * 32;
+    const int qr = min(q0 + wrow0 + l32, N - 1);
+    float2* const wl = s_it + wrow0 * KNN_RS;            // this wave's rows
+    float2* const sg = wl + l32 * KNN_RS + K + h * SEG;  // this lane's survivor segment
+
+    // ---- the query row: MFMA B operand (features h*FH ..) or 3 coordinates, and |x_q|^2
+    float a[FH];
+    float q3[3] = {0.f, 0.f, 0.f};
+    float xxq;
+    if constexpr (MF) {
+        const float* xr = X + (size_t)qr * F + h * FH;
+#pragma unroll
+        for (int s = 0; s < FH; s += 4) {
+            const float4 v = *reinterpret_cast<const float4*>(xr + s);
+            a[s] = v.x; a[s + 1] = v.y; a[s + 2] = v.z; a[s + 3] = v.w;
+        }
+        float part = 0.f;
+#pragma unroll
+        for (int s = 0; s < FH; ++s) part = __fadd_rn(part, __fmul_rn(a[s], a[s]));
+        const float other = __shfl_xor(part, 32);
+        xxq = h ? __fadd_rn(other, part) : __fadd_rn(part, other);     // half 0 + half 1
+    } else {
+        xxq = 0.f;
+#pragma unroll
+        for (int f = 0; f < F; ++f) {
+            q3[f] = X[(size_t)qr * F + f];
+            xxq = __fadd_rn(xxq, __fmul_rn(q3[f], q3[f]));
+        }
+    }
+    float tau = -INFINITY;
+    int cnt = 0, nl = 0;                     // segment fill, list length (per row)
+#ifdef PCS_KNN_COUNT
+    int n_merge = 0, n_surv = 0, n_tiles_merging = 0;
+#endif
+
+    const int ntile = (N + KNN_TC - 1) / KNN_TC;
+    const int t0 = q0 / KNN_TC;
+    // candidate tiles: global -> registers one tile ahead, registers -> LDS after the
+    // current tile's compute, one barrier per tile
+    constexpr int NV = MF ? (KNN_TC * (F / 4) + 255) / 256 : 1;
+    static_assert(NV <= 2, "prefetch holds two float4 per thread");
+    float4 pre0 = {}, pre1 = {};
+    float pre3[3] = {0.f, 0.f, 0.f};
+    auto tile_c0 = [&](int tt) {
+        const int t = t0 + tt;
+        return (t >= ntile ? t - ntile : t) * KNN_TC;
+    };
+    auto fetch = [&](int tt) __attribute__((always_inline)) {
+        const int c0 = tile_c0(tt);
+        const int nc = min(KNN_TC, N - c0);
+        if constexpr (MF) {
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+                const int e = tid + 256 * v;
+                if (e < KNN_TC * (F / 4)) {
+                    const int n = e / (F / 4), f4 = e - n * (F / 4);
+                    const float4 g = *reinterpret_cast<const float4*>(X + (size_t)(c0 + min(n, nc - 1)) * F + 4 * f4);
+                    if (v == 0) pre0 = g; else pre1 = g;
+                }
+            }
+        } else {
+            if (tid < KNN_TC) {
+                const float* xr = X + (size_t)(c0 + min(tid, nc - 1)) * F;
+#pragma unroll
+                for (int f = 0; f < F; ++f) pre3[f] = xr[f];
+            }
+        }
+    };
+    auto put = [&](int buf) __attribute__((always_inline)) {
+        if constexpr (MF) {
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+                const int e = tid + 256 * v;
+                if (e < KNN_TC * (F / 4)) {
+                    const int n = e / (F / 4), f4 = e - n * (F / 4);
+                    *reinterpret_cast<float4*>(&s_c[buf][n * FP + 4 * f4]) = v == 0 ? pre0 : pre1;
+                }
+            }
+        } else {
+            if (tid < KNN_TC) {
+                float xx = 0.f;
+#pragma unroll
+                for (int f = 0; f < F; ++f) {
+                    s_c[buf][tid * F + f] = pre3[f];
+                    xx = __fadd_rn(xx, __fmul_rn(pre3[f], pre3[f]));
+                }
+                s_cxx[buf][0][tid] = xx;
+            }
+        }
+    };
+    fetch(0);
+    put(0);
+    __syncthreads();
+    for (int tt = 0; tt < ntile; ++tt) {
+        const int buf = tt & 1;
+        const int c0 = tile_c0(tt);
+        const int nc = min(KNN_TC, N - c0);
+        if (tt + 1 < ntile) fetch(tt + 1);
+        // ---- pd of candidates c0 + acc_row(i, h) for this lane's row
+        float pd[16];
+        if constexpr (MF) {
+            const float* cb = &s_c[buf][l32 * FP + h * FH];
+            typedef float f32x16 __attribute__((ext_vector_type(16)));
+            f32x16 acc = {};
+            float part = 0.f;
+#pragma unroll
+            for (int s = 0; s < FH; s += 4) {
+                const float4 v = *reinterpret_cast<const float4*>(cb + s);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(v.x, a[s], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(v.y, a[s + 1], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(v.z, a[s + 2], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(v.w, a[s + 3], acc, 0, 0, 0);
+                part = __fadd_rn(part, __fmul_rn(v.x, v.x));
+                part = __fadd_rn(part, __fmul_rn(v.y, v.y));
+                part = __fadd_rn(part, __fmul_rn(v.z, v.z));
+                part = __fadd_rn(part, __fmul_rn(v.w, v.w));
+            }
+            const float other = __shfl_xor(part, 32);
+            if (h == 0) s_cxx[0][w][l32] = __fadd_rn(part, other);   // |x_c|^2 of candidate l32
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const float inner = -2.f * acc[i];
+                pd[i] = __fsub_rn(__fsub_rn(-xxq, inner), s_cxx[0][w][acc_row(i, h)]);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int n = acc_row(i, h);
+                float dot = 0.f;
+#pragma unroll
+                for (int f = 0; f < F; ++f) dot = __fmaf_rn(q3[f], s_c[buf][n * F + f], dot);
+                const float inner = -2.f * dot;
+                pd[i] = __fsub_rn(__fsub_rn(-xxq, inner), s_cxx[buf][0][n]);
+            }
+        }
+#ifdef PCS_KNN_NOSEL
+        tau = INFINITY;       // diagnostic: nothing survives (staging + distances only)
+#endif
+        // ---- branch-free threshold filter into the lane's segment
+        unsigned dropped = 0;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const bool p = acc_row(i, h) < nc && pd[i] >= tau;
+            sg[min(cnt, CAP)] = make_float2(pd[i], __int_as_float(c0 + acc_row(i, h)));
+            dropped |= (p && cnt >= CAP) ? (1u << i) : 0u;
+            cnt += (p && cnt < CAP) ? 1 : 0;
+#ifdef PCS_KNN_COUNT
+            n_surv += p ? 1 : 0;
+#endif
+        }
+        const unsigned long long nm = ballot(dropped != 0 || cnt > CAP - 6);
+        if (nm) {
+#ifdef PCS_KNN_COUNT
+            ++n_tiles_merging;
+#endif
+            unsigned rows = (unsigned)nm | (unsigned)(nm >> 32);
+            while (rows) {
+                const int r = __ffs(rows) - 1;
+                rows &= rows - 1;
+                const int c0n = (int)readlane_u((unsigned)cnt, r);
+                const int c1n = (int)readlane_u((unsigned)cnt, r + 32);
+                const int nlr = (int)readlane_u((unsigned)nl, r);
+#ifdef PCS_KNN_NOMERGE
+                const float nt = tau;  // diagnostic: drop the segments instead of merging
+#else
+                const float nt = knn_select_row<K, SEG>(wl + r * KNN_RS, nlr, c0n, c1n, l);
+#endif
+                const bool mine = l32 == r;
+                tau = mine ? nt : tau;
+                cnt = mine ? 0 : cnt;
+                nl = mine ? min(nlr + c0n + c1n, K) : nl;
+#ifdef PCS_KNN_COUNT
+                n_merge += mine ? 1 : 0;
+#endif
+#ifdef PCS_KNN_STATS
+                if (l == 0) atomicAdd(&g_knn_stats[0], 1ull);
+#endif
+            }
+#ifdef PCS_KNN_STATS
+            atomicAdd(&g_knn_stats[1], (unsigned long long)__popc(dropped));
+#endif
+            // re-append the survivors that found their segment full (their row was merged)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const bool p = ((dropped >> i) & 1u) && pd[i] >= tau;
+                sg[min(cnt, CAP)] = make_float2(pd[i], __int_as_float(c0 + acc_row(i, h)));
+                cnt += p ? 1 : 0;
+            }
+        }
+        if (tt + 1 < ntile) put(buf ^ 1);
+        __syncthreads();
+    }
+    // ---- final merge of every row, written out best first
+#ifdef PCS_KNN_COUNT
+    if (q0 + wrow0 + l32 < N) {
+        int* o = out_idx + ((size_t)b * N + q0 + wrow0 + l32) * K;
+        if (h == 0) { o[0] = n_merge; o[1] = n_surv; o[3] = n_tiles_merging; } else { o[2] = n_surv; }
+    }
+    return;
+#endif
+#ifdef PCS_KNN_NOFINAL
+    if (tau == 12345.f) out_idx[0] = cnt;
+    return;
+#endif
+    for (int r = 0; r < 32; ++r) {
+        const int c0n = (int)readlane_u((unsigned)cnt, r);
+        const int c1n = (int)readlane_u((unsigned)cnt, r + 32);
+        const int nlr = (int)readlane_u((unsigned)nl, r);
+        const int q = q0 + wrow0 + r;
+        int* o = q < N ? out_idx + ((size_t)b * N + q) * K : nullptr;
+        if (o) knn_merge_row<K, SEG>(wl + r * KNN_RS, nlr, c0n, c1n, l, o);
+    }
+}
+
+template <int K>
+constexpr bool knn_tiled() { return (KNN_NMAX - K) / 2 - 1 >= 16; }
+
+// PCS_KNN_LEGACY=1 selects the thread-per-row kernel for every k (A/B and diagnostics)
+static bool knn_legacy() {
+    static const bool v = [] { const char* e = getenv("PCS_KNN_LEGACY"); return e && e[0] == '1'; }();
+    return v;
+}
+
 template <int F, int K>
 static void launch_knn(const float* x, int B, int N, int* out, hipStream_t s) {
+    if constexpr (knn_tiled<K>()) {
+        if (!knn_legacy()) {
+            hipLaunchKernelGGL((knn_tile_kernel<F, K>), dim3((N + KNN_QROWS - 1) / KNN_QROWS, B), dim3(256),
+                               0, s, x, N, out);
+            return;
+        }
+    }
     hipLaunchKernelGGL((knn_kernel<F, K>), dim3((N + 255) / 256, B), dim3(256), 0, s, x, N, out);
 }
 
@@ -144,3 +511,12 @@ PCS_API int pcs_knn(const float* x, int B, int N, int F, int k, int32_t* out_idx
     if (rc) return rc;
     return launch_status("pcs_knn");
 }
+
+#ifdef PCS_KNN_STATS
+// diagnostic build only: (merges, appended survivors) since the last call
+PCS_API int pcs_knn_stats(unsigned long long* out2) {
+    unsigned long long z[2] = {0, 0};
+    if (hipMemcpyFromSymbol(out2, HIP_SYMBOL(pcs::g_knn_stats), sizeof(z)) != hipSuccess) return 1;
+    return hipMemcpyToSymbol(HIP_SYMBOL(pcs::g_knn_stats), z, sizeof(z)) != hipSuccess;
+}
+#endif
