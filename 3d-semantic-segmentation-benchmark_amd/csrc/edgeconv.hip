@@ -1,0 +1,337 @@
+// Fused EdgeConv (reference `EdgeConv`, models/dgcnn/dgcnn.py:60-77, with
+// `get_graph_feature`, dgcnn.py:24-57): per point i with neighbours j_1..j_k
+//   z_(i,j) = W [x_j - x_i ; x_i]      (Conv2d 1x1, bias=False, over the (B, 2C, N, k) edge tensor)
+//   out_i   = max_k LeakyReLU(BN_train(z_(i,j)))
+//
+// The edge tensor is never formed.  With W = [W1 | W2] (Cout x 2C):
+//   z_(i,j) = W1 x_j - W1 x_i + W2 x_i = (Y_j - Y_i) + P_i ,   Y = X W1^T,  P = X W2^T
+// so the 1x1 convolution runs over the N points (two row GEMMs on the engine, k = 20x fewer
+// flops than over the N k edges) and one gather pass (edgeconv_fwd_kernel) forms every edge
+// value once in registers: BatchNorm statistics (fp64 partials over all B N k edges, as the
+// reference's BatchNorm2d), the running max/min over k with their first index (the pooled
+// output is act(s z + t) at the max for s > 0 and at the min for s < 0, both monotone), and
+// the per-point sum over k that the backward needs.
+//
+// Backward (training-mode BN): with dy nonzero only at each (i, c)'s argmax edge,
+//   dZ_e = s dy_e - kB - kC (z_e - mean)                        (BN backward, per channel)
+//   dP_i = sum_k dZ_(i,k) = D_i - k kB - kC (S_i - k mean)      (D = s dy at the argmax, S = sum_k z)
+//   dY_m = sum_{e: j_e = m} dZ_e - dP_m                         (CSR inverse of the kNN graph)
+//   dW   = [dY | dP]^T X ,  dX = dY W1 + dP W2                  (one wgrad, one data-gradient GEMM)
+// The gradients are written interleaved, G[:, 2c] = dY_c and G[:, 2c+1] = dP_c, so that W
+// read as a (2 Cout) x C matrix (row 2c = W1 row c, row 2c+1 = W2 row c) is W's own memory:
+// dW = G^T X lands in W's layout and dX = G W_int needs no weight copy.
+#include "mlp_common.hpp"
+
+namespace pcs {
+
+constexpr int kEdgeFwdBlocks = 1024;
+
+// one thread = one point x 4 channels; 256 / (Cout/4) points per block, grid-stride over points
+__global__ __launch_bounds__(256) void edgeconv_fwd_kernel(const float* __restrict__ Y, float* __restrict__ PQ,
+                                                           const int32_t* __restrict__ idx, int N, int k, int Cout,
+                                                           long long G, float* __restrict__ pz,
+                                                           unsigned char* __restrict__ pa, float* __restrict__ S,
+                                                           double* __restrict__ part) {
+    const int tq = Cout / 4;                       // threads per point
+    const int pb = 256 / tq;                       // points per block pass
+    const int slot = threadIdx.x / tq;
+    const int c = 4 * (threadIdx.x - slot * tq);
+    double s1[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0};
+    if (slot < pb) {
+        for (long long g = (long long)blockIdx.x * pb + slot; g < G; g += (long long)gridDim.x * pb) {
+            const long long cloud = (g / N) * N;
+            const float4 yi = *reinterpret_cast<const float4*>(Y + g * Cout + c);
+            const float4 pi = *reinterpret_cast<const float4*>(PQ + g * Cout + c);
+            const float yv[4] = {yi.x, yi.y, yi.z, yi.w}, pv[4] = {pi.x, pi.y, pi.z, pi.w};
+            float mx[4], mn[4], sm[4];
+            int amx[4] = {0, 0, 0, 0}, amn[4] = {0, 0, 0, 0};
+            const int32_t* nb = idx + g * k;
+            for (int kk = 0; kk < k; ++kk) {
+                const int j = min(max(nb[kk], 0), N - 1);
+                const float4 yj = *reinterpret_cast<const float4*>(Y + (cloud + j) * Cout + c);
+                const float jv[4] = {yj.x, yj.y, yj.z, yj.w};
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const float z = __fadd_rn(__fsub_rn(jv[q], yv[q]), pv[q]);
+                    if (kk == 0) {
+                        mx[q] = mn[q] = sm[q] = z;
+                    } else {
+                        if (z > mx[q]) { mx[q] = z; amx[q] = kk; }
+                        if (z < mn[q]) { mn[q] = z; amn[q] = kk; }
+                        sm[q] = __fadd_rn(sm[q], z);
+                    }
+                    s1[q] += (double)z;
+                    s2[q] += (double)z * (double)z;
+                }
+            }
+            *reinterpret_cast<float4*>(pz + g * Cout + c) = make_float4(mx[0], mx[1], mx[2], mx[3]);
+            *reinterpret_cast<float4*>(pz + (G + g) * Cout + c) = make_float4(mn[0], mn[1], mn[2], mn[3]);
+            *reinterpret_cast<uchar4*>(pa + g * Cout + c) =
+                make_uchar4((unsigned char)amx[0], (unsigned char)amx[1], (unsigned char)amx[2], (unsigned char)amx[3]);
+            *reinterpret_cast<uchar4*>(pa + (G + g) * Cout + c) =
+                make_uchar4((unsigned char)amn[0], (unsigned char)amn[1], (unsigned char)amn[2], (unsigned char)amn[3]);
+            *reinterpret_cast<float4*>(S + g * Cout + c) = make_float4(sm[0], sm[1], sm[2], sm[3]);
+            // P is replaced by Q = P - Y (the backward's per-source-point term)
+            *reinterpret_cast<float4*>(PQ + g * Cout + c) =
+                make_float4(__fsub_rn(pv[0], yv[0]), __fsub_rn(pv[1], yv[1]), __fsub_rn(pv[2], yv[2]),
+                            __fsub_rn(pv[3], yv[3]));
+        }
+    }
+    // block reduce of the BN partials over the point slots -> part[2][Cout][gridDim.x]
+    __shared__ double red[2][256][4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        red[0][threadIdx.x][q] = s1[q];
+        red[1][threadIdx.x][q] = s2[q];
+    }
+    __syncthreads();
+    if (threadIdx.x < tq) {
+        for (int sl = 1; sl < pb; ++sl) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                s1[q] += red[0][sl * tq + threadIdx.x][q];
+                s2[q] += red[1][sl * tq + threadIdx.x][q];
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            part[(size_t)(c + q) * gridDim.x + blockIdx.x] = s1[q];
+            part[((size_t)Cout + c + q) * gridDim.x + blockIdx.x] = s2[q];
+        }
+    }
+}
+
+// z of the pooled (argmax) edge: max for s >= 0, min for s < 0 (pool_finalize's choice)
+__device__ __forceinline__ float zsel(const float* pz, long long GN, long long e, float s) {
+    return pz[s < 0.f ? GN + e : e];
+}
+
+// BN-backward sums over the pooled edges (the only ones with dy != 0): part[2][Cout][gridDim.x]
+__global__ __launch_bounds__(256) void edgeconv_bwd_reduce_kernel(const float* __restrict__ dout,
+                                                                  const float* __restrict__ pz, long long G, int Cout,
+                                                                  const float* __restrict__ coef, float slope,
+                                                                  int rows_per_block, double* __restrict__ part) {
+    __shared__ double r1[4][64], r2[4][64];
+    const int lane = threadIdx.x & 63, ph = threadIdx.x >> 6;
+    const int col = blockIdx.y * 64 + lane;
+    const long long gb = (long long)blockIdx.x * rows_per_block;
+    const long long ge = min(G, gb + rows_per_block);
+    const long long GN = G * Cout;
+    double a = 0.0, b = 0.0;
+    if (col < Cout) {
+        const float s = coef[col], t = coef[Cout + col], mean = coef[2 * Cout + col], inv = coef[3 * Cout + col];
+#pragma unroll 4
+        for (long long g = gb + ph; g < ge; g += 4) {
+            const long long e = g * Cout + col;
+            const float z = zsel(pz, GN, e, s);
+            const float dy = dout[e] * dact_f(z * s + t, ACT_LRELU, slope);
+            a += (double)dy;
+            b += (double)dy * (double)((z - mean) * inv);
+        }
+    }
+    r1[ph][lane] = a;
+    r2[ph][lane] = b;
+    __syncthreads();
+    if (ph == 0 && col < Cout) {
+        part[(size_t)col * gridDim.x + blockIdx.x] = r1[0][lane] + r1[1][lane] + r1[2][lane] + r1[3][lane];
+        part[((size_t)Cout + col) * gridDim.x + blockIdx.x] = r2[0][lane] + r2[1][lane] + r2[2][lane] + r2[3][lane];
+    }
+}
+
+// per (point, channel): D = s dy at the argmax edge, dP = D - k kB - kC (S - k mean) -> G[:, 2c+1]
+__global__ __launch_bounds__(256) void edgeconv_bwd_center_kernel(const float* __restrict__ dout,
+                                                                  const float* __restrict__ pz,
+                                                                  const float* __restrict__ S, long long G, int Cout,
+                                                                  int k, const float* __restrict__ coef,
+                                                                  const float* __restrict__ kBC, float slope,
+                                                                  float* __restrict__ D, float* __restrict__ Gd) {
+    const long long GN = G * Cout;
+    for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < GN; e += (long long)gridDim.x * 256) {
+        const int c = (int)(e % Cout);
+        const long long g = e / Cout;
+        const float s = coef[c], t = coef[Cout + c], mean = coef[2 * Cout + c];
+        const float kb = kBC[c], kc = kBC[Cout + c];
+        const float z = zsel(pz, GN, e, s);
+        const float d = s * (dout[e] * dact_f(z * s + t, ACT_LRELU, slope));
+        D[e] = d;
+        const double dp = (double)d - (double)k * kb - (double)kc * ((double)S[e] - (double)k * mean);
+        Gd[g * 2 * Cout + 2 * c + 1] = (float)dp;
+    }
+}
+
+// per target point m (one wave, lanes over channels): sum over the edges whose neighbour is m
+//   G_in = sum [arg == kk] D_i  - cnt (kB + kC (Y_m - mean)) - kC sum Q_i ,  dY = G_in - dP_m -> G[:, 2c]
+// (z_e = Y_m + Q_i; fp64 accumulation, so the unspecified CSR order does not change the result)
+__global__ __launch_bounds__(256) void edgeconv_bwd_gather_kernel(const float* __restrict__ Y,
+                                                                  const float* __restrict__ Q,
+                                                                  const float* __restrict__ D,
+                                                                  const unsigned char* __restrict__ arg,
+                                                                  const int32_t* __restrict__ off,
+                                                                  const int32_t* __restrict__ ent, long long G,
+                                                                  int Cout, int k, const float* __restrict__ coef,
+                                                                  const float* __restrict__ kBC,
+                                                                  float* __restrict__ Gd) {
+    const long long m = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (m >= G) return;
+    const int a = off[m], zend = off[m + 1];
+    for (int c0 = 0; c0 < Cout; c0 += 64) {
+        const int c = c0 + lane;
+        const int cc = c < Cout ? c : Cout - 1;
+        double accd = 0.0, accq = 0.0;
+        for (int base = a; base < zend; base += 64) {
+            const int n = min(64, zend - base);
+            int row = 0, kk = 0;
+            if (lane < n) {
+                const int s = ent[base + lane];
+                row = s / k;
+                kk = s - row * k;
+            }
+            auto term = [&](int e, double& ad, double& aq) {
+                const long long r = (long long)__builtin_amdgcn_readlane(row, e);
+                const int kv = __builtin_amdgcn_readlane(kk, e);
+                const size_t o = (size_t)r * Cout + cc;
+                const float dv = D[o];
+                const float qv = Q[o];
+                const int av = arg[o];
+                ad += av == kv ? (double)dv : 0.0;
+                aq += (double)qv;
+            };
+            int e = 0;
+            for (; e + 4 <= n; e += 4) {
+                term(e, accd, accq);
+                term(e + 1, accd, accq);
+                term(e + 2, accd, accq);
+                term(e + 3, accd, accq);
+            }
+            for (; e < n; ++e) term(e, accd, accq);
+        }
+        if (c < Cout) {
+            const double cnt = (double)(zend - a);
+            const double kb = kBC[c], kc = kBC[Cout + c], mean = coef[2 * Cout + c];
+            const double ym = Y[m * Cout + c];
+            const double gin = accd - cnt * (kb + kc * (ym - mean)) - kc * accq;
+            const size_t go = (size_t)m * 2 * Cout + 2 * c;
+            Gd[go] = (float)(gin - (double)Gd[go + 1]);
+        }
+    }
+}
+
+static pcs_operand plain(const float* p, int ld) {
+    pcs_operand o{};
+    o.data = p;
+    o.ld = ld;
+    o.mode = PCS_OP_PLAIN;
+    return o;
+}
+
+static int fwd_blocks(long long G, int Cout) {
+    const long long pb = 256 / (Cout / 4);
+    const long long need = (G + pb - 1) / pb;
+    return (int)std::min<long long>(kEdgeFwdBlocks, std::max<long long>(need, 1));
+}
+
+static const int kEdgeRedRows = 512;
+
+}  // namespace pcs
+
+using namespace pcs;
+
+PCS_API int pcs_edgeconv_workspace(int B, int N, int Cout, int backward, size_t* bytes) {
+    PCS_CHECK_ARG(bytes && B >= 1 && N >= 1 && Cout >= 4, "pcs_edgeconv_workspace: bad arguments");
+    const long long G = (long long)B * N;
+    if (!backward) {
+        *bytes = (size_t)fwd_blocks(G, Cout) * 2 * Cout * sizeof(double);
+    } else {
+        const long long nb = (G + kEdgeRedRows - 1) / kEdgeRedRows;
+        // G (interleaved dY|dP) + D + kB/kC + reduce partials
+        *bytes = (size_t)G * 2 * Cout * 4 + (size_t)G * Cout * 4 + (size_t)2 * Cout * 4 + 256 +
+                 (size_t)nb * 2 * Cout * sizeof(double);
+    }
+    return 0;
+}
+
+// Training-mode EdgeConv forward.  X (B*N rows, stride ldx) with C channels, idx (B, N, k)
+// int32 neighbour table (per-cloud indices), W (Cout, 2C) = the Conv2d weight, BN gamma/beta
+// and running stats (updated in place, num_batches_tracked bumped).  Outputs (caller-owned):
+// Y, PQ (B*N x Cout; PQ holds Q = P - Y on return), S (B*N x Cout), pz (2 x B*N x Cout),
+// pa (2 x B*N x Cout u8), coef (4 x Cout: s, t, mean, invstd), out (B*N x Cout) pooled
+// activation, arg (B*N x Cout u8) its neighbour slot.  Reference: dgcnn.py:60-77.
+PCS_API int pcs_edgeconv_fwd(const float* X, int ldx, int C, const int32_t* idx, int B, int N, int k,
+                             const float* W, int Cout, const float* gamma, const float* beta, float* run_mean,
+                             float* run_var, long long* num_batches, float momentum, float eps, float slope,
+                             float* Y, float* PQ, float* S, float* pz, unsigned char* pa, float* coef, float* out,
+                             unsigned char* arg, void* workspace, size_t ws_bytes, void* stream) {
+    PCS_CHECK_ARG(B >= 1 && N >= 1 && k >= 1 && k <= 256 && C >= 1 && Cout >= 4 && Cout % 4 == 0 && Cout <= 1024,
+                  "pcs_edgeconv_fwd: bad sizes B=%d N=%d k=%d C=%d Cout=%d", B, N, k, C, Cout);
+    PCS_CHECK_ARG(X && idx && W && Y && PQ && S && pz && pa && coef && out && arg && workspace,
+                  "pcs_edgeconv_fwd: null pointer");
+    const long long G = (long long)B * N;
+    PCS_CHECK_ARG(G * k < (1ll << 31), "pcs_edgeconv_fwd: too many edges");
+    size_t need = 0;
+    pcs_edgeconv_workspace(B, N, Cout, 0, &need);
+    PCS_CHECK_ARG(ws_bytes >= need, "pcs_edgeconv_fwd: workspace %zu < %zu bytes", ws_bytes, need);
+    hipStream_t st = as_stream(stream);
+    const pcs_operand xa = plain(X, ldx);
+    // Y = X W1^T, P = X W2^T: W's rows read with stride 2C (W2 starts C floats in)
+    if (int e = gemm_rows_ex(&xa, (int)G, C, W, 2 * C, 0, nullptr, Y, Cout, Cout, nullptr, nullptr, nullptr, stream))
+        return e;
+    if (int e = gemm_rows_ex(&xa, (int)G, C, W + C, 2 * C, 0, nullptr, PQ, Cout, Cout, nullptr, nullptr, nullptr,
+                             stream))
+        return e;
+    double* part = static_cast<double*>(workspace);
+    const int nb = fwd_blocks(G, Cout);
+    hipLaunchKernelGGL(edgeconv_fwd_kernel, dim3(nb), dim3(256), 0, st, Y, PQ, idx, N, k, Cout, G, pz, pa, S, part);
+    bn_finalize_launch(part, nb, Cout, G * k, gamma, beta, eps, momentum, run_mean, run_var, coef, coef + Cout,
+                       coef + 2 * Cout, coef + 3 * Cout, num_batches, st);
+    return pool_finalize(pz, pa, G, Cout, coef, coef + Cout, ACT_LRELU, slope, out, arg, st);
+}
+
+// Training-mode EdgeConv backward (the forward's saved tensors; csr_off/csr_ent = pcs_inverse_index
+// of idx with targets N).  Accumulates dW (Cout x 2C), dgamma, dbeta (+=); writes dX (nullable,
+// stride lddx, C % 4 == 0).  dout: gradient of the pooled output (B*N x Cout, dense).
+PCS_API int pcs_edgeconv_bwd(const float* X, int ldx, int C, const int32_t* csr_off, const int32_t* csr_ent, int B,
+                             int N, int k, const float* W, int Cout, const float* Y, const float* Q, const float* S,
+                             const float* pz, const unsigned char* arg, const float* coef, float slope,
+                             const float* dout, float* dX, int lddx, float* dW, float* dgamma, float* dbeta,
+                             void* workspace, size_t ws_bytes, void* stream) {
+    PCS_CHECK_ARG(B >= 1 && N >= 1 && k >= 1 && k <= 256 && C >= 1 && Cout >= 4 && Cout % 4 == 0 && Cout <= 1024,
+                  "pcs_edgeconv_bwd: bad sizes B=%d N=%d k=%d C=%d Cout=%d", B, N, k, C, Cout);
+    PCS_CHECK_ARG(X && csr_off && csr_ent && W && Y && Q && S && pz && arg && coef && dout && dW && workspace,
+                  "pcs_edgeconv_bwd: null pointer");
+    PCS_CHECK_ARG(!dX || (C % 4 == 0 && lddx >= C && lddx % 4 == 0), "pcs_edgeconv_bwd: dX needs C %% 4 == 0");
+    const long long G = (long long)B * N;
+    size_t need = 0;
+    pcs_edgeconv_workspace(B, N, Cout, 1, &need);
+    PCS_CHECK_ARG(ws_bytes >= need, "pcs_edgeconv_bwd: workspace %zu < %zu bytes", ws_bytes, need);
+    hipStream_t st = as_stream(stream);
+    char* w = static_cast<char*>(workspace);
+    float* Gd = reinterpret_cast<float*>(w);
+    w += (size_t)G * 2 * Cout * 4;
+    float* D = reinterpret_cast<float*>(w);
+    w += (size_t)G * Cout * 4;
+    float* kBC = reinterpret_cast<float*>(w);
+    w += (size_t)2 * Cout * 4;
+    w = reinterpret_cast<char*>(((uintptr_t)w + 255) & ~(uintptr_t)255);
+    double* part = reinterpret_cast<double*>(w);
+    const int nb = (int)((G + kEdgeRedRows - 1) / kEdgeRedRows);
+    hipLaunchKernelGGL(edgeconv_bwd_reduce_kernel, dim3(nb, (Cout + 63) / 64), dim3(256), 0, st, dout, pz, G, Cout,
+                       coef, slope, kEdgeRedRows, part);
+    bn_bwd_finalize_launch(part, nb, Cout, G * k, coef, coef + 3 * Cout, dgamma, dbeta, kBC, kBC + Cout, 1, st);
+    const long long GN = G * Cout;
+    const unsigned eg = (unsigned)std::min<long long>((GN + 255) / 256, 65536);
+    hipLaunchKernelGGL(edgeconv_bwd_center_kernel, dim3(eg), dim3(256), 0, st, dout, pz, S, G, Cout, k, coef, kBC,
+                       slope, D, Gd);
+    hipLaunchKernelGGL(edgeconv_bwd_gather_kernel, dim3((unsigned)((G + 3) / 4)), dim3(256), 0, st, Y, Q, D, arg,
+                       csr_off, csr_ent, G, Cout, k, coef, kBC, Gd);
+    if (int e = launch_status("pcs_edgeconv_bwd")) return e;
+    // dW (as 2Cout x C) += G^T X ;  dX = G W_int
+    const pcs_operand ga = plain(Gd, 2 * Cout);
+    const pcs_operand xa = plain(X, ldx);
+    if (int e = pcs_wgrad(&ga, 2 * Cout, &xa, C, (int)G, dW, nullptr, stream)) return e;
+    if (dX)
+        if (int e = gemm_rows_ex(&ga, (int)G, 2 * Cout, W, C, 1, nullptr, dX, lddx, C, nullptr, nullptr, nullptr,
+                                 stream))
+            return e;
+    return 0;
+}

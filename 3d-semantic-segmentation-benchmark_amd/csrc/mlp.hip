@@ -736,6 +736,12 @@ void bn_finalize_launch(const double* part, int nb, int N, long long M, const fl
                        run_mean, run_var, s, t, mean, invstd, nbt);
 }
 
+void bn_bwd_finalize_launch(const double* part, int nb, int N, long long M, const float* s, const float* inv,
+                            float* dgamma, float* dbeta, float* kB, float* kC, int accum, hipStream_t st) {
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(N), dim3(256), 0, st, part, nb, N, M, s, inv, dgamma, dbeta, kB,
+                       kC, accum);
+}
+
 static inline unsigned ew_grid(long long total) {
     long long g = (total + 255) / 256;
     if (g > 8192) g = 8192;

@@ -138,6 +138,9 @@ int direct_row_blocks(int M, int N);
 void bn_finalize_launch(const double* part, int nb, int N, long long M, const float* gamma, const float* beta,
                         float eps, float momentum, float* run_mean, float* run_var, float* s, float* t, float* mean,
                         float* invstd, long long* nbt, hipStream_t st);
+// bn_bwd_finalize_kernel launch: (sum dy, sum dy*xhat) partials -> dgamma/dbeta (+= when accum), kB, kC
+void bn_bwd_finalize_launch(const double* part, int nb, int N, long long M, const float* s, const float* inv,
+                            float* dgamma, float* dbeta, float* kB, float* kC, int accum, hipStream_t st);
 int engine_impl();
 // row GEMM with W row-major N x K (bt = 0, = pcs_gemm_rows) or K x N (bt = 1, LDS engine only)
 int gemm_rows_ex(const pcs_operand* a, int M, int K, const float* W, int ldw, int bt, const float* bias, float* C,

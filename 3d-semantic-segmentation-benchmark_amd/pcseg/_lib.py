@@ -71,6 +71,12 @@ SIGNATURES = {
     'pcs_pool_bwd_reduce_blocks': [I64],
     'pcs_pool_bwd_reduce': [P, P, P, I32, I64, I32, P, P, P, P, I32, F32, P, P],
     'pcs_bn_act': [P, I32, I32, I32, P, P, I32, F32, P, I32, P],
+    # fused EdgeConv
+    'pcs_edgeconv_workspace': [I32, I32, I32, I32, P],
+    'pcs_edgeconv_fwd': [P, I32, I32, P, I32, I32, I32, P, I32, P, P, P, P, P, F32, F32, F32,
+                         P, P, P, P, P, P, P, P, P, ctypes.c_size_t, P],
+    'pcs_edgeconv_bwd': [P, I32, I32, P, P, I32, I32, I32, P, I32, P, P, P, P, P, P, F32,
+                         P, P, I32, P, P, P, P, ctypes.c_size_t, P],
     # inverse neighbour maps
     'pcs_inverse_index_workspace': [I64, I64, P],
     'pcs_inverse_index': [P, I32, I32, I32, P, P, P, ctypes.c_size_t, P],

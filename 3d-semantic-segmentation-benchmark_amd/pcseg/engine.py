@@ -258,6 +258,93 @@ class SharedMLPFn(torch.autograd.Function):
         return (dX, None, None, None, None, *([None] * len(params)))
 
 
+def _edge_ws(B, N, Cout, backward, dev):
+    key = ('edge', B, N, Cout, backward)
+    n = _ws_cache.get(key)
+    if n is None:
+        out = ctypes.c_size_t(0)
+        call('pcs_edgeconv_workspace', B, N, Cout, backward, ctypes.byref(out))
+        n = int(out.value)
+        _ws_cache[key] = n
+    return torch.empty((n,), dtype=torch.uint8, device=dev)
+
+
+class EdgeConvFn(torch.autograd.Function):
+    """Fused EdgeConv (dgcnn.py:60-77) in training mode: point rows X (B*N, ld) with C logical
+    channels and the kNN table idx (B, N, k) int32 -> pooled (B*N, Cout).  The (B, 2C, N, k)
+    edge tensor is never formed: z_(i,j) = (Y_j - Y_i) + P_i with Y = X W1^T, P = X W2^T
+    (csrc/edgeconv.hip); the backward gathers over the CSR inverse of idx."""
+
+    @staticmethod
+    def forward(ctx, X, idx, C, slope, bn, W, gamma, beta):
+        dev = X.device
+        st = stream_ptr(dev)
+        B, N, k = idx.shape
+        M, ldx = X.shape
+        Cout = W.shape[0]
+        Wm = W.reshape(Cout, 2 * C)
+        if not Wm.is_contiguous():
+            Wm = Wm.contiguous()
+        Y, PQ, S, out = (_f32((M, Cout), dev) for _ in range(4))
+        pz = _f32((2, M, Cout), dev)
+        pa = torch.empty((2, M, Cout), dtype=torch.uint8, device=dev)
+        arg = torch.empty((M, Cout), dtype=torch.uint8, device=dev)
+        coef = _f32((4 * Cout,), dev)
+        track = bn.track_running_stats and bn.running_mean is not None
+        momentum = 0.0
+        if track:
+            momentum = bn.momentum if bn.momentum is not None else 1.0 / float(bn.num_batches_tracked + 1)
+        ws = _edge_ws(B, N, Cout, 0, dev)
+        call('pcs_edgeconv_fwd', ptr(X), ldx, C, ptr(idx), B, N, k, ptr(Wm), Cout, ptr(gamma), ptr(beta),
+             ptr(bn.running_mean) if track else None, ptr(bn.running_var) if track else None,
+             ptr(bn.num_batches_tracked) if track else None, float(momentum), float(bn.eps), float(slope),
+             ptr(Y), ptr(PQ), ptr(S), ptr(pz), ptr(pa), ptr(coef), ptr(out), ptr(arg), ptr(ws), ws.numel(), st)
+        ctx.save_for_backward(X, idx, Wm, Y, PQ, S, pz, arg, coef)
+        ctx.meta = (C, float(slope))
+        ctx.params = (W, gamma, beta)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        from . import ops
+        X, idx, Wm, Y, Q, S, pz, arg, coef = ctx.saved_tensors
+        C, slope = ctx.meta
+        W, gamma, beta = ctx.params
+        dev = gout.device
+        st = stream_ptr(dev)
+        B, N, k = idx.shape
+        M, ldx = X.shape
+        Cout = Wm.shape[0]
+        gout = gout.contiguous()
+        off, ent = ops.inverse_index(idx, N)
+        dX = _f32((M, ldx), dev) if ctx.needs_input_grad[0] else None
+        if dX is not None and ldx != C:
+            dX.zero_()
+        ws = _edge_ws(B, N, Cout, 1, dev)
+        dW, dg, db = grad_target(W), grad_target(gamma), grad_target(beta)
+        call('pcs_edgeconv_bwd', ptr(X), ldx, C, ptr(off), ptr(ent), B, N, k, ptr(Wm), Cout, ptr(Y), ptr(Q), ptr(S),
+             ptr(pz), ptr(arg), ptr(coef), slope, ptr(gout), ptr(dX), ldx, ptr(dW), ptr(dg), ptr(db), ptr(ws),
+             ws.numel(), st)
+        notify_grad_ready((W, gamma, beta))
+        return dX, None, None, None, None, None, None, None
+
+
+def edgeconv_fused_ok(conv, bn, cin: int) -> bool:
+    """The fused EdgeConv covers training-mode BN on the LDS engine (eval-mode BN and the
+    LDS-free engine use the materialised-edge path)."""
+    return (bn.training and conv.weight.shape[0] % 4 == 0 and conv.bias is None and _impl() == 0
+            and (cin % 4 == 0 or cin < 4))
+
+
+def edgeconv(x_rows: torch.Tensor, cin: int, idx: torch.Tensor, conv, bn, slope: float) -> torch.Tensor:
+    """x_rows (B*N, ld) point rows, idx (B, N, k) int32 -> pooled (B*N, Cout)."""
+    if not x_rows.is_cuda:
+        raise RuntimeError('pcseg ops run only on the GPU (no CPU fallback); got a CPU tensor')
+    if x_rows.shape[1] % 4 or not x_rows.is_contiguous():
+        x_rows = pad_rows(x_rows[:, :cin])
+    return EdgeConvFn.apply(x_rows, idx.contiguous(), cin, slope, bn, conv.weight, bn.weight, bn.bias)
+
+
 def _impl() -> int:
     """The engine GEMM family in use (its row-block count sizes the workspaces)."""
     return _ENGINE_IMPL[0]

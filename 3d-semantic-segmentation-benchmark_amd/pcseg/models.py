@@ -17,7 +17,7 @@ import torch.nn.functional as F
 
 from . import ops
 from .common import SetAbstraction, FeaturePropagation, InvResMLP, UnitPointNet, GeometryPlan, GeometryPrefetch
-from .engine import shared_mlp, pad_rows, linear_rows
+from .engine import shared_mlp, pad_rows, linear_rows, edgeconv, edgeconv_fused_ok
 from .replay import active as _replay
 
 
@@ -241,8 +241,12 @@ class EdgeConv(nn.Module):
             idx = ops.knn(xp, self.k)
         if rp is not None:
             rp.rec_knn_idx.append(idx.detach().cpu())
+        C = xp.shape[2]
+        if edgeconv_fused_ok(self.conv[0], self.conv[1], C):
+            pooled = edgeconv(xp.reshape(B * N, C), C, idx, self.conv[0], self.conv[1], self.conv[2].negative_slope)
+            return pooled.view(B, N, -1)
         rows = ops.edge_rows(xp, idx)
-        pooled = shared_mlp(rows, 2 * xp.shape[2], [self.conv[0]], [self.conv[1]], 'lrelu',
+        pooled = shared_mlp(rows, 2 * C, [self.conv[0]], [self.conv[1]], 'lrelu',
                             self.conv[2].negative_slope, pool_k=self.k)
         return pooled.view(B, N, -1)
 

@@ -227,6 +227,36 @@ int pcs_mlp_backward(const float* X, int ldx, int kin, int M,
                      const uint8_t* arg, const float* gout, float* dX,
                      void* workspace, size_t ws_bytes, void* stream);
 
+/* ---- fused EdgeConv (training-mode BN) --------------------------------------
+ * Replaces get_graph_feature + Conv2d(2C->Cout, 1x1, bias=False) + BatchNorm2d +
+ * LeakyReLU + max over k (models/dgcnn/dgcnn.py:24-57, 60-77) without forming the
+ * (B, 2C, N, k) edge tensor: z_(i,j) = (Y_j - Y_i) + P_i with Y = X W1^T,
+ * P = X W2^T (W = [W1 | W2]).  Rows are B*N points (X stride ldx, C channels);
+ * idx (B, N, k) int32 per-cloud neighbour indices; Cout % 4 == 0. */
+/* workspace bytes of pcs_edgeconv_fwd (backward = 0) / pcs_edgeconv_bwd (1) */
+int pcs_edgeconv_workspace(int B, int N, int Cout, int backward, size_t* bytes);
+/* forward: Y, PQ (returns Q = P - Y), S = sum_k z (each B*N x Cout), pz / pa
+ * (2 x B*N x Cout: max, min of z over k and their first slot), coef (s, t, mean,
+ * invstd; 4 x Cout), pooled activation out (B*N x Cout) + argmax slot arg (u8);
+ * running stats / num_batches updated in place. */
+int pcs_edgeconv_fwd(const float* X, int ldx, int C, const int32_t* idx, int B, int N,
+                     int k, const float* W, int Cout, const float* gamma,
+                     const float* beta, float* run_mean, float* run_var,
+                     long long* num_batches, float momentum, float eps, float slope,
+                     float* Y, float* PQ, float* S, float* pz, uint8_t* pa,
+                     float* coef, float* out, uint8_t* arg, void* workspace,
+                     size_t ws_bytes, void* stream);
+/* backward from the forward's saved tensors and the CSR inverse of idx
+ * (pcs_inverse_index, targets = N): dW (Cout x 2C), dgamma, dbeta accumulate (+=);
+ * dX (nullable; C % 4 == 0) is written.  dout: gradient of `out`. */
+int pcs_edgeconv_bwd(const float* X, int ldx, int C, const int32_t* csr_off,
+                     const int32_t* csr_ent, int B, int N, int k, const float* W,
+                     int Cout, const float* Y, const float* Q, const float* S,
+                     const float* pz, const uint8_t* arg, const float* coef,
+                     float slope, const float* dout, float* dX, int lddx, float* dW,
+                     float* dgamma, float* dbeta, void* workspace, size_t ws_bytes,
+                     void* stream);
+
 /* ---- launch probe (measurement) -----------------------------------------------
  * While enabled, every engine GEMM launch (pcs_gemm_rows / pcs_wgrad, also those
  * issued inside pcs_mlp_forward/backward) is bracketed by HIP events recorded on its
