@@ -65,6 +65,23 @@ static void zero_f32(float* p, long long n, hipStream_t st) {
     hipLaunchKernelGGL(zero_kernel, dim3((unsigned)g), dim3(256), 0, st, p, n);
 }
 
+// columns [c0, ld) of M rows := 0 (the pad columns a GEMM writing c0 channels leaves untouched)
+__global__ __launch_bounds__(256) void zero_cols_kernel(float* __restrict__ p, long long M, int ld, int c0) {
+    const int w = ld - c0;
+    const long long n = M * w;
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+        const long long r = i / w;
+        p[r * ld + c0 + (i - r * w)] = 0.f;
+    }
+}
+
+static void zero_cols(float* p, long long M, int ld, int c0, hipStream_t st) {
+    if (M <= 0 || c0 >= ld) return;
+    long long g = (M * (ld - c0) + 255) / 256;
+    if (g > 4096) g = 4096;
+    hipLaunchKernelGGL(zero_cols_kernel, dim3((unsigned)g), dim3(256), 0, st, p, M, ld, c0);
+}
+
 // ---------------------------------------------------------------- workspace carving
 struct Carve {
     char* base;
@@ -403,7 +420,7 @@ PCS_API int pcs_mlp_backward(const float* X, int ldx, int kin, int M, const pcs_
             xop = bnbwd_op(dA, Cin, Q, S.alpha[pp], S.kb[pp]);
             da ^= 1;
         } else {
-            if (ldx != kin) zero_f32(dX, (long long)M * ldx, st);
+            zero_cols(dX, M, ldx, kin, st);      // the GEMM writes columns [0, kin)
             if (int e = gemm_rows_ex(&xop, M, C, Bw, ldb, bt, nullptr, dX, ldx, kin, nullptr, nullptr, nullptr, stream))
                 return e;
         }

@@ -8,15 +8,14 @@
 //
 // knn_tile_kernel (k <= 20): a workgroup owns 128 query rows (32 per wave) and streams
 // the cloud through LDS in 32-point candidate tiles.  Each wave computes its 32 x 32
-// block of inner products with v_mfma_f32_32x32x2_f32 (F % 4 == 0; the k-slice of lane
-// half h is features h*F/2 .. h*F/2+F/2-1, so every lane reads one contiguous run) or
-// with VALU fma chains (F = 3), then filters it against each row's running threshold
-// (the current k-th best): the compare IS the wave ballot, so a candidate costs a few
-// VALU ops and only survivors (about k ln(N/k) per row) are appended to the row's LDS
-// list.  When a row's list could overflow it is merged: one item per lane, rank =
-// number of items that beat it (larger pd, ties to the lower index), items of rank < k
-// kept in rank order and the threshold reset to the k-th.  The scan starts at the
-// workgroup's own tile, so spatially ordered clouds tighten the thresholds early.
+// block of inner products with v_mfma_f32_32x32x2_f32 (the k-slice of lane half h is
+// features h*F/2 .. h*F/2+F/2-1, so every lane reads one contiguous run; F = 3 is padded
+// to (x, y, z, 0)), then filters it against each row's running threshold (the current
+// k-th best) into per-lane LDS survivor segments (about k ln(N/k) survivors per row).
+// A row whose segments fill is merged by a radix select (k-th key by a 32-step ballot
+// search, no sort); the final merge ranks the survivors (larger pd first, ties to the
+// lower index).  The scan starts at the workgroup's own tile, so spatially ordered
+// clouds tighten the thresholds early.
 // knn_kernel (k = 40): one thread per query row with a sorted register list.
 #include "pcs_common.hpp"
 
@@ -227,14 +226,15 @@ __device__ __forceinline__ float knn_select_row(float2* L, int nl, int c0, int c
 template <int F, int K>
 __global__ __launch_bounds__(256, 2) void knn_tile_kernel(const float* __restrict__ x, int N,
                                                           int* __restrict__ out_idx) {
-    constexpr bool MF = (F % 4 == 0);
-    constexpr int FP = MF ? F + 4 : F;       // LDS row stride: conflict-free b128 reads
-    constexpr int FH = MF ? F / 2 : 1;       // features per lane half (MFMA k-slice)
+    constexpr bool MF = (F % 4 == 0);        // else F = 3: xyz padded to (x, y, z, 0), k-slice 2
+    static_assert(MF || F == 3, "F must be 3 or a multiple of 4");
+    constexpr int FP = MF ? F + 4 : 4;       // LDS row stride: conflict-free b128 reads
+    constexpr int FH = MF ? F / 2 : 2;       // features per lane half (MFMA k-slice)
     constexpr int SEG = (KNN_NMAX - K) / 2;  // CAP usable slots + 1 dump slot per lane half
     constexpr int CAP = SEG - 1;
     static_assert(CAP >= 16, "a segment must take one tile's 16 candidates after a merge");
     __shared__ __attribute__((aligned(16))) float s_c[2][KNN_TC * FP];   // double-buffered tile
-    __shared__ float s_cxx[2][KNN_WAVES][KNN_TC];
+    __shared__ float s_cxx[KNN_WAVES][KNN_TC];
     __shared__ float2 s_it[KNN_QROWS * KNN_RS];
 
     const int b = blockIdx.y;
@@ -247,9 +247,8 @@ __global__ __launch_bounds__(256, 2) void knn_tile_kernel(const float* __restric
     float2* const wl = s_it + wrow0 * KNN_RS;            // this wave's rows
     float2* const sg = wl + l32 * KNN_RS + K + h * SEG;  // this lane's survivor segment
 
-    // ---- the query row: MFMA B operand (features h*FH ..) or 3 coordinates, and |x_q|^2
+    // ---- the query row: MFMA B operand (features h*FH ..) and |x_q|^2 = half 0 + half 1
     float a[FH];
-    float q3[3] = {0.f, 0.f, 0.f};
     float xxq;
     if constexpr (MF) {
         const float* xr = X + (size_t)qr * F + h * FH;
@@ -263,13 +262,13 @@ __global__ __launch_bounds__(256, 2) void knn_tile_kernel(const float* __restric
         for (int s = 0; s < FH; ++s) part = __fadd_rn(part, __fmul_rn(a[s], a[s]));
         const float other = __shfl_xor(part, 32);
         xxq = h ? __fadd_rn(other, part) : __fadd_rn(part, other);     // half 0 + half 1
-    } else {
-        xxq = 0.f;
-#pragma unroll
-        for (int f = 0; f < F; ++f) {
-            q3[f] = X[(size_t)qr * F + f];
-            xxq = __fadd_rn(xxq, __fmul_rn(q3[f], q3[f]));
-        }
+    } else {                                 // (x*x + y*y) + z*z, the sequential order
+        const float* xr = X + (size_t)qr * 3;
+        a[0] = h ? xr[2] : xr[0];
+        a[1] = h ? 0.f : xr[1];
+        const float part = __fadd_rn(__fmul_rn(a[0], a[0]), __fmul_rn(a[1], a[1]));
+        const float other = __shfl_xor(part, 32);
+        xxq = h ? __fadd_rn(other, part) : __fadd_rn(part, other);
     }
     float tau = -INFINITY;
     int cnt = 0, nl = 0;                     // segment fill, list length (per row)
@@ -321,15 +320,8 @@ __global__ __launch_bounds__(256, 2) void knn_tile_kernel(const float* __restric
                 }
             }
         } else {
-            if (tid < KNN_TC) {
-                float xx = 0.f;
-#pragma unroll
-                for (int f = 0; f < F; ++f) {
-                    s_c[buf][tid * F + f] = pre3[f];
-                    xx = __fadd_rn(xx, __fmul_rn(pre3[f], pre3[f]));
-                }
-                s_cxx[buf][0][tid] = xx;
-            }
+            if (tid < KNN_TC)
+                *reinterpret_cast<float4*>(&s_c[buf][tid * 4]) = make_float4(pre3[0], pre3[1], pre3[2], 0.f);
         }
     };
     fetch(0);
@@ -342,13 +334,19 @@ __global__ __launch_bounds__(256, 2) void knn_tile_kernel(const float* __restric
         if (tt + 1 < ntile) fetch(tt + 1);
         // ---- pd of candidates c0 + acc_row(i, h) for this lane's row
         float pd[16];
-        if constexpr (MF) {
+        {
             const float* cb = &s_c[buf][l32 * FP + h * FH];
             typedef float f32x16 __attribute__((ext_vector_type(16)));
             f32x16 acc = {};
             float part = 0.f;
+            if constexpr (!MF) {
+                const float2 v = *reinterpret_cast<const float2*>(cb);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(v.x, a[0], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(v.y, a[1], acc, 0, 0, 0);
+                part = __fadd_rn(__fmul_rn(v.x, v.x), __fmul_rn(v.y, v.y));
+            }
 #pragma unroll
-            for (int s = 0; s < FH; s += 4) {
+            for (int s = 0; s < (MF ? FH : 0); s += 4) {
                 const float4 v = *reinterpret_cast<const float4*>(cb + s);
                 acc = __builtin_amdgcn_mfma_f32_32x32x2f32(v.x, a[s], acc, 0, 0, 0);
                 acc = __builtin_amdgcn_mfma_f32_32x32x2f32(v.y, a[s + 1], acc, 0, 0, 0);
@@ -360,21 +358,11 @@ __global__ __launch_bounds__(256, 2) void knn_tile_kernel(const float* __restric
                 part = __fadd_rn(part, __fmul_rn(v.w, v.w));
             }
             const float other = __shfl_xor(part, 32);
-            if (h == 0) s_cxx[0][w][l32] = __fadd_rn(part, other);   // |x_c|^2 of candidate l32
+            if (h == 0) s_cxx[w][l32] = __fadd_rn(part, other);   // |x_c|^2 of candidate l32
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
                 const float inner = -2.f * acc[i];
-                pd[i] = __fsub_rn(__fsub_rn(-xxq, inner), s_cxx[0][w][acc_row(i, h)]);
-            }
-        } else {
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const int n = acc_row(i, h);
-                float dot = 0.f;
-#pragma unroll
-                for (int f = 0; f < F; ++f) dot = __fmaf_rn(q3[f], s_c[buf][n * F + f], dot);
-                const float inner = -2.f * dot;
-                pd[i] = __fsub_rn(__fsub_rn(-xxq, inner), s_cxx[buf][0][n]);
+                pd[i] = __fsub_rn(__fsub_rn(-xxq, inner), s_cxx[w][acc_row(i, h)]);
             }
         }
 #ifdef PCS_KNN_NOSEL
