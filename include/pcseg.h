@@ -227,6 +227,16 @@ int pcs_mlp_backward(const float* X, int ldx, int kin, int M,
                      const uint8_t* arg, const float* gout, float* dX,
                      void* workspace, size_t ws_bytes, void* stream);
 
+/* ---- segmentation metrics (Training/metrics.py:3-142) ------------------------
+ * predictions (B, N, C) fp32, labels (B, N, C) fp32 (label_u8 = 0) or uint8 (1),
+ * lengths (B) int32; over points n < lengths[b]: pred = argmax predictions, label =
+ * argmax labels (first maximum); conf[label][pred], correct (label == pred), per
+ * class inter (labels[c] == 1 && pred == c) and uni (labels[c] == 1 || pred == c).
+ * int64 counters are accumulated (+=).  C <= 64. */
+int pcs_seg_metrics(const float* pred, const void* labels, int label_u8,
+                    const int32_t* lengths, int B, int N, int C, int64_t* conf,
+                    int64_t* inter, int64_t* uni, int64_t* correct, void* stream);
+
 /* ---- fused EdgeConv (training-mode BN) --------------------------------------
  * Replaces get_graph_feature + Conv2d(2C->Cout, 1x1, bias=False) + BatchNorm2d +
  * LeakyReLU + max over k (models/dgcnn/dgcnn.py:24-57, 60-77) without forming the

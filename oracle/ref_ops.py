@@ -525,6 +525,68 @@ def masked_onehot_cross_entropy(logits, targets_onehot, pad_starts, eps=1e-9):
 
 
 # --------------------------------------------------------------------------
+# section 8(f) row 3: segmentation metrics       (Training/metrics.py:3-142)
+# predictions (B, N, C) probabilities, labels (B, N, C) one-hot, mask (B,) lengths
+# --------------------------------------------------------------------------
+def overall_accuracy(predictions, labels, mask):                      # metrics.py:3-25
+    correct, total = update_accuracy(predictions, labels, mask)
+    return correct / total
+
+
+def update_accuracy(predictions, labels, mask):                       # metrics.py:28-51
+    B = labels.shape[0]
+    correct = 0
+    for b in range(B):
+        n = mask[b]
+        correct += (labels[b, :n].argmax(-1) == predictions[b, :n].argmax(-1)).sum().item()
+    return correct, mask.sum().item()
+
+
+def confusion_matrix(predictions, labels, mask):                      # metrics.py:53-79
+    B, _, C = labels.shape
+    matrix = torch.zeros((C, C), dtype=torch.int64)
+    for b in range(B):
+        n = mask[b]
+        pc = predictions[b, :n].argmax(-1)
+        lc = labels[b, :n].argmax(-1)
+        for i in range(C):
+            pi = pc[lc == i]
+            for j in range(C):
+                matrix[i, j] += (pi == j).sum().item()
+    return matrix
+
+
+def update_intersection_over_union(predictions, labels, mask):        # metrics.py:113-142
+    B, _, C = labels.shape
+    inter = torch.zeros((C,), dtype=torch.float32)
+    union = torch.zeros((C,), dtype=torch.float32)
+    for c in range(C):
+        for b in range(B):
+            n = mask[b]
+            lm = labels[b, :n, c] == 1
+            pm = predictions[b, :n].argmax(-1) == c
+            inter[c] += torch.logical_and(lm, pm).sum().item()
+            union[c] += torch.logical_or(lm, pm).sum().item()
+    return inter, union
+
+
+def intersection_over_union(predictions, labels, mask):               # metrics.py:82-110
+    B, _, C = labels.shape
+    eps = 1e-6
+    ious = torch.zeros((C,), dtype=torch.float32)
+    for c in range(C):
+        inter = union = 0
+        for b in range(B):
+            n = mask[b]
+            lm = labels[b, :n, c] == 1
+            pm = predictions[b, :n].argmax(-1) == c
+            inter += torch.logical_and(lm, pm).sum().item()
+            union += torch.logical_or(lm, pm).sum().item()
+        ious[c] = (inter + eps) / (union + eps)
+    return ious.mean().item(), ious
+
+
+# --------------------------------------------------------------------------
 # deterministic, key-ordered parameter init shared by oracle and product
 # --------------------------------------------------------------------------
 def seeded_init_(model: nn.Module, seed: int) -> nn.Module:

@@ -32,6 +32,7 @@ import models.PointNeXt.PointNeXt as rpx    # noqa: E402
 import models.dgcnn.dgcnn as rdg            # noqa: E402
 import models.PointNet.PointNet as rpn      # noqa: E402
 import Training.train_model as rtm          # noqa: E402
+import Training.metrics as rmet             # noqa: E402
 
 from pcseg.synthetic import make_batch      # noqa: E402
 from oracle.ref_ops import seeded_init_     # noqa: E402
@@ -276,9 +277,30 @@ def golden_pointnet():
          probs=probs, loss=loss, **grad_summary(m), **buffers(m))
 
 
+def golden_metrics():
+    """Training/metrics.py on softmax outputs with argmax ties, padded lengths, an empty
+    sample and a label row that is not one-hot (labels==1 and argmax then disagree)."""
+    g = torch.Generator().manual_seed(81)
+    B, N, C = 4, 300, 14
+    logits = torch.randn(B, N, C, generator=g)
+    logits[:, ::7, 3] = logits[:, ::7, 5] = 9.0          # exact ties on the argmax
+    probs = torch.softmax(logits, dim=-1)
+    cls = torch.randint(0, C, (B, N), generator=g)
+    labels = torch.nn.functional.one_hot(cls, C).to(torch.uint8)
+    labels[1, 10, :] = 0                                  # an all-zero row inside the length
+    labels[3, 11, (int(cls[3, 11]) + 1) % C] = 1         # two ones in one row
+    lengths = torch.tensor([300, 211, 0, 57], dtype=torch.int32)
+    correct, total = rmet.update_accuracy(probs, labels, lengths)
+    miou, ious = rmet.intersection_over_union(probs, labels, lengths)
+    inter, union = rmet.update_intersection_over_union(probs, labels, lengths)
+    save('metrics.npz', probs=probs, labels=labels, lengths=lengths,
+         oa=rmet.overall_accuracy(probs, labels, lengths), correct=correct, total=total,
+         conf=rmet.confusion_matrix(probs, labels, lengths), miou=miou, ious=ious, inter=inter, union=union)
+
+
 if __name__ == '__main__':
     torch.set_num_threads(8)
     which = sys.argv[1:] or ['fps', 'group', 'interp', 'knn', 'loss', 'pointnetpp', 'pointnext',
-                             'dgcnn', 'pointnet']
+                             'dgcnn', 'pointnet', 'metrics']
     for w in which:
         globals()['golden_' + w]()

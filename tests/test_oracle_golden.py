@@ -145,3 +145,17 @@ def test_pointnet_matches_reference(golden):
     loss = R.masked_onehot_cross_entropy(probs, T(z['labels']), T(z['lengths']))
     loss.backward()
     _check_grads(m, z)
+
+
+def test_metrics_match_reference(golden):
+    """Training/metrics.py restated (oracle) vs the reference's own outputs: argmax ties,
+    padded / empty samples, an all-zero and a two-hot label row."""
+    z = golden('metrics.npz')
+    p, lab, n = T(z['probs']), T(z['labels']), T(z['lengths'])
+    assert R.overall_accuracy(p, lab, n) == float(z['oa'])
+    assert R.update_accuracy(p, lab, n) == (int(z['correct']), int(z['total']))
+    assert torch.equal(R.confusion_matrix(p, lab, n), T(z['conf']))
+    miou, ious = R.intersection_over_union(p, lab, n)
+    assert miou == float(z['miou']) and torch.equal(ious, T(z['ious']))
+    inter, union = R.update_intersection_over_union(p, lab, n)
+    assert torch.equal(inter, T(z['inter'])) and torch.equal(union, T(z['union']))
