@@ -86,6 +86,7 @@ SIGNATURES = {
     'pcs_interp_bwd_csr': [P, I32, I32, P, P, P, I32, I32, I32, P, P],
     # block batches
     'pcs_gather_blocks': [P, P, P, I64, P, P, P],
+    'pcs_pad_onehot': [P, I32, P, P, P, I32, I32, I32, P, P, P],
     # optimizer
     'pcs_adam': [P, P, P, P, I64, F32, F32, F32, F32, F32, F32, F32, P],
     # loss

@@ -128,3 +128,70 @@ class DeviceBlockStore:
         call('pcs_gather_blocks', ptr(self.points), ptr(self.labels), ptr(rows), rows.numel(), ptr(pts), ptr(lab),
              stream_ptr(self.device))
         return pts, lab
+
+
+def preprocess_batch_to_train_format(x, y, mapping, cut=None, sampling=None, device=None):
+    """Reference `preprocess_batch_to_train_format` (Training/train_model.py:89-171),
+    harness B's batch builder: optional per-sample random subsampling, zero padding to
+    the longest sample (or `cut`), one-hot fp32 labels from per-point class names.
+
+    Same arguments, RNG calls (one `torch.randperm(N_i, device=x_i.device)` per sample),
+    errors and returns: (batch_input (B, D, L) -- a transposed view, as the reference's --,
+    label (B, L, C) fp32, lengths (B,) int32 on the CPU, cont = B > 1).  The per-point
+    Python `mapping.index` loop of the reference becomes one dictionary pass per sample
+    (numpy); padding and one-hot encoding are one HIP launch (`pcs_pad_onehot`).  Outputs
+    are on `device` (default: the first sample's device, or cuda when that is the CPU).
+    """
+    import numpy as np
+
+    if sampling is not None:
+        if not (0 < sampling <= 1.0):
+            raise ValueError(f"sampling must be in (0,1], got {sampling}")
+    xs, perms = [], []
+    for xi in x:
+        if sampling is not None:
+            k = max(int(xi.shape[0] * sampling), 1)
+            perm = torch.randperm(xi.shape[0], device=xi.device)[:k]
+            xi = xi[perm]
+            perms.append(perm.cpu().numpy())
+        else:
+            perms.append(None)
+        xs.append(xi)
+    lengths = torch.tensor([xi.shape[0] for xi in xs], dtype=torch.int32)
+    max_length = int(lengths.max().item())
+    if cut is not None:
+        max_length = min(max_length, cut)
+    B = len(xs)
+    D = xs[0].shape[-1]
+    C = len(mapping)
+    dev = torch.device(device) if device is not None else xs[0].device
+    if dev.type != 'cuda':
+        dev = torch.device('cuda')
+    used = torch.clamp(lengths, max=max_length)
+    # class ids of the rows that are kept (the reference looks labels up only below
+    # max_length, so an unknown name beyond the cut is not an error there either)
+    lut = {}
+    for i, name in enumerate(mapping):        # list.index returns the first occurrence
+        lut.setdefault(name, i)
+    ids = []
+    for yi, perm, n in zip(y, perms, used.tolist()):
+        sel = (yi[j] for j in perm[:n]) if perm is not None else (yi[j] for j in range(n))
+        try:
+            ids.append(np.fromiter((lut[v] for v in sel), dtype=np.int32, count=n))
+        except KeyError as e:
+            raise ValueError(f'{e.args[0]!r} is not in list') from None
+    rows = [xi[:n] for xi, n in zip(xs, used.tolist())]
+    pts = torch.cat([r.to(device=dev, dtype=torch.float32) for r in rows]).contiguous()
+    cls = torch.from_numpy(np.concatenate(ids)).to(dev)
+    offsets = torch.zeros(B, dtype=torch.int64)
+    if B > 1:
+        offsets[1:] = torch.cumsum(used[:-1].to(torch.int64), 0)
+    offsets = offsets.to(dev)
+    used_d = used.to(dev)
+    batch_input = torch.empty((B, max_length, D), dtype=torch.float32, device=dev)
+    label = torch.empty((B, max_length, C), dtype=torch.float32, device=dev)
+    call('pcs_pad_onehot', ptr(pts), D, ptr(cls), ptr(offsets), ptr(used_d), B, max_length, C, ptr(batch_input),
+         ptr(label), stream_ptr(dev))
+    if cut is not None:
+        lengths = torch.clamp(lengths, max=cut)
+    return batch_input.transpose(1, 2), label, lengths, B > 1

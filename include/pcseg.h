@@ -227,6 +227,14 @@ int pcs_mlp_backward(const float* X, int ldx, int kin, int M,
                      const uint8_t* arg, const float* gout, float* dX,
                      void* workspace, size_t ws_bytes, void* stream);
 
+/* ---- harness-B batch (Training/train_model.py:89-171, preprocess_batch_to_train_format)
+ * sample i's rows are packed at [offsets[i], offsets[i] + lengths[i]) of points (rows x D)
+ * and ids (class index per row, int32); writes out_points (B, L, D) zero-padded and
+ * out_labels (B, L, C) one-hot fp32 (rows n < lengths[i], lengths[i] <= L). */
+int pcs_pad_onehot(const float* points, int D, const int32_t* ids, const long long* offsets,
+                   const int32_t* lengths, int B, int L, int C, float* out_points,
+                   float* out_labels, void* stream);
+
 /* ---- segmentation metrics (Training/metrics.py:3-142) ------------------------
  * predictions (B, N, C) fp32, labels (B, N, C) fp32 (label_u8 = 0) or uint8 (1),
  * lengths (B) int32; over points n < lengths[b]: pred = argmax predictions, label =

@@ -525,6 +525,39 @@ def masked_onehot_cross_entropy(logits, targets_onehot, pad_starts, eps=1e-9):
 
 
 # --------------------------------------------------------------------------
+# section 8(f) row 2: harness-B batch builder  (Training/train_model.py:89-171)
+# --------------------------------------------------------------------------
+def preprocess_batch_to_train_format(x, y, mapping, cut=None, sampling=None):
+    if sampling is not None:
+        if not (0 < sampling <= 1.0):
+            raise ValueError(f"sampling must be in (0,1], got {sampling}")
+        xs, ys = [], []
+        for xi, yi in zip(x, y):                                 # :122-133
+            perm = torch.randperm(xi.shape[0], device=xi.device)[:max(int(xi.shape[0] * sampling), 1)]
+            xs.append(xi[perm])
+            ys.append([yi[j] for j in perm.cpu().tolist()])
+        x, y = xs, ys
+    lengths = torch.tensor([xi.shape[0] for xi in x], dtype=torch.int32)   # :136
+    L = int(lengths.max().item())
+    if cut is not None:
+        L = min(L, cut)
+    B, D, C = len(x), x[0].shape[-1], len(mapping)
+    out = torch.zeros((B, L, D), device=x[0].device, dtype=x[0].dtype)
+    for i, xi in enumerate(x):                                   # :146-149
+        n = min(xi.shape[0], L)
+        out[i, :n] = xi[:n]
+    label = torch.zeros((B, L, C), dtype=torch.float32, device=out.device)
+    for i, yi in enumerate(y):                                   # :152-159
+        for j, name in enumerate(yi):
+            if j >= L:
+                break
+            label[i, j, mapping.index(name)] = 1.0
+    if cut is not None:
+        lengths = torch.clamp(lengths, max=cut)
+    return out.transpose(1, 2), label, lengths, B > 1
+
+
+# --------------------------------------------------------------------------
 # section 8(f) row 3: segmentation metrics       (Training/metrics.py:3-142)
 # predictions (B, N, C) probabilities, labels (B, N, C) one-hot, mask (B,) lengths
 # --------------------------------------------------------------------------

@@ -277,6 +277,27 @@ def golden_pointnet():
          probs=probs, loss=loss, **grad_summary(m), **buffers(m))
 
 
+def golden_preprocess():
+    """Training/train_model.py:89-171 on ragged samples with string labels: plain, cut,
+    and sampling (RNG state seeded before each call, so replays draw the same perms)."""
+    g = torch.Generator().manual_seed(91)
+    mapping = ['ceiling', 'floor', 'wall', 'beam', 'column', 'window', 'door', 'table', 'chair', 'sofa',
+               'bookcase', 'board', 'clutter', 'stairs']
+    ns = [37, 120, 5, 64]
+    x = [torch.randn(n, 6, generator=g) for n in ns]
+    y = [[mapping[int(v)] for v in torch.randint(0, 14, (n,), generator=g)] for n in ns]
+    out = {}
+    for tag, kw, seed in [('plain', {}, 1), ('cut', {'cut': 50}, 2), ('samp', {'sampling': 0.5}, 3),
+                          ('both', {'cut': 40, 'sampling': 0.7}, 4)]:
+        torch.manual_seed(seed)
+        bi, lab, lengths, cont = rtm.preprocess_batch_to_train_format(x, y, mapping, **kw)
+        out.update({f'{tag}_x': bi.contiguous(), f'{tag}_label': lab, f'{tag}_len': lengths, f'{tag}_cont': cont,
+                    f'{tag}_seed': seed})
+    flat = np.array([v for yi in y for v in yi])
+    save('preprocess.npz', **{f'x{i}': xi for i, xi in enumerate(x)}, ns=np.array(ns), labels=flat,
+         mapping=np.array(mapping), **out)
+
+
 def golden_metrics():
     """Training/metrics.py on softmax outputs with argmax ties, padded lengths, an empty
     sample and a label row that is not one-hot (labels==1 and argmax then disagree)."""
@@ -301,6 +322,6 @@ def golden_metrics():
 if __name__ == '__main__':
     torch.set_num_threads(8)
     which = sys.argv[1:] or ['fps', 'group', 'interp', 'knn', 'loss', 'pointnetpp', 'pointnext',
-                             'dgcnn', 'pointnet', 'metrics']
+                             'dgcnn', 'pointnet', 'metrics', 'preprocess']
     for w in which:
         globals()['golden_' + w]()

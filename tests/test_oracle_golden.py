@@ -159,3 +159,30 @@ def test_metrics_match_reference(golden):
     assert miou == float(z['miou']) and torch.equal(ious, T(z['ious']))
     inter, union = R.update_intersection_over_union(p, lab, n)
     assert torch.equal(inter, T(z['inter'])) and torch.equal(union, T(z['union']))
+
+
+def _preprocess_inputs(z):
+    ns = [int(n) for n in z['ns']]
+    x = [T(z[f'x{i}']) for i in range(len(ns))]
+    flat = [str(v) for v in z['labels']]
+    y, o = [], 0
+    for n in ns:
+        y.append(flat[o:o + n])
+        o += n
+    return x, y, [str(m) for m in z['mapping']]
+
+
+PREPROCESS_CASES = [('plain', {}), ('cut', {'cut': 50}), ('samp', {'sampling': 0.5}),
+                    ('both', {'cut': 40, 'sampling': 0.7})]
+
+
+@pytest.mark.parametrize('tag,kw', PREPROCESS_CASES)
+def test_preprocess_matches_reference(golden, tag, kw):
+    z = golden('preprocess.npz')
+    x, y, mapping = _preprocess_inputs(z)
+    torch.manual_seed(int(z[f'{tag}_seed']))
+    bi, lab, lengths, cont = R.preprocess_batch_to_train_format(x, y, mapping, **kw)
+    assert torch.equal(bi.contiguous(), T(z[f'{tag}_x'])) and bi.shape[1] == x[0].shape[1]
+    assert torch.equal(lab, T(z[f'{tag}_label']))
+    assert torch.equal(lengths, T(z[f'{tag}_len'])) and lengths.dtype == torch.int32
+    assert cont == bool(z[f'{tag}_cont'])
