@@ -12,9 +12,9 @@ from .models import (PointNetpp, PointNetppMSG, PointNeXt, EdgeConv, DGCNN, DGCN
                      TNet, PointNetEncoder, PointNetSeg, knn, get_graph_feature)
 from .loss import masked_onehot_cross_entropy
 from .replay import Replay, replay
-from . import metrics
+from . import metrics, inference
 
 __all__ = ['sample', 'group', 'reduce', 'interpolate', 'MiniPointNet', 'UnitPointNet', 'SetAbstraction',
            'FeaturePropagation', 'InvResMLP', 'PointNetpp', 'PointNetppMSG', 'PointNeXt', 'EdgeConv', 'DGCNN',
            'DGCNNWithColor', 'get_model', 'get_loss', 'TNet', 'PointNetEncoder', 'PointNetSeg',
-           'masked_onehot_cross_entropy', 'Replay', 'replay', 'knn', 'get_graph_feature', 'metrics']
+           'masked_onehot_cross_entropy', 'Replay', 'replay', 'knn', 'get_graph_feature', 'metrics', 'inference']

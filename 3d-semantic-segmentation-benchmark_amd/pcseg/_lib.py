@@ -71,6 +71,8 @@ SIGNATURES = {
     'pcs_pool_bwd_reduce_blocks': [I64],
     'pcs_pool_bwd_reduce': [P, P, P, I32, I64, I32, P, P, P, P, I32, F32, P, P],
     'pcs_bn_act': [P, I32, I32, I32, P, P, I32, F32, P, I32, P],
+    # sliding-window inference
+    'pcs_window_merge': [P, P, I32, I64, I32, I64, I64, P, P, P],
     # metrics
     'pcs_seg_metrics': [P, P, I32, P, I32, I32, I32, P, P, P, P, P],
     # fused EdgeConv

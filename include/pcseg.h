@@ -235,6 +235,14 @@ int pcs_pad_onehot(const float* points, int D, const int32_t* ids, const long lo
                    const int32_t* lengths, int B, int L, int C, float* out_points,
                    float* out_labels, void* stream);
 
+/* ---- sliding-window scene inference, merge step (models/dgcnn/utils.py:67-131)
+ * nw windows start at w*step (win points each, fewer at the end), their logits packed at
+ * rows window_rows[w] .. of window_logits (C per row); per point: mean logits of the
+ * covering windows (summed in window order), pred = argmax, conf = max softmax.  C <= 64. */
+int pcs_window_merge(const float* window_logits, const long long* window_rows, int nw,
+                     long long n, int C, long long step, long long win, long long* pred,
+                     float* conf, void* stream);
+
 /* ---- segmentation metrics (Training/metrics.py:3-142) ------------------------
  * predictions (B, N, C) fp32, labels (B, N, C) fp32 (label_u8 = 0) or uint8 (1),
  * lengths (B) int32; over points n < lengths[b]: pred = argmax predictions, label =

@@ -525,6 +525,28 @@ def masked_onehot_cross_entropy(logits, targets_onehot, pad_starts, eps=1e-9):
 
 
 # --------------------------------------------------------------------------
+# section 8(f) row 4: sliding-window scene inference  (models/dgcnn/utils.py:67-131)
+# --------------------------------------------------------------------------
+def predict_single_scene(model, points, batch_size=4096, overlap=512):
+    model.eval()
+    n = points.shape[0]
+    if n <= batch_size:
+        with torch.no_grad():
+            logits = model(points.T.unsqueeze(0))[0].squeeze(0)
+        return torch.argmax(logits, dim=1), torch.softmax(logits, dim=1).max(dim=1)[0]
+    step = batch_size - overlap
+    all_logits = torch.zeros(n, model.num_classes)
+    counts = torch.zeros(n)
+    with torch.no_grad():
+        for s in range(0, n, step):                              # :112-127
+            e = min(s + batch_size, n)
+            all_logits[s:e] += model(points[s:e].T.unsqueeze(0))[0].squeeze(0)
+            counts[s:e] += 1
+    all_logits = all_logits / counts.unsqueeze(1)
+    return torch.argmax(all_logits, dim=1), torch.softmax(all_logits, dim=1).max(dim=1)[0]
+
+
+# --------------------------------------------------------------------------
 # section 8(f) row 2: harness-B batch builder  (Training/train_model.py:89-171)
 # --------------------------------------------------------------------------
 def preprocess_batch_to_train_format(x, y, mapping, cut=None, sampling=None):
