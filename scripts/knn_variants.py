@@ -15,9 +15,9 @@ for path in [os.path.join(root, 'libpcseg.so')] + sorted(glob.glob(os.path.join(
             assert rc == 0
         run(); run(); torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for _ in range(5): run()
+        for _ in range(20): run()
         torch.cuda.synchronize()
-        print(f'{os.path.basename(path):28s} F={F:2d}: {(time.perf_counter() - t0) / 5 * 1e3:.3f} ms', flush=True)
+        print(f'{os.path.basename(path):28s} F={F:2d}: {(time.perf_counter() - t0) / 20 * 1e3:.3f} ms', flush=True)
         if 'COUNT' in path:
             o = out.view(-1, k).float()
             print(f'   merges/row {o[:, 0].mean():.2f}  survivors/row {(o[:, 1] + o[:, 2]).mean():.1f}  '

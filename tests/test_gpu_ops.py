@@ -202,6 +202,22 @@ def test_dgcnn_knn_agrees_with_oracle(F_, seed):
     assert (got[..., 0] == torch.arange(N)).float().mean() > 0.99   # self first
 
 
+@pytest.mark.parametrize('F_,lo,hi,N', [(3, 0, 8, 2048), (64, -2, 3, 2048), (64, 0, 2, 1000), (3, 0, 4, 333)])
+def test_dgcnn_knn_selection_exact_on_integer_grids(F_, lo, hi, N):
+    """Integer features make every pd exact in fp32 (MFMA included), so the k best are
+    fully determined: larger pd first, exact ties to the lower index.  Coarse grids put
+    many exact ties on the k-th value (the running radix select's tie path, the final
+    rank merge) and ragged N exercises the partial last tile."""
+    B, k = 2, 20
+    g = torch.Generator().manual_seed(F_ * 7 + N)
+    x = torch.randint(lo, hi, (B, N, F_), generator=g).float()
+    xd = x.double()
+    d = torch.cdist(xd, xd) ** 2
+    exp = torch.sort(d.round(), dim=-1, stable=True).indices[..., :k]
+    got = ops.knn(x.contiguous().to(DEV), k).cpu().long()
+    assert torch.equal(got, exp)
+
+
 @pytest.mark.parametrize('dim9', [False, True])
 def test_functional_get_graph_feature_and_knn(dim9):
     """pcseg.get_graph_feature / pcseg.knn: the reference's functional API (dgcnn.py:7-57)."""
