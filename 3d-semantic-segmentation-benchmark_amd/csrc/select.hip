@@ -108,8 +108,13 @@ __device__ __forceinline__ void emit_sorted(unsigned v, unsigned i, int k, int* 
     }
 }
 
+// 1024-thread blocks: 16 waves share one staged cloud (48 KB at N = 4096), so LDS allows
+// 8 waves per SIMD instead of 3 -- the heap surgery is a latency-bound chain of
+// v_readlane / SALU hops per wave, and occupancy is what hides it.
+constexpr int kHeapBlock = 1024;
+
 template <bool STAGE>
-__global__ __launch_bounds__(256) void heap_select_kernel(Geo g, int rows_per_wave) {
+__global__ __launch_bounds__(kHeapBlock) void heap_select_kernel(Geo g, int rows_per_wave) {
     extern __shared__ __attribute__((aligned(16))) float s_xyz[];
     const int b = blockIdx.y;
     const float* X = g.xyz + (size_t)b * g.N * 3;
@@ -467,9 +472,10 @@ static int run_select(Geo g, hipStream_t s, const char* what) {
         PCS_CHECK_ARG(g.K <= 64, "%s: k=%d > 64 not supported on the heap path", what, g.K);
         const int rows_per_wave = 4;
         const int waves = (g.R + rows_per_wave - 1) / rows_per_wave;
-        const dim3 grid((waves + 3) / 4, g.B);
-        if (stage) hipLaunchKernelGGL(heap_select_kernel<true>, grid, dim3(256), xyz_lds, s, g, rows_per_wave);
-        else hipLaunchKernelGGL(heap_select_kernel<false>, grid, dim3(256), 0, s, g, rows_per_wave);
+        constexpr int wpb = kHeapBlock / kWave;
+        const dim3 grid((waves + wpb - 1) / wpb, g.B);
+        if (stage) hipLaunchKernelGGL(heap_select_kernel<true>, grid, dim3(kHeapBlock), xyz_lds, s, g, rows_per_wave);
+        else hipLaunchKernelGGL(heap_select_kernel<false>, grid, dim3(kHeapBlock), 0, s, g, rows_per_wave);
         return launch_status(what);
     }
     // intro path: n < 64k <= 4096 for k <= 64

@@ -178,6 +178,8 @@ def main():
     ap.add_argument('--no-roofline', action='store_true')
     ap.add_argument('--graph', action='store_true',
                     help='capture one training step in a HIP graph and time its replays (N=1, no prefetch)')
+    ap.add_argument('--prefetch-point', default='loss', choices=['loss', 'backward'],
+                    help='where the next batch\'s geometry plan is enqueued')
     ap.add_argument('--no-prefetch', action='store_true',
                     help='do not enqueue the next step\'s FPS/ball-query/3-NN before this step\'s backward')
     args = ap.parse_args()
@@ -224,11 +226,15 @@ def main():
     def step():
         grads.zero_grad()
         loss = pcseg.masked_onehot_cross_entropy(logits_of(model(x)), lab, lengths)
-        if prefetch:
+        if prefetch and args.prefetch_point == 'loss':
             # pipelined input: the next batch's neighbour search (here the same resident
             # blocks, fresh FPS starts) runs on the side stream under this backward
             model.prefetch_geometry(x)
         loss.backward()
+        if prefetch and args.prefetch_point == 'backward':
+            # same, planned once the backward is enqueued: the host work of the plan
+            # overlaps the queued backward instead of delaying its first launch
+            model.prefetch_geometry(x)
         grads.synchronize()
         opt.step()
         return loss
