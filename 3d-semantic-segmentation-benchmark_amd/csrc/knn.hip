@@ -119,6 +119,10 @@ constexpr int KNN_WAVES = 4;
 constexpr int KNN_QROWS = 32 * KNN_WAVES;
 constexpr int KNN_NMAX = 60;    // LDS items per row: top-k list + one survivor segment per lane half
 constexpr int KNN_RS = KNN_NMAX;       // row stride in items
+#ifndef PCS_KNN_SLACK
+#define PCS_KNN_SLACK 0         // merge early when a segment has fewer free slots (0: only on overflow;
+                                // B=32 N=4096: 6 -> 0 is -6 % kNN time, fewer merges, rare re-appends)
+#endif
 
 // accumulator register i of lane half h holds candidate acc_row(i, h) of the tile
 // (v_mfma_f32_32x32x2_f32 C/D layout: row = (i & 3) + 8 (i >> 2) + 4 h, column = lane & 31)
@@ -174,10 +178,11 @@ __device__ __forceinline__ int knn_popc(unsigned long long m) {
 
 // Running merge of row r (r uniform): keep the k best of its list and both survivor
 // segments (n <= 64 items, one per lane) WITHOUT sorting them: the k-th best key T is
-// found by a 32-step bitwise search (count of keys >= candidate via one ballot and an
-// SALU popcount each; a radix-4 variant with three ballots per step measured ~10 %
-// slower: its VALU->SALU hops serialise on VCC), items above T are kept, items equal to
-// T by lowest index, and the kept ones are compacted into the list.  Returns the new threshold (-inf while fewer than k).
+// found by a ballot quickselect (pivot = a lane's key, counts of keys above / at it by
+// ballot + SALU popcount; ~log n rounds instead of the 32 steps of a bitwise search, and a
+// radix-4 search measured slower still: its VALU->SALU hops serialise on VCC), items above
+// T are kept, items equal to T by lowest index, and the kept ones are compacted into the
+// list.  Returns the new threshold (-inf while fewer than k).
 template <int K, int SEG>
 __device__ __forceinline__ float knn_select_row(float2* L, int nl, int c0, int c1, int l) {
     const int n = nl + c0 + c1;
@@ -189,12 +194,31 @@ __device__ __forceinline__ float knn_select_row(float2* L, int nl, int c0, int c
     unsigned long long keep = hm;
     float tnew = -INFINITY;
     if (n > K) {
-        const unsigned key = have ? knn_key(it.x) : 0u;   // key 0 (a NaN pattern) never counts
-        unsigned T = 0;
+        const unsigned key = have ? knn_key(it.x) : 0u;
+        unsigned T;
+#ifdef PCS_KNN_BITSEARCH
+        T = 0;                         // diagnostic: 32-step bitwise search (key 0 never counts)
         for (int bit = 31; bit >= 0; --bit) {
             const unsigned c = T | (1u << bit);
             if (knn_popc(ballot(key >= c)) >= K) T = c;
         }
+#else
+        // quickselect over the lanes: T is the rem-th largest key of `mask`; the pivot is
+        // the mask's lowest lane (items sit in arrival order), each round drops the pivot
+        unsigned long long mask = hm;
+        int rem = K;
+        while (true) {
+            const unsigned pv = readlane_u(key, ffs64(mask));
+            const unsigned long long gt = ballot(key > pv) & mask;
+            const int cg = knn_popc(gt);
+            if (cg >= rem) { mask = gt; continue; }
+            const unsigned long long ge = ballot(key >= pv) & mask;
+            const int ce = knn_popc(ge);
+            if (ce >= rem) { T = pv; break; }
+            rem -= ce;
+            mask &= ~ge;
+        }
+#endif
         keep = ballot(key > T) & hm;
         unsigned long long eq = ballot(key == T) & hm;
         int need = K - knn_popc(keep);
@@ -387,7 +411,7 @@ __global__ __launch_bounds__(256, 2) void knn_tile_kernel(const float* __restric
             n_surv += p ? 1 : 0;
 #endif
         }
-        const unsigned long long nm = ballot(dropped != 0 || cnt > CAP - 6);
+        const unsigned long long nm = ballot(dropped != 0 || cnt > CAP - PCS_KNN_SLACK);
         if (nm) {
 #ifdef PCS_KNN_COUNT
             ++n_tiles_merging;
