@@ -22,6 +22,8 @@
 
 namespace pcs {
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
 template <int CTRL>
 __device__ __forceinline__ unsigned dpp_u(unsigned v) {
     return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
@@ -101,7 +103,12 @@ __global__ __launch_bounds__(BLOCK) void fps_kernel(const float* __restrict__ xy
     if (lds_cloud)
         for (int e = t; e < 3 * N; e += BLOCK) s_cloud[e] = P[e];
 
-    float px[PPT], py[PPT], pz[PPT], best[PPT];
+    // running minima as float BITS: the squared distances are >= +0 (never -0 or NaN), so
+    // unsigned min/max order them exactly like fminf/fmaxf, with no canonicalising op.
+    // Padding slots hold 0: never above a real point's value, and a pad's index (>= N)
+    // always loses the lowest-index tie break to a real point.
+    float px[PPT], py[PPT], pz[PPT];
+    unsigned best[PPT];
 #pragma unroll
     for (int j = 0; j < PPT; ++j) {
         const int p = j * BLOCK + t;
@@ -109,10 +116,10 @@ __global__ __launch_bounds__(BLOCK) void fps_kernel(const float* __restrict__ xy
             px[j] = P[3 * p + 0];
             py[j] = P[3 * p + 1];
             pz[j] = P[3 * p + 2];
-            best[j] = __int_as_float(0x7f800000);
+            best[j] = 0x7f800000u;
         } else {
             px[j] = py[j] = pz[j] = 0.f;
-            best[j] = -1.f;  // never a candidate: fminf(d >= 0, -1) keeps -1
+            best[j] = 0u;
         }
     }
 
@@ -140,16 +147,35 @@ __global__ __launch_bounds__(BLOCK) void fps_kernel(const float* __restrict__ xy
         }
         if (i == C - 1) break;
 
-        float M = -1.f;
+        unsigned M = 0u;
+#ifndef PCS_FPS_SCALAR
+        if constexpr (PPT % 2 == 0) {
+            // two points per packed op (v_pk_add/mul/fma_f32: per-component IEEE fp32, the
+            // same roundings as the scalar chain) -- half the VALU issues of the distances
+            const f32x2 c2x = {cx, cx}, c2y = {cy, cy}, c2z = {cz, cz};
 #pragma unroll
-        for (int j = 0; j < PPT; ++j) {
-            const float dx = px[j] - cx, dy = py[j] - cy, dz = pz[j] - cz;
-            const float d = __fmaf_rn(dz, dz, __fmaf_rn(dy, dy, __fmul_rn(dx, dx)));
-            best[j] = fminf(d, best[j]);                  // == (d < best ? d : best): no NaN, no -0 here
-            M = fmaxf(M, best[j]);
+            for (int j = 0; j < PPT; j += 2) {
+                const f32x2 dx = f32x2{px[j], px[j + 1]} - c2x;
+                const f32x2 dy = f32x2{py[j], py[j + 1]} - c2y;
+                const f32x2 dz = f32x2{pz[j], pz[j + 1]} - c2z;
+                const f32x2 d = __builtin_elementwise_fma(dz, dz, __builtin_elementwise_fma(dy, dy, dx * dx));
+                best[j] = min(__float_as_uint(d.x), best[j]);
+                best[j + 1] = min(__float_as_uint(d.y), best[j + 1]);
+                M = max(M, max(best[j], best[j + 1]));
+            }
+        } else
+#endif
+        {
+#pragma unroll
+            for (int j = 0; j < PPT; ++j) {
+                const float dx = px[j] - cx, dy = py[j] - cy, dz = pz[j] - cz;
+                const float d = __fmaf_rn(dz, dz, __fmaf_rn(dy, dy, __fmul_rn(dx, dx)));
+                best[j] = min(__float_as_uint(d), best[j]);   // == (d < best ? d : best)
+                M = max(M, best[j]);
+            }
         }
         FPS_STAMP(1);
-        const unsigned wk = wave_umax(M >= 0.f ? __float_as_uint(M) + 1u : 0u);
+        const unsigned wk = wave_umax(M + 1u);
         FPS_STAMP(2);
         const int buf = i & 1;
         if (wk != 0) {
@@ -170,7 +196,7 @@ __global__ __launch_bounds__(BLOCK) void fps_kernel(const float* __restrict__ xy
             unsigned cand = 0xFFFFFFFFu;
 #pragma unroll
             for (int j = PPT - 1; j >= 0; --j)
-                cand = best[j] >= lo ? (unsigned)(j * BLOCK + t) : cand;
+                cand = best[j] >= __float_as_uint(lo) ? (unsigned)(j * BLOCK + t) : cand;
             FPS_STAMP(3);
             const unsigned widx = wave_umin(cand);
             FPS_STAMP(4);
