@@ -31,6 +31,8 @@ namespace pcs {
 
 constexpr unsigned kInfBits = 0x7f800000u;
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
 struct Geo {
     const float* cent;  // (B, R, 3) query / centroid coordinates
     const float* xyz;   // (B, N, 3) candidate coordinates
@@ -432,7 +434,21 @@ __global__ __launch_bounds__(256) void three_nn_kernel(Geo g) {
         const int i = h.i0;
         adjust3(h, v, i);
     }
-    for (int m = 3; m < M; ++m) {
+    // candidates in pairs on packed fp32 ops (v_pk_add/mul_f32, no contraction): the same
+    // un-fused ((dx*dx + dy*dy) + dz*dz) roundings per component, half the VALU issues;
+    // the heap still takes them one at a time, in index order
+    const f32x2 q2x = {qx, qx}, q2y = {qy, qy}, q2z = {qz, qz};
+    int m = 3;
+    for (; m + 2 <= M; m += 2) {
+        const float* p = P + 3 * m;
+        const f32x2 dx = f32x2{p[0], p[3]} - q2x;
+        const f32x2 dy = f32x2{p[1], p[4]} - q2y;
+        const f32x2 dz = f32x2{p[2], p[5]} - q2z;
+        const f32x2 d = (dx * dx + dy * dy) + dz * dz;
+        if (d.x < h.v0) adjust3(h, d.x, m);
+        if (d.y < h.v0) adjust3(h, d.y, m + 1);
+    }
+    for (; m < M; ++m) {
         const float d = sqdist_unfused(P[3 * m], P[3 * m + 1], P[3 * m + 2], qx, qy, qz);
         if (d < h.v0) adjust3(h, d, m);
     }
