@@ -818,9 +818,8 @@ using namespace pcs;
 
 // row-GEMM tile (BM x BN) for M rows and N outputs: the largest tile that still
 // gives >= 2 blocks per CU (256 CUs), else the one with the most blocks
-// bwd: the A operand is a rebuilt dZ (BNBWD / POOLBWD, the data-gradient GEMM): its heavier
-// operand transform and BN-backward epilogue run out of registers on 128 x 128 tiles, so it
-// uses the <= 64-wide tile list for every N
+// bwd: the A operand is a rebuilt dZ (BNBWD / POOLBWD, the data-gradient GEMM), with a
+// heavier operand transform and BN-backward epilogue; its tile policy is below
 static void gemm_tile(int M, int N, bool bwd, int* bm, int* bn) {
     // PCS_GEMM_TILE=bm,bn forces one tile shape (tuning sweeps; must be a built variant)
     static const int forced = [] {
@@ -832,9 +831,32 @@ static void gemm_tile(int M, int N, bool bwd, int* bm, int* bn) {
     struct T { int bm, bn; };
     static const T big[] = {{128, 128}, {64, 128}, {64, 64}, {32, 128}};
     static const T mid[] = {{128, 64}, {64, 64}};
-    static const bool dgrad_wide = [] { const char* e = getenv("PCS_DGRAD_WIDE"); return e && atoi(e); }();
-    const bool wide = N > 64 && (!bwd || dgrad_wide);      // PCS_DGRAD_WIDE=1: A/B against wide dgrad tiles
-    const T* c = wide ? big : mid;
+    static const T mid64[] = {{64, 64}, {128, 64}};
+    // Data-gradient tiles by regime (same-box A/B, scripts/gpu_dgrad_ab.sh): the thin,
+    // HBM-latency-bound layers (PointNet++, EdgeConv) run best on 64 x 64 tiles (4 blocks per
+    // CU, more loads in flight: PointNet++ step -1 %); the big MFMA-bound ones (DGCNN
+    // conv5-7: N >= 256 over >= 64K rows) on the wide list despite its register pressure
+    // (DGCNN step -2 %).  PCS_DGRAD_TILES = legacy | small | wide forces one policy (A/B).
+    static const int dgrad_policy = [] {
+        const char* e = getenv("PCS_DGRAD_TILES");
+        if (!e) return 0;
+        return !strcmp(e, "legacy") ? 1 : (!strcmp(e, "small") ? 2 : (!strcmp(e, "wide") ? 3 : 0));
+    }();
+    bool wide;
+    const T* c;
+    if (!bwd) {
+        wide = N > 64;
+        c = wide ? big : mid;
+    } else if (dgrad_policy == 1) {
+        wide = false;
+        c = mid;
+    } else if (dgrad_policy == 2) {
+        wide = false;
+        c = mid64;
+    } else {
+        wide = N > 64 && (dgrad_policy == 3 || (N >= 256 && M >= 65536));
+        c = wide ? big : mid64;
+    }
     const int nc = wide ? 4 : 2;
     if (N <= 32) { *bm = 128; *bn = 32; return; }
     long long best = -1;

@@ -75,13 +75,18 @@ class Xform:
             kk = (r % self.pool_k).to(torch.uint8)
             d = torch.where(self.arg[gsel, :K] == kk[:, None], d[gsel], torch.zeros_like(d[gsel]))
         z = self.z.double()[:, :K]
-        dy = d * dact(z * s + t, self.slope)
+        # the activation-derivative branch is decided on the fp32 pre-activation, as the kernel
+        # (and the reference's fp32 autograd) does: at large M * K a few z*s+t sit within fp32
+        # rounding of 0, and an fp64 decision there flips dact between 1 and the slope
+        pre32 = (self.z[:, :K] * self.s + self.t).double()
+        dy = d * dact(pre32, self.slope)
         return s * dy - self.kb.double() - self.alpha.double() * (z - self.mean.double())
 
 
 SHAPES = [  # M, K, N
     (1000, 9, 32), (4099, 32, 64), (2048, 67, 64), (3000, 128, 128), (515, 259, 256), (777, 384, 512),
     (128, 1408, 96), (64, 20, 36), (131073, 32, 64), (70001, 128, 128), (300000, 12, 32),
+    (65537, 384, 256),   # data-gradient modes: the wide-tile regime (N >= 256 over >= 64K rows)
 ]
 
 
@@ -138,6 +143,7 @@ def test_gemm_rows_vs_fp64(impl, M, K, N, mode):
 KSHAPES = [  # M, K (= cout of the layer), N (= its cin): the data-gradient GEMM on k-major W
     (1000, 32, 12), (4099, 64, 32), (3000, 128, 128), (515, 256, 260), (777, 512, 384), (64, 36, 20),
     (70001, 128, 128), (2000, 13, 128), (300000, 32, 12),
+    (65536, 512, 384), (66001, 256, 260),   # wide-tile regime (DGCNN conv5-7 shapes)
 ]
 
 
