@@ -1035,7 +1035,11 @@ PCS_API int pcs_wgrad(const pcs_operand* x, int N, const pcs_operand* y, int K, 
         return launch_status("pcs_wgrad");
     }
     const int tiles = ((N + BO - 1) / BO) * ((K + BI - 1) / BI);
-    static const int target = [] { const char* e = getenv("PCS_WGRAD_BLOCKS"); return e ? atoi(e) : 1024; }();
+    // row splits: ~1024 blocks, 2048 for the big MFMA-bound contractions (>= 16 GFLOP, e.g.
+    // DGCNN conv5-7: step -1 %; the small overlapped PointNet++ wgrads gain nothing from more);
+    // PCS_WGRAD_BLOCKS forces a target (A/B, scripts/gpu_wgrad_blocks_ab.sh)
+    static const int forced_target = [] { const char* e = getenv("PCS_WGRAD_BLOCKS"); return e ? atoi(e) : 0; }();
+    const int target = forced_target > 0 ? forced_target : (2.0 * M * N * K >= 1.6e10 ? 2048 : 1024);
     int splits = (target + tiles - 1) / tiles;
     int rows = (M + splits - 1) / splits;
     rows = ((rows + 255) / 256) * 256;
