@@ -471,7 +471,17 @@ __global__ __launch_bounds__(256, 2) void knn_tile_kernel(const float* __restric
         const int nlr = (int)readlane_u((unsigned)nl, r);
         const int q = q0 + wrow0 + r;
         int* o = q < N ? out_idx + ((size_t)b * N + q) * K : nullptr;
-        if (o) knn_merge_row<K, SEG>(wl + r * KNN_RS, nlr, c0n, c1n, l, o);
+        if (!o) continue;
+#ifndef PCS_KNN_RANKALL
+        if (nlr + c0n + c1n > K) {
+            // quickselect the k best into the list first, then rank only those k
+            // (k readlane rounds per row instead of up to nl + c0 + c1)
+            knn_select_row<K, SEG>(wl + r * KNN_RS, nlr, c0n, c1n, l);
+            knn_merge_row<K, SEG>(wl + r * KNN_RS, K, 0, 0, l, o);
+            continue;
+        }
+#endif
+        knn_merge_row<K, SEG>(wl + r * KNN_RS, nlr, c0n, c1n, l, o);
     }
 }
 
