@@ -58,9 +58,21 @@ static void probe_clear() {
     g_probe.clear();
 }
 
+// one wave sleeps until `ticks` of the 100 MHz realtime counter have passed
+__global__ __launch_bounds__(64) void spin_kernel(unsigned long long ticks) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(100);
+}
+
 }  // namespace pcs
 
 using namespace pcs;
+
+PCS_API int pcs_spin(int us, void* stream) {
+    PCS_CHECK_ARG(us >= 0 && us <= 1000000, "pcs_spin: us=%d out of [0, 1e6]", us);
+    hipLaunchKernelGGL(spin_kernel, dim3(1), dim3(64), 0, as_stream(stream), (unsigned long long)us * 100ull);
+    return launch_status("pcs_spin");
+}
 
 PCS_API int pcs_probe_begin(void) {
     std::lock_guard<std::mutex> g(g_probe_mu);

@@ -130,6 +130,112 @@ class DeviceBlockStore:
         return pts, lab
 
 
+def _dist_rank_world(rank, world):
+    import torch.distributed as dist
+    if rank is None or world is None:
+        if dist.is_available() and dist.is_initialized():
+            return dist.get_rank(), dist.get_world_size()
+        return 0, 1
+    return rank, world
+
+
+class DistributedBlockSampler:
+    """Block ids for one rank of a data-parallel job (SURVEY.md section 8(e) "Partitioning").
+
+    Every epoch draws ONE permutation of all blocks from a generator seeded with
+    (seed + epoch) -- identical on every rank without communication -- pads it by
+    wrapping to a multiple of the world size (or drops the tail, `drop_last`) and
+    hands rank r the entries r, r + world, r + 2*world, ...  So the ranks' shards of
+    an epoch are disjoint and together cover every block (the reference's
+    DataLoader(shuffle=True) draws one uniform permutation per epoch for its single
+    process, block_datasets.py:166-173).  `shuffle=False` keeps the block order.
+    """
+
+    def __init__(self, num_blocks: int, rank: int | None = None, world: int | None = None, shuffle: bool = True,
+                 seed: int = 0, drop_last: bool = False):
+        self.n = int(num_blocks)
+        self.rank, self.world = _dist_rank_world(rank, world)
+        if not 0 <= self.rank < self.world:
+            raise ValueError(f'rank {self.rank} out of range for world size {self.world}')
+        self.shuffle, self.seed, self.drop_last = shuffle, int(seed), drop_last
+        self.epoch = 0
+        self.per_rank = self.n // self.world if drop_last else -(-self.n // self.world)
+
+    def set_epoch(self, epoch: int) -> None:
+        self.epoch = int(epoch)
+
+    def order(self) -> list[int]:
+        if self.shuffle:
+            g = torch.Generator().manual_seed(self.seed + self.epoch)
+            perm = torch.randperm(self.n, generator=g).tolist()
+        else:
+            perm = list(range(self.n))
+        total = self.per_rank * self.world
+        if total > self.n:                                  # wrap-pad so every rank gets per_rank blocks
+            perm = (perm * (-(-total // max(self.n, 1))))[:total]
+        return perm[:total]
+
+    def __iter__(self):
+        return iter(self.order()[self.rank::self.world])
+
+    def __len__(self) -> int:
+        return self.per_rank
+
+
+class DeviceBlockLoader:
+    """Batches of one rank's blocks from a `DeviceBlockStore`: (points (B, N, 9) f32, labels
+    (B, N, 14) u8, lengths (B,) uint64) on the device, as the reference's DataLoader with
+    `collate_blocks` yields them (block_datasets.py:166-181).  The row sampling of each
+    block draws from a per-rank device generator seeded with (seed, rank, epoch)."""
+
+    def __init__(self, store: DeviceBlockStore, batch_size: int, sampler: DistributedBlockSampler, seed: int = 0):
+        if batch_size < 1:
+            raise ValueError(f'batch_size must be >= 1, got {batch_size}')
+        self.store, self.batch_size, self.sampler, self.seed = store, int(batch_size), sampler, int(seed)
+
+    @property
+    def dataset(self):
+        return self.store
+
+    def set_epoch(self, epoch: int) -> None:
+        self.sampler.set_epoch(epoch)
+
+    def __len__(self) -> int:
+        return -(-len(self.sampler) // self.batch_size)
+
+    def __iter__(self):
+        ids = list(self.sampler)
+        gen = None
+        if self.store.sampling is not None:
+            gen = torch.Generator(device=self.store.device)
+            gen.manual_seed((self.seed * 1_000_003 + self.sampler.rank * 7_919 + self.sampler.epoch) & ((1 << 62) - 1))
+        for s in range(0, len(ids), self.batch_size):
+            yield self.store.batch(ids[s:s + self.batch_size], generator=gen)
+
+
+def create_block_dataloaders(data_dir: str, test_areas, train_batch_size: int = 4, test_batch_size: int = 4,
+                             num_workers: int = 4, train_sampling: int | None = 4096,
+                             test_sampling: int | None = None, train_shuffle: bool = True,
+                             test_shuffle: bool = False, device='cuda', seed: int = 0, rank: int | None = None,
+                             world: int | None = None):
+    """Reference `create_block_dataloaders` (block_datasets.py:133-183): same arguments and
+    area split (train = areas {1..6} minus `test_areas`), returning (train, test) loaders
+    whose blocks are resident in HBM (`DeviceBlockStore`) and whose batches are assembled
+    on the device.  `num_workers` is accepted for signature compatibility (no host workers
+    are needed).  Under torch.distributed (or explicit rank/world) each loader yields only
+    this rank's shard (`DistributedBlockSampler`)."""
+    del num_workers
+    areas = {1, 2, 3, 4, 5, 6}
+    test_areas = set(test_areas)
+    out = []
+    for inc, bs, samp, shuf in ((areas - test_areas, train_batch_size, train_sampling, train_shuffle),
+                                (test_areas, test_batch_size, test_sampling, test_shuffle)):
+        store = DeviceBlockStore(data_dir, inc, sampling=samp, device=device)
+        sampler = DistributedBlockSampler(len(store), rank, world, shuffle=shuf, seed=seed)
+        out.append(DeviceBlockLoader(store, bs, sampler, seed=seed))
+    return out[0], out[1]
+
+
 def preprocess_batch_to_train_format(x, y, mapping, cut=None, sampling=None, device=None):
     """Reference `preprocess_batch_to_train_format` (Training/train_model.py:89-171),
     harness B's batch builder: optional per-sample random subsampling, zero padding to

@@ -22,6 +22,7 @@ import struct
 import torch
 
 from ._lib import call, load, ptr, stream_ptr, Operand, OP_PLAIN, OP_BNACT, OP_BNBWD, OP_POOLBWD
+from .replay import record_pool_arg, record_act_mask, recording
 
 ACT = {'relu': 0, 'lrelu': 1, 'none': 2}
 
@@ -227,6 +228,18 @@ class SharedMLPFn(torch.autograd.Function):
         nws = _workspace(lib, key, M, Kin, ldx, recs, nl, pool_K, 0)
         ws = torch.empty((nws,), dtype=torch.uint8, device=dev)
         call('pcs_mlp_forward', ptr(X), ldx, Kin, M, recs, nl, pool_K, ptr(out), ptr(arg), ptr(ws), nws, st)
+        if arg is not None:
+            record_pool_arg(arg)
+        if recording():
+            # the kernels' activation decision y = z*s + t > 0 (unfused, as in the BNACT load,
+            # pool_finalize and bn_act), per layer in stack order (replay into the fp64 oracle)
+            off = 0
+            for li, C in enumerate(couts):
+                if acts[li][0] != ACT['none']:
+                    Z = Zbuf[M * off:M * (off + C)].view(M, C)
+                    cf = coef[4 * off:4 * off + 2 * C]
+                    record_act_mask(Z * cf[:C] + cf[C:] > 0)
+                off += C
         ctx.save_for_backward(X, Zbuf, coef, *Wms, *([arg] if arg is not None else []))
         ctx.meta = (Kin, pool_K, nl, fixed, couts, arg is not None)
         ctx.params = params
@@ -299,6 +312,9 @@ class EdgeConvFn(torch.autograd.Function):
              ptr(bn.running_mean) if track else None, ptr(bn.running_var) if track else None,
              ptr(bn.num_batches_tracked) if track else None, float(momentum), float(bn.eps), float(slope),
              ptr(Y), ptr(PQ), ptr(S), ptr(pz), ptr(pa), ptr(coef), ptr(out), ptr(arg), ptr(ws), ws.numel(), st)
+        record_pool_arg(arg)
+        if recording():
+            record_act_mask(out > 0)          # LeakyReLU keeps the sign: out > 0 <=> y > 0 at the argmax
         ctx.save_for_backward(X, idx, Wm, Y, PQ, S, pz, arg, coef)
         ctx.meta = (C, float(slope))
         ctx.params = (W, gamma, beta)

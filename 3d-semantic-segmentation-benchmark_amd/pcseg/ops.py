@@ -14,6 +14,7 @@ import torch
 
 from . import _lib
 from ._lib import call, ptr, stream_ptr, check_cuda
+from .replay import record_pool_arg
 
 
 def _c(t: torch.Tensor) -> torch.Tensor:
@@ -156,6 +157,7 @@ class MaxKFn(torch.autograd.Function):
         out = torch.empty((G, Ch), dtype=torch.float32, device=x.device)
         arg = torch.empty((G, Ch), dtype=torch.uint8, device=x.device)
         call('pcs_maxk_fwd', ptr(x), G, K, Ch, ptr(out), ptr(arg), stream_ptr(x.device))
+        record_pool_arg(arg)
         ctx.save_for_backward(arg)
         ctx.K = K
         ctx.mark_non_differentiable(arg)

@@ -22,6 +22,12 @@ class Replay:
         self.rec_group_idx: list[torch.Tensor] = []
         self.rec_interp_idx: list[torch.Tensor] = []
         self.rec_knn_idx: list[torch.Tensor] = []
+        # max-pool argmax decisions (SA / InvResMLP / EdgeConv pools), forward order, (groups, channels)
+        # uint8 -- the parity tests replay them into the fp64 oracle so a near-tie decided one way
+        # here is evaluated the same way there
+        self.rec_pool_arg: list[torch.Tensor] = []
+        # sign decisions (y > 0) of every engine ReLU / LeakyReLU, (rows, channels) bool, forward order
+        self.rec_act_mask: list[torch.Tensor] = []
 
 
 _ACTIVE: list[Replay] = []
@@ -38,3 +44,19 @@ def replay(rp: Replay):
 
 def active() -> Replay | None:
     return _ACTIVE[-1] if _ACTIVE else None
+
+
+def record_pool_arg(arg: torch.Tensor) -> None:
+    rp = active()
+    if rp is not None:
+        rp.rec_pool_arg.append(arg.detach().cpu())
+
+
+def recording() -> bool:
+    return active() is not None
+
+
+def record_act_mask(mask: torch.Tensor) -> None:
+    rp = active()
+    if rp is not None:
+        rp.rec_act_mask.append(mask.detach().cpu())

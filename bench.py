@@ -2,24 +2,35 @@
 """Throughput bench: points/s of one training step (forward + masked one-hot CE +
 backward + gradient all-reduce + Adam step) on 4096-point S3DIS-like blocks.
 
-Workload at N=1 (BASELINE.json configs[1]): PointNet++ SSG, batch 32 per GPU,
-4096 points, fp32, synthetic blocks resident in HBM before timing starts.
-Multi-GPU: one process per GPU (torchrun), data-parallel, RCCL all-reduce of the
-flat gradient buffer, fixed per-GPU batch ("weak" scaling).
+Headline (BASELINE.json metric "points/sec fwd+bwd, 4096-pt S3DIS blocks,
+PointNet++/DGCNN @1/2/4/8 GPU"): `value` is PointNet++ SSG, batch 32 per GPU,
+4096 points (configs[1]); the same JSON line carries the DGCNN EdgeConv half of the
+metric (configs[2]: DGCNN-colour k=20, batch 32 per GPU) as `secondary`, timed the
+same way in the same process.  fp32, synthetic blocks resident in HBM before timing.
 
-Also reported on the same JSON line:
-  roofline      -- the dominant HIP kernel (the engine GEMM variant with the
-                   largest time per step): its algorithmic flops / its launch
-                   time (HIP events on its stream) vs the fp32 MFMA peak;
-  cpu_baseline  -- the CPU oracle (oracle/ref_ops.py, the reference algorithm
-                   restated on PyTorch-CPU) on a bounded sample of the same
-                   workload, in a subprocess with no GPU visible, rank 0 only.
+Multi-GPU: one process per GPU, data-parallel, RCCL all-reduce of the flat gradient
+buffer, fixed per-GPU batch ("weak" scaling).  `--gpus N` either runs under an
+external launcher (torchrun sets WORLD_SIZE, which must equal N) or, without one,
+spawns the N rank processes itself before touching the GPU.
+
+Also reported on the same JSON line, per workload:
+  roofline      -- the dominant HIP kernel (the engine GEMM variant with the largest
+                   time in one probed step): its algorithmic flops and bytes per launch
+                   over its IN-STEP launch time (HIP events on the stream it runs on,
+                   the step enqueued behind a spin so the GPU runs it back to back as
+                   in a GPU-bound step), against the fp32 MFMA peak or the HBM peak by
+                   its arithmetic intensity;
+  cpu_baseline  -- the CPU oracle (oracle/ref_ops.py, the reference algorithm restated
+                   on PyTorch-CPU) on the same batch size, median step time, in a
+                   subprocess with no GPU visible, rank 0 at N=1 only.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import statistics
 import subprocess
 import sys
 import time
@@ -30,18 +41,26 @@ for _p in (REPO, PKG_ROOT):
     if _p not in sys.path:
         sys.path.insert(0, _p)
 
-MODELS = {
-    'pointnetpp': ('PointNetpp', lambda m: m.PointNetpp(14), 'points'),
-    'pointnetpp_msg': ('PointNetppMSG', lambda m: m.PointNetppMSG(14), 'points'),
-    'pointnext': ('PointNeXt', lambda m: m.PointNeXt(14), 'points'),
-    'dgcnn': ('DGCNNWithColor', lambda m: m.DGCNNWithColor(num_classes=14, k=20), 'chfirst6'),
-    'pointnet': ('PointNetSeg', lambda m: m.PointNetSeg(part_classes=14), 'points'),
+# key: (class name, ctor, input kind, default per-GPU batch, default points, BASELINE config)
+WORKLOADS = {
+    'pointnetpp': ('PointNetpp', lambda m: m.PointNetpp(14), 'points', 32, 4096,
+                   'configs[1] PointNet++ SSG seg, 4096 pts, batch 32/GPU'),
+    'dgcnn': ('DGCNNWithColor', lambda m: m.DGCNNWithColor(num_classes=14, k=20), 'chfirst6', 32, 4096,
+              'configs[2] DGCNN EdgeConv seg (colour), 4096 pts, k=20, batch 32/GPU'),
+    'pointnetpp_msg': ('PointNetppMSG', lambda m: m.PointNetppMSG(14), 'points', 32, 4096,
+                       'configs[3] PointNet++ MSG seg, 4096 pts, batch 32/GPU (256 on 8 GPUs)'),
+    'pointnext': ('PointNeXt', lambda m: m.PointNeXt(14), 'points', 16, 24576,
+                  'configs[4] PointNeXt-B seg, 24576 pts, batch 16/GPU (128 on 8 GPUs)'),
+    'pointnet': ('PointNetSeg', lambda m: m.PointNetSeg(part_classes=14), 'points', 32, 4096,
+                 'PointNet seg, 4096 pts, batch 32/GPU (configs[0] model on the GPU)'),
 }
+METRIC = 'points/sec fwd+bwd, 4096-pt S3DIS blocks, PointNet++/DGCNN @1/2/4/8 GPU'
 HBM_PEAK_GBS = 8000.0           # MI355X HBM3E spec (MI355X_MICROARCH.md)
+FP32_PEAK_TFLOPS = 157.3        # fp32 MFMA dense (= fp32 vector) peak
+RIDGE = FP32_PEAK_TFLOPS * 1e12 / (HBM_PEAK_GBS * 1e9)     # flop / byte
 # reference-algorithm fwd+bwd GFLOP per sample (FlopCounterMode on the reference)
 ALGO_GFLOP_PER_SAMPLE = {('pointnetpp', 4096): 5.786, ('pointnext', 4096): 10.791, ('pointnext', 24576): 19.592,
                          ('dgcnn', 4096): 53.468, ('pointnet', 4096): 24.635}
-FP32_PEAK_TFLOPS = 157.3
 
 
 def model_input(pts, kind):
@@ -54,13 +73,29 @@ def logits_of(out):
     return out[0] if isinstance(out, tuple) else out
 
 
+def host_cpu_info():
+    """(threads this process may use, physical cores of the host from sysfs or None)."""
+    aff = len(os.sched_getaffinity(0))
+    phys = set()
+    try:
+        base = '/sys/devices/system/cpu'
+        for d in os.listdir(base):
+            p = os.path.join(base, d, 'topology', 'core_id')
+            if d.startswith('cpu') and d[3:].isdigit() and os.path.exists(p):
+                pkg = open(os.path.join(base, d, 'topology', 'physical_package_id')).read().strip()
+                phys.add((pkg, open(p).read().strip()))
+    except OSError:
+        phys = set()
+    return aff, (len(phys) or None)
+
+
 # ----------------------------------------------------------------------------- CPU baseline worker
 def cpu_baseline_worker(args):
     import torch
     from oracle import ref_ops as R
     from pcseg.synthetic import make_batch
     torch.set_num_threads(args.cpu_threads)
-    name, ctor, kind = MODELS[args.model]
+    name, ctor, kind, _, _, _ = WORKLOADS[args.model]
     model = R.seeded_init_(ctor(R), 0)
     model.train()
     opt = torch.optim.Adam(model.parameters(), lr=1e-3)
@@ -73,42 +108,48 @@ def cpu_baseline_worker(args):
         loss = R.masked_onehot_cross_entropy(logits_of(model(x)), lab, lengths)
         loss.backward()
         opt.step()
+    t0 = time.perf_counter()
     step()
+    warm = time.perf_counter() - t0
+    # timed steps: as many as fit in ~cpu_budget seconds (at least 2)
+    n = max(2, min(args.cpu_steps, int(args.cpu_budget / max(warm, 1e-3))))
     times = []
-    for _ in range(args.cpu_steps):
+    for _ in range(n):
         t0 = time.perf_counter()
         step()
         times.append(time.perf_counter() - t0)
-    best = min(times)
-    print(json.dumps({'value': args.cpu_batch * args.npoints / best, 'unit': 'points/s',
+    med = statistics.median(times)
+    print(json.dumps({'value': args.cpu_batch * args.npoints / med, 'unit': 'points/s',
                       'cores': torch.get_num_threads(), 'kind': 'port',
-                      'sample': f'{name} oracle (PyTorch-CPU restatement of the reference), batch {args.cpu_batch} x '
-                                f'{args.npoints} pts, 1 warm-up + best of {args.cpu_steps} steps '
-                                f'(fwd+CE+bwd+Adam), {sum(times):.1f} s timed'}))
+                      'sample': f'{name} oracle (PyTorch-CPU restatement of the reference, fp32), batch '
+                                f'{args.cpu_batch} x {args.npoints} pts, fwd+CE+bwd+Adam, 1 warm-up + median of '
+                                f'{n} steps ({sum(times):.1f} s timed)'}))
 
 
-def run_cpu_baseline(args):
-    env = dict(os.environ)
-    env['HIP_VISIBLE_DEVICES'] = ''
-    env['CUDA_VISIBLE_DEVICES'] = ''
-    threads = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
-    env['OMP_NUM_THREADS'] = str(threads)
-    cmd = [sys.executable, os.path.abspath(__file__), '--cpu-baseline-worker', '--model', args.model,
-           '--npoints', str(args.npoints), '--cpu-batch', str(args.cpu_batch), '--cpu-steps', str(args.cpu_steps),
-           '--cpu-threads', str(threads)]
+def run_cpu_baseline(args, key, batch, npoints):
+    aff, phys = host_cpu_info()
+    # the box's CPU share for one GPU is 16 threads (OMP_NUM_THREADS there); nproc shows the whole host
+    threads = args.cpu_threads or min(aff, int(os.environ.get('OMP_NUM_THREADS', '16') or 16), 16)
+    env = dict(os.environ, HIP_VISIBLE_DEVICES='', CUDA_VISIBLE_DEVICES='', OMP_NUM_THREADS=str(threads))
+    cmd = [sys.executable, os.path.abspath(__file__), '--cpu-baseline-worker', '--model', key,
+           '--npoints', str(npoints), '--cpu-batch', str(args.cpu_batch or batch), '--cpu-steps',
+           str(args.cpu_steps), '--cpu-threads', str(threads), '--cpu-budget', str(args.cpu_budget)]
     try:
         out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=900, check=True).stdout
-        return json.loads(out.strip().splitlines()[-1])
+        res = json.loads(out.strip().splitlines()[-1])
     except Exception as e:  # noqa: BLE001 -- the baseline is informative, never fatal
-        return {'value': None, 'unit': 'points/s', 'cores': threads, 'kind': 'port', 'sample': f'failed: {e}'}
+        res = {'value': None, 'unit': 'points/s', 'cores': threads, 'kind': 'port', 'sample': f'failed: {e}'}
+    res['host_cpus_visible'] = aff
+    res['host_physical_cores'] = phys
+    return res
 
 
 # ----------------------------------------------------------------------------- roofline of the dominant kernel
-def pmc_traffic(kernel, args):
+def pmc_traffic(kernel, key, batch, npoints):
     """HBM bytes per launch of `kernel` from the committed PMC summary of this workload
-    (scripts/gpu_pmc.sh -> profiles/<round>_pmc_<model>.json; FETCH_SIZE x2 + WRITE_SIZE)."""
+    (scripts/gpu_pmc.sh -> profiles/<round>_pmc_<model>_b<B>_n<N>.json; FETCH_SIZE x2 + WRITE_SIZE)."""
     import glob
-    files = sorted(glob.glob(os.path.join(REPO, 'profiles', f'*_pmc_{args.model}_b{args.batch}_n{args.npoints}.json')))
+    files = sorted(glob.glob(os.path.join(REPO, 'profiles', f'*_pmc_{key}_b{batch}_n{npoints}.json')))
     if not files:
         return None, None
     table = json.load(open(files[-1]))
@@ -118,95 +159,67 @@ def pmc_traffic(kernel, args):
     return None, None
 
 
-def kernel_roofline(step, dev, args):
-    """Run one more training step with every engine GEMM launch recorded by the
-    library's launch probe (pcseg.engine.KernelProbe); the dominant kernel is the
-    variant with the largest summed time in that step.  Its recorded launches are
-    then re-issued back to back (pcs_probe_replay, HIP events on the stream they run
-    on) for the average launch duration -- the figure rocprofv3 --stats reports as
-    AverageNs.  achieved = its algorithmic flops (2*M*K*N per launch) / that duration,
-    vs the fp32 MFMA peak."""
+def kernel_roofline(step, dev, key, batch, npoints, replay=False):
+    """One more training step with every engine GEMM launch bracketed by HIP events on its
+    stream (pcseg.engine.KernelProbe).  The step is enqueued behind a 50 ms spin on the main
+    stream, so the GPU runs the whole step back to back (as it does in the GPU-bound timed
+    loop) and the event pairs time the kernels, not host-enqueue gaps.  The dominant kernel
+    is the variant with the largest summed in-step time; `achieved` = its algorithmic flops
+    (2*M*K*N per launch) or bytes over that in-step time."""
     import torch
     from pcseg.engine import KernelProbe
+    from pcseg._lib import call, stream_ptr
     torch.cuda.synchronize(dev)
+    call('pcs_spin', 50000, stream_ptr(dev))
     with KernelProbe() as kp:
         step()
     summ = kp.summary()
     torch.cuda.synchronize(dev)
-    name, (n, fl, by, sec_ev) = max(summ.items(), key=lambda kv: kv[1][3])
-    sec = kp.replay(name, reps=20) * n
-    tf = fl / sec / 1e12
-    traffic, src = pmc_traffic(name, args)
+    name, (n, fl, by, sec) = max(summ.items(), key=lambda kv: kv[1][3])
+    intensity = fl / by
+    bound = 'mfma' if intensity >= RIDGE else 'hbm'
+    tf, gbs = fl / sec / 1e12, by / sec / 1e9
+    achieved, peak, unit = (tf, FP32_PEAK_TFLOPS, 'TFLOP/s') if bound == 'mfma' else (gbs, HBM_PEAK_GBS, 'GB/s')
+    traffic, src = pmc_traffic(name, key, batch, npoints)
     all_fl = sum(v[1] for v in summ.values())
     all_sec = sum(v[3] for v in summ.values())
-    return {'kernel': name, 'bound': 'mfma', 'achieved': round(tf, 2), 'peak': FP32_PEAK_TFLOPS, 'unit': 'TFLOP/s',
-            'frac': round(tf / FP32_PEAK_TFLOPS, 4), 'traffic': traffic, 'traffic_unit': 'bytes/launch',
-            'traffic_source': src,
-            'launches_per_step': n, 'avg_launch_us': round(sec / n * 1e6, 2),
-            'avg_launch_us_in_step_events': round(sec_ev / n * 1e6, 2),
-            'algo_flops_per_launch': round(fl / n), 'algo_bytes_per_launch': round(by / n),
-            'achieved_hbm_gbs': round(by / sec / 1e9, 1),
-            'all_engine_gemms_in_step_events': {'tflops': round(all_fl / all_sec / 1e12, 2),
-                                                'ms_per_step': round(all_sec * 1e3, 3),
-                                                'launches': sum(v[0] for v in summ.values())}}
+    out = {'kernel': name, 'bound': bound, 'achieved': round(achieved, 2), 'peak': peak, 'unit': unit,
+           'frac': round(achieved / peak, 4), 'traffic': traffic, 'traffic_unit': 'bytes/launch',
+           'traffic_source': src, 'launches_per_step': n, 'avg_launch_us': round(sec / n * 1e6, 2),
+           'timing': 'in-step HIP events, step enqueued behind a spin (no host gaps)',
+           'algo_flops_per_launch': round(fl / n), 'algo_bytes_per_launch': round(by / n),
+           'arith_intensity_flop_per_byte': round(intensity, 2),
+           'achieved_tflops': round(tf, 2), 'frac_of_fp32_mfma_peak': round(tf / FP32_PEAK_TFLOPS, 4),
+           'achieved_hbm_gbs': round(gbs, 1), 'frac_of_hbm_peak': round(gbs / HBM_PEAK_GBS, 4),
+           'all_engine_gemms_in_step': {'tflops': round(all_fl / all_sec / 1e12, 2),
+                                        'ms_per_step': round(all_sec * 1e3, 3),
+                                        'launches': sum(v[0] for v in summ.values())}}
+    if replay:      # isolated back-to-back replay of the recorded launches (rewrites outputs: last)
+        rs = kp.replay(name, reps=20)
+        out['isolated_replay'] = {'avg_launch_us': round(rs * 1e6, 2), 'tflops': round(fl / n / rs / 1e12, 2)}
+    return out
 
 
-def step_roofline(args, ms):
+def step_roofline(key, npoints, batch, ms):
     """Whole-step fraction of the fp32 MFMA roofline with the reference algorithm's flop count."""
-    gf = ALGO_GFLOP_PER_SAMPLE.get((args.model, args.npoints))
+    gf = ALGO_GFLOP_PER_SAMPLE.get((key, npoints))
     if gf is None:
         return None
-    tf = gf * args.batch / (ms * 1e-3) / 1e3
+    tf = gf * batch / (ms * 1e-3) / 1e3
     return {'algo_gflop_per_sample': gf, 'achieved_tflops_per_gpu': round(tf, 2),
             'frac_of_fp32_peak': round(tf / FP32_PEAK_TFLOPS, 4)}
 
 
-# ----------------------------------------------------------------------------- main bench
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=20)
-    ap.add_argument('--warmup', type=int, default=5)
-    ap.add_argument('--model', default='pointnetpp', choices=sorted(MODELS))
-    ap.add_argument('--batch', type=int, default=32, help='per-GPU batch')
-    ap.add_argument('--npoints', type=int, default=4096)
-    ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--cpu-batch', type=int, default=8)
-    ap.add_argument('--cpu-steps', type=int, default=10)
-    ap.add_argument('--cpu-threads', type=int, default=0)
-    ap.add_argument('--cpu-baseline-worker', action='store_true')
-    ap.add_argument('--no-roofline', action='store_true')
-    ap.add_argument('--graph', action='store_true',
-                    help='capture one training step in a HIP graph and time its replays (N=1, no prefetch)')
-    ap.add_argument('--prefetch-point', default='loss', choices=['loss', 'backward'],
-                    help='where the next batch\'s geometry plan is enqueued')
-    ap.add_argument('--no-prefetch', action='store_true',
-                    help='do not enqueue the next step\'s FPS/ball-query/3-NN before this step\'s backward')
-    args = ap.parse_args()
-    if args.cpu_baseline_worker:
-        cpu_baseline_worker(args)
-        return
-
+# ----------------------------------------------------------------------------- one workload
+def run_workload(key, batch, npoints, args, world, rank, dev):
     import torch
     import torch.distributed as dist
-    world = int(os.environ.get('WORLD_SIZE', '1'))
-    rank = int(os.environ.get('RANK', '0'))
-    local = int(os.environ.get('LOCAL_RANK', '0'))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
-    dev = torch.device('cuda', local)
-
-    cpu_res = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu_res = run_cpu_baseline(args)     # before the GPU run: the host is otherwise idle
-
     import pcseg
     from pcseg.ddp import FlatGradAllReduce, broadcast_model
     from pcseg.optim import FlatAdam
     from pcseg.synthetic import make_batch
 
-    name, ctor, kind = MODELS[args.model]
+    name, ctor, kind, _, _, cfg = WORKLOADS[key]
     torch.manual_seed(0)
     model = ctor(pcseg).to(dev).train()     # PyTorch default init (random weights)
     broadcast_model(model)
@@ -216,32 +229,26 @@ def main():
         opt = torch.optim.Adam(model.parameters(), lr=1e-3, capturable=True)
     else:              # one HIP launch over the flat parameter / gradient buffers
         opt = FlatAdam(grads, lr=1e-3)
-    pts, labels, lengths = make_batch(args.batch, args.npoints, seed=1000 * 2 + rank)
+    pts, labels, lengths = make_batch(batch, npoints, seed=1000 * 2 + rank)
     x = model_input(pts.to(dev), kind)
     lab = (labels.float() if kind == 'chfirst6' else labels).to(dev)
     lengths = lengths.to(dev)
-
     prefetch = hasattr(model, 'prefetch_geometry') and not args.no_prefetch and not use_graph
 
     def step():
         grads.zero_grad()
         loss = pcseg.masked_onehot_cross_entropy(logits_of(model(x)), lab, lengths)
-        if prefetch and args.prefetch_point == 'loss':
+        if prefetch:
             # pipelined input: the next batch's neighbour search (here the same resident
             # blocks, fresh FPS starts) runs on the side stream under this backward
             model.prefetch_geometry(x)
         loss.backward()
-        if prefetch and args.prefetch_point == 'backward':
-            # same, planned once the backward is enqueued: the host work of the plan
-            # overlaps the queued backward instead of delaying its first launch
-            model.prefetch_geometry(x)
         grads.synchronize()
         opt.step()
         return loss
 
     eager_step = step
     if use_graph:
-        # warm up on a side stream (allocator + lazy init outside capture), then capture one step
         side = torch.cuda.Stream(dev)
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):
@@ -273,32 +280,138 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t)
     if not torch.isfinite(loss):
-        raise RuntimeError('non-finite loss')
+        raise RuntimeError(f'{name}: non-finite loss')
     roof = None
     if not args.no_roofline:
-        roof = kernel_roofline(eager_step, dev, args)     # every rank runs the step (collectives), rank 0 reports
+        roof = kernel_roofline(eager_step, dev, key, batch, npoints, replay=args.roofline_replay)
+    ms = dt / args.steps * 1e3
+    res = {'value': round(world * batch * npoints * args.steps / dt, 1), 'unit': 'points/s',
+           'ms_per_step': round(ms, 3),
+           'config': {'workload': f'{name} seg, {npoints} pts, batch {batch}/GPU, fwd+CE+bwd'
+                                  f'{"+allreduce" if world > 1 else ""}+Adam',
+                      'baseline_config': cfg, 'model': name, 'global_batch': world * batch, 'npoints': npoints,
+                      'parallelism': f'dp{world}', 'geometry_prefetch': prefetch, 'hip_graph': use_graph},
+           'host_enqueue_ms_per_step': round(t_host / args.steps * 1e3, 3),
+           'roofline': roof, 'step_roofline': step_roofline(key, npoints, batch, ms)}
+    del model, grads, opt
+    torch.cuda.empty_cache()
+    return res
+
+
+# ----------------------------------------------------------------------------- launcher
+def _free_port():
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n):
+    """Start n rank processes of this script (torchrun-style env), before this process has
+    touched the GPU; exit with the worst return code."""
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR='127.0.0.1', MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rcs = [p.wait() for p in procs]
+    return max(rcs, key=abs)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--warmup', type=int, default=5)
+    ap.add_argument('--model', default='pointnetpp', choices=sorted(WORKLOADS))
+    ap.add_argument('--secondary', default='auto', help="second workload on the same line ('auto': dgcnn when "
+                                                        "--model is pointnetpp; 'none' to skip)")
+    ap.add_argument('--batch', type=int, default=0, help='per-GPU batch (default: the workload\'s)')
+    ap.add_argument('--npoints', type=int, default=0, help='points per block (default: the workload\'s)')
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--cpu-batch', type=int, default=0, help='CPU baseline batch (default: the GPU batch)')
+    ap.add_argument('--cpu-steps', type=int, default=5)
+    ap.add_argument('--cpu-budget', type=float, default=12.0, help='seconds of timed CPU steps per workload')
+    ap.add_argument('--cpu-threads', type=int, default=0)
+    ap.add_argument('--cpu-baseline-worker', action='store_true')
+    ap.add_argument('--no-roofline', action='store_true')
+    ap.add_argument('--roofline-replay', action='store_true',
+                    help='also time the dominant kernel\'s launches replayed back to back (rewrites outputs)')
+    ap.add_argument('--graph', action='store_true',
+                    help='capture one training step in a HIP graph and time its replays (N=1, no prefetch)')
+    ap.add_argument('--no-prefetch', action='store_true',
+                    help='do not enqueue the next step\'s FPS/ball-query/3-NN before this step\'s backward')
+    ap.add_argument('--check-launch', action='store_true',
+                    help='launcher self-test: each rank joins a gloo group, prints its env as JSON, exits (no GPU)')
+    args = ap.parse_args()
+    if args.cpu_baseline_worker:
+        cpu_baseline_worker(args)
+        return 0
+    if args.gpus < 1:
+        raise SystemExit('--gpus must be >= 1')
+    if 'WORLD_SIZE' not in os.environ and args.gpus > 1:
+        return spawn_ranks(args.gpus)
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world != args.gpus:
+        raise SystemExit(f'bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks')
+
+    import torch.distributed as dist
+    if args.check_launch:
+        dist.init_process_group('gloo', rank=rank, world_size=world)
+        print(json.dumps({'rank': rank, 'local_rank': local, 'world': dist.get_world_size(),
+                          'master': f"{os.environ.get('MASTER_ADDR')}:{os.environ.get('MASTER_PORT')}"}),
+              flush=True)
+        dist.barrier()
+        dist.destroy_process_group()
+        return 0
+
+    keys = [args.model]
+    sec = args.secondary
+    if sec == 'auto':
+        sec = 'dgcnn' if args.model == 'pointnetpp' else 'none'
+    if sec != 'none':
+        if sec not in WORKLOADS:
+            raise SystemExit(f'unknown --secondary {sec}')
+        keys.append(sec)
+    sizes = {k: (args.batch or WORKLOADS[k][3], args.npoints or WORKLOADS[k][4]) if k == args.model
+             else (WORKLOADS[k][3], WORKLOADS[k][4]) for k in keys}
+
+    cpu_res = {}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        for k in keys:                          # before the GPU run: the host is otherwise idle
+            cpu_res[k] = run_cpu_baseline(args, k, *sizes[k])
+
+    import torch
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        if dist.get_world_size() != args.gpus:
+            raise SystemExit(f'RCCL world {dist.get_world_size()} != --gpus {args.gpus}')
+    dev = torch.device('cuda', local)
+
+    results = {k: run_workload(k, *sizes[k], args, world, rank, dev) for k in keys}
     if rank == 0:
-        ms = dt / args.steps * 1e3
-        value = world * args.batch * args.npoints * args.steps / dt
-        res = {
-            'metric': 'points/sec fwd+bwd, 4096-pt S3DIS blocks, PointNet++/DGCNN @1/2/4/8 GPU',
-            'value': round(value, 1), 'unit': 'points/s', 'n_gpus': world, 'steps': args.steps,
-            'warmup': args.warmup, 'ms_per_step': round(ms, 3), 'higher_is_better': True, 'scaling': 'weak',
-            'vs_baseline': None, 'dtype': 'fp32', 'data': 'synthetic S3DIS-like blocks (pcseg.synthetic), '
-                                                          'random-init weights',
-            'config': {'workload': f'{name} seg, {args.npoints} pts, batch {args.batch}/GPU, fwd+CE+bwd'
-                                   f'{"+allreduce" if world > 1 else ""}+Adam',
-                       'model': name, 'global_batch': world * args.batch, 'npoints': args.npoints,
-                       'parallelism': f'dp{world}', 'geometry_prefetch': prefetch, 'hip_graph': use_graph},
-            'host_enqueue_ms_per_step': round(t_host / args.steps * 1e3, 3),
-            'roofline': roof,
-            'step_roofline': step_roofline(args, ms),
-            'cpu_baseline': cpu_res,
-        }
+        prim = results[args.model]
+        res = {'metric': METRIC, 'value': prim['value'], 'unit': 'points/s', 'n_gpus': world,
+               'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': prim['ms_per_step'],
+               'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'fp32',
+               'data': 'synthetic S3DIS-like blocks (pcseg.synthetic), random-init weights',
+               'config': dict(prim['config'], rccl_world=dist.get_world_size() if world > 1 else 1),
+               'host_enqueue_ms_per_step': prim['host_enqueue_ms_per_step'],
+               'roofline': prim['roofline'], 'step_roofline': prim['step_roofline'],
+               'cpu_baseline': cpu_res.get(args.model)}
+        for k in keys[1:]:
+            r = results[k]
+            r['cpu_baseline'] = cpu_res.get(k)
+            r['metric'] = METRIC
+            res['secondary'] = dict(r, n_gpus=world, dtype='fp32')
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == '__main__':
-    main()
+    sys.exit(main())

@@ -298,6 +298,11 @@ int pcs_probe_get(int i, char* name, int cap, double* flops, double* bytes,
  * the average microseconds per launch -- comparable with rocprofv3's AverageNs for
  * that kernel.  The launches rewrite their outputs. */
 int pcs_probe_replay(const char* name, int reps, float* us_per_launch, int* launches);
+/* Occupy `stream` for about `us` microseconds (one wave sleeping on the realtime
+ * clock), so the host can enqueue a whole probed step before the GPU reaches it: the
+ * probe's event brackets then time the kernels back to back, as they run in a
+ * GPU-bound step, without host-enqueue gaps. */
+int pcs_spin(int us, void* stream);
 
 /* ---- inverse neighbour maps (atomic-free gather backward) ------------------ */
 

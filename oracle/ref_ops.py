@@ -30,13 +30,21 @@ import torch.nn.functional as F
 class Replay:
     """Queues of FPS starts / kNN indices consumed in call order, plus records."""
 
-    def __init__(self, fps_starts=None, knn_idx=None, fps_idx=None, group_idx=None, interp_idx=None):
+    def __init__(self, fps_starts=None, knn_idx=None, fps_idx=None, group_idx=None, interp_idx=None,
+                 pool_arg=None, act_mask=None):
         self.fps_starts = list(fps_starts) if fps_starts is not None else None
         self.knn_idx = list(knn_idx) if knn_idx is not None else None
         # full index replay (used to run the oracle in float64 on the float32 run's neighbour choices)
         self.fps_idx = list(fps_idx) if fps_idx is not None else None
         self.group_idx = list(group_idx) if group_idx is not None else None
         self.interp_idx = list(interp_idx) if interp_idx is not None else None
+        # max-pool argmax decisions of another run (SA / InvResMLP reduce, EdgeConv max over k),
+        # (groups, channels) in forward order: the pool takes the value at that index instead of
+        # re-deciding near-ties (test hook; the reference always takes torch.max)
+        self.pool_arg = list(pool_arg) if pool_arg is not None else None
+        # activation decisions of another run (y > 0 of every engine-site ReLU / LeakyReLU, rows x
+        # channels, forward order): ReLU / LeakyReLU take that sign decision instead of their own
+        self.act_mask = list(act_mask) if act_mask is not None else None
         self.rec_fps_starts: list[torch.Tensor] = []
         self.rec_fps_idx: list[torch.Tensor] = []
         self.rec_group_idx: list[torch.Tensor] = []
@@ -144,8 +152,45 @@ def group(centroid_coords, coords, features, r, K, normalize=False):
 # --------------------------------------------------------------------------
 # a3  reduce                             (common.py:74-91)
 # --------------------------------------------------------------------------
+def _replayed_arg(shape_bcd):
+    rp = _rp()
+    if rp is not None and rp.pool_arg:
+        return rp.pool_arg.pop(0).long().reshape(shape_bcd)
+    return None
+
+
+def act(y: torch.Tensor, slope: float = 0.0, layout: str = 'points') -> torch.Tensor:
+    """F.relu (slope 0) / LeakyReLU(slope) of an engine-site activation; with a replayed sign
+    decision (Replay.act_mask, rows x channels in the product's point-major layout) the
+    branch is taken from it.  layout: 'points' y (B, C, N) <- rows (B*N, C); 'grouped'
+    y (B, C, G, K) <- rows (B*G*K, C)."""
+    rp = _rp()
+    if rp is None or not rp.act_mask:
+        return F.relu(y) if slope == 0.0 else F.leaky_relu(y, slope)
+    m = rp.act_mask.pop(0)
+    if layout == 'grouped':
+        B, C, G, K = y.shape
+        m = m.reshape(B, G, K, C).permute(0, 3, 1, 2)
+    else:
+        B, C, N = y.shape
+        m = m.reshape(B, N, C).permute(0, 2, 1)
+    return torch.where(m, y, y * slope)
+
+
+def _seq_act(seq, x):
+    """Sequential(Conv1d, BatchNorm1d, LeakyReLU[, Dropout]) (dgcnn.py:188-210) with the
+    activation through `act`."""
+    y = act(seq[1](seq[0](x)), seq[2].negative_slope, 'points')
+    for mod in list(seq)[3:]:
+        y = mod(y)
+    return y
+
+
 def reduce(x: torch.Tensor, type: str) -> torch.Tensor:
     if type == 'max':
+        arg = _replayed_arg((x.shape[0], x.shape[1], x.shape[3]))
+        if arg is not None:
+            return x.gather(2, arg.unsqueeze(2)).squeeze(2)
         return torch.max(x, dim=2)[0]
     if type == 'avg':
         # the reference indexes [0] after the mean (common.py:89); kept as is.
@@ -233,7 +278,7 @@ class MiniPointNet(nn.Module):           # common.py:125-150
 
     def forward(self, x):
         for c, b in zip(self.conv, self.batch):
-            x = F.relu(b(c(x)))
+            x = act(b(c(x)), 0.0, 'grouped')
         return x
 
 
@@ -250,7 +295,7 @@ class UnitPointNet(nn.Module):           # common.py:153-178
 
     def forward(self, x):
         for c, b in zip(self.conv, self.batch):
-            x = F.relu(b(c(x)))
+            x = act(b(c(x)), 0.0, 'points')
         return x
 
 
@@ -322,6 +367,61 @@ class PointNetpp(nn.Module):             # models/PointNetpp/PointNetpp.py:6-48
         return self.conv(y).permute(0, 2, 1)
 
 
+class PointNetppMSG(nn.Module):
+    """PointNet++ MSG (BASELINE.json config 4).  NOT in the reference: composed here from the
+    reference's own blocks -- `sample` (common.py:6-34) once per level, then per radius
+    `group` (common.py:37-71) -> MiniPointNet (common.py:125-150) -> `reduce` max
+    (common.py:74-91), the branches concatenated in radius order; FeaturePropagation
+    (common.py:217-243) as in PointNetpp.py:19-22, 42-45 -- with the standard sem-seg MSG
+    widths of SURVEY.md section 8(d).  Same module tree / state_dict keys as pcseg.PointNetppMSG."""
+
+    CFG = [  # (C, radii, Ks, [mlp per scale])
+        (1024, (0.05, 0.1), (16, 32), ([16, 16, 32], [32, 32, 64])),
+        (256, (0.1, 0.2), (16, 32), ([64, 64, 128], [64, 96, 128])),
+        (64, (0.2, 0.4), (16, 32), ([128, 196, 256], [128, 196, 256])),
+        (16, (0.4, 0.8), (16, 32), ([256, 256, 512], [256, 384, 512])),
+    ]
+
+    def __init__(self, part_classes):
+        super().__init__()
+        self.levels = nn.ModuleList()
+        d, skips = 6, [6]
+        for C, radii, Ks, mlps in self.CFG:
+            self.levels.append(nn.ModuleList([SetAbstraction(C, r, d + 3, m, K=k)
+                                              for r, k, m in zip(radii, Ks, mlps)]))
+            d = sum(m[-1] for m in mlps)
+            skips.append(d)
+        self.fp4 = FeaturePropagation(skips[4] + skips[3], [256, 256])
+        self.fp3 = FeaturePropagation(256 + skips[2], [256, 256])
+        self.fp2 = FeaturePropagation(256 + skips[1], [256, 128])
+        self.fp1 = FeaturePropagation(128, [128, 128, 128])
+        self.drop = nn.Dropout(0.5)
+        self.conv = nn.Conv1d(128, part_classes, 1)
+
+    @staticmethod
+    def _level(branches, coords, feats):
+        cc = sample(coords, branches[0].C)                 # one centroid set shared by the scales
+        outs = []
+        for sa in branches:
+            f = group(cc, coords, feats, sa.radius, sa.K, sa.grouping_norm)
+            f = sa.point_net(f.permute(0, 3, 1, 2)).permute(0, 2, 3, 1)
+            outs.append(reduce(f, sa.pooling_type))
+        return cc, torch.cat(outs, dim=-1)
+
+    def forward(self, x):
+        cs, fs = [x[:, :, :3]], [x[:, :, 3:]]
+        for branches in self.levels:
+            c, f = self._level(branches, cs[-1], fs[-1])
+            cs.append(c)
+            fs.append(f)
+        f3 = self.fp4(cs[3], cs[4], fs[3], fs[4])
+        f2 = self.fp3(cs[2], cs[3], fs[2], f3)
+        f1 = self.fp2(cs[1], cs[2], fs[1], f2)
+        f0 = self.fp1(cs[0], cs[1], None, f1)
+        y = self.drop(f0).permute(0, 2, 1)
+        return self.conv(y).permute(0, 2, 1)
+
+
 class PointNeXt(nn.Module):              # models/PointNeXt/PointNeXt.py:17-147
     def __init__(self, part_classes, version='b'):
         super().__init__()
@@ -374,6 +474,13 @@ class EdgeConv(nn.Module):               # models/dgcnn/dgcnn.py:60-77
             nn.LeakyReLU(negative_slope=0.2))
 
     def forward(self, x):
+        rp = _rp()
+        if rp is not None and (rp.pool_arg or rp.act_mask):
+            # replayed decisions: max_k act(y_k) = act(y at the argmax) (act is monotone)
+            e = self.conv[1](self.conv[0](get_graph_feature(x, k=self.k)))      # (B, Cout, N, k)
+            arg = _replayed_arg((e.shape[0], e.shape[2], e.shape[1]))           # (B*N, Cout) -> (B, N, Cout)
+            y = e.gather(3, arg.permute(0, 2, 1).unsqueeze(3)).squeeze(3) if arg is not None else e.max(-1)[0]
+            return act(y, self.conv[2].negative_slope, 'points')
         return self.conv(get_graph_feature(x, k=self.k)).max(dim=-1, keepdim=False)[0]
 
 
@@ -403,8 +510,8 @@ class DGCNN(nn.Module):                  # dgcnn.py:80-162
         x3 = self.conv3(x2)
         x4 = self.conv4(x3)
         xc = torch.cat((x1, x2, x3, x4), dim=1)
-        x5 = self.conv5(xc)
-        x7 = self.conv7(self.conv6(torch.cat((xc, x5), dim=1)))
+        x5 = _seq_act(self.conv5, xc)
+        x7 = _seq_act(self.conv7, _seq_act(self.conv6, torch.cat((xc, x5), dim=1)))
         return self.conv8(x7).transpose(2, 1).contiguous(), x5, None
 
 
@@ -432,9 +539,9 @@ class DGCNNWithColor(nn.Module):         # dgcnn.py:165-257
         x2 = self.conv2(x1)
         x3 = self.conv3(x2)
         x4 = self.conv4(x3)
-        xc = torch.cat((x1, x2, x3, x4, self.color_conv(rgb)), dim=1)
-        x5 = self.conv5(xc)
-        x7 = self.conv7(self.conv6(torch.cat((xc, x5), dim=1)))
+        xc = torch.cat((x1, x2, x3, x4, _seq_act(self.color_conv, rgb)), dim=1)
+        x5 = _seq_act(self.conv5, xc)
+        x7 = _seq_act(self.conv7, _seq_act(self.conv6, torch.cat((xc, x5), dim=1)))
         return self.conv8(x7).transpose(2, 1).contiguous(), x5, None
 
 
@@ -449,9 +556,9 @@ class TNet(nn.Module):                   # models/PointNet/PointNet.py:6-38
 
     def forward(self, x):
         B = x.size(0)
-        x = F.relu(self.bn1(self.conv1(x)))
-        x = F.relu(self.bn2(self.conv2(x)))
-        x = F.relu(self.bn3(self.conv3(x)))
+        x = act(self.bn1(self.conv1(x)))
+        x = act(self.bn2(self.conv2(x)))
+        x = act(self.bn3(self.conv3(x)))
         x = torch.max(x, 2, keepdim=False)[0]
         x = F.relu(self.bn4(self.fc1(x)))
         x = F.relu(self.bn5(self.fc2(x)))
@@ -475,13 +582,13 @@ class PointNetEncoder(nn.Module):        # PointNet.py:41-90
         B, _, N = x.size()
         trans = self.stn(x)
         x = torch.bmm(x.transpose(2, 1), trans).transpose(2, 1)
-        x = F.relu(self.bn1(self.conv1(x)))
+        x = act(self.bn1(self.conv1(x)))
         trans_feat = None
         if self.feature_transform:
             trans_feat = self.fstn(x)
             x = torch.bmm(x.transpose(2, 1), trans_feat).transpose(2, 1)
         pf = x
-        x = F.relu(self.bn2(self.conv2(x)))
+        x = act(self.bn2(self.conv2(x)))
         x = self.bn3(self.conv3(x))
         x = torch.max(x, 2, keepdim=False)[0]
         if self.global_feat:
@@ -501,9 +608,9 @@ class PointNetSeg(nn.Module):            # PointNet.py:119-150
 
     def forward(self, x):
         x, _, _ = self.feat(torch.transpose(x, -1, -2))
-        x = F.relu(self.bn1(self.conv1(x)))
-        x = F.relu(self.bn2(self.conv2(x)))
-        x = F.relu(self.bn3(self.conv3(x)))
+        x = act(self.bn1(self.conv1(x)))
+        x = act(self.bn2(self.conv2(x)))
+        x = act(self.bn3(self.conv3(x)))
         x = self.conv4(x).transpose(2, 1).contiguous()
         x = torch.exp(x)
         return x / torch.sum(x, keepdim=True, dim=-1)

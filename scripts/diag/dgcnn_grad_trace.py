@@ -1,0 +1,103 @@
+"""Diagnostic (GPU box): where does the DGCNN gradient error enter?  Compares the gradient of
+every EdgeConv / head activation between the GPU run, the CPU fp32 oracle and the CPU fp64
+oracle (same kNN graphs, same inputs and weights)."""
+import copy
+import sys
+import os
+
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path[:0] = [REPO, os.path.join(REPO, '3d-semantic-segmentation-benchmark_amd'), os.path.join(REPO, 'tests')]
+import pcseg  # noqa: E402
+import pcseg.models as PM  # noqa: E402
+from oracle import ref_ops as R  # noqa: E402
+from pcseg.synthetic import make_batch  # noqa: E402
+
+B, N, seed = 2, 1024, 107
+pts, labels, lengths = make_batch(B, N, seed=seed)
+x = pts[:, :, :6].contiguous().transpose(1, 2)
+lab = labels.float()
+ref32 = R.seeded_init_(R.DGCNNWithColor(14), seed)
+ref64 = copy.deepcopy(ref32).double()
+prod = pcseg.DGCNNWithColor(14)
+prod.load_state_dict(ref32.state_dict())
+prod = prod.cuda()
+for m in (ref32, ref64, prod):
+    m.train()
+    for mod in m.modules():
+        if isinstance(mod, torch.nn.Dropout):
+            mod.eval()
+
+acts = {}
+
+
+def grab(tag):
+    def hook(mod, inp, out):
+        o = out[0] if isinstance(out, tuple) else out
+        o.retain_grad()
+        acts.setdefault(tag, []).append(o)
+    return hook
+
+
+for m, tag in ((ref32, 'r32'), (ref64, 'r64')):
+    for name in ('conv1', 'conv2', 'conv3', 'conv4', 'color_conv', 'conv5', 'conv6', 'conv7'):
+        getattr(m, name).register_forward_hook(grab(tag))
+# product: wrap forward_points / _seq_rows outputs
+prod_out = []
+orig_fp = PM.EdgeConv.forward_points
+
+
+def fp(self, xp):
+    o = orig_fp(self, xp)
+    o.retain_grad()
+    prod_out.append(o)
+    return o
+
+
+PM.EdgeConv.forward_points = fp
+orig_seq = PM._seq_rows
+
+
+def seq(x_rows, s, kin=None):
+    o = orig_seq(x_rows, s, kin)
+    o.retain_grad()
+    prod_out.append(o)
+    return o
+
+
+PM._seq_rows = seq
+rp = R.Replay()
+with R.replay(rp):
+    l32 = ref32(x)[0]
+R.masked_onehot_cross_entropy(l32, lab, lengths).backward()
+with R.replay(R.Replay(knn_idx=rp.rec_knn_idx)):
+    l64 = ref64(x.double())[0]
+R.masked_onehot_cross_entropy(l64, lab.double(), lengths).backward()
+with pcseg.replay(pcseg.Replay(knn_idx=rp.rec_knn_idx)):
+    lg = prod(x.cuda())[0]
+pcseg.masked_onehot_cross_entropy(lg, lab.cuda(), lengths.cuda()).backward()
+names = ['conv1', 'conv2', 'conv3', 'conv4', 'color', 'conv5', 'conv6', 'conv7']
+for i, nm in enumerate(names):
+    a32, a64 = acts['r32'][i], acts['r64'][i]
+    g = prod_out[i]
+    gp = g.grad.detach().cpu().double().reshape(B, N, -1).transpose(1, 2)
+    vp = g.detach().cpu().double().reshape(B, N, -1).transpose(1, 2)
+    t, tv = a64.grad.reshape(gp.shape), a64.detach().reshape(gp.shape)
+    n, nv = t.norm(), tv.norm()
+    print(f'{nm:6s} act: gpu {float((vp - tv).norm() / nv):.2e} cpu {float((a32.detach().double().reshape(gp.shape) - tv).norm() / nv):.2e}'
+          f'   grad: gpu {float((gp - t).norm() / n):.2e} cpu {float((a32.grad.double().reshape(gp.shape) - t).norm() / n):.2e}')
+for k in ('conv1.conv.0.weight', 'conv4.conv.0.weight', 'conv4.conv.1.weight', 'conv4.conv.1.bias', 'conv5.0.weight'):
+    pg = dict(prod.named_parameters())[k].grad.cpu().double()
+    t = dict(ref64.named_parameters())[k].grad
+    c = dict(ref32.named_parameters())[k].grad.double()
+    print(f'{k:22s} gpu {float((pg - t).norm() / t.norm()):.2e} cpu {float((c - t).norm() / t.norm()):.2e}')
+# activation-mask flips (sign of the LeakyReLU output) vs the fp64 run
+for i, nm in enumerate(names):
+    if nm not in ('conv5', 'conv6', 'conv7', 'color'):
+        continue
+    vp = prod_out[i].detach().cpu().double().reshape(B, N, -1).transpose(1, 2)
+    tv = acts['r64'][i].detach().reshape(vp.shape)
+    cv = acts['r32'][i].detach().double().reshape(vp.shape)
+    print(f'{nm}: sign flips gpu vs fp64 {int(((vp > 0) != (tv > 0)).sum())}, cpu32 vs fp64 '
+          f'{int(((cv > 0) != (tv > 0)).sum())} of {tv.numel()}; min |y| {float(tv.abs().min()):.2e}')

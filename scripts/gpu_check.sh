@@ -1,8 +1,13 @@
-# Iteration check: full GPU parity suite, bench (no CPU baseline), rocprof kernel stats of the bench.
+# GPU suite + smoke + default bench (CPU baselines included) on one MI355X box (via gpurun).
+# usage: scripts/gpu_check.sh <tag> [pytest -k expr]
 set -u
-cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
+cd "$GRAFT_REPO_ROOT"; tag=${1:-check}; kexpr=${2:-}
+out=gpurun_out/$tag; mkdir -p $out
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread ${PYTEST_EXTRA:-} > gpurun_out/pytest_gpu.log 2>&1; rc=$?
-echo "pytest rc=$rc"; tail -6 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python bench.py --no-cpu-baseline --steps 20 --warmup 5 ${BENCH_ARGS:-} > gpurun_out/bench_iter.log 2>&1; rc=$?; echo "bench rc=$rc"; tail -1 gpurun_out/bench_iter.log; [ $rc -eq 0 ] || exit $rc
-cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline --no-roofline ${BENCH_ARGS:-} > "$GRAFT_REPO_ROOT/gpurun_out/prof.log" 2>&1; echo "prof rc=$?"
+if [ -n "$kexpr" ]; then
+  timeout -k 10 1100 python -u -m pytest tests -m gpu --maxfail=25 -q -s -p no:cacheprovider --timeout 900 --timeout-method thread -k "$kexpr" > $out/pytest_gpu.log 2>&1; rc=$?
+else
+  timeout -k 10 1100 python -u -m pytest tests -m gpu --maxfail=25 -q -s -p no:cacheprovider --timeout 900 --timeout-method thread > $out/pytest_gpu.log 2>&1; rc=$?
+fi
+echo "pytest rc=$rc"; grep -E "passed|failed|error" $out/pytest_gpu.log | tail -3
+[ $rc -eq 0 ] || { grep -E "^E |Error|assert" $out/pytest_gpu.log | head -30; exit $rc; }

@@ -36,6 +36,8 @@ import Training.metrics as rmet             # noqa: E402
 
 from pcseg.synthetic import make_batch      # noqa: E402
 from oracle.ref_ops import seeded_init_     # noqa: E402
+sys.path.insert(0, os.path.dirname(HERE))
+from scene_models import PerPointLinear     # noqa: E402  (tests/scene_models.py)
 
 
 def save(name, **arrs):
@@ -240,30 +242,50 @@ def golden_pointnext():
          logits=logits, loss=loss, **grad_summary(m), **buffers(m))
 
 
-def golden_dgcnn():
-    pts, labels, lengths = make_batch(2, 1024, seed=63)
+class KnnRecorder:
+    """Records every kNN graph a reference DGCNN module computes (dgcnn.py:7-21)."""
+
+    def __init__(self, module):
+        self.module, self.rec = module, []
+
+    def __enter__(self):
+        orig, rec = self.module.knn, self.rec
+
+        def knn_rec(xx, k):
+            idx = orig(xx, k)
+            rec.append(idx.clone())
+            return idx
+        self._orig = orig
+        self.module.knn = knn_rec
+        return self
+
+    def __exit__(self, *exc):
+        self.module.knn = self._orig
+
+
+def _golden_dgcnn(name, N, seed):
+    pts, labels, lengths = make_batch(2, N, seed=seed)
     x = pts[:, :, :6].contiguous().transpose(1, 2)          # (B,6,N) non-contiguous, train_model.py:162
     m = seeded_init_(rdg.DGCNNWithColor(num_classes=14, k=20), 999)
-    rec = []
-    orig = rdg.knn
-
-    def knn_rec(xx, k):
-        idx = orig(xx, k)
-        rec.append(idx.clone())
-        return idx
-    rdg.knn = knn_rec
-    try:
+    with KnnRecorder(rdg) as kr:
         m.train()
         dropout_off(m)
         logits, x5, _ = m(x)
         loss = rtm.masked_onehot_cross_entropy(logits, labels.float(), lengths.to(torch.int32))
         loss.backward()
-    finally:
-        rdg.knn = orig
-    save('model_dgcnn_color.npz', x=x.contiguous(), labels=labels, lengths=lengths.to(torch.int64),
-         **{f'knn{i}': r.to(torch.int16) for i, r in enumerate(rec)},
+    save(name, x=x.contiguous(), labels=labels, lengths=lengths.to(torch.int64),
+         **{f'knn{i}': r.to(torch.int16) for i, r in enumerate(kr.rec)},
          logits=logits, x5_sum=x5.double().sum(), x5_head=x5.reshape(-1)[:256], loss=loss,
          **grad_summary(m), **buffers(m))
+
+
+def golden_dgcnn():
+    _golden_dgcnn('model_dgcnn_color.npz', 1024, 63)
+
+
+def golden_dgcnn4096():
+    """BASELINE config 2's block size: N = 4096, k = 20 (the kNN runs over 4096 x 4096 tiles)."""
+    _golden_dgcnn('model_dgcnn_color_4096.npz', 4096, 65)
 
 
 def golden_pointnet():
@@ -275,6 +297,104 @@ def golden_pointnet():
     loss.backward()
     save('model_pointnet.npz', x=pts, labels=labels, lengths=lengths.to(torch.int64),
          probs=probs, loss=loss, **grad_summary(m), **buffers(m))
+
+
+def golden_pointnet4096():
+    """BASELINE config 1's block size (N = 4096), B = 4 (the TNet's BatchNorm1d over the batch is
+    degenerate at B = 2: its gradients are cancellation noise in the reference itself)."""
+    pts, labels, lengths = make_batch(4, 4096, seed=66)
+    m = seeded_init_(rpn.PointNetSeg(part_classes=14), 78)
+    m.train()
+    probs = m(pts)
+    loss = rtm.masked_onehot_cross_entropy(probs, labels, lengths)
+    loss.backward()
+    save('model_pointnet_4096.npz', x=pts, labels=labels, lengths=lengths.to(torch.int64),
+         probs=probs, loss=loss, **grad_summary(m), **buffers(m))
+
+
+def golden_pointnext24576():
+    """BASELINE config 5's block size: PointNeXt-B on one 24 576-point block."""
+    pts, labels, lengths = make_batch(1, 24576, seed=67)
+    m = seeded_init_(rpx.PointNeXt(14), 4322)
+    logits, loss, starts = _run_model(m, pts, labels, lengths, seed_fps=7)
+    save('model_pointnext_24576.npz', x=pts, labels=labels, lengths=lengths.to(torch.int64),
+         **{f'fps_start{i}': s for i, s in enumerate(starts)},
+         logits=logits, loss=loss, **grad_summary(m), **buffers(m))
+
+
+# ---------------------------------------------------------------- section 8(f) rows 1 and 4
+BLOCK_LAYOUT = {1: [(1, 1, 150), (1, 3, 40), (2, 2, 90), (10, 12, 64)], 2: [(3, 1, 70), (3, 2, 17)],
+                3: [(1, 1, 33), (4, 7, 200)], 4: [(1, 4, 55)], 5: [(2, 9, 120)], 6: [(7, 1, 81), (7, 2, 12)]}
+
+
+def golden_blocks():
+    """data_processing/block_datasets.py: the block index from file names (:56-90), per-block
+    sampling with the reference's own RNG draws (:119-128), collate_blocks (:5-29) and
+    create_block_dataloaders' area split + unshuffled batches (:133-183).  The block files
+    are written to a temporary directory in the format preprocess_dataset.py:134 saves."""
+    import tempfile
+    import data_processing.block_datasets as bd
+    g = torch.Generator().manual_seed(93)
+    arrs = {}
+    with tempfile.TemporaryDirectory() as root:
+        for area, blocks in BLOCK_LAYOUT.items():
+            os.makedirs(os.path.join(root, f'area_{area}'))
+            for room, block, n in blocks:
+                pts = torch.randn(n, 9, generator=g)
+                lab = torch.nn.functional.one_hot(torch.randint(0, 14, (n,), generator=g), 14).to(torch.uint8)
+                torch.save((pts, lab), os.path.join(root, f'area_{area}', f'room{room:02d}_block{block:03d}.pt'))
+                arrs[f'file/{area}/{room}/{block}/points'] = pts
+                arrs[f'file/{area}/{room}/{block}/labels'] = lab
+        ds = bd.BlockS3DISDataset(root, {1, 3}, sampling=64)
+        arrs['index_13'] = ds.blocks
+        for i in range(len(ds)):
+            torch.manual_seed(1000 + i)
+            p, l = ds[i]
+            arrs[f'sample64/{i}/points'], arrs[f'sample64/{i}/labels'] = p, l
+        whole = bd.BlockS3DISDataset(root, {1, 3})
+        cp, cl, cn = bd.collate_blocks([whole[i] for i in (5, 0, 2)])
+        arrs.update({'collate/points': cp, 'collate/labels': cl, 'collate/lengths': cn.to(torch.int64)})
+        train, test = bd.create_block_dataloaders(root, {2, 5}, train_batch_size=3, test_batch_size=2,
+                                                  num_workers=0, train_sampling=None, test_sampling=None,
+                                                  train_shuffle=False, test_shuffle=False)
+        arrs['split/train'], arrs['split/test'] = train.dataset.blocks, test.dataset.blocks
+        for tag, loader in (('train', train), ('test', test)):
+            for j, (p, l, n) in enumerate(loader):
+                arrs[f'{tag}_batch/{j}/points'], arrs[f'{tag}_batch/{j}/labels'] = p, l
+                arrs[f'{tag}_batch/{j}/lengths'] = n.to(torch.int64)
+    save('blocks.npz', **arrs)
+
+
+def golden_scene():
+    """models/dgcnn/utils.py:67-131 sliding-window inference, captured from the reference with
+    (a) a per-point linear stand-in (window / overlap / average / argmax logic, exact) and
+    (b) an eval-mode DGCNNWithColor with its per-window kNN graphs recorded for replay."""
+    sys.path.insert(0, os.path.join(REF, 'models', 'dgcnn'))
+    import utils as rut                      # reference models/dgcnn/utils.py (imports `dgcnn`)
+    import dgcnn as rdg2
+    arrs = {}
+    for tag, (n, bs, ov) in {'a': (2500, 1024, 128), 'b': (700, 1024, 128), 'c': (3000, 512, 64),
+                             'd': (4096, 4096, 512)}.items():
+        pts, _, _ = make_batch(1, n, seed=n + 7)
+        scene = pts[0, :, :6].contiguous()
+        lin = PerPointLinear(6, 13, seed=n)
+        p, c = rut.predict_single_scene(lin, scene, device='cpu', batch_size=bs, overlap=ov)
+        arrs.update({f'{tag}/scene': scene, f'{tag}/meta': np.array([n, bs, ov]), f'{tag}/lin_w': lin.weight,
+                     f'{tag}/lin_b': lin.bias, f'{tag}/lin_pred': p, f'{tag}/lin_conf': c})
+    # eval-mode DGCNN with non-trivial running statistics (scene a)
+    n, bs, ov = 2500, 1024, 128
+    scene = arrs['a/scene']
+    m = seeded_init_(rdg2.DGCNNWithColor(num_classes=13, k=20), 2500 + 1024)
+    g = torch.Generator().manual_seed(2500 + 1024 + 1)
+    for mod in m.modules():
+        if isinstance(mod, (torch.nn.BatchNorm1d, torch.nn.BatchNorm2d)):
+            mod.running_mean.copy_(torch.randn(mod.running_mean.shape, generator=g) * 0.1)
+            mod.running_var.copy_(torch.rand(mod.running_var.shape, generator=g) + 0.5)
+    with KnnRecorder(rdg2) as kr:
+        p, c = rut.predict_single_scene(m, scene, device='cpu', batch_size=bs, overlap=ov)
+    arrs.update({'dgcnn/pred': p, 'dgcnn/conf': c, 'dgcnn/init_seed': 2500 + 1024,
+                 **{f'dgcnn/knn{i}': r.to(torch.int16) for i, r in enumerate(kr.rec)}})
+    save('scene.npz', **arrs)
 
 
 def golden_preprocess():
@@ -322,6 +442,7 @@ def golden_metrics():
 if __name__ == '__main__':
     torch.set_num_threads(8)
     which = sys.argv[1:] or ['fps', 'group', 'interp', 'knn', 'loss', 'pointnetpp', 'pointnext',
-                             'dgcnn', 'pointnet', 'metrics', 'preprocess']
+                             'dgcnn', 'pointnet', 'metrics', 'preprocess', 'dgcnn4096', 'pointnet4096',
+                             'pointnext24576', 'blocks', 'scene']
     for w in which:
         globals()['golden_' + w]()

@@ -80,7 +80,7 @@ def test_constructor_signatures_match_reference(name):
 
 @pytest.mark.parametrize('ctor', [lambda m: m.PointNetpp(14), lambda m: m.PointNeXt(14),
                                   lambda m: m.DGCNNWithColor(14), lambda m: m.DGCNN(13),
-                                  lambda m: m.PointNetSeg(14)])
+                                  lambda m: m.PointNetSeg(14), lambda m: m.PointNetppMSG(14)])
 def test_state_dict_layout_matches_reference(ctor):
     a, b = ctor(pcseg).state_dict(), ctor(R).state_dict()
     assert list(a) == list(b)

@@ -72,3 +72,153 @@ def test_device_store_sampling_semantics(blockdir):
         assert torch.equal(lab[b].cpu(), l[rows])
         if n > S:                                                                  # randperm(n)[:S]: distinct
             assert rows.unique().numel() == S
+
+
+# ---------------------------------------------------------------- pinned by tests/golden/blocks.npz
+@pytest.fixture(scope='module')
+def golden_blocks(tmp_path_factory, golden):
+    """The block directory golden_blocks() wrote (tests/golden/make_golden.py), rebuilt from the
+    fixture, plus the fixture itself."""
+    z = golden('blocks.npz')
+    root = tmp_path_factory.mktemp('golden_blocks')
+    for k in z.files:
+        if k.startswith('file/') and k.endswith('/points'):
+            _, a, r, b, _ = k.split('/')
+            os.makedirs(root / f'area_{a}', exist_ok=True)
+            torch.save((torch.from_numpy(z[k]), torch.from_numpy(z[k.replace('/points', '/labels')])),
+                       root / f'area_{a}' / f'room{int(r):02d}_block{int(b):03d}.pt')
+    return str(root), z
+
+
+def _T(a):
+    return torch.from_numpy(a)
+
+
+def test_oracle_block_index_and_sampling_match_reference(golden_blocks):
+    root, z = golden_blocks
+    blocks = RD.block_index(root, {1, 3})
+    assert torch.equal(blocks, _T(z['index_13']))
+    for i in range(blocks.shape[0]):
+        torch.manual_seed(1000 + i)                   # the reference's own global-RNG draw
+        p, l = RD.get_block(root, blocks, i, sampling=64)
+        assert torch.equal(p, _T(z[f'sample64/{i}/points'])) and torch.equal(l, _T(z[f'sample64/{i}/labels']))
+
+
+def test_oracle_collate_and_split_match_reference(golden_blocks):
+    root, z = golden_blocks
+    whole = RD.block_index(root, {1, 3})
+    cp, cl, cn = RD.collate_blocks([RD.get_block(root, whole, i) for i in (5, 0, 2)])
+    assert torch.equal(cp, _T(z['collate/points'])) and torch.equal(cl, _T(z['collate/labels']))
+    assert torch.equal(cn.to(torch.int64), _T(z['collate/lengths'])) and cn.dtype == torch.uint64
+    train, test = RD.block_splits(root, {2, 5})
+    assert torch.equal(train, _T(z['split/train'])) and torch.equal(test, _T(z['split/test']))
+    for tag, blocks, bs in (('train', train, 3), ('test', test, 2)):
+        for j, (p, l, n) in enumerate(RD.unshuffled_batches(root, blocks, bs)):
+            assert torch.equal(p, _T(z[f'{tag}_batch/{j}/points']))
+            assert torch.equal(l, _T(z[f'{tag}_batch/{j}/labels']))
+            assert torch.equal(n.to(torch.int64), _T(z[f'{tag}_batch/{j}/lengths']))
+        assert f'{tag}_batch/{j + 1}/points' not in z.files
+
+
+def test_product_index_split_and_collate_match_reference(golden_blocks):
+    root, z = golden_blocks
+    assert torch.equal(D.block_index(root, {1, 3}), _T(z['index_13']))
+    assert torch.equal(D.block_index(root, {1, 3, 4, 6}), _T(z['split/train']))
+    batch = [RD.get_block(root, RD.block_index(root, {1, 3}), i) for i in (5, 0, 2)]
+    for a, k in zip(D.collate_blocks(batch), ('points', 'labels', 'lengths')):
+        assert torch.equal(a if k != 'lengths' else a.to(torch.int64), _T(z[f'collate/{k}']))
+
+
+@pytest.mark.gpu
+def test_device_loaders_unshuffled_match_reference_batches(golden_blocks):
+    root, z = golden_blocks
+    train, test = D.create_block_dataloaders(root, {2, 5}, train_batch_size=3, test_batch_size=2,
+                                             num_workers=0, train_sampling=None, test_sampling=None,
+                                             train_shuffle=False, test_shuffle=False)
+    assert torch.equal(train.dataset.blocks, _T(z['split/train']))
+    for tag, loader in (('train', train), ('test', test)):
+        n = 0
+        for j, (p, l, ln) in enumerate(loader):
+            assert torch.equal(p.cpu(), _T(z[f'{tag}_batch/{j}/points']))
+            assert torch.equal(l.cpu(), _T(z[f'{tag}_batch/{j}/labels']))
+            assert torch.equal(ln.cpu().to(torch.int64), _T(z[f'{tag}_batch/{j}/lengths']))
+            n += 1
+        assert n == len(loader) and f'{tag}_batch/{n}/points' not in z.files
+
+
+@pytest.mark.gpu
+def test_device_loader_sampling_is_per_rank_and_reproducible(golden_blocks):
+    root, _ = golden_blocks
+    tr0, _ = D.create_block_dataloaders(root, {2, 5}, train_batch_size=2, train_sampling=64, seed=3, rank=0,
+                                        world=2)
+    tr1, _ = D.create_block_dataloaders(root, {2, 5}, train_batch_size=2, train_sampling=64, seed=3, rank=1,
+                                        world=2)
+    a = [p.cpu() for p, _, _ in tr0]
+    b = [p.cpu() for p, _, _ in tr0]
+    assert all(torch.equal(x, y) for x, y in zip(a, b))          # same (seed, rank, epoch): same draws
+    tr0.set_epoch(1)
+    c = [p.cpu() for p, _, _ in tr0]
+    assert not all(torch.equal(x, y) for x, y in zip(a, c))      # a new epoch: new order and draws
+    assert tr0.sampler.order() == tr1.sampler.order() or tr0.sampler.epoch != tr1.sampler.epoch
+    assert len(tr0) == len(tr1) == 3                             # 9 train blocks -> 5 per rank (padded), B=2
+
+
+# ---------------------------------------------------------------- distributed block sampler
+@pytest.mark.parametrize('n,world,drop_last', [(13, 2, False), (12, 4, False), (13, 4, True), (3, 4, False)])
+def test_sampler_shards_partition_each_epoch(n, world, drop_last):
+    for epoch in range(3):
+        shards = []
+        for r in range(world):
+            s = D.DistributedBlockSampler(n, rank=r, world=world, seed=11, drop_last=drop_last)
+            s.set_epoch(epoch)
+            shards.append(list(s))
+            assert len(shards[-1]) == len(s)
+        flat = [i for sh in shards for i in sh]
+        if drop_last:
+            assert len(set(flat)) == len(flat) == (n // world) * world
+        else:
+            assert set(flat) == set(range(n)) and len(flat) == -(-n // world) * world
+            if n % world == 0:
+                assert len(set(flat)) == n                          # disjoint when nothing is padded
+    s0 = D.DistributedBlockSampler(n, rank=0, world=world, seed=11)
+    s0.set_epoch(0)
+    e0 = list(s0)
+    s0.set_epoch(1)
+    assert list(s0) != e0 or n <= world
+
+
+def _sampler_worker(rank, world, port, n, out):
+    import torch.distributed as dist
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        s = D.DistributedBlockSampler(n, seed=5)            # rank / world from the process group
+        assert (s.rank, s.world) == (rank, world)
+        res = []
+        for epoch in range(2):
+            s.set_epoch(epoch)
+            mine = torch.tensor(list(s), dtype=torch.int64)
+            got = [torch.zeros_like(mine) for _ in range(world)]
+            dist.all_gather(got, mine)
+            res.append(torch.stack(got))
+        out[rank] = res
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sampler_world2_gloo_disjoint_and_covering():
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as sk:
+        sk.bind(('127.0.0.1', 0))
+        port = sk.getsockname()[1]
+    n, world = 10, 2
+    out = mp.Manager().dict()
+    mp.spawn(_sampler_worker, args=(world, port, n, out), nprocs=world, join=True)
+    for epoch in range(2):
+        a, b = out[0][epoch], out[1][epoch]
+        assert torch.equal(a, b)                             # every rank sees the same assignment
+        assert set(a[0].tolist()).isdisjoint(a[1].tolist())
+        assert sorted(a.reshape(-1).tolist()) == list(range(n))
+    assert not torch.equal(out[0][0], out[0][1])             # a fresh permutation per epoch

@@ -3,21 +3,20 @@
 Two anchors:
   * golden fixtures captured from the reference itself (tests/golden/*.npz):
     same seeded weights, same input blocks, replayed FPS starts / kNN graphs.
-    Forward outputs, loss and BN running statistics must agree within 1e-3
-    (norm-relative, BASELINE.json north_star).
   * a three-way check on EVERY tensor (logits, every parameter gradient, every
     running statistic): GPU fp32 vs the reference algorithm in CPU fp32 (the
     oracle, itself pinned to the reference) vs the same algorithm in CPU fp64 on
-    the same neighbour indices.  Training-mode BatchNorm turns many gradients
-    into sums with heavy cancellation (pre-BN conv biases are analytically 0),
-    so two correct fp32 implementations differ there by far more than 1e-3; a
-    tensor passes when the GPU error vs fp64 is <= 1e-3 of its norm OR no more
-    than 10x the CPU reference's own fp32 error (tests/fp64_check.py).  In
-    practice the GPU error is at or below the CPU reference's on every tensor.
-On the golden fixtures the gradients get the same three-way check (weights,
-inputs and FPS draws of the fixture), plus a coarse 2e-2 / 5e-2 norm-relative
-comparison with the fixture's own gradient summaries (catches wrong indices /
-scatters, which give O(1) errors).
+    the same neighbour indices (tests/fp64_check.py).  Every WEIGHT gradient must be
+    within 1e-3 of the fp64 truth (north_star's tolerance) or no farther from it than 3x
+    the reference's own fp32 evaluation is (the reference's fp32 weight gradients are not
+    reproducible to 1e-3 even against themselves: DESIGN.md section 5); only biases / BN
+    betas / running stats may pass by the 10x reference-noise or module-floor clauses, and
+    the clause every tensor passed by is printed (pytest -s shows it).
+The fixture's own gradient summaries (L2 norm and a seeded probe dot) must agree
+within 1e-3 x the norm + 2x the reference fp32's own error on that tensor (the
+GPU and the fixture are each that close to the fp64 truth); the probe dot's
+tolerance is twice that (a random +-1 probe scales an error vector's norm by
+about 1/sqrt(3)).
 """
 import numpy as np
 import pytest
@@ -26,7 +25,7 @@ import torch
 import pcseg
 from pcseg.synthetic import make_batch
 from oracle import ref_ops as R
-from fp64_check import three_way, failures
+from fp64_check import three_way, failures, report, is_weight
 
 pytestmark = pytest.mark.gpu
 DEV = 'cuda'
@@ -54,38 +53,52 @@ def prepare(prod_ctor, ref_ctor, seed):
     return prod, ref
 
 
-GRAD_RTOL_GOLDEN = 2e-2
-
-
-def _assert_three_way(rows):
+def _assert_three_way(rows, tag=''):
+    print(f'\n-- three-way clauses {tag}\n' + report(rows, rtol=RTOL))
     bad = failures(rows, rtol=RTOL, factor=10.0)
     assert not bad, bad
+    return rows
 
 
-def check_grad_summaries(model, z, rtol=GRAD_RTOL_GOLDEN):
+def check_grad_summaries(model, z, rows):
+    """The fixture's per-parameter L2 / probe dot vs the GPU gradients.  The fixture is the
+    reference's fp32 run with its OWN discrete decisions (argmax / activation-sign near-ties), so
+    the yardstick is that run's distance to the fp64 truth (last field of the three-way rows).
+    Weights: 1e-3 x norm + 4 x that distance -- the triangle bound once the GPU passes the
+    three-way; the other tensors add the three-way's 10x clause and module floor (pre-BN biases
+    are analytically zero: their value is rounding noise in any fp32 evaluation).  The probe dot
+    of an error vector is about its norm / sqrt(3): twice the norm tolerance."""
+    err = {name: (ecf, n) for name, _, _, n, ecf in rows}     # the fixture is the reference's own-decision run
+    top = {}
+    for name, _, _, n, _ in rows:
+        if name != 'logits' and 'running' not in name:
+            top[name.split('.')[0]] = max(top.get(name.split('.')[0], 0.0), n)
     g = torch.Generator().manual_seed(7)
-    gmax = max(float(z['g_l2/' + k]) for k, _ in model.named_parameters())
     for k, p in sorted(model.named_parameters()):
         gr = p.grad.detach().cpu() if p.grad is not None else torch.zeros(p.shape)
         probe = torch.rand(gr.shape, generator=g) * 2 - 1
         flat = gr.reshape(-1).double()
-        scale = max(float(z['g_l2/' + k]), 1e-3 * gmax)
+        ec, n = err[k]
+        if is_weight(k):
+            tol = RTOL * max(n, float(z['g_l2/' + k])) + 4 * ec
+        else:
+            tol = RTOL * max(n, float(z['g_l2/' + k])) + 11 * ec + RTOL * top[k.split('.')[0]]
         d_l2 = abs(float(flat.norm()) - float(z['g_l2/' + k]))
-        assert d_l2 <= rtol * scale, (k, d_l2, scale)
+        assert d_l2 <= tol, (k, d_l2, tol)
         d_dot = abs(float((flat * probe.reshape(-1).double()).sum()) - float(z['g_dot/' + k]))
-        assert d_dot <= rtol * scale * max(1.0, flat.numel() ** 0.5), (k, d_dot, scale)
+        assert d_dot <= 2 * tol, (k, d_dot, 2 * tol)
 
 
-def check_buffers(model, z, rtol=RTOL):
-    """BN running statistics vs the fixture, norm-relative per tensor (the three-way check covers
-    them exactly); tiny-batch layers (e.g. PointNeXt's irmlp4 at M = B*16 rows) are noisier, so
-    the bound is relaxed to 1e-2 where the reference's own fp32 statistics are that noisy."""
+def check_buffers(model, z, rows):
+    """BN running statistics vs the fixture: 1e-3 x norm + 11 x the reference fp32's own error
+    (the three-way bound for running statistics is 10x that error, plus the fixture's own)."""
+    err = {name: (ecf, n) for name, _, _, n, ecf in rows}
     for k, v in model.state_dict().items():
         if 'running' in k:
             ref = T(z['buf/' + k]).double()
-            err = float((v.cpu().double() - ref).norm())
-            assert err <= max(rtol, 1e-2 if 'irmlp4' in k or 'sa4' in k else rtol) * float(ref.norm()) + 1e-6, \
-                (k, err, float(ref.norm()))
+            d = float((v.cpu().double() - ref).norm())
+            ec, n = err[k]
+            assert d <= RTOL * float(ref.norm()) + 11 * ec + 1e-7, (k, d, float(ref.norm()), ec)
 
 
 def close(a, b, rtol=RTOL):
@@ -129,6 +142,9 @@ def fps_starts(z):
 @pytest.mark.parametrize('name,prod,ref,seed', [
     ('model_pointnetpp.npz', lambda: pcseg.PointNetpp(14), lambda: R.PointNetpp(14), 1234),
     ('model_pointnext.npz', lambda: pcseg.PointNeXt(14), lambda: R.PointNeXt(14), 4321),
+    # BASELINE config 5's block: PointNeXt-B on 24 576 points (SA1 FPS 24 576 -> 1024, FP1 24 576 <- 1024)
+    pytest.param('model_pointnext_24576.npz', lambda: pcseg.PointNeXt(14), lambda: R.PointNeXt(14), 4322,
+                 marks=pytest.mark.timeout(900)),
 ])
 def test_pointnet2_family_vs_reference_golden(golden, name, prod, ref, seed):
     z = golden(name)
@@ -137,37 +153,42 @@ def test_pointnet2_family_vs_reference_golden(golden, name, prod, ref, seed):
         logits = model(T(z['x']).to(DEV))
     close_or_within_reference_noise(logits, z, 'logits', ref, seed, T(z['x']))
     loss = pcseg.masked_onehot_cross_entropy(logits, T(z['labels']).to(DEV), T(z['lengths']).to(DEV))
-    assert abs(float(loss) - float(z['loss'])) <= RTOL * abs(float(z['loss']))
+    assert abs(float(loss.detach()) - float(z['loss'])) <= RTOL * abs(float(z['loss']))
     loss.backward()
-    check_buffers(model, z)
     # every gradient tensor, on the golden inputs/weights/FPS draws: three-way vs fp64 truth
-    _assert_three_way(three_way(prod, ref, 0, 0, 0, inputs=(T(z['x']), T(z['labels']), T(z['lengths'])),
-                                init_seed=seed, fps_starts=fps_starts(z)))
-    check_grad_summaries(model, z, rtol=5e-2)
+    rows = _assert_three_way(three_way(prod, ref, 0, 0, 0, inputs=(T(z['x']), T(z['labels']), T(z['lengths'])),
+                                       init_seed=seed, fps_starts=fps_starts(z)), name)
+    check_buffers(model, z, rows)
+    check_grad_summaries(model, z, rows)
 
 
-def test_dgcnn_color_vs_reference_golden(golden):
-    z = golden('model_dgcnn_color.npz')
+@pytest.mark.parametrize('name', ['model_dgcnn_color.npz',
+                                  pytest.param('model_dgcnn_color_4096.npz', marks=pytest.mark.timeout(600))])
+def test_dgcnn_color_vs_reference_golden(golden, name):
+    """N = 1024 and BASELINE config 2's block size N = 4096 (k = 20), kNN graphs replayed
+    from the reference's own run."""
+    z = golden(name)
+    N = z['x'].shape[2]
     model, _ = prepare(lambda: pcseg.DGCNNWithColor(num_classes=14, k=20),
                        lambda: R.DGCNNWithColor(num_classes=14, k=20), 999)
     x = T(z['x']).to(DEV).transpose(1, 2).contiguous().transpose(1, 2)   # non-contiguous (B,6,N) like harness B
     knn = [T(z[f'knn{i}']).long() for i in range(4)]
     with pcseg.replay(pcseg.Replay(knn_idx=knn)):
         logits, x5, trans = model(x)
-    assert trans is None and x5.shape == (2, 1024, 1024)
+    assert trans is None and x5.shape == (2, 1024, N)
     assert close(logits, T(z['logits']))
     assert abs(float(x5.double().sum()) - float(z['x5_sum'])) <= RTOL * float(x5.double().abs().sum())
     loss = pcseg.masked_onehot_cross_entropy(logits, T(z['labels']).float().to(DEV),
                                              T(z['lengths']).to(torch.int32).to(DEV))
-    assert abs(float(loss) - float(z['loss'])) <= RTOL * abs(float(z['loss']))
+    assert abs(float(loss.detach()) - float(z['loss'])) <= RTOL * abs(float(z['loss']))
     loss.backward()
-    check_buffers(model, z)
-    check_grad_summaries(model, z)
     xin = T(z['x']).transpose(1, 2).contiguous().transpose(1, 2)
-    _assert_three_way(three_way(lambda: pcseg.DGCNNWithColor(num_classes=14, k=20),
-                                lambda: R.DGCNNWithColor(num_classes=14, k=20), 0, 0, 0,
-                                inputs=(xin, T(z['labels']).float(), T(z['lengths']).to(torch.int32)),
-                                init_seed=999, knn_idx=[T(z[f'knn{i}']).long() for i in range(4)]))
+    rows = _assert_three_way(three_way(lambda: pcseg.DGCNNWithColor(num_classes=14, k=20),
+                                       lambda: R.DGCNNWithColor(num_classes=14, k=20), 0, 0, 0,
+                                       inputs=(xin, T(z['labels']).float(), T(z['lengths']).to(torch.int32)),
+                                       init_seed=999, knn_idx=[T(z[f'knn{i}']).long() for i in range(4)]), name)
+    check_buffers(model, z, rows)
+    check_grad_summaries(model, z, rows)
 
 
 def test_pointnet_vs_reference_golden(golden):
@@ -176,51 +197,86 @@ def test_pointnet_vs_reference_golden(golden):
     probs = model(T(z['x']).to(DEV))
     assert close(probs, T(z['probs']))
     loss = pcseg.masked_onehot_cross_entropy(probs, T(z['labels']).to(DEV), T(z['lengths']).to(DEV))
-    assert abs(float(loss) - float(z['loss'])) <= RTOL * abs(float(z['loss']))
+    assert abs(float(loss.detach()) - float(z['loss'])) <= RTOL * abs(float(z['loss']))
     # gradients: the fixture's B=2 makes the TNet's BatchNorm1d degenerate (2 samples), so its
-    # gradients are cancellation noise in the reference itself; they are covered by the B=4
-    # three-way test below instead.
+    # gradients are cancellation noise in the reference itself; the N=4096, B=4 fixture below
+    # checks them.
+
+
+def test_pointnet_4096_vs_reference_golden(golden):
+    """PointNet on 4096-point blocks (BASELINE config 1's block size), B=4, every gradient."""
+    z = golden('model_pointnet_4096.npz')
+    model, _ = prepare(lambda: pcseg.PointNetSeg(part_classes=14), lambda: R.PointNetSeg(part_classes=14), 78)
+    probs = model(T(z['x']).to(DEV))
+    assert close(probs, T(z['probs']))
+    loss = pcseg.masked_onehot_cross_entropy(probs, T(z['labels']).to(DEV), T(z['lengths']).to(DEV))
+    assert abs(float(loss.detach()) - float(z['loss'])) <= RTOL * abs(float(z['loss']))
+    loss.backward()
+    rows = _assert_three_way(three_way(lambda: pcseg.PointNetSeg(part_classes=14),
+                                       lambda: R.PointNetSeg(part_classes=14), 0, 0, 0,
+                                       inputs=(T(z['x']), T(z['labels']), T(z['lengths'])), init_seed=78),
+                             'pointnet 4096')
+    check_buffers(model, z, rows)
+    check_grad_summaries(model, z, rows)
 
 
 @pytest.mark.parametrize('B,N,seed,uniform,pad', [(4, 4096, 101, False, 0), (2, 4096, 102, True, 0),
                                                   (3, 2048, 103, False, 300)])
 def test_pointnetpp_three_way_all_tensors(B, N, seed, uniform, pad):
-    _assert_three_way(three_way(lambda: pcseg.PointNetpp(14), lambda: R.PointNetpp(14), B, N, seed, uniform, pad))
+    _assert_three_way(three_way(lambda: pcseg.PointNetpp(14), lambda: R.PointNetpp(14), B, N, seed, uniform, pad),
+                      f'pointnetpp B={B} N={N}')
 
 
 def test_pointnext_three_way_all_tensors():
-    _assert_three_way(three_way(lambda: pcseg.PointNeXt(14), lambda: R.PointNeXt(14), 2, 4096, 104))
+    _assert_three_way(three_way(lambda: pcseg.PointNeXt(14), lambda: R.PointNeXt(14), 2, 4096, 104), 'pointnext')
+
+
+def test_msg_three_way_all_tensors():
+    """PointNet++ MSG (BASELINE config 4, not in the reference) against the oracle's composition
+    of the reference's own sample / group / MiniPointNet / reduce / FeaturePropagation
+    (oracle/ref_ops.py::PointNetppMSG): shared centroids per level, both radii's ball sets
+    index-exact, branch concat order, FP widths -- every tensor three-way."""
+    _assert_three_way(three_way(lambda: pcseg.PointNetppMSG(14), lambda: R.PointNetppMSG(14), 2, 4096, 109),
+                      'msg')
 
 
 def test_dgcnn_three_way_all_tensors():
     _assert_three_way(three_way(lambda: pcseg.DGCNNWithColor(14), lambda: R.DGCNNWithColor(14), 2, 1024, 107,
-                                chfirst=True))
+                                chfirst=True), 'dgcnn')
+
+
+def test_dgcnn_xyz_three_way_all_tensors():
+    """The xyz-only DGCNN (dgcnn.py:80-162) with a 6-channel input (it keeps xyz, :134-137)."""
+    _assert_three_way(three_way(lambda: pcseg.DGCNN(13), lambda: R.DGCNN(13), 2, 1024, 110, chfirst=True,
+                                label_classes=13), 'dgcnn xyz')
 
 
 def test_pointnet_three_way_all_tensors():
     # B=4: the TNet's BatchNorm1d over B samples is degenerate at B=2 (and raises at B=1 in the reference)
     _assert_three_way(three_way(lambda: pcseg.PointNetSeg(part_classes=14), lambda: R.PointNetSeg(part_classes=14),
-                                4, 1024, 108))
+                                4, 1024, 108), 'pointnet')
 
 
-def test_dgcnn_without_replay_reports_knn_agreement():
+@pytest.mark.parametrize('F_', [3, 64])
+def test_dgcnn_without_replay_reports_knn_agreement(F_):
     """No replay: the GPU builds its own kNN graphs; most rows must agree with the oracle's."""
-    pts, labels, lengths = make_batch(2, 1024, seed=105)
+    pts, labels, lengths = make_batch(2, 1024 if F_ == 3 else 4096, seed=105)
     x = pts[:, :, :6].contiguous().transpose(1, 2)
     model, ref = prepare(lambda: pcseg.DGCNNWithColor(14), lambda: R.DGCNNWithColor(14), 5)
     rr, rg = R.Replay(), pcseg.Replay()
-    with R.replay(rr):
+    with R.replay(rr), torch.no_grad():
         rl, _, _ = ref(x)
-    with pcseg.replay(rg):
+    with pcseg.replay(rg), torch.no_grad():
         gl, _, _ = model(x.to(DEV))
-    first = (rg.rec_knn_idx[0].long().sort(-1).values == rr.rec_knn_idx[0].sort(-1).values).all(-1)
-    assert first.float().mean() > 0.99
+    layer = 0 if F_ == 3 else 1          # xyz graph, then the first 64-d feature graph
+    same = (rg.rec_knn_idx[layer].long().sort(-1).values == rr.rec_knn_idx[layer].sort(-1).values).all(-1)
+    assert same.float().mean() > 0.99
     rel = float((gl.detach().cpu() - rl.detach()).norm() / rl.detach().norm())
     assert rel < 0.05
 
 
 def test_msg_and_dgcnn_xyz_train_step():
-    """Models without a reference oracle: one Adam step runs and the loss is finite."""
+    """One Adam step runs and the loss is finite (full B=2, N=4096 step on the product)."""
     pts, labels, lengths = make_batch(2, 4096, seed=106)
     for model, inp in [(pcseg.PointNetppMSG(14), pts), (pcseg.DGCNN(13), pts[:, :, :3].transpose(1, 2))]:
         model = model.to(DEV).train()

@@ -182,9 +182,10 @@ def test_edge_fwd_bwd():
 
 
 # ----------------------------------------------------------------------------- DGCNN kNN
-@pytest.mark.parametrize('F_,seed', [(3, 1), (64, 2)])
-def test_dgcnn_knn_agrees_with_oracle(F_, seed):
-    B, N, k = 2, 2048, 20
+@pytest.mark.parametrize('F_,seed,N', [(3, 1, 2048), (64, 2, 2048), (3, 3, 4096), (64, 4, 4096)])
+def test_dgcnn_knn_agrees_with_oracle(F_, seed, N):
+    """N = 4096 is BASELINE config 2's block: 4096 x 4096 distance tiles per cloud."""
+    B, k = 2, 20
     if F_ == 3:
         x = cloud(B, N, seed).transpose(1, 2).contiguous()
     else:
@@ -202,7 +203,8 @@ def test_dgcnn_knn_agrees_with_oracle(F_, seed):
     assert (got[..., 0] == torch.arange(N)).float().mean() > 0.99   # self first
 
 
-@pytest.mark.parametrize('F_,lo,hi,N', [(3, 0, 8, 2048), (64, -2, 3, 2048), (64, 0, 2, 1000), (3, 0, 4, 333)])
+@pytest.mark.parametrize('F_,lo,hi,N', [(3, 0, 8, 2048), (64, -2, 3, 2048), (64, 0, 2, 1000), (3, 0, 4, 333),
+                                        (3, 0, 16, 4096), (64, -1, 2, 4096)])
 def test_dgcnn_knn_selection_exact_on_integer_grids(F_, lo, hi, N):
     """Integer features make every pd exact in fp32 (MFMA included), so the k best are
     fully determined: larger pd first, exact ties to the lower index.  Coarse grids put
@@ -216,6 +218,17 @@ def test_dgcnn_knn_selection_exact_on_integer_grids(F_, lo, hi, N):
     exp = torch.sort(d.round(), dim=-1, stable=True).indices[..., :k]
     got = ops.knn(x.contiguous().to(DEV), k).cpu().long()
     assert torch.equal(got, exp)
+
+
+def test_dgcnn_knn_vs_reference_graph_at_4096(golden):
+    """The xyz graph the reference itself built for BASELINE config 2's block size
+    (tests/golden/model_dgcnn_color_4096.npz, knn0: B=2, N=4096, k=20)."""
+    z = golden('model_dgcnn_color_4096.npz')
+    xyz = T(z['x'])[:, :3].transpose(1, 2).contiguous()
+    ref = T(z['knn0']).long()
+    got = ops.knn(xyz.to(DEV), 20).cpu().long()
+    same = (got.sort(-1).values == ref.sort(-1).values).all(-1)
+    assert same.float().mean() > 0.995, float(same.float().mean())
 
 
 @pytest.mark.parametrize('dim9', [False, True])

@@ -186,3 +186,76 @@ def test_preprocess_matches_reference(golden, tag, kw):
     assert torch.equal(lab, T(z[f'{tag}_label']))
     assert torch.equal(lengths, T(z[f'{tag}_len'])) and lengths.dtype == torch.int32
     assert cont == bool(z[f'{tag}_cont'])
+
+
+# ---------------------------------------------------------------- configs' real sizes
+@pytest.mark.parametrize('name,ctor,seed', [
+    ('model_pointnext_24576.npz', lambda: R.PointNeXt(14), 4322),          # BASELINE config 5 block size
+])
+def test_pointnext_24576_matches_reference(golden, name, ctor, seed):
+    test_pointnet2_family_matches_reference(golden, name, ctor, seed)
+
+
+def test_dgcnn_color_4096_matches_reference(golden):
+    """BASELINE config 2's block size (N = 4096, k = 20), with the reference's kNN graphs."""
+    z = golden('model_dgcnn_color_4096.npz')
+    m = R.seeded_init_(R.DGCNNWithColor(num_classes=14, k=20), 999)
+    m.train()
+    _dropout_off(m)
+    x = T(z['x']).transpose(1, 2).contiguous().transpose(1, 2)
+    # the first graph (xyz) is recomputed, not replayed: the oracle's kNN must reproduce it
+    assert torch.equal(R.knn(x[:, :3], 20).to(torch.int16), T(z['knn0']))
+    with R.replay(R.Replay(knn_idx=[T(z[f'knn{i}']).long() for i in range(4)])):
+        logits, x5, _ = m(x)
+    assert torch.allclose(logits, T(z['logits']), rtol=1e-4, atol=1e-5)
+    loss = R.masked_onehot_cross_entropy(logits, T(z['labels']).float(), T(z['lengths']).to(torch.int32))
+    assert abs(float(loss) - float(z['loss'])) < 1e-5
+    loss.backward()
+    _check_grads(m, z)
+    _check_buffers(m, z)
+
+
+def test_pointnet_4096_matches_reference(golden):
+    z = golden('model_pointnet_4096.npz')
+    m = R.seeded_init_(R.PointNetSeg(part_classes=14), 78)
+    m.train()
+    probs = m(T(z['x']))
+    assert torch.allclose(probs, T(z['probs']), rtol=1e-4, atol=1e-6)
+    loss = R.masked_onehot_cross_entropy(probs, T(z['labels']), T(z['lengths']))
+    loss.backward()
+    _check_grads(m, z)
+    _check_buffers(m, z)
+
+
+# ---------------------------------------------------------------- section 8(f) row 4: sliding windows
+@pytest.mark.parametrize('tag', ['a', 'b', 'c', 'd'])
+def test_predict_single_scene_windows_match_reference(golden, tag):
+    from scene_models import PerPointLinear
+    z = golden('scene.npz')
+    n, bs, ov = (int(v) for v in z[f'{tag}/meta'])
+    lin = PerPointLinear(6, 13, seed=n)
+    assert torch.equal(lin.weight.data, T(z[f'{tag}/lin_w']))
+    p, c = R.predict_single_scene(lin, T(z[f'{tag}/scene']), batch_size=bs, overlap=ov)
+    assert torch.equal(p, T(z[f'{tag}/lin_pred'])) and torch.equal(c, T(z[f'{tag}/lin_conf']))
+
+
+def scene_dgcnn(z, cls=None):
+    """The eval-mode DGCNNWithColor of golden_scene (seeded weights, randomised running stats)."""
+    seed = int(z['dgcnn/init_seed'])
+    m = R.seeded_init_((cls or R.DGCNNWithColor)(num_classes=13, k=20), seed)
+    g = torch.Generator().manual_seed(seed + 1)
+    for mod in m.modules():
+        if isinstance(mod, (torch.nn.BatchNorm1d, torch.nn.BatchNorm2d)):
+            mod.running_mean.copy_(torch.randn(mod.running_mean.shape, generator=g) * 0.1)
+            mod.running_var.copy_(torch.rand(mod.running_var.shape, generator=g) + 0.5)
+    return m
+
+
+def test_predict_single_scene_dgcnn_matches_reference(golden):
+    z = golden('scene.npz')
+    m = scene_dgcnn(z)
+    knn = [T(z[f'dgcnn/knn{i}']).long() for i in range(sum(k.startswith('dgcnn/knn') for k in z.files))]
+    with R.replay(R.Replay(knn_idx=knn)):
+        p, c = R.predict_single_scene(m, T(z['a/scene']), batch_size=1024, overlap=128)
+    assert torch.equal(p, T(z['dgcnn/pred']))
+    assert torch.allclose(c, T(z['dgcnn/conf']), rtol=1e-5, atol=1e-7)
