@@ -11,10 +11,13 @@
 // Build: one workgroup per cloud, one launch per map.  Every slot of cloud b
 // reads a point of cloud b, so cloud b's entries are exactly positions
 // [b*per_batch, (b+1)*per_batch) and the clouds are independent: LDS histogram of
-// the cloud's targets -> in-LDS exclusive scan -> LDS-atomic scatter of the slots.
-// The order of slots inside one point's list is therefore unspecified; the
-// consumers accumulate in fp64, where the sum of a point's fp32 terms is exact
-// (or rounds at 2^-53) whatever the order, so the fp32 result is reproducible.
+// the cloud's targets -> in-LDS exclusive scan -> LDS-atomic scatter of the slots
+// into scratch (arbitrary order inside a list).  A second kernel sorts every list, one
+// wave per list: a slot's position is the number of the list's slots below it (lists
+// average ~8 entries; the longest, ball-query padding hubs, a few hundred, take
+// ceil(L/64) * L wave steps).  Every list ends up in ascending slot order whatever the
+// scatter's order, and the consumers walk a list in that order (fp64 accumulation),
+// so the backward is bitwise reproducible.
 #include "pcs_common.hpp"
 
 namespace pcs {
@@ -64,7 +67,7 @@ template <bool kLds>
 __global__ __launch_bounds__(kInvThreads) void inverse_index_kernel(const int32_t* __restrict__ idx, int per_batch,
                                                                     int targets, int nbatch,
                                                                     int32_t* __restrict__ offsets,
-                                                                    int32_t* __restrict__ entries, int* gcnt) {
+                                                                    int* gcnt, int32_t* __restrict__ scratch) {
     extern __shared__ int smem[];
     int* wsum = smem;                                   // kInvThreads/64 + 1
     int* cnt = kLds ? smem + 32 : gcnt + (size_t)blockIdx.x * targets;
@@ -83,12 +86,84 @@ __global__ __launch_bounds__(kInvThreads) void inverse_index_kernel(const int32_
     for (int t = tid; t < targets; t += kInvThreads) off[t] = (int32_t)(base + cnt[t]);
     if (b == nbatch - 1 && tid == 0) offsets[(size_t)nbatch * targets] = (int32_t)(base + per_batch);
     __syncthreads();
+    // scatter (list order = atomic arrival order)
+    int32_t* scr = scratch + base;
     for (int s = tid; s < per_batch; s += kInvThreads) {
         const unsigned t = (unsigned)id[s];
-        if (t < (unsigned)targets) {
-            const int pos = atomicAdd(&cnt[t], 1);
-            entries[base + pos] = (int32_t)(base + s);
+        if (t < (unsigned)targets) scr[atomicAdd(&cnt[t], 1)] = (int32_t)(base + s);
+    }
+}
+
+// entries[off[T] ...] = list T's slots in ascending order, one wave per list.  Short lists
+// (<= 64, nearly all of them): each lane's rank = the number of the list's slots below its
+// own, counted over v_readlane broadcasts.  Longer lists (ball-query padding hubs, a few
+// hundred; kNN hubs of zero-padded clouds, thousands): runs of kSortLds slots are bitonic-
+// sorted in the wave's LDS slice; a single run is the answer, several runs are merged by
+// rank (own index in the run + a binary search in every other run).  O(L log^2 L) per list.
+constexpr int kSortLds = 1024;
+
+__device__ inline void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// bitonic sort of v[0, P) (P a power of two >= 128) by one wave
+__device__ void wave_bitonic(int* v, int P, int lane) {
+    for (int k = 2; k <= P; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = lane; i < P / 2; i += 64) {
+                const int lo = 2 * i - (i & (j - 1)), hi = lo + j;
+                const int x = v[lo], y = v[hi];
+                if ((x > y) == ((lo & k) == 0)) { v[lo] = y; v[hi] = x; }
+            }
+            wave_sync();
         }
+}
+
+__global__ __launch_bounds__(256) void inverse_sort_kernel(const int32_t* __restrict__ off, int32_t* scratch,
+                                                           int n_lists, int32_t* __restrict__ entries) {
+    __shared__ int lds[4][kSortLds];
+    const int w = threadIdx.x >> 6;
+    const int T = blockIdx.x * 4 + w;
+    const int lane = threadIdx.x & 63;
+    if (T >= n_lists) return;
+    const int a = off[T], z = off[T + 1], L = z - a;
+    if (L <= 64) {
+        const int v = lane < L ? scratch[a + lane] : 0;
+        int r = 0;
+        for (int e = 0; e < L; ++e) r += __builtin_amdgcn_readlane(v, e) < v;
+        if (lane < L) entries[a + r] = v;
+        return;
+    }
+    int* v = lds[w];
+    for (int r0 = a; r0 < z; r0 += kSortLds) {          // sort each run in LDS
+        const int n = min(kSortLds, z - r0);
+        int P = 128;
+        while (P < n) P <<= 1;
+        for (int i = lane; i < P; i += 64) v[i] = i < n ? scratch[r0 + i] : INT_MAX;
+        wave_sync();
+        wave_bitonic(v, P, lane);
+        int32_t* dst = L <= kSortLds ? entries : scratch;
+        for (int i = lane; i < n; i += 64) dst[r0 + i] = v[i];
+        wave_sync();
+    }
+    if (L <= kSortLds) return;
+    for (int i = a + lane; i < z; i += 64) {             // merge the sorted runs by rank
+        const int x = scratch[i];
+        const int mine = (i - a) / kSortLds;
+        int rank = (i - a) - mine * kSortLds;
+        for (int r0 = a, run = 0; r0 < z; r0 += kSortLds, ++run) {
+            if (run == mine) continue;
+            int lo = r0, hi = min(r0 + kSortLds, z);     // count of run elements < x
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (scratch[mid] < x) lo = mid + 1;
+                else hi = mid;
+            }
+            rank += lo - r0;
+        }
+        entries[a + rank] = x;
     }
 }
 
@@ -182,41 +257,80 @@ __global__ __launch_bounds__(256) void interp_bwd_csr_kernel(const float* __rest
     }
 }
 
+// get_graph_feature backward (dgcnn.py:41-53, rows [x_j - x_i, x_i] of stride ld): point t's
+// gradient = sum_j (g_b[t,j] - g_a[t,j]) over its own k rows, plus g_a of every edge row
+// whose neighbour is t (its inverse-map list, ascending).  One wave per point, lanes over
+// channels, fp64 accumulation in a fixed order.
+__global__ __launch_bounds__(256) void edge_bwd_csr_kernel(const float* __restrict__ gout, int ld, int k,
+                                                           const int32_t* __restrict__ off,
+                                                           const int32_t* __restrict__ ent, int targets, int D,
+                                                           float* __restrict__ gx) {
+    const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (t >= targets) return;
+    const int a = off[t], z = off[t + 1];
+    for (int c0 = 0; c0 < D; c0 += 64) {
+        const int c = c0 + lane;
+        const int cc = c < D ? c : D - 1;
+        double acc = 0.0;
+        for (int j = 0; j < k; ++j) {
+            const float* g = gout + ((size_t)t * k + j) * ld;
+            acc += (double)g[D + cc];
+            acc -= (double)g[cc];
+        }
+        for (int base = a; base < z; base += 64) {
+            const int n = min(64, z - base);
+            const int mine = lane < n ? ent[base + lane] : 0;
+            for (int e = 0; e < n; ++e) acc += (double)gout[(size_t)__builtin_amdgcn_readlane(mine, e) * ld + cc];
+        }
+        if (c < D) gx[(size_t)t * D + c] = (float)acc;
+    }
+}
+
 }  // namespace pcs
 
 using namespace pcs;
 
-// workspace bytes of pcs_inverse_index: none while one cloud's targets fit the LDS counters
+// workspace bytes of pcs_inverse_index: the scatter's scratch lists (one int per slot) and,
+// when one cloud's targets overflow the LDS counters, the global counters
+static size_t inv_ws_bytes(long long n_slots, long long n_targets) {
+    return ((size_t)n_slots * 4 + 255) / 256 * 256 + (size_t)n_targets * 4;
+}
+
 PCS_API int pcs_inverse_index_workspace(long long n_slots, long long n_targets, size_t* bytes) {
     PCS_CHECK_ARG(n_slots >= 1 && n_slots < (1ll << 31) && n_targets >= 1 && n_targets < (1ll << 31) && bytes,
                   "pcs_inverse_index_workspace: bad sizes");
-    *bytes = (size_t)n_targets * 4;   // upper bound (global counters), also valid for the LDS path
+    *bytes = inv_ws_bytes(n_slots, n_targets);
     return 0;
 }
 
 // idx: (B * per_batch) int32 neighbour table, values in [0, targets); offsets (B*targets + 1),
 // entries (B * per_batch): slots reading source (b, p) are entries[offsets[b*targets+p] ..
-// offsets[b*targets+p+1]) (order within a list unspecified).
+// offsets[b*targets+p+1]), ascending.
 PCS_API int pcs_inverse_index(const int32_t* idx, int B, int per_batch, int targets, int32_t* offsets,
                               int32_t* entries, void* workspace, size_t ws_bytes, void* stream) {
     PCS_CHECK_ARG(B >= 1 && per_batch >= 1 && targets >= 1, "pcs_inverse_index: bad sizes");
     const long long n = (long long)B * per_batch, T = (long long)B * targets;
     PCS_CHECK_ARG(n < (1ll << 31) && T < (1ll << 31), "pcs_inverse_index: too many slots/targets");
     PCS_CHECK_ARG(idx && offsets && entries, "pcs_inverse_index: null pointer");
+    PCS_CHECK_ARG(workspace && ws_bytes >= inv_ws_bytes(n, T), "pcs_inverse_index: workspace %zu < %zu bytes",
+                  ws_bytes, inv_ws_bytes(n, T));
     hipStream_t s = as_stream(stream);
+    int32_t* scratch = static_cast<int32_t*>(workspace);
+    int* gcnt = reinterpret_cast<int*>(static_cast<char*>(workspace) + ((size_t)n * 4 + 255) / 256 * 256);
     if (targets <= kInvLdsTargets) {
         static const hipError_t attr = hipFuncSetAttribute(
             reinterpret_cast<const void*>(&inverse_index_kernel<true>), hipFuncAttributeMaxDynamicSharedMemorySize,
             (32 + kInvLdsTargets) * (int)sizeof(int));
         (void)attr;
         hipLaunchKernelGGL(inverse_index_kernel<true>, dim3(B), dim3(kInvThreads), (32 + targets) * sizeof(int), s,
-                           idx, per_batch, targets, B, offsets, entries, (int*)nullptr);
+                           idx, per_batch, targets, B, offsets, (int*)nullptr, scratch);
     } else {
-        PCS_CHECK_ARG(workspace && ws_bytes >= (size_t)T * 4, "pcs_inverse_index: workspace %zu < %lld bytes",
-                      ws_bytes, T * 4);
         hipLaunchKernelGGL(inverse_index_kernel<false>, dim3(B), dim3(kInvThreads), 32 * sizeof(int), s, idx,
-                           per_batch, targets, B, offsets, entries, (int*)workspace);
+                           per_batch, targets, B, offsets, gcnt, scratch);
     }
+    hipLaunchKernelGGL(inverse_sort_kernel, dim3((unsigned)((T + 3) / 4)), dim3(256), 0, s, offsets, scratch, (int)T,
+                       entries);
     return launch_status("pcs_inverse_index");
 }
 
@@ -243,4 +357,17 @@ PCS_API int pcs_interp_bwd_csr(const float* grad_out, int ld_gout, int col_off, 
     hipLaunchKernelGGL(interp_bwd_csr_kernel, dim3((unsigned)((targets + 3) / 4)), dim3(256), 0, as_stream(stream),
                        grad_out, ld_gout, col_off, dist, offsets, entries, (int)targets, D, grad_pts);
     return launch_status("pcs_interp_bwd_csr");
+}
+
+// grad_x (B, N, D) = backward of get_graph_feature over the inverse map of idx (targets N)
+// (overwrites).  Reference: dgcnn.py:41-53.
+PCS_API int pcs_edge_bwd(const float* grad_out, int ld_gout, const int32_t* offsets, const int32_t* entries, int B,
+                         int N, int k, int D, float* grad_x, void* stream) {
+    PCS_CHECK_ARG(B >= 1 && N >= 1 && k >= 1 && D >= 1 && ld_gout >= 2 * D, "pcs_edge_bwd: bad sizes");
+    const long long targets = (long long)B * N;
+    PCS_CHECK_ARG(targets * k < (1ll << 31) && targets * D < (1ll << 31), "pcs_edge_bwd: too many elements");
+    PCS_CHECK_ARG(grad_out && offsets && entries && grad_x, "pcs_edge_bwd: null pointer");
+    hipLaunchKernelGGL(edge_bwd_csr_kernel, dim3((unsigned)((targets + 3) / 4)), dim3(256), 0, as_stream(stream),
+                       grad_out, ld_gout, k, offsets, entries, (int)targets, D, grad_x);
+    return launch_status("pcs_edge_bwd");
 }

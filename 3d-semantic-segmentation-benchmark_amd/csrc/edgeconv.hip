@@ -237,16 +237,16 @@ static const int kEdgeRedRows = 512;
 
 using namespace pcs;
 
-PCS_API int pcs_edgeconv_workspace(int B, int N, int Cout, int backward, size_t* bytes) {
-    PCS_CHECK_ARG(bytes && B >= 1 && N >= 1 && Cout >= 4, "pcs_edgeconv_workspace: bad arguments");
+PCS_API int pcs_edgeconv_workspace(int B, int N, int C, int Cout, int backward, size_t* bytes) {
+    PCS_CHECK_ARG(bytes && B >= 1 && N >= 1 && C >= 1 && Cout >= 4, "pcs_edgeconv_workspace: bad arguments");
     const long long G = (long long)B * N;
     if (!backward) {
         *bytes = (size_t)fwd_blocks(G, Cout) * 2 * Cout * sizeof(double);
     } else {
         const long long nb = (G + kEdgeRedRows - 1) / kEdgeRedRows;
-        // G (interleaved dY|dP) + D + kB/kC + reduce partials
+        // G (interleaved dY|dP) + D + kB/kC + reduce partials + the weight gradient's partial tiles
         *bytes = (size_t)G * 2 * Cout * 4 + (size_t)G * Cout * 4 + (size_t)2 * Cout * 4 + 256 +
-                 (size_t)nb * 2 * Cout * sizeof(double);
+                 (size_t)nb * 2 * Cout * sizeof(double) + 256 + wgrad_ws_bytes(2 * Cout, C, (int)G);
     }
     return 0;
 }
@@ -269,7 +269,7 @@ PCS_API int pcs_edgeconv_fwd(const float* X, int ldx, int C, const int32_t* idx,
     const long long G = (long long)B * N;
     PCS_CHECK_ARG(G * k < (1ll << 31), "pcs_edgeconv_fwd: too many edges");
     size_t need = 0;
-    pcs_edgeconv_workspace(B, N, Cout, 0, &need);
+    pcs_edgeconv_workspace(B, N, C, Cout, 0, &need);
     PCS_CHECK_ARG(ws_bytes >= need, "pcs_edgeconv_fwd: workspace %zu < %zu bytes", ws_bytes, need);
     hipStream_t st = as_stream(stream);
     const pcs_operand xa = plain(X, ldx);
@@ -302,7 +302,7 @@ PCS_API int pcs_edgeconv_bwd(const float* X, int ldx, int C, const int32_t* csr_
     PCS_CHECK_ARG(!dX || (C % 4 == 0 && lddx >= C && lddx % 4 == 0), "pcs_edgeconv_bwd: dX needs C %% 4 == 0");
     const long long G = (long long)B * N;
     size_t need = 0;
-    pcs_edgeconv_workspace(B, N, Cout, 1, &need);
+    pcs_edgeconv_workspace(B, N, C, Cout, 1, &need);
     PCS_CHECK_ARG(ws_bytes >= need, "pcs_edgeconv_bwd: workspace %zu < %zu bytes", ws_bytes, need);
     hipStream_t st = as_stream(stream);
     char* w = static_cast<char*>(workspace);
@@ -315,6 +315,9 @@ PCS_API int pcs_edgeconv_bwd(const float* X, int ldx, int C, const int32_t* csr_
     w = reinterpret_cast<char*>(((uintptr_t)w + 255) & ~(uintptr_t)255);
     double* part = reinterpret_cast<double*>(w);
     const int nb = (int)((G + kEdgeRedRows - 1) / kEdgeRedRows);
+    w += (size_t)nb * 2 * Cout * sizeof(double);
+    w = reinterpret_cast<char*>(((uintptr_t)w + 255) & ~(uintptr_t)255);
+    const size_t wg_bytes = wgrad_ws_bytes(2 * Cout, C, (int)G);
     hipLaunchKernelGGL(edgeconv_bwd_reduce_kernel, dim3(nb, (Cout + 63) / 64), dim3(256), 0, st, dout, pz, G, Cout,
                        coef, slope, kEdgeRedRows, part);
     bn_bwd_finalize_launch(part, nb, Cout, G * k, coef, coef + 3 * Cout, dgamma, dbeta, kBC, kBC + Cout, 1, st);
@@ -328,7 +331,7 @@ PCS_API int pcs_edgeconv_bwd(const float* X, int ldx, int C, const int32_t* csr_
     // dW (as 2Cout x C) += G^T X ;  dX = G W_int
     const pcs_operand ga = plain(Gd, 2 * Cout);
     const pcs_operand xa = plain(X, ldx);
-    if (int e = pcs_wgrad(&ga, 2 * Cout, &xa, C, (int)G, dW, nullptr, stream)) return e;
+    if (int e = wgrad_launch(&ga, 2 * Cout, &xa, C, (int)G, dW, nullptr, w, wg_bytes, stream)) return e;
     if (dX)
         if (int e = gemm_rows_ex(&ga, (int)G, 2 * Cout, W, C, 1, nullptr, dX, lddx, C, nullptr, nullptr, nullptr,
                                  stream))

@@ -123,6 +123,8 @@ struct BwdScratch {
     float* alpha[2];
     float* wt;
     float* dA[2];
+    char* wg;              // wgrad partial tiles (shared by the call's wgrads: one side stream)
+    size_t wg_bytes;
 };
 
 static size_t carve_backward(Carve& cv, int M, int kin, int ldx, const pcs_mlp_layer* L, int nl, int pool_k,
@@ -139,15 +141,17 @@ static size_t carve_backward(Carve& cv, int M, int kin, int ldx, const pcs_mlp_l
     s.wt = cv.take<float>(wt);
     s.dA[0] = cv.take<float>(da);
     s.dA[1] = cv.take<float>(da);
+    size_t wg = 0;
+    for (int l = 0; l < nl; ++l)
+        if (L[l].dW) wg = std::max(wg, wgrad_ws_bytes((int)L[l].cout, (int)L[l].cin, M));
+    s.wg_bytes = wg;
+    s.wg = cv.take<char>(wg);
     if (out) *out = s;
     return cv.used;
 }
 
 // the top layer's pooling is fused into its GEMM epilogue (z-space max/min + pool_finalize)
-static bool fused_pool(int pool_k) {
-    static const bool on = [] { const char* e = getenv("PCS_FUSED_POOL"); return !e || atoi(e) != 0; }();
-    return on && (pool_k == 16 || pool_k == 32) && engine_impl() == 0;
-}
+static bool fused_pool(int pool_k) { return pool_k == 16 || pool_k == 32; }
 
 struct FwdScratch {
     double* part;
@@ -173,16 +177,17 @@ static size_t carve_forward(Carve& cv, int M, int kin, const pcs_mlp_layer* L, i
 // stream (forked from the caller's stream by an event), so it overlaps the dgrad and the
 // BN-backward finalize of the same layer; the caller's stream joins it before the next
 // layer's dgrad, whose outputs (the dA buffer and the BN-backward coefficients) recycle
-// the buffers this wgrad reads.  PCS_WGRAD_OVERLAP=0 keeps everything on one stream.
+// the buffers this wgrad reads.  A backward call holds its lane's lock from the first fork to
+// the final join, so concurrent callers on one device never share the event ring; all of a
+// call's wgrads run in order on the side stream and share one partial-tile workspace.
 struct WgradLane {
     hipStream_t side = nullptr;
     hipEvent_t ev[8] = {};
     int next = 0;
+    std::mutex use;
 };
 
 static WgradLane* wgrad_lane() {
-    static const bool on = [] { const char* e = getenv("PCS_WGRAD_OVERLAP"); return !e || atoi(e) != 0; }();
-    if (!on) return nullptr;
     static WgradLane lanes[16];
     static std::mutex mu;
     int dev = 0;
@@ -237,8 +242,8 @@ static int check_layers(int M, int kin, int ldx, const pcs_mlp_layer* L, int nl,
         PCS_CHECK_ARG(L[l].cin == cin, "%s: layer %d: cin=%lld, expected %d", who, l, (long long)L[l].cin, cin);
         PCS_CHECK_ARG(L[l].cout >= 4 && L[l].cout % 4 == 0, "%s: layer %d: cout=%lld must be a multiple of 4", who,
                       l, (long long)L[l].cout);
-        PCS_CHECK_ARG(L[l].ldw >= L[l].cin && (L[l].ldw % 4 == 0 || (l == 0 && engine_impl() == 0)),
-                      "%s: layer %d: ldw=%lld (a multiple of 4 except for the first layer on the LDS engine)", who, l,
+        PCS_CHECK_ARG(L[l].ldw >= L[l].cin && (L[l].ldw % 4 == 0 || l == 0),
+                      "%s: layer %d: ldw=%lld (a multiple of 4 except for the first layer)", who, l,
                       (long long)L[l].ldw);
         PCS_CHECK_ARG(L[l].use_batch || (L[l].run_mean && L[l].run_var),
                       "%s: layer %d: eval-mode BatchNorm needs running statistics", who, l);
@@ -355,6 +360,8 @@ PCS_API int pcs_mlp_backward(const float* X, int ldx, int kin, int M, const pcs_
 
     int da = 0;
     WgradLane* lane = wgrad_lane();
+    std::unique_lock<std::mutex> lane_lock;
+    if (lane) lane_lock = std::unique_lock<std::mutex>(lane->use);
     hipEvent_t pending = nullptr;          // the last wgrad launched on the side stream
     hipEvent_t prev = nullptr;             // the wgrad of the layer above (joined before this dgrad)
     auto join = [&]() {
@@ -362,6 +369,11 @@ PCS_API int pcs_mlp_backward(const float* X, int ldx, int kin, int M, const pcs_
             (void)hipStreamWaitEvent(st, pending, 0);
             pending = nullptr;
         }
+    };
+    // every exit after the first fork joins the side stream (its work reads this call's buffers)
+    auto fail = [&](int e) {
+        join();
+        return e;
     };
     for (int l = nl - 1; l >= 0; --l) {
         const pcs_mlp_layer& P = layers[l];
@@ -374,28 +386,24 @@ PCS_API int pcs_mlp_backward(const float* X, int ldx, int kin, int M, const pcs_
                 (void)hipStreamWaitEvent(lane->side, ready, 0);
                 ws_stream = lane->side;
             }
-            if (l > 0) {
-                const pcs_mlp_layer& Q = layers[l - 1];
-                const pcs_operand y = bnact_op(Q.Z, Cin, Q);
-                if (int e = pcs_wgrad(&xop, C, &y, Cin, M, P.dW, P.db, ws_stream)) { join(); return e; }
-            } else {
-                const pcs_operand y = plain_op(X, ldx);
-                if (int e = pcs_wgrad(&xop, C, &y, kin, M, P.dW, P.db, ws_stream)) { join(); return e; }
-            }
-            if (lane) {
+            const pcs_mlp_layer* Q = l > 0 ? &layers[l - 1] : nullptr;
+            const pcs_operand y = Q ? bnact_op(Q->Z, Cin, *Q) : plain_op(X, ldx);
+            const int e = pcs::wgrad_launch(&xop, C, &y, Cin, M, P.dW, P.db, S.wg, S.wg_bytes, ws_stream);
+            if (lane) {                    // recorded even on error, so the join below covers it
                 prev = pending;
                 pending = lane_event(lane);
                 (void)hipEventRecord(pending, lane->side);
             }
+            if (e) return fail(e);
         }
         if (prev) {                        // the layer above's wgrad read the buffers this dgrad recycles
             (void)hipStreamWaitEvent(st, prev, 0);
             prev = nullptr;
         }
         if (l == 0 && !dX) break;
-        // dgrad B operand: B[k = cout][n = cin] = W[k][n] -- read k-major straight from W by the
-        // LDS engine (bt = 1); the LDS-free family takes the transpose Wt (cin x cout)
-        const bool bt = engine_impl() == 0 && P.ldw % 4 == 0;
+        // dgrad B operand: B[k = cout][n = cin] = W[k][n], read k-major straight from W (bt = 1);
+        // a first layer whose row stride is not a multiple of 4 goes through the transpose Wt
+        const bool bt = P.ldw % 4 == 0;
         const float* Bw = P.W;
         int ldb = (int)P.ldw;
         if (!bt) {
@@ -410,19 +418,19 @@ PCS_API int pcs_mlp_backward(const float* X, int ldx, int kin, int M, const pcs_
             const int nbg = pcs_gemm_row_blocks_dgrad(M, Cin);
             pcs_operand epi = bnbwd_op(nullptr, 0, Q, nullptr, nullptr);
             if (int e = gemm_rows_ex(&xop, M, C, Bw, ldb, bt, nullptr, dA, Cin, Cin, nullptr, &epi, S.part, stream))
-                return e;
+                return fail(e);
             pp ^= 1;
             const float* sq = Q.coef;
             if (int e = pcs_bn_bwd_finalize(S.part, nbg, Cin, M, sq, sq + 3 * Cin, Q.dgamma, Q.dbeta, S.kb[pp],
                                             S.alpha[pp], 1, stream))
-                return e;
+                return fail(e);
             if (!Q.use_batch) { zero_f32(S.kb[pp], Cin, st); zero_f32(S.alpha[pp], Cin, st); }
             xop = bnbwd_op(dA, Cin, Q, S.alpha[pp], S.kb[pp]);
             da ^= 1;
         } else {
             zero_cols(dX, M, ldx, kin, st);      // the GEMM writes columns [0, kin)
             if (int e = gemm_rows_ex(&xop, M, C, Bw, ldb, bt, nullptr, dX, ldx, kin, nullptr, nullptr, nullptr, stream))
-                return e;
+                return fail(e);
         }
     }
     join();

@@ -258,9 +258,8 @@ PCS_API int pcs_fps(const float* xyz, int B, int N, int C, const int32_t* start,
     PCS_CHECK_ARG(xyz && start && out_idx && out_xyz, "pcs_fps: null pointer");
     if (B == 0) return 0;
     hipStream_t s = as_stream(stream);
-    // threads per cloud: PCS_FPS_BLOCK (64/256/512/1024) overrides the default, for tuning
-    static const int forced = [] { const char* e = getenv("PCS_FPS_BLOCK"); return e ? atoi(e) : 0; }();
-    const int blk = forced ? forced : (N <= 256 ? 64 : (N <= 2048 ? 256 : (N <= 8192 ? 512 : 1024)));
+    // threads per cloud by size (round-1 sweep)
+    const int blk = N <= 256 ? 64 : (N <= 2048 ? 256 : (N <= 8192 ? 512 : 1024));
     const int ppt = (N + blk - 1) / blk;
 #define PCS_FPS_CASE(BL, PP) if (blk == BL && ppt <= PP) { launch_fps<BL, PP>(xyz, B, N, C, start, out_idx, out_xyz, s); } else
     PCS_FPS_CASE(64, 1) PCS_FPS_CASE(64, 2) PCS_FPS_CASE(64, 4) PCS_FPS_CASE(64, 8)

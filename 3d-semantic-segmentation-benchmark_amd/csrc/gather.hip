@@ -77,17 +77,6 @@ __global__ __launch_bounds__(256) void group_fwd_q_kernel(const float* __restric
     }
 }
 
-__global__ void group_bwd_kernel(const float* __restrict__ gout, const int* __restrict__ idx, int C, int N, int K,
-                                 int D, int W, float* __restrict__ gfeats, long long total) {
-    for (long long t = gtid(); t < total; t += gstride()) {
-        const long long row = t / D;
-        const int ch = (int)(t - row * D);
-        const int b = (int)(row / ((long long)K * C));
-        const int p = idx[row];
-        atomicAdd(&gfeats[((long long)b * N + p) * D + ch], gout[row * W + 3 + ch]);
-    }
-}
-
 // ------------------------------------------------------------------ max over K
 __global__ void maxk_fwd_kernel(const float* __restrict__ x, int K, int Ch, float* __restrict__ out,
                                 unsigned char* __restrict__ arg, long long total) {
@@ -174,25 +163,6 @@ __global__ __launch_bounds__(256) void interp_cat_q_kernel(const float* __restri
     }
 }
 
-__global__ void interp_bwd_kernel(const float* __restrict__ gout, const int* __restrict__ idx,
-                                  const float* __restrict__ dist, int N, int M, int D, int ld_gout, int col_off,
-                                  float* __restrict__ gpts, long long total) {
-    for (long long t = gtid(); t < total; t += gstride()) {
-        const long long row = t / D;
-        const int ch = (int)(t - row * D);
-        const int b = (int)(row / N);
-        const float w0 = 1.0f / (dist[row * 3 + 0] + 1e-9f);
-        const float w1 = 1.0f / (dist[row * 3 + 1] + 1e-9f);
-        const float w2 = 1.0f / (dist[row * 3 + 2] + 1e-9f);
-        const float nrm = (w0 + w1) + w2;
-        const float gq = gout[row * ld_gout + col_off + ch] / nrm;
-        float* G = gpts + (long long)b * M * D + ch;
-        atomicAdd(&G[(long long)idx[row * 3 + 0] * D], gq * w0);
-        atomicAdd(&G[(long long)idx[row * 3 + 1] * D], gq * w1);
-        atomicAdd(&G[(long long)idx[row * 3 + 2] * D], gq * w2);
-    }
-}
-
 // ------------------------------------------------------------------ EdgeConv graph feature
 // out row (b,i,j) = [x[nbr] - x[i], x[i]]  (2D channels, row stride W >= 2D, pad zeroed),
 // x point-major (B, N, D)
@@ -211,25 +181,6 @@ __global__ void edge_fwd_kernel(const float* __restrict__ x, const int* __restri
         } else {
             out[t] = xi;
         }
-    }
-}
-
-// gx[i] += sum_j (g_b[i,j] - g_a[i,j]);  gx[nbr] += g_a[i,j]
-__global__ void edge_bwd_kernel(const float* __restrict__ gout, const int* __restrict__ idx, int N, int k, int D,
-                                int W, float* __restrict__ gx, long long total) {
-    for (long long t = gtid(); t < total; t += gstride()) {
-        const long long pi = t / D;             // b*N + i
-        const int ch = (int)(t - pi * D);
-        const int b = (int)(pi / N);
-        float acc = 0.f;
-        for (int j = 0; j < k; ++j) {
-            const long long row = pi * k + j;
-            const float ga = gout[row * W + ch];
-            const float gb = gout[row * W + D + ch];
-            acc += gb - ga;
-            atomicAdd(&gx[((long long)b * N + idx[row]) * D + ch], ga);
-        }
-        atomicAdd(&gx[pi * D + ch], acc);
     }
 }
 
@@ -252,19 +203,6 @@ PCS_API int pcs_group_fwd(const float* xyz, const float* feats, const float* cen
     hipLaunchKernelGGL(group_fwd_kernel, grid_for(total), dim3(256), 0, as_stream(stream), xyz, feats, centroids,
                        idx, C, N, K, D, r, normalize, out, ld_out, total);
     return launch_status("pcs_group_fwd");
-}
-
-// Backward of the feature gather: grad_feats (B, N, D) += scatter of grad_out[..., 3:]
-// (grad_feats must be zeroed by the caller).
-PCS_API int pcs_group_bwd(const float* grad_out, int ld_gout, const int32_t* idx, int B, int N, int C, int K, int D,
-                          float* grad_feats, void* stream) {
-    PCS_CHECK_ARG(B >= 0 && N >= 1 && C >= 0 && K >= 1 && D >= 0 && ld_gout >= 3 + D, "pcs_group_bwd: bad sizes");
-    const long long total = (long long)B * C * K * D;
-    if (total == 0) return 0;
-    PCS_CHECK_ARG(grad_out && idx && grad_feats, "pcs_group_bwd: null pointer");
-    hipLaunchKernelGGL(group_bwd_kernel, grid_for(total), dim3(256), 0, as_stream(stream), grad_out, idx, C, N, K, D,
-                       ld_gout, grad_feats, total);
-    return launch_status("pcs_group_bwd");
 }
 
 // Reference: common.py:85-86.  x (G*K, Ch) -> out (G, Ch), argmax (G, Ch) u8 (first max).
@@ -311,19 +249,6 @@ PCS_API int pcs_interp_fwd(const float* pts, const int32_t* idx, const float* di
     return launch_status("pcs_interp_fwd");
 }
 
-// grad_pts (B, M, D) += IDW-weighted scatter (caller zeroes grad_pts).
-PCS_API int pcs_interp_bwd(const float* grad_out, const int32_t* idx, const float* dist, int B, int N, int M, int D,
-                           int ld_gout, int col_off, float* grad_pts, void* stream) {
-    PCS_CHECK_ARG(B >= 0 && N >= 0 && M >= 3 && D >= 1 && ld_gout >= col_off + D && col_off >= 0,
-                  "pcs_interp_bwd: bad sizes");
-    const long long total = (long long)B * N * D;
-    if (total == 0) return 0;
-    PCS_CHECK_ARG(grad_out && idx && dist && grad_pts, "pcs_interp_bwd: null pointer");
-    hipLaunchKernelGGL(interp_bwd_kernel, grid_for(total), dim3(256), 0, as_stream(stream), grad_out, idx, dist, N, M,
-                       D, ld_gout, col_off, grad_pts, total);
-    return launch_status("pcs_interp_bwd");
-}
-
 // Reference: dgcnn.py:41-53.  x (B, N, D) point-major; idx (B, N, k); out (B*N*k, 2D).
 PCS_API int pcs_edge_fwd(const float* x, const int32_t* idx, int B, int N, int k, int D, float* out, int ld_out,
                          void* stream) {
@@ -334,18 +259,6 @@ PCS_API int pcs_edge_fwd(const float* x, const int32_t* idx, int B, int N, int k
     hipLaunchKernelGGL(edge_fwd_kernel, grid_for(total), dim3(256), 0, as_stream(stream), x, idx, N, k, D, ld_out, out,
                        total);
     return launch_status("pcs_edge_fwd");
-}
-
-// grad_x (B, N, D) += backward of the graph feature (caller zeroes grad_x).
-PCS_API int pcs_edge_bwd(const float* grad_out, int ld_gout, const int32_t* idx, int B, int N, int k, int D,
-                         float* grad_x, void* stream) {
-    PCS_CHECK_ARG(B >= 0 && N >= 1 && k >= 1 && D >= 1 && ld_gout >= 2 * D, "pcs_edge_bwd: bad sizes");
-    const long long total = (long long)B * N * D;
-    if (total == 0) return 0;
-    PCS_CHECK_ARG(grad_out && idx && grad_x, "pcs_edge_bwd: null pointer");
-    hipLaunchKernelGGL(edge_bwd_kernel, grid_for(total), dim3(256), 0, as_stream(stream), grad_out, idx, N, k, D,
-                       ld_gout, grad_x, total);
-    return launch_status("pcs_edge_bwd");
 }
 
 // Reference FeaturePropagation (common.py:115-122, 238-240): rows (B*N, ld_out) =

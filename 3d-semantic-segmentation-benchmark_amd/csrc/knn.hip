@@ -488,20 +488,12 @@ __global__ __launch_bounds__(256, 2) void knn_tile_kernel(const float* __restric
 template <int K>
 constexpr bool knn_tiled() { return (KNN_NMAX - K) / 2 - 1 >= 16; }
 
-// PCS_KNN_LEGACY=1 selects the thread-per-row kernel for every k (A/B and diagnostics)
-static bool knn_legacy() {
-    static const bool v = [] { const char* e = getenv("PCS_KNN_LEGACY"); return e && e[0] == '1'; }();
-    return v;
-}
-
 template <int F, int K>
 static void launch_knn(const float* x, int B, int N, int* out, hipStream_t s) {
     if constexpr (knn_tiled<K>()) {
-        if (!knn_legacy()) {
-            hipLaunchKernelGGL((knn_tile_kernel<F, K>), dim3((N + KNN_QROWS - 1) / KNN_QROWS, B), dim3(256),
-                               0, s, x, N, out);
-            return;
-        }
+        hipLaunchKernelGGL((knn_tile_kernel<F, K>), dim3((N + KNN_QROWS - 1) / KNN_QROWS, B), dim3(256), 0, s, x,
+                           N, out);
+        return;
     }
     hipLaunchKernelGGL((knn_kernel<F, K>), dim3((N + 255) / 256, B), dim3(256), 0, s, x, N, out);
 }

@@ -16,8 +16,8 @@
 //  * pooling reads Z once: max_k act(z*s+t) with the first argmax;
 //  * backward: dgrad GEMM (dA_prev = dZ . W) whose epilogue already reduces the
 //    previous layer's BN-backward sums (sum dy, sum dy*xhat); wgrad GEMM
-//    (dW = dZ^T . T(A_prev)) split over rows with fp32 atomics; dZ is
-//    materialised once per layer by an elementwise kernel.
+//    (dW = dZ^T . T(A_prev)) split over rows, each split's partial tile stored and
+//    summed in a fixed order by a second kernel (deterministic: no float atomics).
 // Statistics are accumulated in fp64 (as ATen's CPU batch norm does).
 #include "mlp_common.hpp"
 
@@ -299,13 +299,16 @@ __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(GemmArgs g) {
 }
 
 // ------------------------------------------------------------------ weight gradient
-// dW[n][k] += sum_r X[r][n] * Y[r][k] ; db[n] += sum_r X[r][n]   (rows split over gridDim.x)
+// part[split][n][k] = sum_{r in split} X[r][n] * Y[r][k] ; pdb[split][n] = sum_{r in split} X[r][n]
+// (rows split over gridDim.x; wgrad_reduce_kernel adds the splits into dW / db in split order)
 // X = the layer's dZ (through its BNBWD/POOLBWD transform: rebuilt from the output
 // gradient and Z on load), Y = the layer's input (through the previous layer's BNACT).
 // Same LDS/fragment scheme as the row GEMM with the ROW index as the reduction
 // axis: X and Y slabs of 32 rows are stored transposed ([channel][row], 144-B
 // stride) so each lane's fragment is 16 consecutive rows.  Each block accumulates its
-// row range in the MFMA's fp32 accumulators and blocks combine with fp32 atomics.
+// row range in the MFMA's fp32 accumulators and stores its partial tile: every element of
+// part[split] is written by exactly one block, and the reduce sums the splits in order, so
+// two identical backward passes give bitwise-identical gradients.
 
 //
 // Wave grid: WGO x WGI waves split the BO x BI tile and WR = 4 / (WGO * WGI) waves split
@@ -313,14 +316,15 @@ __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(GemmArgs g) {
 // disjoint row quarters/halves of the slab and add their partial tiles separately).
 template <int BO, int BI, int XM, int YM, int NS>
 __global__ __launch_bounds__(256, 2) void wgrad_kernel(Operand xo, int N, Operand yo, int K, int M,
-                                                       int rows_per_block, float* __restrict__ dW,
-                                                       float* __restrict__ db) {
+                                                       int rows_per_block, float* __restrict__ part,
+                                                       float* __restrict__ pdb) {
     constexpr int BR = 32, LDR = BR + 4;
     constexpr int WGO = BO >= 64 ? 2 : 1, WGI = BI >= 64 ? 2 : 1, WR = 4 / (WGO * WGI);
     constexpr int QPW = 4 / WR;                       // 4-row fragment groups (q) per wave per half-slab
     constexpr int TM = BO / WGO / 32, TN = BI / WGI / 32;
     constexpr int XV = BR * BO / 4 / 256, YV = BR * BI / 4 / 256;
     static_assert(TM >= 1 && TN >= 1 && XV >= 1 && YV >= 1, "wgrad tile");
+    static_assert(WR == 1, "one wave per output fragment: the partial tile is stored, not accumulated");
     __shared__ __attribute__((aligned(16))) float Xs[2][BO][LDR];
     __shared__ __attribute__((aligned(16))) float Ys[2][BI][LDR];
     __shared__ float dbs[256 / (BO / 4)][BO];
@@ -332,7 +336,8 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(Operand xo, int N, Operan
     const int k0 = (blockIdx.y % tiles_i) * BI;
     const int rb = blockIdx.x * rows_per_block;
     const int re = min(M, rb + rows_per_block);
-    const bool do_db = (db != nullptr) && (k0 == 0);
+    const bool do_db = (pdb != nullptr) && (k0 == 0);
+    float* __restrict__ tile_part = part + (size_t)blockIdx.x * N * K;
 
     // Transposed LDS stores without bank conflicts: each 32-lane half stores 4 rows x 8
     // channel quads, and the row index is XOR-swizzled in 4-row groups by the channel
@@ -458,7 +463,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(Operand xo, int N, Operan
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int n = n0 + wo * (BO / WGO) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                if (n < N && kcol < K) atomicAdd(&dW[(size_t)n * K + kcol], acc[i][j][r]);
+                if (n < N && kcol < K) tile_part[(size_t)n * K + kcol] = acc[i][j][r];
             }
         }
     if (do_db) {
@@ -471,8 +476,46 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(Operand xo, int N, Operan
             float a = 0.f;
 #pragma unroll
             for (int gi = 0; gi < 256 / (BO / 4); ++gi) a += dbs[gi][tid];
-            atomicAdd(&db[n0 + tid], a);
+            pdb[(size_t)blockIdx.x * N + n0 + tid] = a;
         }
+    }
+}
+
+// dW[e] += sum_{s < splits} part[s][e] (e < nk) and db[e] += sum_s pdb[s][e] (e < N, the
+// blocks past dW's): the weight and bias gradients from the wgrad's per-split partials.
+// 16 elements per block, 16 threads per element: thread g sums splits g, g + 16, ... (fp64,
+// 4 interleaved accumulators), then the 16 thread sums are added in order through LDS -- a
+// fixed summation tree, so the result is reproducible bit for bit.
+constexpr int kRedElems = 16, kRedGroups = 16;
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, int splits, long long nk,
+                                                           float* __restrict__ dW, const float* __restrict__ pdb,
+                                                           int N, float* __restrict__ db) {
+    __shared__ double red[kRedGroups][kRedElems];
+    const int el = threadIdx.x % kRedElems, g = threadIdx.x / kRedElems;
+    const long long wblocks = (nk + kRedElems - 1) / kRedElems;
+    const bool bias = blockIdx.x >= wblocks;
+    const float* src = bias ? pdb : part;
+    float* out = bias ? db : dW;
+    const long long n = bias ? N : nk;
+    const long long e = (bias ? blockIdx.x - wblocks : (long long)blockIdx.x) * kRedElems + el;
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+    if (e < n) {
+        int sp = g;
+        for (; sp + 3 * kRedGroups < splits; sp += 4 * kRedGroups) {
+            a0 += (double)src[(size_t)sp * n + e];
+            a1 += (double)src[(size_t)(sp + kRedGroups) * n + e];
+            a2 += (double)src[(size_t)(sp + 2 * kRedGroups) * n + e];
+            a3 += (double)src[(size_t)(sp + 3 * kRedGroups) * n + e];
+        }
+        for (; sp < splits; sp += kRedGroups) a0 += (double)src[(size_t)sp * n + e];
+    }
+    red[g][el] = (a0 + a1) + (a2 + a3);
+    __syncthreads();
+    if (g == 0 && e < n) {
+        double a = red[0][el];
+#pragma unroll
+        for (int i = 1; i < kRedGroups; ++i) a += red[i][el];
+        out[e] = (float)((double)out[e] + a);
     }
 }
 
@@ -767,48 +810,26 @@ static void launch_gemm(const GemmArgs& g, int gx, bool bt, hipStream_t s) {
     }
 }
 
-// register stages of thin wgrad tiles (PCS_WGRAD_STAGES: 2 or 4) and whether 32-wide
-// wgrad tiles are used for <= 32 channels (PCS_WGRAD_THIN32)
-static int wgrad_stages() {
-    static const int v = [] { const char* e = getenv("PCS_WGRAD_STAGES"); return e && atoi(e) == 4 ? 4 : 2; }();
-    return v;
-}
-static int wgrad_thin32() {
-    static const int v = [] { const char* e = getenv("PCS_WGRAD_THIN32"); return e ? atoi(e) : 0; }();
-    return v;
-}
-
 template <int BO, int BI, int XM>
 static void launch_wgrad_y(dim3 grid, hipStream_t st, const Operand& x, int N, const Operand& y, int K, int M,
-                           int rows, float* dW, float* db) {
-    // thin tiles keep wgrad_stages() slabs of loads in flight, wide tiles one
-    if constexpr (BO <= 64 && BI <= 64) {
-        if (wgrad_stages() == 4) {
-            if (y.mode == OP_BNACT)
-                hipLaunchKernelGGL((wgrad_kernel<BO, BI, XM, OP_BNACT, 4>), grid, dim3(256), 0, st, x, N, y, K, M, rows,
-                                   dW, db);
-            else
-                hipLaunchKernelGGL((wgrad_kernel<BO, BI, XM, OP_PLAIN, 4>), grid, dim3(256), 0, st, x, N, y, K, M, rows,
-                                   dW, db);
-            return;
-        }
-    }
+                           int rows, float* part, float* pdb) {
+    // thin tiles keep two slabs of loads in flight, wide tiles one
     constexpr int NS = BO <= 64 && BI <= 64 ? 2 : 1;
     if (y.mode == OP_BNACT)
-        hipLaunchKernelGGL((wgrad_kernel<BO, BI, XM, OP_BNACT, NS>), grid, dim3(256), 0, st, x, N, y, K, M, rows, dW,
-                           db);
+        hipLaunchKernelGGL((wgrad_kernel<BO, BI, XM, OP_BNACT, NS>), grid, dim3(256), 0, st, x, N, y, K, M, rows, part,
+                           pdb);
     else
-        hipLaunchKernelGGL((wgrad_kernel<BO, BI, XM, OP_PLAIN, NS>), grid, dim3(256), 0, st, x, N, y, K, M, rows, dW,
-                           db);
+        hipLaunchKernelGGL((wgrad_kernel<BO, BI, XM, OP_PLAIN, NS>), grid, dim3(256), 0, st, x, N, y, K, M, rows, part,
+                           pdb);
 }
 
 template <int BO, int BI>
 static void launch_wgrad(dim3 grid, hipStream_t st, const Operand& x, int N, const Operand& y, int K, int M, int rows,
-                         float* dW, float* db) {
+                         float* part, float* pdb) {
     switch (x.mode) {
-    case OP_PLAIN: launch_wgrad_y<BO, BI, OP_PLAIN>(grid, st, x, N, y, K, M, rows, dW, db); break;
-    case OP_BNBWD: launch_wgrad_y<BO, BI, OP_BNBWD>(grid, st, x, N, y, K, M, rows, dW, db); break;
-    default: launch_wgrad_y<BO, BI, OP_POOLBWD>(grid, st, x, N, y, K, M, rows, dW, db); break;
+    case OP_PLAIN: launch_wgrad_y<BO, BI, OP_PLAIN>(grid, st, x, N, y, K, M, rows, part, pdb); break;
+    case OP_BNBWD: launch_wgrad_y<BO, BI, OP_BNBWD>(grid, st, x, N, y, K, M, rows, part, pdb); break;
+    default: launch_wgrad_y<BO, BI, OP_POOLBWD>(grid, st, x, N, y, K, M, rows, part, pdb); break;
     }
 }
 
@@ -821,40 +842,21 @@ using namespace pcs;
 // bwd: the A operand is a rebuilt dZ (BNBWD / POOLBWD, the data-gradient GEMM), with a
 // heavier operand transform and BN-backward epilogue; its tile policy is below
 static void gemm_tile(int M, int N, bool bwd, int* bm, int* bn) {
-    // PCS_GEMM_TILE=bm,bn forces one tile shape (tuning sweeps; must be a built variant)
-    static const int forced = [] {
-        const char* e = getenv("PCS_GEMM_TILE");
-        int a = 0, b = 0;
-        return (e && sscanf(e, "%d,%d", &a, &b) == 2) ? a * 1000 + b : 0;
-    }();
-    if (forced) { *bm = forced / 1000; *bn = forced % 1000; return; }
     struct T { int bm, bn; };
     static const T big[] = {{128, 128}, {64, 128}, {64, 64}, {32, 128}};
     static const T mid[] = {{128, 64}, {64, 64}};
     static const T mid64[] = {{64, 64}, {128, 64}};
-    // Data-gradient tiles by regime (same-box A/B, scripts/gpu_dgrad_ab.sh): the thin,
-    // HBM-latency-bound layers (PointNet++, EdgeConv) run best on 64 x 64 tiles (4 blocks per
-    // CU, more loads in flight: PointNet++ step -1 %); the big MFMA-bound ones (DGCNN
-    // conv5-7: N >= 256 over >= 64K rows) on the wide list despite its register pressure
-    // (DGCNN step -2 %).  PCS_DGRAD_TILES = legacy | small | wide forces one policy (A/B).
-    static const int dgrad_policy = [] {
-        const char* e = getenv("PCS_DGRAD_TILES");
-        if (!e) return 0;
-        return !strcmp(e, "legacy") ? 1 : (!strcmp(e, "small") ? 2 : (!strcmp(e, "wide") ? 3 : 0));
-    }();
+    // Data-gradient tiles by regime (same-box A/B, round 1): the thin, HBM-latency-bound
+    // layers (PointNet++, EdgeConv) run best on 64 x 64 tiles (4 blocks per CU, more loads in
+    // flight: PointNet++ step -1 %); the big MFMA-bound ones (DGCNN conv5-7: N >= 256 over
+    // >= 64K rows) on the wide list despite its register pressure (DGCNN step -2 %).
     bool wide;
     const T* c;
     if (!bwd) {
         wide = N > 64;
         c = wide ? big : mid;
-    } else if (dgrad_policy == 1) {
-        wide = false;
-        c = mid;
-    } else if (dgrad_policy == 2) {
-        wide = false;
-        c = mid64;
     } else {
-        wide = N > 64 && (dgrad_policy == 3 || (N >= 256 && M >= 65536));
+        wide = N > 64 && N >= 256 && M >= 65536;
         c = wide ? big : mid64;
     }
     const int nc = wide ? 4 : 2;
@@ -869,12 +871,9 @@ static void gemm_tile(int M, int N, bool bwd, int* bm, int* bn) {
 
 // Persistent grid of the row GEMM: as many row blocks per column tile as fit on the chip
 // at once (LDS-limited blocks per CU x 256 CUs), each walking its row tiles with the next
-// tile's first slab prefetched under the current tile's epilogue.  PCS_GEMM_PERSIST=0
-// restores one block per tile (for A/B timing).
+// tile's first slab prefetched under the current tile's epilogue.
 static int gemm_grid_x(int M, int N, int bm, int bn) {
-    static const int persist = [] { const char* e = getenv("PCS_GEMM_PERSIST"); return e ? atoi(e) : 1; }();
     const int mtiles = (M + bm - 1) / bm;
-    if (!persist) return mtiles;
     const int lds = 4 * (bm + bn) * 2 * GLDK + 16 * bn;         // As + Bs + red (bytes)
     int per_cu = (160 * 1024) / lds;
     per_cu = per_cu < 1 ? 1 : (per_cu > 4 ? 4 : per_cu);
@@ -900,7 +899,6 @@ static double operand_bytes(const pcs_operand& o, int M, int K) {
 
 // number of row blocks the row GEMM uses for M rows and N outputs (sizes the stats workspace)
 static int row_blocks(int M, int N, bool bwd) {
-    if (engine_impl() == 1) return direct_row_blocks(M, N);
     int bm, bn;
     gemm_tile(M, N, bwd, &bm, &bn);
     return gemm_grid_x(M, N, bm, bn);
@@ -944,44 +942,34 @@ static Operand to_dev(const pcs_operand* o) {
 int pcs::gemm_rows_ex(const pcs_operand* a, int M, int K, const float* W, int ldw, int bt, const float* bias, float* C,
                  int ldc, int N, double* stats, const pcs_operand* epi, double* bstats, void* stream, float* pz,
                  unsigned char* pa, int pool_k) {
-    PCS_CHECK_ARG(pool_k == 0 || ((pool_k == 16 || pool_k == 32) && M % pool_k == 0 && pz && pa && !bt &&
-                                  engine_impl() == 0),
-                  "pcs_gemm_rows: fused pooling needs pool_k 16|32 dividing M, pz/pa, the LDS engine");
+    PCS_CHECK_ARG(pool_k == 0 || ((pool_k == 16 || pool_k == 32) && M % pool_k == 0 && pz && pa && !bt),
+                  "pcs_gemm_rows: fused pooling needs pool_k 16|32 dividing M and pz/pa");
     PCS_CHECK_ARG(M >= 0 && K >= 1 && N >= 1, "pcs_gemm_rows: bad sizes M=%d K=%d N=%d", M, K, N);
     if (int e = check_operand(a, K, "pcs_gemm_rows", "A")) return e;
     PCS_CHECK_ARG(W && C, "pcs_gemm_rows: null pointer");
     PCS_CHECK_ARG(!(stats && bstats), "pcs_gemm_rows: stats and bstats are exclusive");
     PCS_CHECK_ARG(!bstats || (epi && epi->z && epi->s && epi->t && epi->mean && epi->inv),
                   "pcs_gemm_rows: bstats needs epi z/s/t/mean/inv");
-    PCS_CHECK_ARG((ldw % 4 == 0 || (!bt && engine_impl() == 0)) && ldw >= (bt ? N : K),
-                  "pcs_gemm_rows: ldw=%d must be >= %d (and a multiple of 4 for k-major W or the LDS-free engine)",
-                  ldw, bt ? N : K);
-    PCS_CHECK_ARG(!bt || (engine_impl() == 0 && a->mode != PCS_OP_BNACT), "pcs_gemm_rows: k-major W needs the LDS engine and a PLAIN/BNBWD/POOLBWD A");
+    PCS_CHECK_ARG((ldw % 4 == 0 || !bt) && ldw >= (bt ? N : K),
+                  "pcs_gemm_rows: ldw=%d must be >= %d (and a multiple of 4 for k-major W)", ldw, bt ? N : K);
+    PCS_CHECK_ARG(!bt || a->mode != PCS_OP_BNACT, "pcs_gemm_rows: k-major W needs a PLAIN/BNBWD/POOLBWD A");
     if (M == 0) return 0;
     GemmArgs g{to_dev(a), M, K, W, ldw, bias, C, ldc, N, stats, to_dev(epi), bstats, pz, pa, pool_k};
     hipStream_t s = as_stream(stream);
     int probe = -1;
     if (probe_enabled()) {
         char nm[96];
-        if (engine_impl() == 1) {
-            direct_gemm_name(M, N, a->mode, nm, sizeof nm);
-        } else {
-            int bm, bn, wm, wn;
-            gemm_tile(M, N, a->mode >= PCS_OP_BNBWD, &bm, &bn);
-            gemm_waves(bm, bn, &wm, &wn);
-            snprintf(nm, sizeof nm, "pcs::gemm_rows_kernel<%d, %d, %d, %d, %d, %s>", bm, bn, wm, wn, a->mode,
-                     bt ? "true" : "false");
-        }
+        int bm, bn, wm, wn;
+        gemm_tile(M, N, a->mode >= PCS_OP_BNBWD, &bm, &bn);
+        gemm_waves(bm, bn, &wm, &wn);
+        snprintf(nm, sizeof nm, "pcs::gemm_rows_kernel<%d, %d, %d, %d, %d, %s>", bm, bn, wm, wn, a->mode,
+                 bt ? "true" : "false");
         const double bytes = operand_bytes(*a, M, K) + 4.0 * M * N * (bstats ? 2 : 1);
         const pcs_operand ac = *a, ec = epi ? *epi : pcs_operand{};
         const bool he = epi != nullptr;
         probe = probe_start(nm, 2.0 * M * K * N, bytes, s, [=]() {
             gemm_rows_ex(&ac, M, K, W, ldw, bt, bias, C, ldc, N, stats, he ? &ec : nullptr, bstats, stream);
         });
-    }
-    if (engine_impl() == 1 && launch_gemm_direct(g, s)) {
-        probe_stop(probe, s);
-        return launch_status("pcs_gemm_rows");
     }
     int bm, bn;
     gemm_tile(M, N, a->mode >= PCS_OP_BNBWD, &bm, &bn);
@@ -1007,9 +995,34 @@ PCS_API int pcs_gemm_rows_kmajor(const pcs_operand* a, int M, int K, const float
     return gemm_rows_ex(a, M, K, W, ldw, 1, nullptr, C, ldc, N, nullptr, epi, bstats, stream);
 }
 
-// dW (N x K) += T(X)^T . T(Y) over M rows; db (N) += column sums of T(X). dW/db zeroed by caller.
-PCS_API int pcs_wgrad(const pcs_operand* x, int N, const pcs_operand* y, int K, int M, float* dW, float* db,
-                      void* stream) {
+// wgrad tile (BO x BI) and its row split for N x K over M rows: ~1024 blocks, 2048 for the big
+// MFMA-bound contractions (>= 16 GFLOP, e.g. DGCNN conv5-7: step -1 %, round 1).  Round 2
+// re-checked 256 / 512 / 1024 blocks with the partial-tile reduce: within +-8 % per shape,
+// no consistent winner (scripts/gemm_bench.py).
+static void wgrad_plan(int N, int K, int M, int* BO, int* BI, int* splits, int* rows) {
+    *BO = N > 64 ? 128 : 64;
+    *BI = K > 64 ? 128 : 64;
+    const int tiles = ((N + *BO - 1) / *BO) * ((K + *BI - 1) / *BI);
+    const int target = 2.0 * M * N * K >= 1.6e10 ? 2048 : 1024;
+    int sp = (target + tiles - 1) / tiles;
+    int r = (M + sp - 1) / sp;
+    r = ((r + 255) / 256) * 256;
+    if (r < 256) r = 256;
+    *rows = r;
+    *splits = (M + r - 1) / r;
+}
+
+size_t pcs::wgrad_ws_bytes(int N, int K, int M) {
+    if (M <= 0) return 0;
+    int BO, BI, sp, rows;
+    wgrad_plan(N, K, M, &BO, &BI, &sp, &rows);
+    return (size_t)sp * ((size_t)N * K + N) * sizeof(float) + 256;
+}
+
+// dW (N x K) += T(X)^T . T(Y) over M rows; db (N) += column sums of T(X) (nullable).  Each row
+// split's partial goes to the workspace, then one reduce per output adds the splits in order.
+int pcs::wgrad_launch(const pcs_operand* x, int N, const pcs_operand* y, int K, int M, float* dW, float* db, void* ws,
+                      size_t ws_bytes, void* stream) {
     PCS_CHECK_ARG(M >= 0 && N >= 1 && K >= 1, "pcs_wgrad: bad sizes");
     if (int e = check_operand(x, N, "pcs_wgrad", "X")) return e;
     if (int e = check_operand(y, K, "pcs_wgrad", "Y")) return e;
@@ -1017,44 +1030,48 @@ PCS_API int pcs_wgrad(const pcs_operand* x, int N, const pcs_operand* y, int K, 
     PCS_CHECK_ARG(y->mode <= PCS_OP_BNACT, "pcs_wgrad: Y operand must be PLAIN or BNACT");
     PCS_CHECK_ARG(dW && N % 4 == 0, "pcs_wgrad: dW null or N not a multiple of 4");
     if (M == 0) return 0;
-    const int lo = wgrad_thin32() ? 32 : 64;
-    const int BO = N > 64 ? 128 : (N > lo ? 64 : lo), BI = K > 64 ? 128 : (K > lo ? 64 : lo);
+    const size_t need = wgrad_ws_bytes(N, K, M);
+    PCS_CHECK_ARG(ws && ws_bytes >= need, "pcs_wgrad: workspace too small (%zu < %zu)", ws_bytes, need);
+    int BO, BI, splits, rows;
+    wgrad_plan(N, K, M, &BO, &BI, &splits, &rows);
+    float* part = reinterpret_cast<float*>((reinterpret_cast<uintptr_t>(ws) + 255) & ~uintptr_t(255));
+    float* pdb = db ? part + (size_t)splits * N * K : nullptr;
+    hipStream_t st = as_stream(stream);
+    const int tiles = ((N + BO - 1) / BO) * ((K + BI - 1) / BI);
+    const dim3 grid(splits, tiles);
+    const Operand xd = to_dev(x), yd = to_dev(y);
+    // the partial-tile launch alone (the probe's replay rewrites only the workspace)
+    auto tiles_launch = [=]() {
+        if (BO == 128 && BI == 128) launch_wgrad<128, 128>(grid, st, xd, N, yd, K, M, rows, part, pdb);
+        else if (BO == 128) launch_wgrad<128, 64>(grid, st, xd, N, yd, K, M, rows, part, pdb);
+        else if (BI == 128) launch_wgrad<64, 128>(grid, st, xd, N, yd, K, M, rows, part, pdb);
+        else launch_wgrad<64, 64>(grid, st, xd, N, yd, K, M, rows, part, pdb);
+    };
     int probe = -1;
     if (probe_enabled()) {
         char nm[96];
-        if (engine_impl() == 1) direct_wgrad_name(N, K, x->mode, y->mode, nm, sizeof nm);
-        else snprintf(nm, sizeof nm, "pcs::wgrad_kernel<%d, %d, %d, %d, %d>", BO, BI, x->mode, y->mode,
-                      BO <= 64 && BI <= 64 ? wgrad_stages() : 1);
-        const pcs_operand xc = *x, yc = *y;
-        probe = probe_start(nm, 2.0 * M * N * K, operand_bytes(*x, M, N) + operand_bytes(*y, M, K),
-                            as_stream(stream), [=]() { pcs_wgrad(&xc, N, &yc, K, M, dW, db, stream); });
+        snprintf(nm, sizeof nm, "pcs::wgrad_kernel<%d, %d, %d, %d, %d>", BO, BI, x->mode, y->mode,
+                 BO <= 64 && BI <= 64 ? 2 : 1);
+        probe = probe_start(nm, 2.0 * M * N * K, operand_bytes(*x, M, N) + operand_bytes(*y, M, K), st,
+                            tiles_launch);
     }
-    if (engine_impl() == 1 &&
-        launch_wgrad_direct(to_dev(x), N, to_dev(y), K, M, dW, db, as_stream(stream))) {
-        probe_stop(probe, as_stream(stream));
-        return launch_status("pcs_wgrad");
-    }
-    const int tiles = ((N + BO - 1) / BO) * ((K + BI - 1) / BI);
-    // row splits: ~1024 blocks, 2048 for the big MFMA-bound contractions (>= 16 GFLOP, e.g.
-    // DGCNN conv5-7: step -1 %; the small overlapped PointNet++ wgrads gain nothing from more);
-    // PCS_WGRAD_BLOCKS forces a target (A/B, scripts/gpu_wgrad_blocks_ab.sh)
-    static const int forced_target = [] { const char* e = getenv("PCS_WGRAD_BLOCKS"); return e ? atoi(e) : 0; }();
-    const int target = forced_target > 0 ? forced_target : (2.0 * M * N * K >= 1.6e10 ? 2048 : 1024);
-    int splits = (target + tiles - 1) / tiles;
-    int rows = (M + splits - 1) / splits;
-    rows = ((rows + 255) / 256) * 256;
-    if (rows < 256) rows = 256;
-    splits = (M + rows - 1) / rows;
-    const dim3 grid(splits, tiles);
-    hipStream_t st = as_stream(stream);
-    const Operand xd = to_dev(x), yd = to_dev(y);
-#define PCS_WG(o, i) \
-    if (BO == o && BI == i) { launch_wgrad<o, i>(grid, st, xd, N, yd, K, M, rows, dW, db); }
-    PCS_WG(128, 128) else PCS_WG(128, 64) else PCS_WG(128, 32) else PCS_WG(64, 128) else PCS_WG(64, 64)
-    else PCS_WG(64, 32) else PCS_WG(32, 128) else PCS_WG(32, 64) else PCS_WG(32, 32)
-#undef PCS_WG
+    tiles_launch();
     probe_stop(probe, st);
+    const long long nk = (long long)N * K;
+    const long long blocks = (nk + kRedElems - 1) / kRedElems + (db ? (N + kRedElems - 1) / kRedElems : 0);
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, st, part, splits, nk, dW, pdb, N, db);
     return launch_status("pcs_wgrad");
+}
+
+PCS_API int pcs_wgrad_workspace(int N, int K, int M, size_t* bytes) {
+    PCS_CHECK_ARG(bytes && N >= 1 && K >= 1 && M >= 0, "pcs_wgrad_workspace: bad arguments");
+    *bytes = wgrad_ws_bytes(N, K, M);
+    return 0;
+}
+
+PCS_API int pcs_wgrad(const pcs_operand* x, int N, const pcs_operand* y, int K, int M, float* dW, float* db,
+                      void* workspace, size_t ws_bytes, void* stream) {
+    return wgrad_launch(x, N, y, K, M, dW, db, workspace, ws_bytes, stream);
 }
 
 // BN forward finalize: part [2][N][nb] -> s, t, mean, invstd; running stats updated in place (nullable).

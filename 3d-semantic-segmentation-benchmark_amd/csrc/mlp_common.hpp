@@ -129,11 +129,6 @@ struct GemmArgs {
     float* pz; unsigned char* pa; int pool_k;
 };
 
-// LDS-free kernels (gemm_direct.hip); return false when the shape is not covered
-bool launch_gemm_direct(const GemmArgs& g, hipStream_t s);
-bool launch_wgrad_direct(const Operand& x, int N, const Operand& y, int K, int M, float* dW, float* db,
-                         hipStream_t s);
-int direct_row_blocks(int M, int N);
 // bn_finalize_kernel launch that also bumps BatchNorm.num_batches_tracked (nbt, nullable)
 void bn_finalize_launch(const double* part, int nb, int N, long long M, const float* gamma, const float* beta,
                         float eps, float momentum, float* run_mean, float* run_var, float* s, float* t, float* mean,
@@ -141,7 +136,6 @@ void bn_finalize_launch(const double* part, int nb, int N, long long M, const fl
 // bn_bwd_finalize_kernel launch: (sum dy, sum dy*xhat) partials -> dgamma/dbeta (+= when accum), kB, kC
 void bn_bwd_finalize_launch(const double* part, int nb, int N, long long M, const float* s, const float* inv,
                             float* dgamma, float* dbeta, float* kB, float* kC, int accum, hipStream_t st);
-int engine_impl();
 // row GEMM with W row-major N x K (bt = 0, = pcs_gemm_rows) or K x N (bt = 1, LDS engine only)
 int gemm_rows_ex(const pcs_operand* a, int M, int K, const float* W, int ldw, int bt, const float* bias, float* C,
                  int ldc, int N, double* stats, const pcs_operand* epi, double* bstats, void* stream,
@@ -151,12 +145,13 @@ int gemm_rows_ex(const pcs_operand* a, int M, int K, const float* W, int ldw, in
 // monotone in z, so this is max_k act(s*z_k + t) with its first argmax
 int pool_finalize(const float* pz, const unsigned char* pa, long long G, int N, const float* s, const float* t,
                   int act, float slope, float* out, unsigned char* arg, hipStream_t st);
-// kernel names of the LDS-free family (as rocprofv3 reports them) for the launch probe
-void direct_gemm_name(int M, int N, int mode, char* buf, int cap);
-void direct_wgrad_name(int N, int K, int xm, int ym, char* buf, int cap);
 // engine launch probe (probe.cpp)
 bool probe_enabled();
 int probe_start(const char* name, double flops, double bytes, hipStream_t s, std::function<void()> relaunch);
-void probe_stop(int idx, hipStream_t s);   // 0 = LDS-staged kernels, 1 = LDS-free (PCS_GEMM_IMPL)
+void probe_stop(int idx, hipStream_t s);
+// weight gradient with deterministic partials: workspace bytes for (N, K, M), and the launch
+size_t wgrad_ws_bytes(int N, int K, int M);
+int wgrad_launch(const pcs_operand* x, int N, const pcs_operand* y, int K, int M, float* dW, float* db, void* ws,
+                 size_t ws_bytes, void* stream);
 
 }  // namespace pcs

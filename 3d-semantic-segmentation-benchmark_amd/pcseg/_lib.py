@@ -40,18 +40,15 @@ SIGNATURES = {
     'pcs_knn_select': [P, P, I32, I32, I32, I32, P, P, P],
     'pcs_knn': [P, I32, I32, I32, I32, P, P],
     'pcs_group_fwd': [P, P, P, P, I32, I32, I32, I32, I32, F32, I32, P, I32, P],
-    'pcs_group_bwd': [P, I32, P, I32, I32, I32, I32, I32, P, P],
     'pcs_maxk_fwd': [P, I64, I32, I32, P, P, P],
     'pcs_maxk_bwd': [P, P, I64, I32, I32, P, P],
     'pcs_interp_fwd': [P, P, P, I32, I32, I32, I32, P, I32, I32, P],
     'pcs_interp_cat_fwd': [P, I32, P, P, P, I32, I32, I32, I32, P, I32, P],
-    'pcs_interp_bwd': [P, P, P, I32, I32, I32, I32, I32, I32, P, P],
     'pcs_edge_fwd': [P, P, I32, I32, I32, I32, P, I32, P],
-    'pcs_edge_bwd': [P, I32, P, I32, I32, I32, I32, P, P],
+    'pcs_edge_bwd': [P, I32, P, P, I32, I32, I32, I32, P, P],
     # shared-MLP engine
     'pcs_gemm_row_blocks': [I32, I32],
     'pcs_gemm_row_blocks_dgrad': [I32, I32],
-    'pcs_engine_select': [I32],
     'pcs_probe_begin': [],
     'pcs_probe_end': [],
     'pcs_probe_get': [I32, ctypes.c_char_p, I32, P, P, P],
@@ -63,7 +60,8 @@ SIGNATURES = {
     'pcs_operand_size': [],
     'pcs_gemm_rows': [OPP, I32, I32, P, I32, P, P, I32, I32, P, OPP, P, P],
     'pcs_gemm_rows_kmajor': [OPP, I32, I32, P, I32, P, I32, I32, OPP, P, P],
-    'pcs_wgrad': [OPP, I32, OPP, I32, I32, P, P, P],
+    'pcs_wgrad_workspace': [I32, I32, I32, P],
+    'pcs_wgrad': [OPP, I32, OPP, I32, I32, P, P, P, ctypes.c_size_t, P],
     'pcs_bn_finalize': [P, I32, I32, I64, P, P, F32, F32, P, P, P, P, P, P, P],
     'pcs_bn_bwd_finalize': [P, I32, I32, I64, P, P, P, P, P, P, I32, P],
     'pcs_bn_bwd_reduce_blocks': [I32],
@@ -77,7 +75,7 @@ SIGNATURES = {
     # metrics
     'pcs_seg_metrics': [P, P, I32, P, I32, I32, I32, P, P, P, P, P],
     # fused EdgeConv
-    'pcs_edgeconv_workspace': [I32, I32, I32, I32, P],
+    'pcs_edgeconv_workspace': [I32, I32, I32, I32, I32, P],
     'pcs_edgeconv_fwd': [P, I32, I32, P, I32, I32, I32, P, I32, P, P, P, P, P, F32, F32, F32,
                          P, P, P, P, P, P, P, P, P, ctypes.c_size_t, P],
     'pcs_edgeconv_bwd': [P, I32, I32, P, P, I32, I32, I32, P, I32, P, P, P, P, P, P, F32,

@@ -132,9 +132,24 @@ def gemm_rows_kmajor(a: Operand, M, K, W, ldw, C, ldc, N, epi: Operand | None = 
     call('pcs_gemm_rows_kmajor', a, M, K, ptr(W), ldw, ptr(C), ldc, N, epi, ptr(bstats), st)
 
 
-def wgrad(x: Operand, N, y: Operand, K, M, dW, db, st):
-    """dW[N,K] += T(X)^T . T(Y) over M rows, db += colsum(T(X))."""
-    call('pcs_wgrad', x, N, y, K, M, ptr(dW), ptr(db), st)
+def wgrad_workspace(N, K, M) -> int:
+    """Bytes of pcs_wgrad's partial-tile workspace for an N x K gradient over M rows."""
+    key = ('wgrad', N, K, M)
+    n = _ws_cache.get(key)
+    if n is None:
+        out = ctypes.c_size_t(0)
+        call('pcs_wgrad_workspace', N, K, M, ctypes.byref(out))
+        n = _ws_cache[key] = int(out.value)
+    return n
+
+
+def wgrad(x: Operand, N, y: Operand, K, M, dW, db, st, ws=None):
+    """dW[N,K] += T(X)^T . T(Y) over M rows, db += colsum(T(X)) (deterministic: per-split
+    partial tiles in `ws`, allocated here when not given, added in a fixed order)."""
+    nws = wgrad_workspace(N, K, M)
+    if ws is None:
+        ws = torch.empty((nws,), dtype=torch.uint8, device=dW.device)
+    call('pcs_wgrad', x, N, y, K, M, ptr(dW), ptr(db), ptr(ws), ws.numel(), st)
 
 
 def _f64(shape, dev):
@@ -193,11 +208,11 @@ class SharedMLPFn(torch.autograd.Function):
             if C % 4:
                 raise ValueError(f'engine: layer width {C} must be a multiple of 4')
             Wm = W.reshape(C, -1)
-            if Wm.shape[1] % 4 and (li > 0 or _impl() != 0):    # 16-B weight rows (the pad columns are zero)
+            if Wm.shape[1] % 4 and li > 0:    # 16-B weight rows (the pad columns are zero)
                 Wp = torch.zeros((C, ld4(Wm.shape[1])), dtype=torch.float32, device=dev)
                 Wp[:, :Wm.shape[1]] = Wm
                 Wm = Wp
-            elif not Wm.is_contiguous():        # (the LDS engine reads an unpadded first layer as is)
+            elif not Wm.is_contiguous():        # (an unpadded first layer is read as is)
                 Wm = Wm.contiguous()
             Wms.append(Wm)
             use_batch = bn.training or bn.running_mean is None
@@ -224,7 +239,7 @@ class SharedMLPFn(torch.autograd.Function):
         else:
             out = _f32((M, CL), dev)
             arg = None
-        key = (M, Kin, ldx, tuple(couts), pool_K, 0, _impl())
+        key = (M, Kin, ldx, tuple(couts), pool_K, 0)
         nws = _workspace(lib, key, M, Kin, ldx, recs, nl, pool_K, 0)
         ws = torch.empty((nws,), dtype=torch.uint8, device=dev)
         call('pcs_mlp_forward', ptr(X), ldx, Kin, M, recs, nl, pool_K, ptr(out), ptr(arg), ptr(ws), nws, st)
@@ -263,7 +278,7 @@ class SharedMLPFn(torch.autograd.Function):
         dX = None
         if ctx.needs_input_grad[0]:
             dX = _f32((M, ldx), dev)
-        key = (M, Kin, ldx, tuple(couts), pool_K, 1, _impl())
+        key = (M, Kin, ldx, tuple(couts), pool_K, 1)
         nws = _workspace(lib, key, M, Kin, ldx, recs, nl, pool_K, 1)
         ws = torch.empty((nws,), dtype=torch.uint8, device=dev)
         call('pcs_mlp_backward', ptr(X), ldx, Kin, M, recs, nl, pool_K, ptr(arg), ptr(gout), ptr(dX), ptr(ws), nws, st)
@@ -271,12 +286,12 @@ class SharedMLPFn(torch.autograd.Function):
         return (dX, None, None, None, None, *([None] * len(params)))
 
 
-def _edge_ws(B, N, Cout, backward, dev):
-    key = ('edge', B, N, Cout, backward)
+def _edge_ws(B, N, C, Cout, backward, dev):
+    key = ('edge', B, N, C, Cout, backward)
     n = _ws_cache.get(key)
     if n is None:
         out = ctypes.c_size_t(0)
-        call('pcs_edgeconv_workspace', B, N, Cout, backward, ctypes.byref(out))
+        call('pcs_edgeconv_workspace', B, N, C, Cout, backward, ctypes.byref(out))
         n = int(out.value)
         _ws_cache[key] = n
     return torch.empty((n,), dtype=torch.uint8, device=dev)
@@ -307,7 +322,7 @@ class EdgeConvFn(torch.autograd.Function):
         momentum = 0.0
         if track:
             momentum = bn.momentum if bn.momentum is not None else 1.0 / float(bn.num_batches_tracked + 1)
-        ws = _edge_ws(B, N, Cout, 0, dev)
+        ws = _edge_ws(B, N, C, Cout, 0, dev)
         call('pcs_edgeconv_fwd', ptr(X), ldx, C, ptr(idx), B, N, k, ptr(Wm), Cout, ptr(gamma), ptr(beta),
              ptr(bn.running_mean) if track else None, ptr(bn.running_var) if track else None,
              ptr(bn.num_batches_tracked) if track else None, float(momentum), float(bn.eps), float(slope),
@@ -336,7 +351,7 @@ class EdgeConvFn(torch.autograd.Function):
         dX = _f32((M, ldx), dev) if ctx.needs_input_grad[0] else None
         if dX is not None and ldx != C:
             dX.zero_()
-        ws = _edge_ws(B, N, Cout, 1, dev)
+        ws = _edge_ws(B, N, C, Cout, 1, dev)
         dW, dg, db = grad_target(W), grad_target(gamma), grad_target(beta)
         call('pcs_edgeconv_bwd', ptr(X), ldx, C, ptr(off), ptr(ent), B, N, k, ptr(Wm), Cout, ptr(Y), ptr(Q), ptr(S),
              ptr(pz), ptr(arg), ptr(coef), slope, ptr(gout), ptr(dX), ldx, ptr(dW), ptr(dg), ptr(db), ptr(ws),
@@ -346,9 +361,8 @@ class EdgeConvFn(torch.autograd.Function):
 
 
 def edgeconv_fused_ok(conv, bn, cin: int) -> bool:
-    """The fused EdgeConv covers training-mode BN on the LDS engine (eval-mode BN and the
-    LDS-free engine use the materialised-edge path)."""
-    return (bn.training and conv.weight.shape[0] % 4 == 0 and conv.bias is None and _impl() == 0
+    """The fused EdgeConv covers training-mode BN (eval-mode BN uses the materialised-edge path)."""
+    return (bn.training and conv.weight.shape[0] % 4 == 0 and conv.bias is None
             and (cin % 4 == 0 or cin < 4))
 
 
@@ -359,20 +373,6 @@ def edgeconv(x_rows: torch.Tensor, cin: int, idx: torch.Tensor, conv, bn, slope:
     if x_rows.shape[1] % 4 or not x_rows.is_contiguous():
         x_rows = pad_rows(x_rows[:, :cin])
     return EdgeConvFn.apply(x_rows, idx.contiguous(), cin, slope, bn, conv.weight, bn.weight, bn.bias)
-
-
-def _impl() -> int:
-    """The engine GEMM family in use (its row-block count sizes the workspaces)."""
-    return _ENGINE_IMPL[0]
-
-
-_ENGINE_IMPL = [0]
-
-
-def select_engine(impl: int) -> None:
-    """0 = LDS-staged persistent GEMMs (default), 1 = LDS-free (pcs_engine_select)."""
-    call('pcs_engine_select', int(impl))
-    _ENGINE_IMPL[0] = int(impl)
 
 
 def shared_mlp(x_rows: torch.Tensor, kin: int, convs, bns, act='relu', slope=0.0,
@@ -433,12 +433,8 @@ class RowLinearFn(torch.autograd.Function):
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             dx = _f32((M, K), dev)
-            if _impl() == 0:                    # dgrad B[k=class][n=cin] = Wm[class][cin], read k-major
-                gemm_rows_kmajor(gop, M, N, Wm, K, dx, K, K, st=st)
-            else:
-                Wt = torch.zeros((K, N4), dtype=torch.float32, device=dev)
-                Wt[:, :N] = Wm.t()
-                gemm_rows(gop, M, N, Wt, N4, None, dx, K, K, st=st)
+            # dgrad B[k=class][n=cin] = Wm[class][cin], read k-major
+            gemm_rows_kmajor(gop, M, N, Wm, K, dx, K, K, st=st)
         if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
             dwp = torch.zeros((N4, K), dtype=torch.float32, device=dev)
             dbp = torch.zeros((N4,), dtype=torch.float32, device=dev) if ctx.has_bias else None

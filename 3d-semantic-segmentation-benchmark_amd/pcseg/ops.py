@@ -78,7 +78,7 @@ def knn(x: torch.Tensor, k: int) -> torch.Tensor:
 def inverse_index(idx: torch.Tensor, targets: int):
     """CSR inverse of a neighbour table idx (B, S, k) int32 with values in [0, targets):
     (offsets (B*targets+1,), entries (B*S*k,)) int32 -- the slots reading each source point,
-    ascending (stable rocPRIM radix sort).  Feeds the atomic-free gather backward."""
+    ascending.  Feeds the atomic-free, fixed-order gather backward."""
     check_cuda(idx)
     idx = _c(idx.to(torch.int32))
     B = idx.shape[0]
@@ -128,13 +128,11 @@ class GroupFn(torch.autograd.Function):
         gfeats = None
         if ctx.has_feats and ctx.needs_input_grad[1]:
             gout = _c(gout)
-            if ctx.has_inv:             # atomic-free gather over the inverse map
-                gfeats = torch.empty((B, N, D), dtype=torch.float32, device=gout.device)
-                call('pcs_group_bwd_csr', ptr(gout), ld, ptr(saved[1]), ptr(saved[2]), B, N, D, ptr(gfeats),
-                     stream_ptr(gout.device))
-            else:
-                gfeats = torch.zeros((B, N, D), dtype=torch.float32, device=gout.device)
-                call('pcs_group_bwd', ptr(gout), ld, ptr(idx), B, N, C, K, D, ptr(gfeats), stream_ptr(gout.device))
+            # gather over the inverse map (built here when the forward was not handed one)
+            off, ent = saved[1:3] if ctx.has_inv else inverse_index(idx, N)
+            gfeats = torch.empty((B, N, D), dtype=torch.float32, device=gout.device)
+            call('pcs_group_bwd_csr', ptr(gout), ld, ptr(off), ptr(ent), B, N, D, ptr(gfeats),
+                 stream_ptr(gout.device))
         return None, gfeats, None, None, None, None, None
 
 
@@ -215,14 +213,11 @@ class InterpCatFn(torch.autograd.Function):
         g1 = gout.view(B, N, W)[:, :, :D1] if (ctx.has_f1 and ctx.needs_input_grad[0]) else None
         g2 = None
         if ctx.needs_input_grad[1]:
-            if ctx.has_inv:             # atomic-free gather over the inverse map
-                g2 = torch.empty((B, M, D2), dtype=torch.float32, device=gout.device)
-                call('pcs_interp_bwd_csr', ptr(gout), W, D1, ptr(dist), ptr(saved[2]), ptr(saved[3]), B, M, D2,
-                     ptr(g2), stream_ptr(gout.device))
-            else:
-                g2 = torch.zeros((B, M, D2), dtype=torch.float32, device=gout.device)
-                call('pcs_interp_bwd', ptr(gout), ptr(idx), ptr(dist), B, N, M, D2, W, D1, ptr(g2),
-                     stream_ptr(gout.device))
+            # gather over the inverse map (built here when the forward was not handed one)
+            off, ent = saved[2:4] if ctx.has_inv else inverse_index(idx, M)
+            g2 = torch.empty((B, M, D2), dtype=torch.float32, device=gout.device)
+            call('pcs_interp_bwd_csr', ptr(gout), W, D1, ptr(dist), ptr(off), ptr(ent), B, M, D2,
+                 ptr(g2), stream_ptr(gout.device))
         return g1, g2, None, None, None
 
 
@@ -252,8 +247,9 @@ class EdgeFn(torch.autograd.Function):
         (idx,) = ctx.saved_tensors
         B, N, k, D, ld = ctx.dims
         gout = _c(gout)
-        gx = torch.zeros((B, N, D), dtype=torch.float32, device=gout.device)
-        call('pcs_edge_bwd', ptr(gout), ld, ptr(idx), B, N, k, D, ptr(gx), stream_ptr(gout.device))
+        off, ent = inverse_index(idx, N)
+        gx = torch.empty((B, N, D), dtype=torch.float32, device=gout.device)
+        call('pcs_edge_bwd', ptr(gout), ld, ptr(off), ptr(ent), B, N, k, D, ptr(gx), stream_ptr(gout.device))
         return gx, None
 
 

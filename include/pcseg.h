@@ -65,10 +65,7 @@ int pcs_knn(const float* x, int B, int N, int F, int k, int32_t* out_idx,
 int pcs_group_fwd(const float* xyz, const float* feats, const float* centroids,
                   const int32_t* idx, int B, int N, int C, int K, int D,
                   float r, int normalize, float* out, int ld_out, void* stream);
-/* grad_feats (B,N,D) += scatter(grad_out[:, 3:3+D])   (accumulating);
- * rows of grad_out have stride ld_gout (>= 3+D; pad columns zeroed by fwd) */
-int pcs_group_bwd(const float* grad_out, int ld_gout, const int32_t* idx, int B,
-                  int N, int C, int K, int D, float* grad_feats, void* stream);
+/* (its backward is pcs_group_bwd_csr over the inverse map of idx, below) */
 
 /* models/utils/common.py:85-86 `reduce(x,'max')` over K:
  * x (G*K, Ch) -> out (G, Ch), argmax (G, Ch) uint8 (first max). */
@@ -89,18 +86,17 @@ int pcs_interp_fwd(const float* pts, const int32_t* idx, const float* dist,
 int pcs_interp_cat_fwd(const float* f1, int D1, const float* pts, const int32_t* idx,
                        const float* dist, int B, int N, int M, int D2, float* out,
                        int ld_out, void* stream);
-/* grad_pts (B,M,D) += weighted scatter   (accumulating) */
-int pcs_interp_bwd(const float* grad_out, const int32_t* idx, const float* dist,
-                   int B, int N, int M, int D, int ld_gout, int col_off,
-                   float* grad_pts, void* stream);
+/* (its backward is pcs_interp_bwd_csr over the inverse map of idx, below) */
 
 /* models/dgcnn/dgcnn.py:41-53 `get_graph_feature`: x (B,N,D) point-major,
  * idx (B,N,k); out (B*N*k, 2D) rows [x_j - x_i, x_i]. */
 int pcs_edge_fwd(const float* x, const int32_t* idx, int B, int N, int k,
                  int D, float* out, int ld_out, void* stream);
-/* grad_x (B,N,D) += backward of the above   (accumulating) */
-int pcs_edge_bwd(const float* grad_out, int ld_gout, const int32_t* idx, int B,
-                 int N, int k, int D, float* grad_x, void* stream);
+/* grad_x (B,N,D) = backward of the above (overwrites), over the inverse map of
+ * idx (pcs_inverse_index, targets = N): fixed-order fp64 sums, no atomics. */
+int pcs_edge_bwd(const float* grad_out, int ld_gout, const int32_t* offsets,
+                 const int32_t* entries, int B, int N, int k, int D, float* grad_x,
+                 void* stream);
 
 /* ---- shared-MLP engine: 1x1 conv + training-mode BN + ReLU/LeakyReLU ------
  * models/utils/common.py:125-178 (MiniPointNet/UnitPointNet), dgcnn.py:67-76,
@@ -127,10 +123,6 @@ typedef struct pcs_operand {
     const uint8_t* arg; int pool_k;
 } pcs_operand;
 
-/* engine GEMM kernels: 0 = LDS-staged persistent (default), 1 = LDS-free.
- * Process-wide tuning/testing knob (also env PCS_GEMM_IMPL); call it only while
- * no engine work is being enqueued.  pcs_gemm_row_blocks depends on it. */
-int pcs_engine_select(int impl);
 /* row blocks of pcs_gemm_rows with a PLAIN / BNACT A (sizes its stats/bstats workspace) */
 int pcs_gemm_row_blocks(int M, int N);
 /* row blocks of pcs_gemm_rows / pcs_gemm_rows_kmajor when A is BNBWD or POOLBWD (the
@@ -151,9 +143,13 @@ int pcs_gemm_rows_kmajor(const pcs_operand* a, int M, int K, const float* W, int
                          double* bstats, void* stream);
 /* dW (N x K) += T(X)^T . T(Y) over M rows; db (N, nullable) += column sums of
  * T(X).  X: PLAIN/BNBWD/POOLBWD (the layer's dZ), Y: PLAIN/BNACT (its input).
- * (accumulating) */
+ * (accumulating) Deterministic: each row split's partial tile is stored in the
+ * workspace (pcs_wgrad_workspace bytes) and the splits are added in a fixed order,
+ * so identical calls give bitwise-identical dW/db.  The workspace is in use until
+ * the call's work on `stream` completes. */
+int pcs_wgrad_workspace(int N, int K, int M, size_t* bytes);
 int pcs_wgrad(const pcs_operand* x, int N, const pcs_operand* y, int K, int M,
-              float* dW, float* db, void* stream);
+              float* dW, float* db, void* workspace, size_t ws_bytes, void* stream);
 /* BN forward finalize: partials -> scale s, shift t, mean, invstd; running
  * mean/var updated with `momentum` and the unbiased variance (nullable). */
 int pcs_bn_finalize(const double* part, int nb, int N, long long M,
@@ -260,7 +256,7 @@ int pcs_seg_metrics(const float* pred, const void* labels, int label_u8,
  * P = X W2^T (W = [W1 | W2]).  Rows are B*N points (X stride ldx, C channels);
  * idx (B, N, k) int32 per-cloud neighbour indices; Cout % 4 == 0. */
 /* workspace bytes of pcs_edgeconv_fwd (backward = 0) / pcs_edgeconv_bwd (1) */
-int pcs_edgeconv_workspace(int B, int N, int Cout, int backward, size_t* bytes);
+int pcs_edgeconv_workspace(int B, int N, int C, int Cout, int backward, size_t* bytes);
 /* forward: Y, PQ (returns Q = P - Y), S = sum_k z (each B*N x Cout), pz / pa
  * (2 x B*N x Cout: max, min of z over k and their first slot), coef (s, t, mean,
  * invstd; 4 x Cout), pooled activation out (B*N x Cout) + argmax slot arg (u8);

@@ -136,7 +136,7 @@ def test_engine_abi_argument_checks_without_gpu():
     assert b'mode' in lib.pcs_last_error()
     # pooled-backward operands need the argmax and 1 <= pool_k <= 256
     pb = _lib.Operand(fake, 32, _lib.OP_POOLBWD, fake, fake, 0, 0.0, fake, 32, fake, None, fake, fake, None, 0)
-    assert lib.pcs_wgrad(pb, 32, op, 12, 64, fake, None, None) != 0
+    assert lib.pcs_wgrad(pb, 32, op, 12, 64, fake, None, None, 0, None) != 0
     assert b'pool_k' in lib.pcs_last_error()
     # the wgrad Y operand cannot be a backward transform
-    assert lib.pcs_wgrad(op, 32, pb, 32, 64, fake, None, None) != 0
+    assert lib.pcs_wgrad(op, 32, pb, 32, 64, fake, None, None, 0, None) != 0

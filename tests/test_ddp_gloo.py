@@ -177,7 +177,7 @@ def _gpu_worker(rank, world, port, out, overlap=True):
                 loc = float((local[off:off + n] - expect[off:off + n]).norm() / (expect[off:off + n].norm() + 1e-30))
                 print(f'DDPDIAG {name} rel={e:.3e} local_vs_mean={loc:.3e}', flush=True)
                 off += n
-        assert rel < 1e-5, rel                 # fp32 atomics make wgrad order run-dependent
+        assert rel < 1e-5, rel                 # the all-reduce sums in another order than the local mean
         assert all(h is not None for h in grads._handles) or not grads._handles
     finally:
         dist.destroy_process_group()

@@ -179,6 +179,17 @@ def test_edge_fwd_bwd():
     (ref * w).sum().backward()
     (got * w.to(DEV)).sum().backward()
     assert torch.allclose(xd.grad.cpu().transpose(1, 2), xr.grad, rtol=1e-5, atol=1e-5)
+    # fp64 truth of the same terms: each point's sum is accumulated in fp64 and rounded once
+    w64 = w.double()
+    ga, gb = w64[:, :D], w64[:, D:]                                  # (B, D, N, k)
+    truth = (gb - ga).sum(-1)
+    truth.scatter_add_(2, idx.reshape(B, 1, N * k).expand(-1, D, -1), ga.reshape(B, D, N * k))
+    assert torch.equal(xd.grad.cpu().transpose(1, 2), truth.float())
+    g1 = xd.grad.clone()
+    xd.grad = None
+    again = ops.edge_rows(xd, idx.to(torch.int32).to(DEV)).view(B, N, k, 2 * D).permute(0, 3, 1, 2)
+    (again * w.to(DEV)).sum().backward()
+    assert torch.equal(g1, xd.grad)
 
 
 # ----------------------------------------------------------------------------- DGCNN kNN
@@ -276,18 +287,16 @@ def test_inverse_index_and_group_bwd_csr(B, N, C, K, r):
     cent = xyz[:, :C].contiguous()
     idx = ops.ball_query(cent, xyz, r, K)
     off, ent = ops.inverse_index(idx, N)
-    # the CSR lists exactly the slots reading each point (order within a list unspecified)
+    # the CSR lists exactly the slots reading each point, each list ascending: the
+    # entries are the stable sort of the slots by target
     flat = idx.reshape(B, -1).long().cpu()
     key = (torch.arange(B).unsqueeze(1) * N + flat).reshape(-1)
     order = torch.sort(key, stable=True).indices
     counts = torch.bincount(key, minlength=B * N)
     offs = torch.cat([torch.zeros(1, dtype=torch.long), counts.cumsum(0)])
     assert torch.equal(off.long().cpu(), offs)
-    seg = torch.repeat_interleave(torch.arange(B * N), counts)
-    got = ent.long().cpu()
-    # sort each list by slot: (segment, slot) lexicographic == the stable order
-    assert torch.equal(got[torch.argsort(seg * (B * C * K) + got)], order)
-    # gather backward == atomic backward (same terms; CSR sums in fp64)
+    assert torch.equal(ent.long().cpu(), order)
+    # backward with the forward's map == backward that builds the map itself, bitwise
     D = 19
     feats = torch.randn(B, N, D, device=DEV)
     fa = feats.clone().requires_grad_(True)
@@ -298,9 +307,11 @@ def test_inverse_index_and_group_bwd_csr(B, N, C, K, r):
     w = torch.randn_like(ya)
     (ya * w).sum().backward()
     (yb * w).sum().backward()
-    # same terms, different summation (fp32 atomics vs fp64 gather): sums of up
-    # to ~K*C/N*... randn terms, so compare with an absolute floor at the fp32 ulp of the terms
-    assert torch.allclose(fa.grad, fb.grad, rtol=1e-5, atol=1e-4), float((fa.grad - fb.grad).abs().max())
+    assert torch.equal(fa.grad, fb.grad)
+    # against an fp64 scatter of the same terms (the GPU sums each list in fp64, rounds once)
+    gw = w.double().cpu().view(B, C * K, -1)[:, :, 3:3 + D]
+    ref = torch.zeros(B, N, D, dtype=torch.float64).scatter_add_(1, flat.unsqueeze(-1).expand(-1, -1, D), gw)
+    assert torch.equal(fb.grad.cpu(), ref.float())
     # deterministic
     fb.grad = None
     (ops.group_rows(xyz, fb, cent, idx, r, False, (off, ent)) * w).sum().backward()
@@ -310,7 +321,7 @@ def test_inverse_index_and_group_bwd_csr(B, N, C, K, r):
     assert torch.equal(g1, fb.grad)
 
 
-def test_interp_bwd_csr_matches_atomic():
+def test_interp_bwd_csr_with_and_without_forward_map():
     B, N, M, D1, D2 = 2, 4096, 1024, 8, 64
     c1 = cloud(B, N, seed=42).to(DEV)
     c2 = c1[:, :M].contiguous()
@@ -325,27 +336,32 @@ def test_interp_bwd_csr_matches_atomic():
     w = torch.randn_like(ya)
     (ya * w).sum().backward()
     (yb * w).sum().backward()
-    assert torch.allclose(f2a.grad, f2b.grad, rtol=1e-5, atol=1e-5)
+    assert torch.equal(f2a.grad, f2b.grad)
 
 
 @pytest.mark.parametrize('B,S,k,targets,kind', [(3, 500, 7, 1000, 'random'), (2, 1024, 32, 4096, 'same'),
                                                   (2, 3000, 3, 40000, 'random'), (1, 2048, 32, 50000, 'same'),
-                                                  (2, 1, 1, 1, 'random')])
+                                                  (2, 1, 1, 1, 'random'), (2, 1024, 32, 4096, 'skewed'),
+                                                  (2, 4096, 20, 4096, 'skewed')])
 def test_inverse_index_random_tables(B, S, k, targets, kind):
     """CSR of arbitrary tables: LDS-counter path (targets <= 32768) and global-counter path,
-    including the degenerate table where every slot reads the same point."""
+    including the degenerate table where every slot reads the same point, and skewed tables
+    whose hub lists take the LDS bitonic (65..1024 entries) and run-merge (> 1024) sorts."""
     g = torch.Generator().manual_seed(7)
     if kind == 'same':
         idx = torch.full((B, S, k), targets // 3, dtype=torch.int32)
+    elif kind == 'skewed':
+        w = 1.0 / torch.arange(1, targets + 1, dtype=torch.float64) ** 1.1
+        idx = torch.multinomial(w, B * S * k, replacement=True, generator=g).view(B, S, k).to(torch.int32)
     else:
         idx = torch.randint(0, targets, (B, S, k), generator=g, dtype=torch.int32)
     off, ent = ops.inverse_index(idx.to(DEV), targets)
     key = (torch.arange(B).unsqueeze(1) * targets + idx.reshape(B, -1).long()).reshape(-1)
     counts = torch.bincount(key, minlength=B * targets)
     assert torch.equal(off.long().cpu(), torch.cat([torch.zeros(1, dtype=torch.long), counts.cumsum(0)]))
-    seg = torch.repeat_interleave(torch.arange(B * targets), counts)
-    got = ent.long().cpu()
-    assert torch.equal(got[torch.argsort(seg * (B * S * k) + got)], torch.sort(key, stable=True).indices)
+    assert torch.equal(ent.long().cpu(), torch.sort(key, stable=True).indices)      # ascending lists
+    if kind == 'skewed':
+        assert counts.max() > 1024 and ((counts > 64) & (counts <= 1024)).any()
 
 
 @pytest.mark.parametrize('D1,D2', [(0, 128), (64, 256), (12, 8)])
