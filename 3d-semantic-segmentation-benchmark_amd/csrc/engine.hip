@@ -117,7 +117,13 @@ static size_t max_partials(int M, int kin, const pcs_mlp_layer* L, int nl, int p
     return m;
 }
 
+// A layer whose input is wide reads its dZ once per column tile of its data- and
+// weight-gradient GEMMs (ceil(cin / 128) tiles each); from 3 tiles on, one pass that
+// materialises dZ (mlp.hip dz_kernel) is cheaper than rebuilding it on every load.
+static bool materialize_dz_of(const pcs_mlp_layer& P) { return (P.cin + 127) / 128 >= 3; }
+
 struct BwdScratch {
+    float* dz;             // the top layer's materialised dZ (M x cout), when it is wide
     double* part;
     float* kb[2];
     float* alpha[2];
@@ -146,6 +152,7 @@ static size_t carve_backward(Carve& cv, int M, int kin, int ldx, const pcs_mlp_l
         if (L[l].dW) wg = std::max(wg, wgrad_ws_bytes((int)L[l].cout, (int)L[l].cin, M));
     s.wg_bytes = wg;
     s.wg = cv.take<char>(wg);
+    s.dz = materialize_dz_of(L[nl - 1]) ? cv.take<float>((size_t)M * (size_t)L[nl - 1].cout) : nullptr;
     if (out) *out = s;
     return cv.used;
 }
@@ -378,6 +385,13 @@ PCS_API int pcs_mlp_backward(const float* X, int ldx, int kin, int M, const pcs_
     for (int l = nl - 1; l >= 0; --l) {
         const pcs_mlp_layer& P = layers[l];
         const int C = (int)P.cout, Cin = (int)P.cin;
+        if (materialize_dz_of(P) && (P.dW || l > 0 || dX)) {
+            // the top layer's into its own buffer (gout is the caller's), inner ones in place
+            // over the dA buffer the rebuilt operand reads
+            float* dst = l == nl - 1 ? S.dz : const_cast<float*>(xop.data);
+            if (int e = materialize_dz(&xop, M, C, dst, C, st)) return fail(e);
+            xop = plain_op(dst, C);
+        }
         if (P.dW) {
             void* ws_stream = stream;
             if (lane) {                    // fork: the side stream waits for dZ's inputs

@@ -839,7 +839,7 @@ using namespace pcs;
 
 // row-GEMM tile (BM x BN) for M rows and N outputs: the largest tile that still
 // gives >= 2 blocks per CU (256 CUs), else the one with the most blocks
-// bwd: the A operand is a rebuilt dZ (BNBWD / POOLBWD, the data-gradient GEMM), with a
+// bwd: the data-gradient GEMM (k-major W, or an A rebuilt from dZ: BNBWD / POOLBWD), with a
 // heavier operand transform and BN-backward epilogue; its tile policy is below
 static void gemm_tile(int M, int N, bool bwd, int* bm, int* bn) {
     struct T { int bm, bn; };
@@ -933,6 +933,43 @@ static Operand to_dev(const pcs_operand* o) {
     return r;
 }
 
+// dZ (M x C, row stride ldo) = the BNBWD / POOLBWD transform of operand o, materialised: the
+// same load_quad / load_raw / xform4 the GEMM loaders apply, so the values are bitwise those
+// the GEMMs would rebuild on load.  Wide layers read dZ once per column tile of their data /
+// weight gradient; for ceil(Cin / 128) >= 3 one pass here is cheaper than rebuilding it in
+// every tile (DGCNN conv5-7: -2.1 ms of GEMM time for +0.5 ms here, scripts/dgcnn_head_ab.py).
+template <int MODE>
+__global__ __launch_bounds__(256) void dz_kernel(Operand o, int total4, int nq, float* __restrict__ out, int ldo) {
+    const int C = 4 * nq;
+    for (int e = blockIdx.x * 256 + threadIdx.x; e < total4; e += gridDim.x * 256) {
+        const int r = e / nq;
+        const int c = 4 * (e - r * nq);
+        Quad q;
+        load_quad<MODE>(o, c, C, q);
+        float4 v, z;
+        unsigned a = 0;
+        load_raw<MODE>(o, r, c, v, z, a);
+        *reinterpret_cast<float4*>(out + (size_t)r * ldo + c) = xform4<MODE>(o, v, z, a, r, q, c, C);
+    }
+}
+
+int pcs::materialize_dz(const pcs_operand* x, int M, int C, float* out, int ldo, hipStream_t st) {
+    PCS_CHECK_ARG(x && (x->mode == PCS_OP_BNBWD || x->mode == PCS_OP_POOLBWD) && C % 4 == 0 && ldo % 4 == 0 &&
+                      ldo >= C && out,
+                  "materialize_dz: needs a BNBWD/POOLBWD operand, C %% 4 == 0, ldo >= C");
+    const long long total4 = (long long)M * (C / 4);
+    PCS_CHECK_ARG(total4 < (1ll << 31), "materialize_dz: too many elements");
+    if (total4 == 0) return 0;
+    const Operand o = to_dev(x);
+    if (x->mode == PCS_OP_BNBWD)
+        hipLaunchKernelGGL(dz_kernel<OP_BNBWD>, dim3(ew_grid(total4)), dim3(256), 0, st, o, (int)total4, C / 4, out,
+                           ldo);
+    else
+        hipLaunchKernelGGL(dz_kernel<OP_POOLBWD>, dim3(ew_grid(total4)), dim3(256), 0, st, o, (int)total4, C / 4, out,
+                           ldo);
+    return launch_status("materialize_dz");
+}
+
 // C = T(A) . W^T (+bias), W row-major N x K (row stride ldw).
 // stats (nullable): [2][N][row_blocks] fp64 partial (sum, sumsq) of C.
 // bstats (nullable): fused BN-backward partials of the layer whose pre-BN output is epi->z (same shape as C):
@@ -960,7 +997,7 @@ int pcs::gemm_rows_ex(const pcs_operand* a, int M, int K, const float* W, int ld
     if (probe_enabled()) {
         char nm[96];
         int bm, bn, wm, wn;
-        gemm_tile(M, N, a->mode >= PCS_OP_BNBWD, &bm, &bn);
+        gemm_tile(M, N, a->mode >= PCS_OP_BNBWD || bt, &bm, &bn);
         gemm_waves(bm, bn, &wm, &wn);
         snprintf(nm, sizeof nm, "pcs::gemm_rows_kernel<%d, %d, %d, %d, %d, %s>", bm, bn, wm, wn, a->mode,
                  bt ? "true" : "false");
@@ -972,7 +1009,7 @@ int pcs::gemm_rows_ex(const pcs_operand* a, int M, int K, const float* W, int ld
         });
     }
     int bm, bn;
-    gemm_tile(M, N, a->mode >= PCS_OP_BNBWD, &bm, &bn);
+    gemm_tile(M, N, a->mode >= PCS_OP_BNBWD || bt, &bm, &bn);
     const int gx = gemm_grid_x(M, N, bm, bn);
     const bool b = bt != 0;
     if (bn == 32) launch_gemm<128, 32, 4, 1>(g, gx, b, s);

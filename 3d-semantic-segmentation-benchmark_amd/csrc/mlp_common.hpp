@@ -136,7 +136,9 @@ void bn_finalize_launch(const double* part, int nb, int N, long long M, const fl
 // bn_bwd_finalize_kernel launch: (sum dy, sum dy*xhat) partials -> dgamma/dbeta (+= when accum), kB, kC
 void bn_bwd_finalize_launch(const double* part, int nb, int N, long long M, const float* s, const float* inv,
                             float* dgamma, float* dbeta, float* kB, float* kC, int accum, hipStream_t st);
-// row GEMM with W row-major N x K (bt = 0, = pcs_gemm_rows) or K x N (bt = 1, LDS engine only)
+// out (M x C, stride ldo) = the BNBWD / POOLBWD operand x materialised (bitwise the on-load values)
+int materialize_dz(const pcs_operand* x, int M, int C, float* out, int ldo, hipStream_t st);
+// row GEMM with W row-major N x K (bt = 0, = pcs_gemm_rows) or K x N (bt = 1)
 int gemm_rows_ex(const pcs_operand* a, int M, int K, const float* W, int ldw, int bt, const float* bias, float* C,
                  int ldc, int N, double* stats, const pcs_operand* epi, double* bstats, void* stream,
                  float* pz = nullptr, unsigned char* pa = nullptr, int pool_k = 0);

@@ -125,8 +125,8 @@ typedef struct pcs_operand {
 
 /* row blocks of pcs_gemm_rows with a PLAIN / BNACT A (sizes its stats/bstats workspace) */
 int pcs_gemm_row_blocks(int M, int N);
-/* row blocks of pcs_gemm_rows / pcs_gemm_rows_kmajor when A is BNBWD or POOLBWD (the
- * data-gradient form; sizes its bstats workspace) */
+/* row blocks of pcs_gemm_rows_kmajor, or of pcs_gemm_rows when A is BNBWD or POOLBWD
+ * (the data-gradient form; sizes its bstats workspace) */
 int pcs_gemm_row_blocks_dgrad(int M, int N);
 /* C (M x N, ldc) = T(A) . W^T (+bias), W row-major N x K with row stride ldw.
  * stats: partial (sum, sum^2) of C per channel.  bstats: fused BN-backward

@@ -157,7 +157,7 @@ def test_gemm_rows_kmajor_vs_fp64(M, K, N, mode):
     st = stream_ptr(torch.device(DEV))
     tol = 2e-6 * math.sqrt(K)
     if N % 4 == 0:
-        nb = (load().pcs_gemm_row_blocks_dgrad if mode >= OP_BNBWD else load().pcs_gemm_row_blocks)(M, N)
+        nb = load().pcs_gemm_row_blocks_dgrad(M, N)          # k-major: always the data-gradient grid
         ze = torch.randn(M, N, device=DEV, generator=g)
         se, te = torch.rand(N, device=DEV, generator=g) + 0.5, torch.randn(N, device=DEV, generator=g) * 0.3
         me, ie = torch.randn(N, device=DEV, generator=g) * 0.1, torch.rand(N, device=DEV, generator=g) + 0.5
