@@ -117,13 +117,17 @@ static size_t max_partials(int M, int kin, const pcs_mlp_layer* L, int nl, int p
     return m;
 }
 
-// A layer whose input is wide reads its dZ once per column tile of its data- and
-// weight-gradient GEMMs (ceil(cin / 128) tiles each); from 3 tiles on, one pass that
-// materialises dZ (mlp.hip dz_kernel) is cheaper than rebuilding it on every load.
-static bool materialize_dz_of(const pcs_mlp_layer& P) { return (P.cin + 127) / 128 >= 3; }
+// A layer's backward GEMMs read its dZ once per column tile (dz_passes); rebuilt on load,
+// every pass reads two arrays (dy and Z), materialised once (read 2, write 1) every pass
+// reads one.  From 4 passes on the materialised form moves fewer bytes (DGCNN conv5-7:
+// -2.1 ms of GEMM time for +0.5 ms of materialising, scripts/dgcnn_head_ab.py).
+static bool materialize_dz_of(const pcs_mlp_layer& P, int M, bool dgrad) {
+    return dz_passes(M, (int)P.cout, (int)P.cin, dgrad, P.dW != nullptr) >= 4;
+}
 
 struct BwdScratch {
     float* dz;             // the top layer's materialised dZ (M x cout), when it is wide
+    bool dz_ok(bool top) const { return !top || dz != nullptr; }
     double* part;
     float* kb[2];
     float* alpha[2];
@@ -152,7 +156,7 @@ static size_t carve_backward(Carve& cv, int M, int kin, int ldx, const pcs_mlp_l
         if (L[l].dW) wg = std::max(wg, wgrad_ws_bytes((int)L[l].cout, (int)L[l].cin, M));
     s.wg_bytes = wg;
     s.wg = cv.take<char>(wg);
-    s.dz = materialize_dz_of(L[nl - 1]) ? cv.take<float>((size_t)M * (size_t)L[nl - 1].cout) : nullptr;
+    s.dz = materialize_dz_of(L[nl - 1], M, true) ? cv.take<float>((size_t)M * (size_t)L[nl - 1].cout) : nullptr;
     if (out) *out = s;
     return cv.used;
 }
@@ -385,7 +389,7 @@ PCS_API int pcs_mlp_backward(const float* X, int ldx, int kin, int M, const pcs_
     for (int l = nl - 1; l >= 0; --l) {
         const pcs_mlp_layer& P = layers[l];
         const int C = (int)P.cout, Cin = (int)P.cin;
-        if (materialize_dz_of(P) && (P.dW || l > 0 || dX)) {
+        if (materialize_dz_of(P, M, l > 0 || dX) && S.dz_ok(l == nl - 1)) {
             // the top layer's into its own buffer (gout is the caller's), inner ones in place
             // over the dA buffer the rebuilt operand reads
             float* dst = l == nl - 1 ? S.dz : const_cast<float*>(xop.data);

@@ -1049,6 +1049,24 @@ static void wgrad_plan(int N, int K, int M, int* BO, int* BI, int* splits, int* 
     *splits = (M + r - 1) / r;
 }
 
+// Column passes over a layer's dZ (M x C rows; cin = its input width) by its backward
+// GEMMs: the data gradient (M x cin output) re-reads dZ once per column tile, the weight
+// gradient (C x cin) once per cin tile.
+int pcs::dz_passes(int M, int C, int cin, bool dgrad, bool wgrad) {
+    int n = 0;
+    if (dgrad) {
+        int bm, bn;
+        gemm_tile(M, cin, true, &bm, &bn);
+        n += (cin + bn - 1) / bn;
+    }
+    if (wgrad) {
+        int BO, BI, sp, rows;
+        wgrad_plan(C, cin, M, &BO, &BI, &sp, &rows);
+        n += (cin + BI - 1) / BI;
+    }
+    return n;
+}
+
 size_t pcs::wgrad_ws_bytes(int N, int K, int M) {
     if (M <= 0) return 0;
     int BO, BI, sp, rows;

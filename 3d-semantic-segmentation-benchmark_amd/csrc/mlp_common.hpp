@@ -136,6 +136,8 @@ void bn_finalize_launch(const double* part, int nb, int N, long long M, const fl
 // bn_bwd_finalize_kernel launch: (sum dy, sum dy*xhat) partials -> dgamma/dbeta (+= when accum), kB, kC
 void bn_bwd_finalize_launch(const double* part, int nb, int N, long long M, const float* s, const float* inv,
                             float* dgamma, float* dbeta, float* kB, float* kC, int accum, hipStream_t st);
+// column passes of a layer's backward GEMMs over its dZ (M x C; cin = the layer's input width)
+int dz_passes(int M, int C, int cin, bool dgrad, bool wgrad);
 // out (M x C, stride ldo) = the BNBWD / POOLBWD operand x materialised (bitwise the on-load values)
 int materialize_dz(const pcs_operand* x, int M, int C, float* out, int ldo, hipStream_t st);
 // row GEMM with W row-major N x K (bt = 0, = pcs_gemm_rows) or K x N (bt = 1)
