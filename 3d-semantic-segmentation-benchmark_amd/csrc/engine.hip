@@ -18,6 +18,7 @@
 
 #include <algorithm>
 #include <mutex>
+#include <vector>
 
 namespace pcs {
 
@@ -129,10 +130,11 @@ struct BwdScratch {
     float* dz;             // the top layer's materialised dZ (M x cout), when it is wide
     bool dz_ok(bool top) const { return !top || dz != nullptr; }
     double* part;
-    float* kb[2];
-    float* alpha[2];
+    float* kb[3];          // BN-backward coefficients and data gradients rotate over 3
+    float* alpha[3];       // buffers: a layer's wgrad (side stream) may still read one while
+                           // the next two layers' dgrads run
     float* wt;
-    float* dA[2];
+    float* dA[3];
     char* wg;              // wgrad partial tiles (shared by the call's wgrads: one side stream)
     size_t wg_bytes;
 };
@@ -142,15 +144,15 @@ static size_t carve_backward(Carve& cv, int M, int kin, int ldx, const pcs_mlp_l
     const int mc = std::max(max_cout(L, nl), ldx);
     BwdScratch s{};
     s.part = cv.take<double>(max_partials(M, kin, L, nl, pool_k, true));
-    for (int i = 0; i < 2; ++i) { s.kb[i] = cv.take<float>(mc); s.alpha[i] = cv.take<float>(mc); }
+    for (int i = 0; i < 3; ++i) { s.kb[i] = cv.take<float>(mc); s.alpha[i] = cv.take<float>(mc); }
     size_t wt = 0, da = 0;
     for (int l = 0; l < nl; ++l) {
         wt = std::max(wt, (size_t)L[l].cout * (size_t)L[l].ldw);
         if (l > 0) da = std::max(da, (size_t)M * (size_t)L[l].cin);
     }
     s.wt = cv.take<float>(wt);
-    s.dA[0] = cv.take<float>(da);
-    s.dA[1] = cv.take<float>(da);
+    // the third buffer only when a stack is deep enough to rotate through it
+    for (int i = 0; i < 3; ++i) s.dA[i] = i < 2 || nl > 3 ? cv.take<float>(da) : nullptr;
     size_t wg = 0;
     for (int l = 0; l < nl; ++l)
         if (L[l].dW) wg = std::max(wg, wgrad_ws_bytes((int)L[l].cout, (int)L[l].cin, M));
@@ -374,7 +376,10 @@ PCS_API int pcs_mlp_backward(const float* X, int ldx, int kin, int M, const pcs_
     std::unique_lock<std::mutex> lane_lock;
     if (lane) lane_lock = std::unique_lock<std::mutex>(lane->use);
     hipEvent_t pending = nullptr;          // the last wgrad launched on the side stream
-    hipEvent_t prev = nullptr;             // the wgrad of the layer above (joined before this dgrad)
+    // done[l]: layer l's wgrad finished.  The dgrad of layer l recycles the dA / kb / alpha
+    // buffers (3-way rotation) that layer l + 2's wgrad read, so it waits for that one only:
+    // the layer above's wgrad keeps running under this dgrad.
+    std::vector<hipEvent_t> done(nl, nullptr);
     auto join = [&]() {
         if (pending) {
             (void)hipStreamWaitEvent(st, pending, 0);
@@ -408,16 +413,13 @@ PCS_API int pcs_mlp_backward(const float* X, int ldx, int kin, int M, const pcs_
             const pcs_operand y = Q ? bnact_op(Q->Z, Cin, *Q) : plain_op(X, ldx);
             const int e = pcs::wgrad_launch(&xop, C, &y, Cin, M, P.dW, P.db, S.wg, S.wg_bytes, ws_stream);
             if (lane) {                    // recorded even on error, so the join below covers it
-                prev = pending;
                 pending = lane_event(lane);
                 (void)hipEventRecord(pending, lane->side);
+                done[l] = pending;
             }
             if (e) return fail(e);
         }
-        if (prev) {                        // the layer above's wgrad read the buffers this dgrad recycles
-            (void)hipStreamWaitEvent(st, prev, 0);
-            prev = nullptr;
-        }
+        if (l + 2 < nl && done[l + 2]) (void)hipStreamWaitEvent(st, done[l + 2], 0);
         if (l == 0 && !dX) break;
         // dgrad B operand: B[k = cout][n = cin] = W[k][n], read k-major straight from W (bt = 1);
         // a first layer whose row stride is not a multiple of 4 goes through the transpose Wt
@@ -437,14 +439,14 @@ PCS_API int pcs_mlp_backward(const float* X, int ldx, int kin, int M, const pcs_
             pcs_operand epi = bnbwd_op(nullptr, 0, Q, nullptr, nullptr);
             if (int e = gemm_rows_ex(&xop, M, C, Bw, ldb, bt, nullptr, dA, Cin, Cin, nullptr, &epi, S.part, stream))
                 return fail(e);
-            pp ^= 1;
+            pp = (pp + 1) % 3;
             const float* sq = Q.coef;
             if (int e = pcs_bn_bwd_finalize(S.part, nbg, Cin, M, sq, sq + 3 * Cin, Q.dgamma, Q.dbeta, S.kb[pp],
                                             S.alpha[pp], 1, stream))
                 return fail(e);
             if (!Q.use_batch) { zero_f32(S.kb[pp], Cin, st); zero_f32(S.alpha[pp], Cin, st); }
             xop = bnbwd_op(dA, Cin, Q, S.alpha[pp], S.kb[pp]);
-            da ^= 1;
+            da = (da + 1) % 3;
         } else {
             zero_cols(dX, M, ldx, kin, st);      // the GEMM writes columns [0, kin)
             if (int e = gemm_rows_ex(&xop, M, C, Bw, ldb, bt, nullptr, dX, ldx, kin, nullptr, nullptr, nullptr, stream))
