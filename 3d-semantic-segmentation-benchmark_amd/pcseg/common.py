@@ -160,7 +160,38 @@ class GeometryPlan:
 
     @staticmethod
     def _wait(ev):
-        torch.cuda.current_stream().wait_event(ev)
+        if ev is not None:
+            torch.cuda.current_stream().wait_event(ev)
+
+    def tensors(self) -> list:
+        """Every tensor of the plan, in a fixed order (same structure -> same list layout)."""
+        out = list(self.coords)
+        for bl in self.balls:
+            for idx, inv in bl:
+                out += [idx, *(inv or ())]
+        for idx, dist, inv in self.nn:
+            out += [idx, dist, *(inv or ())]
+        return out
+
+    def settle(self) -> None:
+        """Forget the side-stream events once the plan is known complete (after a device
+        synchronize): a plan built outside a HIP-graph capture can then be read inside one."""
+        self.events = [None] * len(self.events)
+        if hasattr(self, 'nn_event'):
+            self.nn_event = None
+
+    def copy_from(self, other: 'GeometryPlan') -> None:
+        """Overwrite this plan's tensors with `other`'s (same levels and sizes) on the current
+        stream, after other's side-stream work: the double buffer of a graph-captured step,
+        whose forward reads this plan while it computes the next one."""
+        for ev in other.events:
+            self._wait(ev)
+        self._wait(getattr(other, 'nn_event', None))
+        mine, theirs = self.tensors(), other.tensors()
+        if len(mine) != len(theirs) or any(a.shape != b.shape for a, b in zip(mine, theirs)):
+            raise ValueError('GeometryPlan.copy_from: plans of different structure')
+        for a, b in zip(mine, theirs):
+            a.copy_(b)
 
     def sa(self, level: int, q: int = 0):
         """(centroids, ball idx, inverse map or None) of level >= 1 for its q-th query,

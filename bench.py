@@ -249,15 +249,44 @@ def run_workload(key, batch, npoints, args, world, rank, dev):
 
     eager_step = step
     if use_graph:
+        graph_prefetch = hasattr(model, 'prefetch_geometry') and not args.no_prefetch
         side = torch.cuda.Stream(dev)
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):
             for _ in range(max(args.warmup, 2)):
                 step()
+            plan = None
+            if graph_prefetch:
+                # double-buffered geometry: the captured forward reads `plan`; the captured
+                # prefetch computes the next step's plan under the backward and the step ends
+                # by copying it into `plan` (a few MB of indices), ready for the next replay
+                model.prefetch_geometry(x)
+                plan = model._pcs_prefetched[2]
+                torch.cuda.synchronize(dev)
+                plan.settle()
         torch.cuda.current_stream(dev).wait_stream(side)
+
+        def graph_body():
+            if plan is not None:
+                model._pcs_prefetched = (x, x._version, plan)
+            grads.zero_grad()
+            loss = pcseg.masked_onehot_cross_entropy(logits_of(model(x)), lab, lengths)
+            nxt = None
+            if plan is not None:
+                model.prefetch_geometry(x)
+                nxt = model._pcs_prefetched[2]
+            loss.backward()
+            grads.synchronize()
+            opt.step()
+            if nxt is not None:
+                plan.copy_from(nxt)
+                model._pcs_prefetched = None
+            return loss
+
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
-            static_loss = step()
+            static_loss = graph_body()
+        prefetch = plan is not None
 
         def step():
             graph.replay()

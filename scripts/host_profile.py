@@ -22,11 +22,12 @@ from pcseg.synthetic import make_batch  # noqa: E402
 
 model_name = sys.argv[1] if len(sys.argv) > 1 else 'pointnetpp'
 B = int(sys.argv[2]) if len(sys.argv) > 2 else 32
-name, ctor, kind = bench.MODELS[model_name]
+name, ctor, kind = bench.WORKLOADS[model_name][:3]
 dev = torch.device('cuda', 0)
 model = ctor(pcseg).to(dev).train()
 grads = FlatGradAllReduce(model)
-opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+from pcseg.optim import FlatAdam  # noqa: E402
+opt = FlatAdam(grads, lr=1e-3)
 pts, labels, lengths = make_batch(B, 4096, seed=7)
 x = bench.model_input(pts.to(dev), kind)
 lab = (labels.float() if kind == 'chfirst6' else labels).to(dev)

@@ -313,6 +313,32 @@ def test_prefetched_geometry_matches_inline(ctor):
     assert torch.equal(inline, again)
 
 
+def test_geometry_plan_copy_from_double_buffer():
+    """GeometryPlan.copy_from (bench.py --graph's double-buffered geometry): after copying
+    plan B into plan A's tensors, a forward that consumes A gives exactly the logits of a
+    forward that consumes B."""
+    torch.manual_seed(0)
+    model = pcseg.PointNetpp(14).to(DEV).train()
+    dropout_off(model)
+    pts, _, _ = make_batch(2, 4096, seed=32)
+    x = pts.to(DEV)
+    torch.manual_seed(1)
+    model.prefetch_geometry(x)
+    a = model._pcs_prefetched[2]
+    torch.manual_seed(2)
+    model.prefetch_geometry(x)
+    b = model._pcs_prefetched[2]
+    torch.cuda.synchronize()
+    assert any(not torch.equal(u, v) for u, v in zip(a.tensors(), b.tensors()))   # fresh FPS starts
+    model._pcs_prefetched = (x, x._version, b)
+    ref = model(x).detach().clone()
+    a.settle()
+    a.copy_from(b)
+    assert all(torch.equal(u, v) for u, v in zip(a.tensors(), b.tensors()))
+    model._pcs_prefetched = (x, x._version, a)
+    assert torch.equal(model(x).detach(), ref)
+
+
 # ---------------------------------------------------------------- bitwise reproducibility
 DET_MODELS = {
     'pointnetpp': (lambda: pcseg.PointNetpp(14), lambda p: p),
