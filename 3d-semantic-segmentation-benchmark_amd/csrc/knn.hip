@@ -6,16 +6,15 @@
 // device; parity for DGCNN uses neighbour-index replay and this
 // kernel is checked by set agreement + distance-margin tests.
 //
-// knn_tile_kernel (k <= 20): a workgroup owns 128 query rows (32 per wave) and streams
-// the cloud through LDS in 32-point candidate tiles.  Each wave computes its 32 x 32
-// block of inner products with v_mfma_f32_32x32x2_f32 (the k-slice of lane half h is
-// features h*F/2 .. h*F/2+F/2-1, so every lane reads one contiguous run; F = 3 is padded
-// to (x, y, z, 0)), then filters it against each row's running threshold (the current
-// k-th best) into per-lane LDS survivor segments (about k ln(N/k) survivors per row).
-// A row whose segments fill is merged by a radix select (k-th key by a 32-step ballot
-// search, no sort); the final merge ranks the survivors (larger pd first, ties to the
-// lower index).  The scan starts at the workgroup's own tile, so spatially ordered
-// clouds tighten the thresholds early.
+// knn_wave_kernel (k <= 20): each wave owns 32 query rows and streams the cloud in 32-point
+// candidate tiles straight into its MFMA operands.  It computes its 32 x 32 block of inner
+// products with v_mfma_f32_32x32x2_f32 (the k-slice of lane half h is features
+// h*F/2 .. h*F/2+F/2-1, so every lane reads one contiguous run; F = 3 is padded to
+// (x, y, z, 0)), then filters it against each row's running threshold (the current k-th
+// best) into per-lane LDS survivor segments (about k ln(N/k) survivors per row).  A row
+// whose segments fill is merged by a ballot quickselect (no sort); the final merge ranks
+// the survivors (larger pd first, ties to the lower index).  The scan starts at the wave's
+// own tile, so spatially ordered clouds tighten the thresholds early.
 // knn_kernel (k = 40): one thread per query row with a sorted register list.
 #include "pcs_common.hpp"
 
@@ -128,9 +127,6 @@ constexpr int KNN_RS = KNN_NMAX;       // row stride in items
 // (v_mfma_f32_32x32x2_f32 C/D layout: row = (i & 3) + 8 (i >> 2) + 4 h, column = lane & 31)
 __device__ __forceinline__ constexpr int acc_row(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
 
-#ifdef PCS_KNN_STATS
-__device__ unsigned long long g_knn_stats[2];   // merges, dropped-and-re-appended survivors (diagnostic build)
-#endif
 
 // Merge row r of this wave (r uniform): its top-k list (nl items) and the two lane-half
 // survivor segments (c0, c1 items) -- n <= 64 items, one per lane.  rank = number of items
@@ -248,37 +244,54 @@ __device__ __forceinline__ float knn_select_row(float2* L, int nl, int c0, int c
     return tnew;
 }
 
-// One workgroup = 128 query rows (32 per wave, row = lane & 31 of both lane halves).  The
-// MFMA computes the transposed block (candidates x queries), so each lane holds 16
-// candidates of ONE row: filtering is per lane, branch-free: every candidate is written
-// to the lane's LDS segment at its fill count (a rejected one is overwritten by the next),
-// and the count advances only for survivors.  A full segment flags the survivor as
-// dropped; after the wave merges the flagged rows the dropped survivors are re-appended.
-template <int F, int K>
-__global__ __launch_bounds__(256, 2) void knn_tile_kernel(const float* __restrict__ x, int N,
-                                                          int* __restrict__ out_idx) {
-    constexpr bool MF = (F % 4 == 0);        // else F = 3: xyz padded to (x, y, z, 0), k-slice 2
+// One workgroup = 4 independent waves x 32 query rows (row = lane & 31 of both lane halves).
+// Every wave streams the candidate tiles straight from global memory (L2-resident: one cloud
+// is N*F*4 bytes) into its MFMA operand registers, one tile ahead; no block barrier, so one
+// wave's running merge overlaps the others' MFMA / filter work (round 2: -23 % at F = 3,
+// -14 % at F = 64 against an LDS-staged tile ring with a barrier per tile, bitwise-equal
+// neighbour lists; 2- and 1-wave blocks measured slower).  The MFMA computes the transposed
+// block (candidates x queries), so each lane holds 16 candidates of ONE row: filtering is per
+// lane, branch-free: every candidate is written to the lane's LDS segment at its fill count
+// (a rejected one is overwritten by the next), and the count advances only for survivors.
+// A full segment flags the survivor as dropped; after the wave merges the flagged rows the
+// dropped survivors are re-appended.  Blocks of one cloud are mapped onto one XCD
+// (blockIdx round-robins over the 8 XCDs), so each XCD's L2 holds the clouds it works on.
+template <int F, int K, int WPB>
+__global__ __launch_bounds__(64 * WPB, 2) void knn_wave_kernel(const float* __restrict__ x, int B, int N, int rblocks,
+                                                            int* __restrict__ out_idx) {
+    constexpr bool MF = (F % 4 == 0);
     static_assert(MF || F == 3, "F must be 3 or a multiple of 4");
-    constexpr int FP = MF ? F + 4 : 4;       // LDS row stride: conflict-free b128 reads
-    constexpr int FH = MF ? F / 2 : 2;       // features per lane half (MFMA k-slice)
-    constexpr int SEG = (KNN_NMAX - K) / 2;  // CAP usable slots + 1 dump slot per lane half
+    constexpr int FH = MF ? F / 2 : 2;
+    constexpr int NQ = MF ? FH / 4 : 1;      // float4 per lane per tile
+    constexpr int SEG = (KNN_NMAX - K) / 2;
     constexpr int CAP = SEG - 1;
     static_assert(CAP >= 16, "a segment must take one tile's 16 candidates after a merge");
-    __shared__ __attribute__((aligned(16))) float s_c[2][KNN_TC * FP];   // double-buffered tile
-    __shared__ float s_cxx[KNN_WAVES][KNN_TC];
-    __shared__ float2 s_it[KNN_QROWS * KNN_RS];
+    __shared__ float s_cxx[WPB][KNN_TC];
+    __shared__ float2 s_it[32 * WPB * KNN_RS];
 
-    const int b = blockIdx.y;
-    const int q0 = blockIdx.x * KNN_QROWS;
+    // XCD-aware block -> (cloud, row block): linear block L runs on XCD L % 8; give each XCD
+    // whole clouds when the grid tiles evenly, else the plain row-major order
+    const int L = blockIdx.x;
+    const int total = B * rblocks;
+    int b, rb;
+    if (total % 8 == 0 && (total / 8) % rblocks == 0) {
+        const int per = total / 8;                   // blocks per XCD (whole clouds)
+        const int j = (L % 8) * per + L / 8;
+        b = j / rblocks;
+        rb = j - b * rblocks;
+    } else {
+        b = L / rblocks;
+        rb = L - b * rblocks;
+    }
+    const int q0 = rb * 32 * WPB;
     const int tid = threadIdx.x;
     const int w = tid >> 6, l = tid & 63, h = l >> 5, l32 = l & 31;
     const float* X = x + (size_t)b * N * F;
     const int wrow0 = w * 32;
     const int qr = min(q0 + wrow0 + l32, N - 1);
-    float2* const wl = s_it + wrow0 * KNN_RS;            // this wave's rows
-    float2* const sg = wl + l32 * KNN_RS + K + h * SEG;  // this lane's survivor segment
+    float2* const wl = s_it + wrow0 * KNN_RS;
+    float2* const sg = wl + l32 * KNN_RS + K + h * SEG;
 
-    // ---- the query row: MFMA B operand (features h*FH ..) and |x_q|^2 = half 0 + half 1
     float a[FH];
     float xxq;
     if constexpr (MF) {
@@ -292,8 +305,8 @@ __global__ __launch_bounds__(256, 2) void knn_tile_kernel(const float* __restric
 #pragma unroll
         for (int s = 0; s < FH; ++s) part = __fadd_rn(part, __fmul_rn(a[s], a[s]));
         const float other = __shfl_xor(part, 32);
-        xxq = h ? __fadd_rn(other, part) : __fadd_rn(part, other);     // half 0 + half 1
-    } else {                                 // (x*x + y*y) + z*z, the sequential order
+        xxq = h ? __fadd_rn(other, part) : __fadd_rn(part, other);
+    } else {
         const float* xr = X + (size_t)qr * 3;
         a[0] = h ? xr[2] : xr[0];
         a[1] = h ? 0.f : xr[1];
@@ -302,104 +315,66 @@ __global__ __launch_bounds__(256, 2) void knn_tile_kernel(const float* __restric
         xxq = h ? __fadd_rn(other, part) : __fadd_rn(part, other);
     }
     float tau = -INFINITY;
-    int cnt = 0, nl = 0;                     // segment fill, list length (per row)
-#ifdef PCS_KNN_COUNT
-    int n_merge = 0, n_surv = 0, n_tiles_merging = 0;
-#endif
+    int cnt = 0, nl = 0;
 
     const int ntile = (N + KNN_TC - 1) / KNN_TC;
-    const int t0 = q0 / KNN_TC;
-    // candidate tiles: global -> registers one tile ahead, registers -> LDS after the
-    // current tile's compute, one barrier per tile
-    constexpr int NV = MF ? (KNN_TC * (F / 4) + 255) / 256 : 1;
-    static_assert(NV <= 2, "prefetch holds two float4 per thread");
-    float4 pre0 = {}, pre1 = {};
-    float pre3[3] = {0.f, 0.f, 0.f};
+    const int t0 = (q0 + wrow0) / KNN_TC;                 // start at the wave's own rows
     auto tile_c0 = [&](int tt) {
         const int t = t0 + tt;
         return (t >= ntile ? t - ntile : t) * KNN_TC;
     };
-    auto fetch = [&](int tt) __attribute__((always_inline)) {
+    // this lane's candidate (l32) of tile tt: features h*FH .. (F = 3: (x, y) | (z, 0))
+    float4 cur[NQ], nxt[NQ];
+    auto fetch = [&](int tt, float4* dst) __attribute__((always_inline)) {
         const int c0 = tile_c0(tt);
-        const int nc = min(KNN_TC, N - c0);
+        const int n = c0 + min(l32, N - c0 - 1);
         if constexpr (MF) {
+            const float4* src = reinterpret_cast<const float4*>(X + (size_t)n * F + h * FH);
 #pragma unroll
-            for (int v = 0; v < NV; ++v) {
-                const int e = tid + 256 * v;
-                if (e < KNN_TC * (F / 4)) {
-                    const int n = e / (F / 4), f4 = e - n * (F / 4);
-                    const float4 g = *reinterpret_cast<const float4*>(X + (size_t)(c0 + min(n, nc - 1)) * F + 4 * f4);
-                    if (v == 0) pre0 = g; else pre1 = g;
-                }
-            }
+            for (int q = 0; q < NQ; ++q) dst[q] = src[q];
         } else {
-            if (tid < KNN_TC) {
-                const float* xr = X + (size_t)(c0 + min(tid, nc - 1)) * F;
-#pragma unroll
-                for (int f = 0; f < F; ++f) pre3[f] = xr[f];
-            }
+            const float* xr = X + (size_t)n * 3;
+            dst[0] = h ? make_float4(xr[2], 0.f, 0.f, 0.f) : make_float4(xr[0], xr[1], 0.f, 0.f);
         }
     };
-    auto put = [&](int buf) __attribute__((always_inline)) {
-        if constexpr (MF) {
-#pragma unroll
-            for (int v = 0; v < NV; ++v) {
-                const int e = tid + 256 * v;
-                if (e < KNN_TC * (F / 4)) {
-                    const int n = e / (F / 4), f4 = e - n * (F / 4);
-                    *reinterpret_cast<float4*>(&s_c[buf][n * FP + 4 * f4]) = v == 0 ? pre0 : pre1;
-                }
-            }
-        } else {
-            if (tid < KNN_TC)
-                *reinterpret_cast<float4*>(&s_c[buf][tid * 4]) = make_float4(pre3[0], pre3[1], pre3[2], 0.f);
-        }
-    };
-    fetch(0);
-    put(0);
-    __syncthreads();
+    fetch(0, cur);
     for (int tt = 0; tt < ntile; ++tt) {
-        const int buf = tt & 1;
         const int c0 = tile_c0(tt);
         const int nc = min(KNN_TC, N - c0);
-        if (tt + 1 < ntile) fetch(tt + 1);
-        // ---- pd of candidates c0 + acc_row(i, h) for this lane's row
+        if (tt + 1 < ntile) fetch(tt + 1, nxt);
         float pd[16];
         {
-            const float* cb = &s_c[buf][l32 * FP + h * FH];
             typedef float f32x16 __attribute__((ext_vector_type(16)));
             f32x16 acc = {};
             float part = 0.f;
             if constexpr (!MF) {
-                const float2 v = *reinterpret_cast<const float2*>(cb);
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(v.x, a[0], acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(v.y, a[1], acc, 0, 0, 0);
-                part = __fadd_rn(__fmul_rn(v.x, v.x), __fmul_rn(v.y, v.y));
-            }
+                const float vx = cur[0].x, vy = cur[0].y;
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(vx, a[0], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(vy, a[1], acc, 0, 0, 0);
+                part = __fadd_rn(__fmul_rn(vx, vx), __fmul_rn(vy, vy));
+            } else {
 #pragma unroll
-            for (int s = 0; s < (MF ? FH : 0); s += 4) {
-                const float4 v = *reinterpret_cast<const float4*>(cb + s);
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(v.x, a[s], acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(v.y, a[s + 1], acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(v.z, a[s + 2], acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(v.w, a[s + 3], acc, 0, 0, 0);
-                part = __fadd_rn(part, __fmul_rn(v.x, v.x));
-                part = __fadd_rn(part, __fmul_rn(v.y, v.y));
-                part = __fadd_rn(part, __fmul_rn(v.z, v.z));
-                part = __fadd_rn(part, __fmul_rn(v.w, v.w));
+                for (int q = 0; q < NQ; ++q) {
+                    const float4 v = cur[q];
+                    const int s = 4 * q;
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(v.x, a[s], acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(v.y, a[s + 1], acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(v.z, a[s + 2], acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(v.w, a[s + 3], acc, 0, 0, 0);
+                    part = __fadd_rn(part, __fmul_rn(v.x, v.x));
+                    part = __fadd_rn(part, __fmul_rn(v.y, v.y));
+                    part = __fadd_rn(part, __fmul_rn(v.z, v.z));
+                    part = __fadd_rn(part, __fmul_rn(v.w, v.w));
+                }
             }
             const float other = __shfl_xor(part, 32);
-            if (h == 0) s_cxx[w][l32] = __fadd_rn(part, other);   // |x_c|^2 of candidate l32
+            if (h == 0) s_cxx[w][l32] = __fadd_rn(part, other);
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
                 const float inner = -2.f * acc[i];
                 pd[i] = __fsub_rn(__fsub_rn(-xxq, inner), s_cxx[w][acc_row(i, h)]);
             }
         }
-#ifdef PCS_KNN_NOSEL
-        tau = INFINITY;       // diagnostic: nothing survives (staging + distances only)
-#endif
-        // ---- branch-free threshold filter into the lane's segment
         unsigned dropped = 0;
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
@@ -407,15 +382,9 @@ __global__ __launch_bounds__(256, 2) void knn_tile_kernel(const float* __restric
             sg[min(cnt, CAP)] = make_float2(pd[i], __int_as_float(c0 + acc_row(i, h)));
             dropped |= (p && cnt >= CAP) ? (1u << i) : 0u;
             cnt += (p && cnt < CAP) ? 1 : 0;
-#ifdef PCS_KNN_COUNT
-            n_surv += p ? 1 : 0;
-#endif
         }
         const unsigned long long nm = ballot(dropped != 0 || cnt > CAP - PCS_KNN_SLACK);
         if (nm) {
-#ifdef PCS_KNN_COUNT
-            ++n_tiles_merging;
-#endif
             unsigned rows = (unsigned)nm | (unsigned)(nm >> 32);
             while (rows) {
                 const int r = __ffs(rows) - 1;
@@ -423,26 +392,12 @@ __global__ __launch_bounds__(256, 2) void knn_tile_kernel(const float* __restric
                 const int c0n = (int)readlane_u((unsigned)cnt, r);
                 const int c1n = (int)readlane_u((unsigned)cnt, r + 32);
                 const int nlr = (int)readlane_u((unsigned)nl, r);
-#ifdef PCS_KNN_NOMERGE
-                const float nt = tau;  // diagnostic: drop the segments instead of merging
-#else
                 const float nt = knn_select_row<K, SEG>(wl + r * KNN_RS, nlr, c0n, c1n, l);
-#endif
                 const bool mine = l32 == r;
                 tau = mine ? nt : tau;
                 cnt = mine ? 0 : cnt;
                 nl = mine ? min(nlr + c0n + c1n, K) : nl;
-#ifdef PCS_KNN_COUNT
-                n_merge += mine ? 1 : 0;
-#endif
-#ifdef PCS_KNN_STATS
-                if (l == 0) atomicAdd(&g_knn_stats[0], 1ull);
-#endif
             }
-#ifdef PCS_KNN_STATS
-            atomicAdd(&g_knn_stats[1], (unsigned long long)__popc(dropped));
-#endif
-            // re-append the survivors that found their segment full (their row was merged)
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
                 const bool p = ((dropped >> i) & 1u) && pd[i] >= tau;
@@ -450,21 +405,9 @@ __global__ __launch_bounds__(256, 2) void knn_tile_kernel(const float* __restric
                 cnt += p ? 1 : 0;
             }
         }
-        if (tt + 1 < ntile) put(buf ^ 1);
-        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) cur[q] = nxt[q];
     }
-    // ---- final merge of every row, written out best first
-#ifdef PCS_KNN_COUNT
-    if (q0 + wrow0 + l32 < N) {
-        int* o = out_idx + ((size_t)b * N + q0 + wrow0 + l32) * K;
-        if (h == 0) { o[0] = n_merge; o[1] = n_surv; o[3] = n_tiles_merging; } else { o[2] = n_surv; }
-    }
-    return;
-#endif
-#ifdef PCS_KNN_NOFINAL
-    if (tau == 12345.f) out_idx[0] = cnt;
-    return;
-#endif
     for (int r = 0; r < 32; ++r) {
         const int c0n = (int)readlane_u((unsigned)cnt, r);
         const int c1n = (int)readlane_u((unsigned)cnt, r + 32);
@@ -472,15 +415,11 @@ __global__ __launch_bounds__(256, 2) void knn_tile_kernel(const float* __restric
         const int q = q0 + wrow0 + r;
         int* o = q < N ? out_idx + ((size_t)b * N + q) * K : nullptr;
         if (!o) continue;
-#ifndef PCS_KNN_RANKALL
         if (nlr + c0n + c1n > K) {
-            // quickselect the k best into the list first, then rank only those k
-            // (k readlane rounds per row instead of up to nl + c0 + c1)
             knn_select_row<K, SEG>(wl + r * KNN_RS, nlr, c0n, c1n, l);
             knn_merge_row<K, SEG>(wl + r * KNN_RS, K, 0, 0, l, o);
             continue;
         }
-#endif
         knn_merge_row<K, SEG>(wl + r * KNN_RS, nlr, c0n, c1n, l, o);
     }
 }
@@ -491,8 +430,9 @@ constexpr bool knn_tiled() { return (KNN_NMAX - K) / 2 - 1 >= 16; }
 template <int F, int K>
 static void launch_knn(const float* x, int B, int N, int* out, hipStream_t s) {
     if constexpr (knn_tiled<K>()) {
-        hipLaunchKernelGGL((knn_tile_kernel<F, K>), dim3((N + KNN_QROWS - 1) / KNN_QROWS, B), dim3(256), 0, s, x,
-                           N, out);
+        const int rb = (N + KNN_QROWS - 1) / KNN_QROWS;
+        hipLaunchKernelGGL((knn_wave_kernel<F, K, KNN_WAVES>), dim3(rb * B), dim3(64 * KNN_WAVES), 0, s, x, B, N, rb,
+                           out);
         return;
     }
     hipLaunchKernelGGL((knn_kernel<F, K>), dim3((N + 255) / 256, B), dim3(256), 0, s, x, N, out);
@@ -533,11 +473,4 @@ PCS_API int pcs_knn(const float* x, int B, int N, int F, int k, int32_t* out_idx
     return launch_status("pcs_knn");
 }
 
-#ifdef PCS_KNN_STATS
-// diagnostic build only: (merges, appended survivors) since the last call
-PCS_API int pcs_knn_stats(unsigned long long* out2) {
-    unsigned long long z[2] = {0, 0};
-    if (hipMemcpyFromSymbol(out2, HIP_SYMBOL(pcs::g_knn_stats), sizeof(z)) != hipSuccess) return 1;
-    return hipMemcpyToSymbol(HIP_SYMBOL(pcs::g_knn_stats), z, sizeof(z)) != hipSuccess;
-}
-#endif
+
