@@ -333,9 +333,9 @@ PCS_API int pcs_mlp_forward(const float* X, int ldx, int kin, int M, pcs_mlp_lay
     return pcs_bn_act(T.Z, C, M, C, T.coef, T.coef + C, (int)T.act, (float)T.slope, out, C, stream);
 }
 
-PCS_API int pcs_mlp_backward(const float* X, int ldx, int kin, int M, const pcs_mlp_layer* layers, int nl,
-                             int pool_k, const uint8_t* arg, const float* gout, float* dX, void* ws, size_t ws_bytes,
-                             void* stream) {
+static int mlp_backward(const float* X, int ldx, int kin, int M, const pcs_mlp_layer* layers, int nl, int pool_k,
+                        const uint8_t* arg, const float* gout, float* dX, void* ws, size_t ws_bytes, void* stream,
+                        bool defer) {
     if (int e = check_layers(M, kin, ldx, layers, nl, pool_k, "pcs_mlp_backward")) return e;
     PCS_CHECK_ARG(X && gout && (!pool_k || arg), "pcs_mlp_backward: null pointer");
     if (M == 0) return 0;
@@ -453,6 +453,35 @@ PCS_API int pcs_mlp_backward(const float* X, int ldx, int kin, int M, const pcs_
                 return fail(e);
         }
     }
-    join();
+    if (!defer) join();
     return launch_status("pcs_mlp_backward");
+}
+
+PCS_API int pcs_mlp_backward(const float* X, int ldx, int kin, int M, const pcs_mlp_layer* layers, int nl,
+                             int pool_k, const uint8_t* arg, const float* gout, float* dX, void* ws, size_t ws_bytes,
+                             void* stream) {
+    return mlp_backward(X, ldx, kin, M, layers, nl, pool_k, arg, gout, dX, ws, ws_bytes, stream, false);
+}
+
+PCS_API int pcs_mlp_backward_deferred(const float* X, int ldx, int kin, int M, const pcs_mlp_layer* layers, int nl,
+                                      int pool_k, const uint8_t* arg, const float* gout, float* dX, void* ws,
+                                      size_t ws_bytes, void* stream) {
+    return mlp_backward(X, ldx, kin, M, layers, nl, pool_k, arg, gout, dX, ws, ws_bytes, stream, true);
+}
+
+PCS_API int pcs_wgrad_lane(void** side_stream) {
+    PCS_CHECK_ARG(side_stream, "pcs_wgrad_lane: null pointer");
+    WgradLane* lane = wgrad_lane();
+    *side_stream = lane ? lane->side : nullptr;
+    return 0;
+}
+
+PCS_API int pcs_wgrad_lane_join(void* stream) {
+    WgradLane* lane = wgrad_lane();
+    if (!lane) return 0;
+    std::lock_guard<std::mutex> g(lane->use);
+    hipEvent_t e = lane_event(lane);
+    if (hipEventRecord(e, lane->side) != hipSuccess || hipStreamWaitEvent(as_stream(stream), e, 0) != hipSuccess)
+        return launch_status("pcs_wgrad_lane_join");
+    return 0;
 }

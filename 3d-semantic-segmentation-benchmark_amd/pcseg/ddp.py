@@ -14,6 +14,8 @@ from __future__ import annotations
 import torch
 import torch.distributed as dist
 
+from .engine import wgrad_lane
+
 
 def broadcast_model(model: torch.nn.Module, src: int = 0) -> None:
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
@@ -91,7 +93,16 @@ class FlatGradAllReduce:
         if self._pending[b] == 0 and not self._launched[b]:
             s, e, _ = self.buckets[b]
             self._launched[b] = True
-            self._handles.append(dist.all_reduce(self.flat[s:e], op=dist.ReduceOp.SUM, async_op=True))
+            lane = wgrad_lane(self.flat.device) if self.flat.is_cuda else None
+            if lane is None:
+                self._handles.append(dist.all_reduce(self.flat[s:e], op=dist.ReduceOp.SUM, async_op=True))
+            else:
+                # the bucket's weight gradients may still be running on the engine's wgrad lane
+                # (pcs_mlp_backward_deferred): issue the reduction behind both the lane and the
+                # current stream, without making the current stream wait for the lane
+                lane.wait_stream(torch.cuda.current_stream(self.flat.device))
+                with torch.cuda.stream(lane):
+                    self._handles.append(dist.all_reduce(self.flat[s:e], op=dist.ReduceOp.SUM, async_op=True))
 
     def synchronize(self) -> None:
         """Finish all bucket reductions and average (call before optimizer.step())."""

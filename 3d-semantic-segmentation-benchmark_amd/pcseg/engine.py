@@ -165,6 +165,45 @@ _REC = struct.Struct('<QqqqQQQQQQddqqdQQQQQQqqq')
 _ws_cache: dict = {}
 
 
+# --------------------------------------------------------------------------- wgrad lane
+# A stack's weight gradients run on the device's wgrad lane (a native side stream).  With
+# pcs_mlp_backward_deferred they keep running after the stack's backward returns, under the
+# next autograd nodes, and one join per backward pass (an autograd engine callback) makes
+# the caller's stream wait for them before anything reads the gradients.
+_lanes: dict = {}
+_join_queued: set = set()
+
+
+def wgrad_lane(dev: torch.device):
+    """torch.cuda.ExternalStream of the device's wgrad lane (None if the library has none)."""
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    if idx not in _lanes:
+        out = ctypes.c_void_p(0)
+        with torch.cuda.device(idx):
+            call('pcs_wgrad_lane', ctypes.byref(out))
+        _lanes[idx] = torch.cuda.ExternalStream(out.value, device=torch.device('cuda', idx)) if out.value else None
+    return _lanes[idx]
+
+
+def _queue_lane_join(dev: torch.device) -> None:
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    if idx in _join_queued:
+        return
+    _join_queued.add(idx)
+
+    def join():
+        _join_queued.discard(idx)
+        with torch.cuda.device(idx):
+            call('pcs_wgrad_lane_join', stream_ptr(torch.device('cuda', idx)))
+    torch.autograd.Variable._execution_engine.queue_callback(join)
+
+
+def lane_join(dev: torch.device) -> None:
+    """Make the current stream wait for every weight gradient pending on the device's lane."""
+    with torch.cuda.device(dev):
+        call('pcs_wgrad_lane_join', stream_ptr(dev))
+
+
 def _workspace(lib, key, M, kin, ldx, recs, nl, pool_k, backward):
     n = _ws_cache.get(key)
     if n is None:
@@ -281,7 +320,17 @@ class SharedMLPFn(torch.autograd.Function):
         key = (M, Kin, ldx, tuple(couts), pool_K, 1)
         nws = _workspace(lib, key, M, Kin, ldx, recs, nl, pool_K, 1)
         ws = torch.empty((nws,), dtype=torch.uint8, device=dev)
-        call('pcs_mlp_backward', ptr(X), ldx, Kin, M, recs, nl, pool_K, ptr(arg), ptr(gout), ptr(dX), ptr(ws), nws, st)
+        lane = wgrad_lane(dev)
+        if lane is None:
+            call('pcs_mlp_backward', ptr(X), ldx, Kin, M, recs, nl, pool_K, ptr(arg), ptr(gout), ptr(dX), ptr(ws), nws,
+                 st)
+        else:
+            call('pcs_mlp_backward_deferred', ptr(X), ldx, Kin, M, recs, nl, pool_K, ptr(arg), ptr(gout), ptr(dX),
+                 ptr(ws), nws, st)
+            # the lane still reads these: the caching allocator must not hand them out before it is done
+            for t in (X, saved[1], saved[2], gout, ws, *([arg] if arg is not None else [])):
+                t.record_stream(lane)
+            _queue_lane_join(dev)
         notify_grad_ready(params)
         return (dX, None, None, None, None, *([None] * len(params)))
 

@@ -222,6 +222,18 @@ int pcs_mlp_backward(const float* X, int ldx, int kin, int M,
                      const pcs_mlp_layer* layers, int nl, int pool_k,
                      const uint8_t* arg, const float* gout, float* dX,
                      void* workspace, size_t ws_bytes, void* stream);
+/* The same, but the weight gradients are left running on the device's wgrad lane (a side
+ * stream) after return, so they overlap the caller's next work.  Until
+ * pcs_wgrad_lane_join(stream) has been enqueued, dW/db are not ready and X, gout, the
+ * layers' Z/coef and the workspace must stay allocated (lane stream: pcs_wgrad_lane). */
+int pcs_mlp_backward_deferred(const float* X, int ldx, int kin, int M,
+                              const pcs_mlp_layer* layers, int nl, int pool_k,
+                              const uint8_t* arg, const float* gout, float* dX,
+                              void* workspace, size_t ws_bytes, void* stream);
+/* the current device's wgrad lane stream (null if none could be created) */
+int pcs_wgrad_lane(void** side_stream);
+/* `stream` waits for every weight gradient enqueued on the current device's lane so far */
+int pcs_wgrad_lane_join(void* stream);
 
 /* ---- harness-B batch (Training/train_model.py:89-171, preprocess_batch_to_train_format)
  * sample i's rows are packed at [offsets[i], offsets[i] + lengths[i]) of points (rows x D)
