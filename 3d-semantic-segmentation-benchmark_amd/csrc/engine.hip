@@ -137,6 +137,8 @@ struct BwdScratch {
     float* dA[3];
     char* wg;              // wgrad partial tiles (shared by the call's wgrads: one side stream)
     size_t wg_bytes;
+    char* wg0;             // the first layer's, when its wgrad runs on the caller's stream
+    size_t wg0_bytes;
 };
 
 static size_t carve_backward(Carve& cv, int M, int kin, int ldx, const pcs_mlp_layer* L, int nl, int pool_k,
@@ -158,6 +160,8 @@ static size_t carve_backward(Carve& cv, int M, int kin, int ldx, const pcs_mlp_l
         if (L[l].dW) wg = std::max(wg, wgrad_ws_bytes((int)L[l].cout, (int)L[l].cin, M));
     s.wg_bytes = wg;
     s.wg = cv.take<char>(wg);
+    s.wg0_bytes = L[0].dW ? wgrad_ws_bytes((int)L[0].cout, (int)L[0].cin, M) : 0;
+    s.wg0 = cv.take<char>(s.wg0_bytes);
     s.dz = materialize_dz_of(L[nl - 1], M, true) ? cv.take<float>((size_t)M * (size_t)L[nl - 1].cout) : nullptr;
     if (out) *out = s;
     return cv.used;
@@ -401,7 +405,14 @@ static int mlp_backward(const float* X, int ldx, int kin, int M, const pcs_mlp_l
             if (int e = materialize_dz(&xop, M, C, dst, C, st)) return fail(e);
             xop = plain_op(dst, C);
         }
-        if (P.dW) {
+        // the first layer's wgrad goes to the caller's stream when no dgrad follows it (the
+        // stack's input needs no gradient): it then runs beside the lane's pending wgrads
+        // instead of queueing behind them at the end of the backward
+        const bool wg_here = l == 0 && !dX && nl > 1;
+        if (P.dW && wg_here) {
+            const pcs_operand y = plain_op(X, ldx);
+            if (int e = pcs::wgrad_launch(&xop, C, &y, Cin, M, P.dW, P.db, S.wg0, S.wg0_bytes, stream)) return fail(e);
+        } else if (P.dW) {
             void* ws_stream = stream;
             if (lane) {                    // fork: the side stream waits for dZ's inputs
                 hipEvent_t ready = lane_event(lane);
