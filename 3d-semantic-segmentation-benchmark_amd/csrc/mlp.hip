@@ -1042,6 +1042,10 @@ static void wgrad_plan(int N, int K, int M, int* BO, int* BI, int* splits, int* 
     const int tiles = ((N + *BO - 1) / *BO) * ((K + *BI - 1) / *BI);
     const int target = 2.0 * M * N * K >= 1.6e10 ? 2048 : 1024;
     int sp = (target + tiles - 1) / tiles;
+    // the partial tiles (sp x N x K floats, written once and read once by the reduce) stay
+    // below half the operands' bytes M x (N + K), as long as >= 512 blocks remain
+    const long long cap = std::max<long long>((512 + tiles - 1) / tiles, (long long)M * (N + K) / (2LL * N * K));
+    if (sp > cap) sp = (int)cap;
     int r = (M + sp - 1) / sp;
     r = ((r + 255) / 256) * 256;
     if (r < 256) r = 256;

@@ -1,10 +1,19 @@
-# HBM traffic per kernel from PMC counters (two separate passes, kernel-trace only; see
-# MI355X_MICROARCH.md "HBM": FETCH_SIZE is doubled on gfx950, WRITE_SIZE exact).
+# HBM traffic per kernel from PMC counters, one model per pair of passes (FETCH_SIZE, WRITE_SIZE:
+# separate runs, kernel-trace only; MI355X_MICROARCH.md "HBM": FETCH_SIZE doubled on gfx950).
+# usage: scripts/gpu_pmc.sh <tag> [model ...]   -> gpurun_out/pmc_<tag>/<model>.{txt,json}
 set -u
-cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
+cd "$GRAFT_REPO_ROOT"
+tag=${1:-r02}; shift || true
+models=${*:-pointnetpp dgcnn}
+out="$GRAFT_REPO_ROOT/gpurun_out/pmc_$tag"; mkdir -p "$out"
 export TMPDIR=/tmp
-ARGS="--steps 3 --warmup 2 --no-cpu-baseline --no-roofline ${BENCH_ARGS:-}"
-cd /tmp
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$GRAFT_REPO_ROOT/gpurun_out/pmc_fetch" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" $ARGS > "$GRAFT_REPO_ROOT/gpurun_out/pmc_fetch.log" 2>&1; rc=$?; echo "pmc fetch rc=$rc"; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$GRAFT_REPO_ROOT/gpurun_out/pmc_write" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" $ARGS > "$GRAFT_REPO_ROOT/gpurun_out/pmc_write.log" 2>&1; rc=$?; echo "pmc write rc=$rc"; [ $rc -eq 0 ] || exit $rc
-cd "$GRAFT_REPO_ROOT" && python scripts/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write > gpurun_out/pmc_traffic.txt 2>&1; echo "pmc parse rc=$?"; head -30 gpurun_out/pmc_traffic.txt
+for m in $models; do
+  ARGS="--model $m --steps 3 --warmup 2 --no-cpu-baseline --no-roofline --secondary none"
+  for c in FETCH_SIZE WRITE_SIZE; do
+    cd /tmp && timeout -k 10 300 rocprofv3 --pmc $c --kernel-trace -d "$out/${m}_$c" -o run --output-format csv -- \
+       python3 "$GRAFT_REPO_ROOT/bench.py" $ARGS > "$out/${m}_$c.log" 2>&1; rc=$?
+    echo "$m pmc $c rc=$rc"; [ $rc -eq 0 ] || exit $rc
+  done
+  cd "$GRAFT_REPO_ROOT" && python3 scripts/pmc_traffic.py "$out/${m}_FETCH_SIZE" "$out/${m}_WRITE_SIZE" \
+     --json "$out/$m.json" > "$out/$m.txt" 2>&1; echo "$m parse rc=$?"; head -5 "$out/$m.txt"
+done

@@ -9,7 +9,7 @@ out=gpurun_out/prof_$tag; mkdir -p $out
 export TMPDIR=/tmp
 for m in $models; do
   cd /tmp && timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$out/$m" -o run --output-format csv -- \
-     python3 "$GRAFT_REPO_ROOT/bench.py" --model $m --steps 10 --warmup 3 --no-cpu-baseline --no-roofline \
+     python3 "$GRAFT_REPO_ROOT/bench.py" --model $m --steps 10 --warmup 3 --no-cpu-baseline --no-roofline --secondary none \
      > "$GRAFT_REPO_ROOT/$out/$m.log" 2>&1; rc=$?
   cd "$GRAFT_REPO_ROOT"; echo "$m prof rc=$rc"; tail -1 $out/$m.log | cut -c1-300
   [ $rc -eq 0 ] || exit $rc
