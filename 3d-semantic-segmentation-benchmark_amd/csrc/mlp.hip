@@ -21,6 +21,8 @@
 // Statistics are accumulated in fp64 (as ATen's CPU batch norm does).
 #include "mlp_common.hpp"
 
+#include <type_traits>
+
 #include <stdlib.h>
 
 namespace pcs {
@@ -46,7 +48,13 @@ __device__ __forceinline__ int lds_swz(int c) { return ((c >> 3) & 7) << 2; }
 // BT: B is stored k-major, B[k][n] = W[k*ldw + n] (the data-gradient GEMM reads the layer's
 // own weight matrix, no transpose): quads are loaded along n and written transposed into
 // Bs with the lds_swz row swizzle (the fragment reads apply the same swizzle).
-template <int BM, int BN, int WM, int WN, int AM, bool BT>
+// EPI: what the epilogue computes besides storing C, fixed at compile time so the per-element
+// epilogue is straight-line code: EPI_STATS (BN partials of C), EPI_BWD (BN-backward partials
+// of the previous layer), EPI_POOL (fused max/min over K rows), or EPI_GENERIC (decided from
+// the arguments at run time: the combinations the engine never issues).
+constexpr int EPI_STATS = 1, EPI_BWD = 2, EPI_POOL = 4, EPI_GENERIC = 8;
+
+template <int BM, int BN, int WM, int WN, int AM, bool BT, int EPI>
 __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(GemmArgs g) {
     constexpr int WTM = BM / WM, WTN = BN / WN;
     constexpr int TM = WTM / 32, TN = WTN / 32;
@@ -58,7 +66,8 @@ __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(GemmArgs g) {
     __shared__ __attribute__((aligned(16))) float Bs[2][BN][GLDK];
     __shared__ double red[2][WM][BN];
 
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (scalar) index
     const int wm = wave / WN, wn = wave % WN;
     const int n0 = blockIdx.y * BN;
     const int h = lane >> 5, l32 = lane & 31;
@@ -145,8 +154,10 @@ __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(GemmArgs g) {
     // ---- persistent loop: this block owns row tiles blockIdx.x + t*gridDim.x; the (tile, slab)
     // iterations are flattened so the NEXT tile's first slab is loading while this tile's
     // epilogue stores C (no exposed prologue per tile)
-    const bool want_stats = g.stats != nullptr;
-    const bool want_b = g.bstats != nullptr;
+    constexpr bool GEN = (EPI & EPI_GENERIC) != 0;
+    const bool want_stats = GEN ? g.stats != nullptr : (EPI & EPI_STATS) != 0;
+    const bool want_b = GEN ? g.bstats != nullptr : (EPI & EPI_BWD) != 0;
+    const bool do_pool = GEN ? g.pool_k != 0 : (EPI & EPI_POOL) != 0;
     double s1[TN], s2[TN];
 #pragma unroll
     for (int j = 0; j < TN; ++j) { s1[j] = 0.0; s2[j] = 0.0; }
@@ -195,78 +206,101 @@ __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(GemmArgs g) {
             // ---- tile epilogue: bias, store, per-channel partial reductions.  The fused
             // BN-backward epilogue's Z loads are issued for a whole column strip first
             // (clamped addresses, no branches) so their latency is paid once, not per element.
+            // A tile whose rows and columns are all in range (every tile but a ragged last
+            // one) takes the FULL path: no per-element bounds checks, and C / Z addressed as a
+            // wave-uniform 64-bit row base + a 32-bit per-lane offset (saddr loads / stores)
+            // instead of a 64-bit multiply-add per element.
+            auto epilogue = [&](auto full_t) __attribute__((always_inline)) {
+                constexpr bool FULL = decltype(full_t)::value;
 #pragma unroll
-            for (int j = 0; j < TN; ++j) {
-                const int col = n0 + wn * WTN + j * 32 + l32;
-                const bool cok = col < g.N;
-                const int colc = cok ? col : g.N - 1;
-                const float bv = (g.bias && cok) ? g.bias[col] : 0.f;
-                float sp = 0.f, tp = 0.f, mp = 0.f, ip = 0.f;
-                if (want_b) { sp = g.e.s[colc]; tp = g.e.t[colc]; mp = g.e.mean[colc]; ip = g.e.inv[colc]; }
+                for (int j = 0; j < TN; ++j) {
+                    const int col = n0 + wn * WTN + j * 32 + l32;
+                    const bool cok = FULL || col < g.N;
+                    const int colc = cok ? col : g.N - 1;
+                    const float bv = (g.bias && cok) ? g.bias[col] : 0.f;
+                    float sp = 0.f, tp = 0.f, mp = 0.f, ip = 0.f;
+                    if (want_b) { sp = g.e.s[colc]; tp = g.e.t[colc]; mp = g.e.mean[colc]; ip = g.e.inv[colc]; }
 #pragma unroll
-                for (int i = 0; i < TM; ++i) {
-                // fused pooling state of this lane's rows of the 32-row block (a group of 32, or
-                // one group of 16 per hb): running max/min of C and the first row reaching it
-                float pmx = -INFINITY, pmn = INFINITY;
-                int imx = 4 * h, imn = 4 * h;
+                    for (int i = 0; i < TM; ++i) {
+                    const int rb = __builtin_amdgcn_readfirstlane(m0 + wm * WTM + i * 32);   // wave-uniform
+                    float* const Cb = g.C + (size_t)rb * g.ldc;
+                    const float* const Zb = g.e.z + (size_t)rb * g.e.ldz;
+                    // fused pooling state of this lane's rows of the 32-row block (a group of 32, or
+                    // one group of 16 per hb): running max/min of C and the first row reaching it
+                    float pmx = -INFINITY, pmn = INFINITY;
+                    int imx = 4 * h, imn = 4 * h;
 #pragma unroll
-                for (int hb = 0; hb < 2; ++hb) {     // Z loads batched 8 at a time (register budget)
-                    if (g.pool_k == 16 && hb == 1) { pmx = -INFINITY; pmn = INFINITY; imx = imn = 16 + 4 * h; }
-                    float zt[8];
-                    if (want_b) {
+                    for (int hb = 0; hb < 2; ++hb) {     // Z loads batched 8 at a time (register budget)
+                        if (do_pool && g.pool_k == 16 && hb == 1) { pmx = -INFINITY; pmn = INFINITY; imx = imn = 16 + 4 * h; }
+                        float zt[8];
+                        if (want_b) {
+#pragma unroll
+                            for (int rr = 0; rr < 8; ++rr) {
+                                const int r = 8 * hb + rr;
+                                const int rl = (r & 3) + 8 * (r >> 2) + 4 * h;
+                                if constexpr (FULL) {
+                                    const unsigned bo = 4u * (unsigned)(rl * g.e.ldz + col);   // 32-bit byte offset
+                                    zt[rr] = *reinterpret_cast<const float*>(reinterpret_cast<const char*>(Zb) + bo);
+                                } else {
+                                    const int row = min(rb + rl, g.M - 1);
+                                    zt[rr] = g.e.z[(size_t)row * g.e.ldz + colc];
+                                }
+                            }
+                        }
 #pragma unroll
                         for (int rr = 0; rr < 8; ++rr) {
                             const int r = 8 * hb + rr;
-                            const int row = min(m0 + wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h, g.M - 1);
-                            zt[rr] = g.e.z[(size_t)row * g.e.ldz + colc];
+                            const int rl = (r & 3) + 8 * (r >> 2) + 4 * h;
+                            const bool ok = FULL || (rb + rl < g.M && cok);
+                            const float v = acc[i][j][r] + bv;
+                            if constexpr (FULL) {
+                                const unsigned bo = 4u * (unsigned)(rl * g.ldc + col);
+                                *reinterpret_cast<float*>(reinterpret_cast<char*>(Cb) + bo) = v;
+                            } else {
+                                if (ok) g.C[(size_t)(rb + rl) * g.ldc + col] = v;
+                            }
+                            if (do_pool) {
+                                const int rib = rl;                          // increasing in r: first wins
+                                if (v > pmx) { pmx = v; imx = rib; }
+                                if (v < pmn) { pmn = v; imn = rib; }
+                            }
+                            if (want_stats) {
+                                const double d = ok ? (double)v : 0.0;
+                                s1[j] += d;
+                                s2[j] += d * d;
+                            }
+                            if (want_b) {
+                                const float z = zt[rr];
+                                const float dy = v * dact_f(z * sp + tp, g.e.act, g.e.slope);
+                                const float xh = (z - mp) * ip;
+                                const double dd = ok ? (double)dy : 0.0;
+                                s1[j] += dd;
+                                s2[j] += dd * (double)xh;
+                            }
+                            acc[i][j][r] = 0.f;
+                        }
+                        if (do_pool && (g.pool_k == 16 || hb == 1)) {
+                            // merge with the other lane half (same column, the other rows), first row on ties
+                            const float ox = __shfl_xor(pmx, 32), on = __shfl_xor(pmn, 32);
+                            const int oix = __shfl_xor(imx, 32), oin = __shfl_xor(imn, 32);
+                            if (ox > pmx || (ox == pmx && oix < imx)) { pmx = ox; imx = oix; }
+                            if (on < pmn || (on == pmn && oin < imn)) { pmn = on; imn = oin; }
+                            const int r0 = rb + (g.pool_k == 16 ? 16 * hb : 0);
+                            if (h == 0 && cok && r0 < g.M) {
+                                const size_t G = (size_t)(g.M / g.pool_k), gi = (size_t)(r0 / g.pool_k);
+                                const int base = g.pool_k == 16 ? 16 * hb : 0;
+                                g.pz[gi * g.N + col] = pmx;
+                                g.pz[(G + gi) * g.N + col] = pmn;
+                                g.pa[gi * g.N + col] = (unsigned char)(imx - base);
+                                g.pa[(G + gi) * g.N + col] = (unsigned char)(imn - base);
+                            }
                         }
                     }
-#pragma unroll
-                    for (int rr = 0; rr < 8; ++rr) {
-                        const int r = 8 * hb + rr;
-                        const int row = m0 + wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                        const bool ok = row < g.M && cok;
-                        const float v = acc[i][j][r] + bv;
-                        if (ok) g.C[(size_t)row * g.ldc + col] = v;
-                        if (g.pool_k) {
-                            const int rib = (r & 3) + 8 * (r >> 2) + 4 * h;   // increasing in r: first wins
-                            if (v > pmx) { pmx = v; imx = rib; }
-                            if (v < pmn) { pmn = v; imn = rib; }
-                        }
-                        if (want_stats) {
-                            const double d = ok ? (double)v : 0.0;
-                            s1[j] += d;
-                            s2[j] += d * d;
-                        }
-                        if (want_b) {
-                            const float z = zt[rr];
-                            const float dy = v * dact_f(z * sp + tp, g.e.act, g.e.slope);
-                            const float xh = (z - mp) * ip;
-                            const double dd = ok ? (double)dy : 0.0;
-                            s1[j] += dd;
-                            s2[j] += dd * (double)xh;
-                        }
-                        acc[i][j][r] = 0.f;
-                    }
-                    if (g.pool_k && (g.pool_k == 16 || hb == 1)) {
-                        // merge with the other lane half (same column, the other rows), first row on ties
-                        const float ox = __shfl_xor(pmx, 32), on = __shfl_xor(pmn, 32);
-                        const int oix = __shfl_xor(imx, 32), oin = __shfl_xor(imn, 32);
-                        if (ox > pmx || (ox == pmx && oix < imx)) { pmx = ox; imx = oix; }
-                        if (on < pmn || (on == pmn && oin < imn)) { pmn = on; imn = oin; }
-                        const int r0 = m0 + wm * WTM + i * 32 + (g.pool_k == 16 ? 16 * hb : 0);
-                        if (h == 0 && cok && r0 < g.M) {
-                            const size_t G = (size_t)(g.M / g.pool_k), gi = (size_t)(r0 / g.pool_k);
-                            const int base = g.pool_k == 16 ? 16 * hb : 0;
-                            g.pz[gi * g.N + col] = pmx;
-                            g.pz[(G + gi) * g.N + col] = pmn;
-                            g.pa[gi * g.N + col] = (unsigned char)(imx - base);
-                            g.pa[(G + gi) * g.N + col] = (unsigned char)(imn - base);
-                        }
                     }
                 }
-                }
-            }
+            };
+            if (m0 + BM <= g.M && n0 + BN <= g.N) epilogue(std::true_type{});
+            else epilogue(std::false_type{});
         }
         if (it + 1 < total) sstore(buf ^ 1, m0n, kn * GBK);
         __syncthreads();
@@ -794,20 +828,50 @@ static inline unsigned ew_grid(long long total) {
 template <int BM, int BN, int WM, int WN>
 static void launch_gemm(const GemmArgs& g, int gx, bool bt, hipStream_t s) {
     const dim3 grid(gx, (g.N + BN - 1) / BN);
-    if (bt) {   // data-gradient GEMMs: dZ operand (rebuilt on load) or a plain gradient
+    const int e = (g.stats ? EPI_STATS : 0) | (g.bstats ? EPI_BWD : 0) | (g.pool_k ? EPI_POOL : 0);
+#define PCS_GEMM(AMODE, BTV, EPIV) \
+    hipLaunchKernelGGL((gemm_rows_kernel<BM, BN, WM, WN, AMODE, BTV, EPIV>), grid, dim3(256), 0, s, g)
+    if (bt) {   // data-gradient GEMMs: dZ operand (rebuilt on load) or a plain / materialised one
         switch (g.a.mode) {
-        case OP_PLAIN: hipLaunchKernelGGL((gemm_rows_kernel<BM, BN, WM, WN, OP_PLAIN, true>), grid, dim3(256), 0, s, g); break;
-        case OP_BNBWD: hipLaunchKernelGGL((gemm_rows_kernel<BM, BN, WM, WN, OP_BNBWD, true>), grid, dim3(256), 0, s, g); break;
-        default: hipLaunchKernelGGL((gemm_rows_kernel<BM, BN, WM, WN, OP_POOLBWD, true>), grid, dim3(256), 0, s, g); break;
+#define PCS_BT(AMODE) \
+    if (e == 0) PCS_GEMM(AMODE, true, 0); \
+    else if (e == EPI_BWD) PCS_GEMM(AMODE, true, EPI_BWD); \
+    else PCS_GEMM(AMODE, true, EPI_GENERIC);
+        case OP_PLAIN: PCS_BT(OP_PLAIN) break;
+        case OP_BNBWD: PCS_BT(OP_BNBWD) break;
+        default: PCS_BT(OP_POOLBWD) break;
+#undef PCS_BT
         }
         return;
     }
+#define PCS_FWD(AMODE) \
+    if (e == 0) PCS_GEMM(AMODE, false, 0); \
+    else if (e == EPI_STATS) PCS_GEMM(AMODE, false, EPI_STATS); \
+    else if (e == (EPI_STATS | EPI_POOL)) PCS_GEMM(AMODE, false, EPI_STATS | EPI_POOL); \
+    else PCS_GEMM(AMODE, false, EPI_GENERIC);
     switch (g.a.mode) {
-    case OP_PLAIN: hipLaunchKernelGGL((gemm_rows_kernel<BM, BN, WM, WN, OP_PLAIN, false>), grid, dim3(256), 0, s, g); break;
-    case OP_BNACT: hipLaunchKernelGGL((gemm_rows_kernel<BM, BN, WM, WN, OP_BNACT, false>), grid, dim3(256), 0, s, g); break;
-    case OP_BNBWD: hipLaunchKernelGGL((gemm_rows_kernel<BM, BN, WM, WN, OP_BNBWD, false>), grid, dim3(256), 0, s, g); break;
-    default: hipLaunchKernelGGL((gemm_rows_kernel<BM, BN, WM, WN, OP_POOLBWD, false>), grid, dim3(256), 0, s, g); break;
+    case OP_PLAIN: PCS_FWD(OP_PLAIN) break;
+    case OP_BNACT: PCS_FWD(OP_BNACT) break;
+    case OP_BNBWD:
+        if (e == 0) PCS_GEMM(OP_BNBWD, false, 0);
+        else PCS_GEMM(OP_BNBWD, false, EPI_GENERIC);
+        break;
+    default:
+        if (e == 0) PCS_GEMM(OP_POOLBWD, false, 0);
+        else PCS_GEMM(OP_POOLBWD, false, EPI_GENERIC);
+        break;
     }
+#undef PCS_FWD
+#undef PCS_GEMM
+}
+
+// the EPI template argument launch_gemm picks for these arguments (mirrors it)
+static int gemm_epi(int mode, bool bt, bool stats, bool bstats, bool pool) {
+    const int e = (stats ? EPI_STATS : 0) | (bstats ? EPI_BWD : 0) | (pool ? EPI_POOL : 0);
+    if (bt) return (e == 0 || e == EPI_BWD) ? e : EPI_GENERIC;
+    if (mode == OP_PLAIN || mode == OP_BNACT)
+        return (e == 0 || e == EPI_STATS || e == (EPI_STATS | EPI_POOL)) ? e : EPI_GENERIC;
+    return e == 0 ? 0 : EPI_GENERIC;
 }
 
 template <int BO, int BI, int XM>
@@ -990,6 +1054,9 @@ int pcs::gemm_rows_ex(const pcs_operand* a, int M, int K, const float* W, int ld
     PCS_CHECK_ARG((ldw % 4 == 0 || !bt) && ldw >= (bt ? N : K),
                   "pcs_gemm_rows: ldw=%d must be >= %d (and a multiple of 4 for k-major W)", ldw, bt ? N : K);
     PCS_CHECK_ARG(!bt || a->mode != PCS_OP_BNACT, "pcs_gemm_rows: k-major W needs a PLAIN/BNBWD/POOLBWD A");
+    // the epilogue addresses a 32-row block of C / epi Z with 32-bit offsets
+    PCS_CHECK_ARG((long long)ldc * 32 + N < (1ll << 31) && (!epi || (long long)epi->ldz * 32 + N < (1ll << 31)),
+                  "pcs_gemm_rows: row stride too large (ldc=%d)", ldc);
     if (M == 0) return 0;
     GemmArgs g{to_dev(a), M, K, W, ldw, bias, C, ldc, N, stats, to_dev(epi), bstats, pz, pa, pool_k};
     hipStream_t s = as_stream(stream);
@@ -999,8 +1066,8 @@ int pcs::gemm_rows_ex(const pcs_operand* a, int M, int K, const float* W, int ld
         int bm, bn, wm, wn;
         gemm_tile(M, N, a->mode >= PCS_OP_BNBWD || bt, &bm, &bn);
         gemm_waves(bm, bn, &wm, &wn);
-        snprintf(nm, sizeof nm, "pcs::gemm_rows_kernel<%d, %d, %d, %d, %d, %s>", bm, bn, wm, wn, a->mode,
-                 bt ? "true" : "false");
+        snprintf(nm, sizeof nm, "pcs::gemm_rows_kernel<%d, %d, %d, %d, %d, %s, %d>", bm, bn, wm, wn, a->mode,
+                 bt ? "true" : "false", gemm_epi(a->mode, bt != 0, stats != nullptr, bstats != nullptr, pool_k != 0));
         const double bytes = operand_bytes(*a, M, K) + 4.0 * M * N * (bstats ? 2 : 1);
         const pcs_operand ac = *a, ec = epi ? *epi : pcs_operand{};
         const bool he = epi != nullptr;
