@@ -338,10 +338,12 @@ PCS_API int pcs_mlp_forward(const float* X, int ldx, int kin, int M, pcs_mlp_lay
 }
 
 static int mlp_backward(const float* X, int ldx, int kin, int M, const pcs_mlp_layer* layers, int nl, int pool_k,
-                        const uint8_t* arg, const float* gout, float* dX, void* ws, size_t ws_bytes, void* stream,
-                        bool defer) {
+                        const uint8_t* arg, const float* gout, int ldg, float* dX, void* ws, size_t ws_bytes,
+                        void* stream, bool defer) {
     if (int e = check_layers(M, kin, ldx, layers, nl, pool_k, "pcs_mlp_backward")) return e;
     PCS_CHECK_ARG(X && gout && (!pool_k || arg), "pcs_mlp_backward: null pointer");
+    PCS_CHECK_ARG(ldg >= (int)layers[nl - 1].cout && ldg % 4 == 0 && (!pool_k || ldg == (int)layers[nl - 1].cout),
+                  "pcs_mlp_backward: ldg=%d (a multiple of 4 >= cout; pooled gradients are dense)", ldg);
     if (M == 0) return 0;
     hipStream_t st = as_stream(stream);
     Carve cv{static_cast<char*>(ws), 0, ws_bytes};
@@ -362,7 +364,7 @@ static int mlp_backward(const float* X, int ldx, int kin, int M, const pcs_mlp_l
             return e;
     } else {
         nb = pcs_bn_bwd_reduce_blocks(M);
-        if (int e = pcs_bn_bwd_reduce(gout, CL, T.Z, CL, M, CL, sT, sT + CL, sT + 2 * CL, sT + 3 * CL, (int)T.act,
+        if (int e = pcs_bn_bwd_reduce(gout, ldg, T.Z, CL, M, CL, sT, sT + CL, sT + 2 * CL, sT + 3 * CL, (int)T.act,
                                       (float)T.slope, S.part, stream))
             return e;
     }
@@ -372,7 +374,7 @@ static int mlp_backward(const float* X, int ldx, int kin, int M, const pcs_mlp_l
         return e;
     if (!T.use_batch) { zero_f32(S.kb[pp], CL, st); zero_f32(S.alpha[pp], CL, st); }
     // the top layer's dZ is never materialised: both consumers rebuild it on load
-    pcs_operand xop = bnbwd_op(gout, CL, T, S.alpha[pp], S.kb[pp]);
+    pcs_operand xop = bnbwd_op(gout, ldg, T, S.alpha[pp], S.kb[pp]);
     if (pool_k) { xop.mode = PCS_OP_POOLBWD; xop.arg = arg; xop.pool_k = pool_k; }
 
     int da = 0;
@@ -469,15 +471,15 @@ static int mlp_backward(const float* X, int ldx, int kin, int M, const pcs_mlp_l
 }
 
 PCS_API int pcs_mlp_backward(const float* X, int ldx, int kin, int M, const pcs_mlp_layer* layers, int nl,
-                             int pool_k, const uint8_t* arg, const float* gout, float* dX, void* ws, size_t ws_bytes,
-                             void* stream) {
-    return mlp_backward(X, ldx, kin, M, layers, nl, pool_k, arg, gout, dX, ws, ws_bytes, stream, false);
+                             int pool_k, const uint8_t* arg, const float* gout, int ldg, float* dX, void* ws,
+                             size_t ws_bytes, void* stream) {
+    return mlp_backward(X, ldx, kin, M, layers, nl, pool_k, arg, gout, ldg, dX, ws, ws_bytes, stream, false);
 }
 
 PCS_API int pcs_mlp_backward_deferred(const float* X, int ldx, int kin, int M, const pcs_mlp_layer* layers, int nl,
-                                      int pool_k, const uint8_t* arg, const float* gout, float* dX, void* ws,
-                                      size_t ws_bytes, void* stream) {
-    return mlp_backward(X, ldx, kin, M, layers, nl, pool_k, arg, gout, dX, ws, ws_bytes, stream, true);
+                                      int pool_k, const uint8_t* arg, const float* gout, int ldg, float* dX,
+                                      void* ws, size_t ws_bytes, void* stream) {
+    return mlp_backward(X, ldx, kin, M, layers, nl, pool_k, arg, gout, ldg, dX, ws, ws_bytes, stream, true);
 }
 
 PCS_API int pcs_wgrad_lane(void** side_stream) {

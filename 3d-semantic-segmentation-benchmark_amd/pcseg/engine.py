@@ -310,7 +310,12 @@ class SharedMLPFn(torch.autograd.Function):
         st = stream_ptr(dev)
         lib = load()
         M, ldx = X.shape
-        gout = gout.contiguous()
+        # a row-strided gradient (e.g. a column slice of a concatenation's gradient) is read
+        # in place; anything else is made dense
+        if not (gout.dim() == 2 and gout.stride(1) == 1 and gout.stride(0) % 4 == 0 and gout.data_ptr() % 16 == 0
+                and (pool_K == 0 or gout.is_contiguous())):
+            gout = gout.contiguous()
+        ldg = gout.stride(0)
         recs = b''.join(_REC.pack(*f, _nz(grad_target(params[4 * li])), _nz(grad_target(params[4 * li + 1])),
                                   _nz(grad_target(params[4 * li + 2])), _nz(grad_target(params[4 * li + 3])), 0, 0, 0)
                         for li, f in enumerate(fixed))
@@ -322,11 +327,11 @@ class SharedMLPFn(torch.autograd.Function):
         ws = torch.empty((nws,), dtype=torch.uint8, device=dev)
         lane = wgrad_lane(dev)
         if lane is None:
-            call('pcs_mlp_backward', ptr(X), ldx, Kin, M, recs, nl, pool_K, ptr(arg), ptr(gout), ptr(dX), ptr(ws), nws,
-                 st)
+            call('pcs_mlp_backward', ptr(X), ldx, Kin, M, recs, nl, pool_K, ptr(arg), ptr(gout), ldg, ptr(dX), ptr(ws),
+                 nws, st)
         else:
-            call('pcs_mlp_backward_deferred', ptr(X), ldx, Kin, M, recs, nl, pool_K, ptr(arg), ptr(gout), ptr(dX),
-                 ptr(ws), nws, st)
+            call('pcs_mlp_backward_deferred', ptr(X), ldx, Kin, M, recs, nl, pool_K, ptr(arg), ptr(gout), ldg,
+                 ptr(dX), ptr(ws), nws, st)
             # the lane still reads these: the caching allocator must not hand them out before it is done
             for t in (X, saved[1], saved[2], gout, ws, *([arg] if arg is not None else [])):
                 t.record_stream(lane)
@@ -379,6 +384,20 @@ class EdgeConvFn(torch.autograd.Function):
         record_pool_arg(arg)
         if recording():
             record_act_mask(out > 0)          # LeakyReLU keeps the sign: out > 0 <=> y > 0 at the argmax
+        ctx.inv = None
+        if any(ctx.needs_input_grad):
+            # the backward's inverse map of idx depends on idx only: build it now on the side
+            # stream, under the rest of the forward, instead of on the backward's critical path
+            from . import ops
+            from .common import side_stream
+            main, side = torch.cuda.current_stream(dev), side_stream(dev)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                off, ent = ops.inverse_index(idx, N)
+                ev = torch.cuda.Event()
+                ev.record(side)
+            idx.record_stream(side)
+            ctx.inv = (off, ent, ev)
         ctx.save_for_backward(X, idx, Wm, Y, PQ, S, pz, arg, coef)
         ctx.meta = (C, float(slope))
         ctx.params = (W, gamma, beta)
@@ -396,7 +415,14 @@ class EdgeConvFn(torch.autograd.Function):
         M, ldx = X.shape
         Cout = Wm.shape[0]
         gout = gout.contiguous()
-        off, ent = ops.inverse_index(idx, N)
+        if ctx.inv is not None:
+            off, ent, ev = ctx.inv
+            torch.cuda.current_stream(dev).wait_event(ev)
+            off.record_stream(torch.cuda.current_stream(dev))
+            ent.record_stream(torch.cuda.current_stream(dev))
+            ctx.inv = None
+        else:
+            off, ent = ops.inverse_index(idx, N)
         dX = _f32((M, ldx), dev) if ctx.needs_input_grad[0] else None
         if dX is not None and ldx != C:
             dX.zero_()
