@@ -462,8 +462,22 @@ static int mlp_backward(const float* X, int ldx, int kin, int M, const pcs_mlp_l
             da = (da + 1) % 3;
         } else {
             zero_cols(dX, M, ldx, kin, st);      // the GEMM writes columns [0, kin)
-            if (int e = gemm_rows_ex(&xop, M, C, Bw, ldb, bt, nullptr, dX, ldx, kin, nullptr, nullptr, nullptr, stream))
+            if (xop.mode == PCS_OP_PLAIN && gemm_nt_ok(xop.data, xop.ld, S.wt, C, M, kin, C)) {
+                // a wide layer's materialised dZ: W^T once (kin x C, a few MB) and the wide GEMM,
+                // dX = dZ . (W^T)^T with both operands contiguous along C
+                if (bt) {
+                    const dim3 g((Cin + 31) / 32, (C + 31) / 32);
+                    hipLaunchKernelGGL(transpose_kernel, g, dim3(256), 0, st, P.W, C, Cin, (int)P.ldw, S.wt);
+                }
+                Bw = S.wt;
+                ldb = C;
+                if (int e = gemm_rows_ex(&xop, M, C, Bw, ldb, 0, nullptr, dX, ldx, kin, nullptr, nullptr, nullptr,
+                                         stream))
+                    return fail(e);
+            } else if (int e = gemm_rows_ex(&xop, M, C, Bw, ldb, bt, nullptr, dX, ldx, kin, nullptr, nullptr, nullptr,
+                                            stream)) {
                 return fail(e);
+            }
         }
     }
     if (!defer) join();

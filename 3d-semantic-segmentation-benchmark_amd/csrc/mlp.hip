@@ -962,7 +962,11 @@ static double operand_bytes(const pcs_operand& o, int M, int K) {
 }
 
 // number of row blocks the row GEMM uses for M rows and N outputs (sizes the stats workspace)
+// Forward GEMMs in the wide regime (gemm_nt_regime) write one BN partial per 256-row tile,
+// whichever kernel runs them (gemm_nt, or the row GEMM with that many persistent blocks when
+// the operand needs an on-load transform), so the partial count depends on (M, N) only.
 static int row_blocks(int M, int N, bool bwd) {
+    if (!bwd && gemm_nt_regime(M, N)) return gemm_nt_row_tiles(M);
     int bm, bn;
     gemm_tile(M, N, bwd, &bm, &bn);
     return gemm_grid_x(M, N, bm, bn);
@@ -1058,8 +1062,25 @@ int pcs::gemm_rows_ex(const pcs_operand* a, int M, int K, const float* W, int ld
     PCS_CHECK_ARG((long long)ldc * 32 + N < (1ll << 31) && (!epi || (long long)epi->ldz * 32 + N < (1ll << 31)),
                   "pcs_gemm_rows: row stride too large (ldc=%d)", ldc);
     if (M == 0) return 0;
-    GemmArgs g{to_dev(a), M, K, W, ldw, bias, C, ldc, N, stats, to_dev(epi), bstats, pz, pa, pool_k};
     hipStream_t s = as_stream(stream);
+    // plain operands of a wide layer, no fused epilogue but BN statistics: the LDS-DMA wide GEMM
+    if (!bt && a->mode == PCS_OP_PLAIN && !pool_k && !bstats && gemm_nt_ok(a->data, a->ld, W, ldw, M, N, K)) {
+        int probe = -1;
+        if (probe_enabled()) {
+            char nm[96];
+            const bool b256 = (((N + 127) / 128) * 128 - N) >= (((N + 255) / 256) * 256 - N);
+            snprintf(nm, sizeof nm, "pcs::gemm_nt_kernel<%d, %d, %d, %s>", b256 ? 256 : 128, b256 ? 2 : 4,
+                     b256 ? 4 : 2, stats ? "true" : "false");
+            const pcs_operand ac = *a;
+            probe = probe_start(nm, 2.0 * M * K * N, 4.0 * M * K + 4.0 * M * N, s, [=]() {
+                gemm_rows_ex(&ac, M, K, W, ldw, 0, bias, C, ldc, N, stats, nullptr, nullptr, stream);
+            });
+        }
+        const int e = gemm_nt(a->data, a->ld, W, ldw, M, N, K, bias, C, ldc, stats, s);
+        probe_stop(probe, s);
+        return e;
+    }
+    GemmArgs g{to_dev(a), M, K, W, ldw, bias, C, ldc, N, stats, to_dev(epi), bstats, pz, pa, pool_k};
     int probe = -1;
     if (probe_enabled()) {
         char nm[96];
@@ -1076,8 +1097,10 @@ int pcs::gemm_rows_ex(const pcs_operand* a, int M, int K, const float* W, int ld
         });
     }
     int bm, bn;
-    gemm_tile(M, N, a->mode >= PCS_OP_BNBWD || bt, &bm, &bn);
-    const int gx = gemm_grid_x(M, N, bm, bn);
+    const bool bwd = a->mode >= PCS_OP_BNBWD || bt;
+    gemm_tile(M, N, bwd, &bm, &bn);
+    // stats partials: one per row block as row_blocks() counts them (<= the row tiles: persistent)
+    const int gx = (stats || bstats) ? row_blocks(M, N, bwd) : gemm_grid_x(M, N, bm, bn);
     const bool b = bt != 0;
     if (bn == 32) launch_gemm<128, 32, 4, 1>(g, gx, b, s);
     else if (bm == 128 && bn == 64) launch_gemm<128, 64, 4, 1>(g, gx, b, s);
@@ -1142,7 +1165,9 @@ size_t pcs::wgrad_ws_bytes(int N, int K, int M) {
     if (M <= 0) return 0;
     int BO, BI, sp, rows;
     wgrad_plan(N, K, M, &BO, &BI, &sp, &rows);
-    return (size_t)sp * ((size_t)N * K + N) * sizeof(float) + 256;
+    const size_t b = (size_t)sp * ((size_t)N * K + N) * sizeof(float) + 256;
+    // the wide kernel (plain operands) may take the launch: size for either
+    return std::max(b, wgrad_nt_ws_bytes(N, K, M));
 }
 
 // dW (N x K) += T(X)^T . T(Y) over M rows; db (N) += column sums of T(X) (nullable).  Each row
@@ -1158,11 +1183,27 @@ int pcs::wgrad_launch(const pcs_operand* x, int N, const pcs_operand* y, int K, 
     if (M == 0) return 0;
     const size_t need = wgrad_ws_bytes(N, K, M);
     PCS_CHECK_ARG(ws && ws_bytes >= need, "pcs_wgrad: workspace too small (%zu < %zu)", ws_bytes, need);
+    float* part = reinterpret_cast<float*>((reinterpret_cast<uintptr_t>(ws) + 255) & ~uintptr_t(255));
+    hipStream_t st = as_stream(stream);
+    if (x->mode == PCS_OP_PLAIN && y->mode == PCS_OP_PLAIN && !db && wgrad_nt_ok(x->data, x->ld, y->data, y->ld, M, N, K)) {
+        // a wide layer's materialised dZ and plain input: the LDS-DMA wide weight gradient
+        int probe = -1;
+        if (probe_enabled()) {
+            const float *xd = x->data, *yd = y->data;
+            const int lx = x->ld, ly = y->ld;
+            probe = probe_start(wgrad_nt_name(N, K, M), 2.0 * M * N * K, 4.0 * M * (N + K), st,
+                                [=]() { wgrad_nt(xd, lx, yd, ly, M, N, K, part, st); });
+        }
+        const int sp = wgrad_nt(x->data, x->ld, y->data, y->ld, M, N, K, part, st);
+        probe_stop(probe, st);
+        const long long nk = (long long)N * K;
+        hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((nk + kRedElems - 1) / kRedElems)), dim3(256), 0, st,
+                           part, sp, nk, dW, (const float*)nullptr, N, (float*)nullptr);
+        return launch_status("pcs_wgrad");
+    }
     int BO, BI, splits, rows;
     wgrad_plan(N, K, M, &BO, &BI, &splits, &rows);
-    float* part = reinterpret_cast<float*>((reinterpret_cast<uintptr_t>(ws) + 255) & ~uintptr_t(255));
     float* pdb = db ? part + (size_t)splits * N * K : nullptr;
-    hipStream_t st = as_stream(stream);
     const int tiles = ((N + BO - 1) / BO) * ((K + BI - 1) / BI);
     const dim3 grid(splits, tiles);
     const Operand xd = to_dev(x), yd = to_dev(y);

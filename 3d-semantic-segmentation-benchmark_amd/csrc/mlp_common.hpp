@@ -144,6 +144,17 @@ int materialize_dz(const pcs_operand* x, int M, int C, float* out, int ldo, hipS
 int gemm_rows_ex(const pcs_operand* a, int M, int K, const float* W, int ldw, int bt, const float* bias, float* C,
                  int ldc, int N, double* stats, const pcs_operand* epi, double* bstats, void* stream,
                  float* pz = nullptr, unsigned char* pa = nullptr, int pool_k = 0);
+// wide-layer GEMM on plain operands (gemm_big.hip): C = A . B^T, A (M x R), B (N x R) row-major
+bool gemm_nt_regime(int M, int N);                 // (M, N) the wide path is built for
+int gemm_nt_row_tiles(int M);                      // its BN-partial row blocks
+bool gemm_nt_ok(const float* A, int lda, const float* B, int ldb, int M, int N, int R);
+int gemm_nt(const float* A, int lda, const float* B, int ldb, int M, int N, int R, const float* bias, float* C, int ldc,
+            double* stats, hipStream_t st);
+// wide weight gradient on plain operands (gemm_big.hip): partial tiles per row split
+bool wgrad_nt_ok(const float* X, int ldx, const float* Y, int ldy, int M, int N, int K);
+size_t wgrad_nt_ws_bytes(int N, int K, int M);
+int wgrad_nt(const float* X, int ldx, const float* Y, int ldy, int M, int N, int K, float* part, hipStream_t st);
+const char* wgrad_nt_name(int N, int K, int M);
 // pooled output of a stack from the GEMM's fused z-space max/min (pz/pa of gemm_rows_ex):
 // out = act(s*z + t) with z = max (s > 0), min (s < 0) or any (s == 0, arg 0) -- act(s*z+t) is
 // monotone in z, so this is max_k act(s*z_k + t) with its first argmax

@@ -63,6 +63,8 @@ SIGNATURES = {
     'pcs_operand_size': [],
     'pcs_gemm_rows': [OPP, I32, I32, P, I32, P, P, I32, I32, P, OPP, P, P],
     'pcs_gemm_rows_kmajor': [OPP, I32, I32, P, I32, P, I32, I32, OPP, P, P],
+    'pcs_gemm_nt': [P, I32, P, I32, I32, I32, I32, P, P, I32, P, P],
+    'pcs_gemm_nt_row_tiles': [I32],
     'pcs_wgrad_workspace': [I32, I32, I32, P],
     'pcs_wgrad': [OPP, I32, OPP, I32, I32, P, P, P, ctypes.c_size_t, P],
     'pcs_bn_finalize': [P, I32, I32, I64, P, P, F32, F32, P, P, P, P, P, P, P],

@@ -25,12 +25,18 @@ def broadcast_model(model: torch.nn.Module, src: int = 0) -> None:
             dist.broadcast(t.data, src)
 
 
+def _align(n: int) -> int:
+    return (n + 63) // 64 * 64
+
+
 class FlatGradAllReduce:
     """Flat gradient buffer + bucketed, backward-overlapped all-reduce (mean)."""
 
     def __init__(self, model: torch.nn.Module, bucket_bytes: int = 4 << 20, overlap: bool = True):
         self.params = [p for p in model.parameters() if p.requires_grad]
-        total = sum(p.numel() for p in self.params)
+        # every parameter (and its gradient) starts on a 256-B boundary of the flat buffers: the
+        # wide GEMMs stage weights by 16-B LDS-DMA and take only aligned operands
+        total = sum(_align(p.numel()) for p in self.params)
         dev = self.params[0].device
         self.flat = torch.zeros(total, dtype=torch.float32, device=dev)
         self.world = dist.get_world_size() if dist.is_initialized() else 1
@@ -45,7 +51,7 @@ class FlatGradAllReduce:
             n = p.numel()
             self.views[p] = self.flat[off:off + n].view_as(p)
             cur.append(p)
-            off += n
+            off += _align(n)
             if (off - cur_start) * 4 >= bucket_bytes:
                 self.buckets.append((cur_start, off, cur))
                 cur_start, cur = off, []

@@ -24,7 +24,7 @@ class FlatAdam:
         self.grads = grads
         self.lr, self.betas, self.eps, self.weight_decay = float(lr), tuple(betas), float(eps), float(weight_decay)
         flat_g = grads.flat
-        self.flat = torch.empty_like(flat_g)
+        self.flat = torch.zeros_like(flat_g)       # (alignment pads between parameters stay 0)
         base = flat_g.storage_offset()
         with torch.no_grad():
             for p in grads.params:

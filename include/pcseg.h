@@ -141,6 +141,16 @@ int pcs_gemm_rows(const pcs_operand* a, int M, int K, const float* W, int ldw,
 int pcs_gemm_rows_kmajor(const pcs_operand* a, int M, int K, const float* W, int ldw,
                          float* C, int ldc, int N, const pcs_operand* epi,
                          double* bstats, void* stream);
+/* Wide-layer GEMM on plain operands (DGCNN conv5..conv7 forward and data gradient,
+ * models/dgcnn/dgcnn.py:188-207 -- the conv1d products the reference runs in ATen):
+ * C (M x N, ldc) = A (M x R, lda) . B (N x R, ldb)^T (+ bias), both operands
+ * row-major with the contraction axis contiguous.  stats (nullable): [2][N][row
+ * tiles] fp64 partial (sum, sum^2) of C (pcs_gemm_nt_row_tiles(M) tiles, the
+ * layout pcs_bn_finalize reads).  Needs M >= 65536, N >= 256, R % 32 == 0, lda
+ * and ldb multiples of 4 (>= R), 16-B aligned A and B. */
+int pcs_gemm_nt(const float* A, int lda, const float* B, int ldb, int M, int N, int R,
+                const float* bias, float* C, int ldc, double* stats, void* stream);
+int pcs_gemm_nt_row_tiles(int M);
 /* dW (N x K) += T(X)^T . T(Y) over M rows; db (N, nullable) += column sums of
  * T(X).  X: PLAIN/BNBWD/POOLBWD (the layer's dZ), Y: PLAIN/BNACT (its input).
  * (accumulating) Deterministic: each row split's partial tile is stored in the

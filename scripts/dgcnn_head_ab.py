@@ -61,6 +61,12 @@ for name, K, N in SHAPES:
         dW = torch.zeros(N, K, device=dev)
         ws = torch.empty(1 << 28, dtype=torch.uint8, device=dev)
         res[f'wgrad {tag}'] = timeit(lambda: wgrad(xo, N, operand(X, K), K, M, dW, None, st, ws))
+    if os.environ.get('HEAD_TORCH', '1') == '1':     # vendor fp32 GEMM (hipBLASLt/rocBLAS) as a ceiling reference
+        torch.backends.cuda.matmul.allow_tf32 = False
+        res['torch fwd'] = timeit(lambda: torch.mm(X, W.t(), out=Z))
+        res['torch dgrad'] = timeit(lambda: torch.mm(dZ, W, out=dA))
+        dWt = torch.empty(N, K, device=dev)
+        res['torch wgrad'] = timeit(lambda: torch.mm(dZ.t(), X, out=dWt))
     line = f'{name} M={M} K={K} N={N}: fwd {us_f:7.0f} us {fl / us_f / 1e6:5.1f} TF'
     for k, us in res.items():
         line += f' | {k} {us:7.0f} us {fl / us / 1e6:5.1f} TF'

@@ -1,0 +1,114 @@
+"""Wide-layer GEMM A/B on the GPU: pcs_gemm_nt (LDS-DMA, 256-row tiles) vs the row GEMM
+(pcs_gemm_rows / pcs_gemm_rows_kmajor) vs torch.mm (vendor fp32 GEMM) on the DGCNN head
+shapes (conv5..conv7 forward and data gradient, M = 32 x 4096), interleaved in one process.
+Also checks pcs_gemm_nt against an fp64 product and its BN partials against fp64 sums."""
+import os
+import sys
+
+sys.path[:0] = [os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                             '3d-semantic-segmentation-benchmark_amd')]
+import torch  # noqa: E402
+from pcseg._lib import stream_ptr, load  # noqa: E402
+from pcseg.engine import operand, gemm_rows, gemm_rows_kmajor  # noqa: E402
+
+dev = 'cuda'
+torch.manual_seed(0)
+torch.backends.cuda.matmul.allow_tf32 = False
+M = int(os.environ.get('NT_M', str(32 * 4096)))
+REPS = int(os.environ.get('GEMM_REPS', '10'))
+ROUNDS = int(os.environ.get('NT_ROUNDS', '3'))
+lib = load()
+st = stream_ptr(torch.device(dev))
+p = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
+
+
+def timeit(fn):
+    fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(REPS):
+        fn()
+    e1.record()
+    e1.synchronize()
+    return e0.elapsed_time(e1) / REPS * 1e3
+
+
+# (name, R = contraction, N = outputs, kind)
+SHAPES = [('conv5.fwd', 384, 1024), ('conv6.fwd', 1408, 512), ('conv7.fwd', 512, 256),
+          ('conv5.dgrad', 1024, 384), ('conv6.dgrad', 512, 1408), ('conv7.dgrad', 256, 512)]
+for name, R, N in SHAPES:
+    A = torch.randn(M, R, device=dev)
+    B = torch.randn(N, R, device=dev) / R ** 0.5
+    C = torch.empty(M, N, device=dev)
+    C2 = torch.empty(M, N, device=dev)
+    nt = lib.pcs_gemm_nt_row_tiles(M)
+    stats = torch.empty(2, N, nt, dtype=torch.float64, device=dev)
+    run_nt = lambda: lib.pcs_gemm_nt(p(A), R, p(B), R, M, N, R, None, p(C), N, p(stats), st)  # noqa: E731
+    assert run_nt() == 0
+    torch.cuda.synchronize()
+    ref = A.double() @ B.double().t()
+    err = ((C.double() - ref).norm() / ref.norm()).item()
+    s1 = stats[0].sum(1)
+    s2 = stats[1].sum(1)
+    e1 = ((s1 - C.double().sum(0)).abs().max() / C.double().abs().sum(0).max()).item()
+    e2 = ((s2 - (C.double() ** 2).sum(0)).abs().max() / (C.double() ** 2).sum(0).max()).item()
+    # the row GEMM on the same product: forward form (W row-major) or the k-major dgrad form
+    Bt = B.t().contiguous()                 # (R x N): the layer's W when this is a data gradient
+    nb = lib.pcs_gemm_row_blocks(M, N)
+    part = torch.empty(2, N, nb, dtype=torch.float64, device=dev)
+    if name.endswith('fwd'):
+        run_rows = lambda: gemm_rows(operand(A, R), M, R, B, R, None, C2, N, N, part, st=st)  # noqa: E731
+    else:
+        run_rows = lambda: gemm_rows_kmajor(operand(A, R), M, R, Bt, N, C2, N, N, st=st)  # noqa: E731
+    run_torch = lambda: torch.mm(A, B.t(), out=C2)  # noqa: E731
+    res = {'nt': [], 'rows': [], 'torch': []}
+    for _ in range(ROUNDS):
+        res['nt'].append(timeit(run_nt))
+        res['rows'].append(timeit(run_rows))
+        res['torch'].append(timeit(run_torch))
+    fl = 2.0 * M * R * N
+    line = f'{name:12s} M={M} R={R} N={N}: relerr {err:.2e} stats {e1:.1e}/{e2:.1e}'
+    for k, v in res.items():
+        us = sorted(v)[len(v) // 2]
+        line += f' | {k} {us:7.0f} us {fl / us / 1e6:6.1f} TF'
+    print(line, flush=True)
+    del A, B, C, C2, ref
+    torch.cuda.empty_cache()
+
+# ---- weight gradients dW (N x K) = dZ^T . X over M rows: the wide kernel (plain operands, no
+# bias) vs the row-split wgrad (forced by asking for a bias gradient too) vs torch.mm
+from pcseg.engine import wgrad  # noqa: E402
+for name, K, N in [('conv5.wgrad', 384, 1024), ('conv6.wgrad', 1408, 512), ('conv7.wgrad', 512, 256)]:
+    X = torch.randn(M, K, device=dev)
+    dZ = torch.randn(M, N, device=dev)
+    dW = torch.zeros(N, K, device=dev)
+    db = torch.zeros(N, device=dev)
+    ws = torch.empty(1 << 28, dtype=torch.uint8, device=dev)
+    run_nt = lambda: wgrad(operand(dZ, N), N, operand(X, K), K, M, dW, None, st, ws)  # noqa: E731
+    run_old = lambda: wgrad(operand(dZ, N), N, operand(X, K), K, M, dW, db, st, ws)  # noqa: E731
+    dWt = torch.empty(N, K, device=dev)
+    run_torch = lambda: torch.mm(dZ.t(), X, out=dWt)  # noqa: E731
+    dW.zero_()
+    run_nt()
+    torch.cuda.synchronize()
+    ref = dZ.double().t() @ X.double()
+    err = ((dW.double() - ref).norm() / ref.norm()).item()
+    dW2 = dW.clone()
+    dW.zero_()
+    run_nt()
+    torch.cuda.synchronize()
+    det = bool(torch.equal(dW, dW2))
+    res = {'nt': [], 'old': [], 'torch': []}
+    for _ in range(ROUNDS):
+        res['nt'].append(timeit(run_nt))
+        res['old'].append(timeit(run_old))
+        res['torch'].append(timeit(run_torch))
+    fl = 2.0 * M * K * N
+    line = f'{name:12s} M={M} K={K} N={N}: relerr {err:.2e} bitwise-repeatable {det}'
+    for k, v in res.items():
+        us = sorted(v)[len(v) // 2]
+        line += f' | {k} {us:7.0f} us {fl / us / 1e6:6.1f} TF'
+    print(line, flush=True)
+    del X, dZ, ws, ref
+    torch.cuda.empty_cache()
