@@ -286,9 +286,13 @@ PCS_API int pcs_mlp_workspace(int M, int kin, int ldx, const pcs_mlp_layer* laye
 }
 
 PCS_API int pcs_mlp_forward(const float* X, int ldx, int kin, int M, pcs_mlp_layer* layers, int nl, int pool_k,
-                            float* out, uint8_t* arg, void* ws, size_t ws_bytes, void* stream) {
+                            float* out, int ldo, uint8_t* arg, void* ws, size_t ws_bytes, void* stream) {
     if (int e = check_layers(M, kin, ldx, layers, nl, pool_k, "pcs_mlp_forward")) return e;
     PCS_CHECK_ARG(X && out && (!pool_k || arg), "pcs_mlp_forward: null pointer");
+    const int CT = (int)layers[nl - 1].cout;
+    if (ldo == 0) ldo = CT;
+    PCS_CHECK_ARG(!pool_k ? (ldo >= CT && ldo % 4 == 0) : ldo == CT,
+                  "pcs_mlp_forward: ldo=%d (a multiple of 4 >= cout; pooled outputs are dense)", ldo);
     if (M == 0) return 0;
     hipStream_t st = as_stream(stream);
     Carve cv{static_cast<char*>(ws), 0, ws_bytes};
@@ -334,13 +338,15 @@ PCS_API int pcs_mlp_forward(const float* X, int ldx, int kin, int M, pcs_mlp_lay
     if (pool_k)
         return pcs_pool_fwd(T.Z, C, M / pool_k, pool_k, T.coef, T.coef + C, (int)T.act, (float)T.slope, out, arg,
                             stream);
-    return pcs_bn_act(T.Z, C, M, C, T.coef, T.coef + C, (int)T.act, (float)T.slope, out, C, stream);
+    return pcs_bn_act(T.Z, C, M, C, T.coef, T.coef + C, (int)T.act, (float)T.slope, out, ldo, stream);
 }
 
 static int mlp_backward(const float* X, int ldx, int kin, int M, const pcs_mlp_layer* layers, int nl, int pool_k,
-                        const uint8_t* arg, const float* gout, int ldg, float* dX, void* ws, size_t ws_bytes,
-                        void* stream, bool defer) {
+                        const uint8_t* arg, const float* gout, int ldg, float* dX, int lddx, void* ws,
+                        size_t ws_bytes, void* stream, bool defer) {
     if (int e = check_layers(M, kin, ldx, layers, nl, pool_k, "pcs_mlp_backward")) return e;
+    if (lddx == 0) lddx = ldx;
+    PCS_CHECK_ARG(lddx >= kin && lddx % 4 == 0, "pcs_mlp_backward: lddx=%d (a multiple of 4 >= kin=%d)", lddx, kin);
     PCS_CHECK_ARG(X && gout && (!pool_k || arg), "pcs_mlp_backward: null pointer");
     PCS_CHECK_ARG(ldg >= (int)layers[nl - 1].cout && ldg % 4 == 0 && (!pool_k || ldg == (int)layers[nl - 1].cout),
                   "pcs_mlp_backward: ldg=%d (a multiple of 4 >= cout; pooled gradients are dense)", ldg);
@@ -461,7 +467,7 @@ static int mlp_backward(const float* X, int ldx, int kin, int M, const pcs_mlp_l
             xop = bnbwd_op(dA, Cin, Q, S.alpha[pp], S.kb[pp]);
             da = (da + 1) % 3;
         } else {
-            zero_cols(dX, M, ldx, kin, st);      // the GEMM writes columns [0, kin)
+            zero_cols(dX, M, lddx, kin, st);     // the GEMM writes columns [0, kin)
             if (xop.mode == PCS_OP_PLAIN && gemm_nt_ok(xop.data, xop.ld, S.wt, C, M, kin, C)) {
                 // a wide layer's materialised dZ: W^T once (kin x C, a few MB) and the wide GEMM,
                 // dX = dZ . (W^T)^T with both operands contiguous along C
@@ -471,10 +477,10 @@ static int mlp_backward(const float* X, int ldx, int kin, int M, const pcs_mlp_l
                 }
                 Bw = S.wt;
                 ldb = C;
-                if (int e = gemm_rows_ex(&xop, M, C, Bw, ldb, 0, nullptr, dX, ldx, kin, nullptr, nullptr, nullptr,
+                if (int e = gemm_rows_ex(&xop, M, C, Bw, ldb, 0, nullptr, dX, lddx, kin, nullptr, nullptr, nullptr,
                                          stream))
                     return fail(e);
-            } else if (int e = gemm_rows_ex(&xop, M, C, Bw, ldb, bt, nullptr, dX, ldx, kin, nullptr, nullptr, nullptr,
+            } else if (int e = gemm_rows_ex(&xop, M, C, Bw, ldb, bt, nullptr, dX, lddx, kin, nullptr, nullptr, nullptr,
                                             stream)) {
                 return fail(e);
             }
@@ -485,15 +491,15 @@ static int mlp_backward(const float* X, int ldx, int kin, int M, const pcs_mlp_l
 }
 
 PCS_API int pcs_mlp_backward(const float* X, int ldx, int kin, int M, const pcs_mlp_layer* layers, int nl,
-                             int pool_k, const uint8_t* arg, const float* gout, int ldg, float* dX, void* ws,
-                             size_t ws_bytes, void* stream) {
-    return mlp_backward(X, ldx, kin, M, layers, nl, pool_k, arg, gout, ldg, dX, ws, ws_bytes, stream, false);
+                             int pool_k, const uint8_t* arg, const float* gout, int ldg, float* dX, int lddx,
+                             void* ws, size_t ws_bytes, void* stream) {
+    return mlp_backward(X, ldx, kin, M, layers, nl, pool_k, arg, gout, ldg, dX, lddx, ws, ws_bytes, stream, false);
 }
 
 PCS_API int pcs_mlp_backward_deferred(const float* X, int ldx, int kin, int M, const pcs_mlp_layer* layers, int nl,
                                       int pool_k, const uint8_t* arg, const float* gout, int ldg, float* dX,
-                                      void* ws, size_t ws_bytes, void* stream) {
-    return mlp_backward(X, ldx, kin, M, layers, nl, pool_k, arg, gout, ldg, dX, ws, ws_bytes, stream, true);
+                                      int lddx, void* ws, size_t ws_bytes, void* stream) {
+    return mlp_backward(X, ldx, kin, M, layers, nl, pool_k, arg, gout, ldg, dX, lddx, ws, ws_bytes, stream, true);
 }
 
 PCS_API int pcs_wgrad_lane(void** side_stream) {

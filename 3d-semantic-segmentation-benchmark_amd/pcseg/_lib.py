@@ -55,9 +55,10 @@ SIGNATURES = {
     'pcs_probe_replay': [ctypes.c_char_p, I32, P, P],
     'pcs_spin': [I32, P],
     'pcs_mlp_workspace': [I32, I32, I32, ctypes.c_char_p, I32, I32, I32, P],
-    'pcs_mlp_forward': [P, I32, I32, I32, ctypes.c_char_p, I32, I32, P, P, P, ctypes.c_size_t, P],
-    'pcs_mlp_backward': [P, I32, I32, I32, ctypes.c_char_p, I32, I32, P, P, I32, P, P, ctypes.c_size_t, P],
-    'pcs_mlp_backward_deferred': [P, I32, I32, I32, ctypes.c_char_p, I32, I32, P, P, I32, P, P, ctypes.c_size_t, P],
+    'pcs_mlp_forward': [P, I32, I32, I32, ctypes.c_char_p, I32, I32, P, I32, P, P, ctypes.c_size_t, P],
+    'pcs_mlp_backward': [P, I32, I32, I32, ctypes.c_char_p, I32, I32, P, P, I32, P, I32, P, ctypes.c_size_t, P],
+    'pcs_mlp_backward_deferred': [P, I32, I32, I32, ctypes.c_char_p, I32, I32, P, P, I32, P, I32, P,
+                                  ctypes.c_size_t, P],
     'pcs_wgrad_lane': [P],
     'pcs_wgrad_lane_join': [P],
     'pcs_operand_size': [],

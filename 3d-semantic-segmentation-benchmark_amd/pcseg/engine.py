@@ -228,11 +228,12 @@ class SharedMLPFn(torch.autograd.Function):
     record per layer."""
 
     @staticmethod
-    def forward(ctx, X, Kin, pool_K, acts, bns, *params):
+    def forward(ctx, X, Kin, pool_K, acts, bns, dest, *params):
         dev = X.device
         st = stream_ptr(dev)
         lib = load()
-        M, ldx = X.shape
+        M = X.shape[0]
+        ldx = X.stride(0)       # X may be a column block of a wider buffer (row stride > width)
         nl = len(bns)
         couts = [params[4 * li].shape[0] for li in range(nl)]
         tot = sum(couts)
@@ -270,18 +271,23 @@ class SharedMLPFn(torch.autograd.Function):
             cin = C
         recs = b''.join(_REC.pack(*f, 0, 0, 0, 0, 0, 0, 0) for f in fixed)
         CL = couts[-1]
+        ldo = 0
         if pool_K:
             G = M // pool_K
             out = _f32((G, CL), dev)
             arg = torch.empty((G, CL), dtype=torch.uint8, device=dev)
             ctx.mark_non_differentiable(arg)
+        elif dest is not None:
+            out = dest[0]           # (M, CL) column block of a caller buffer (see storage_alias)
+            ldo = out.stride(0)
+            arg = None
         else:
             out = _f32((M, CL), dev)
             arg = None
         key = (M, Kin, ldx, tuple(couts), pool_K, 0)
         nws = _workspace(lib, key, M, Kin, ldx, recs, nl, pool_K, 0)
         ws = torch.empty((nws,), dtype=torch.uint8, device=dev)
-        call('pcs_mlp_forward', ptr(X), ldx, Kin, M, recs, nl, pool_K, ptr(out), ptr(arg), ptr(ws), nws, st)
+        call('pcs_mlp_forward', ptr(X), ldx, Kin, M, recs, nl, pool_K, ptr(out), ldo, ptr(arg), ptr(ws), nws, st)
         if arg is not None:
             record_pool_arg(arg)
         if recording():
@@ -309,7 +315,7 @@ class SharedMLPFn(torch.autograd.Function):
         dev = gout.device
         st = stream_ptr(dev)
         lib = load()
-        M, ldx = X.shape
+        M, ldx = X.shape[0], X.stride(0)
         # a row-strided gradient (e.g. a column slice of a concatenation's gradient) is read
         # in place; anything else is made dense
         if not (gout.dim() == 2 and gout.stride(1) == 1 and gout.stride(0) % 4 == 0 and gout.data_ptr() % 16 == 0
@@ -321,23 +327,23 @@ class SharedMLPFn(torch.autograd.Function):
                         for li, f in enumerate(fixed))
         dX = None
         if ctx.needs_input_grad[0]:
-            dX = _f32((M, ldx), dev)
+            dX = _f32((M, X.shape[1]), dev)       # dense, X's width (its pad columns zeroed)
         key = (M, Kin, ldx, tuple(couts), pool_K, 1)
         nws = _workspace(lib, key, M, Kin, ldx, recs, nl, pool_K, 1)
         ws = torch.empty((nws,), dtype=torch.uint8, device=dev)
         lane = wgrad_lane(dev)
         if lane is None:
-            call('pcs_mlp_backward', ptr(X), ldx, Kin, M, recs, nl, pool_K, ptr(arg), ptr(gout), ldg, ptr(dX), ptr(ws),
-                 nws, st)
+            call('pcs_mlp_backward', ptr(X), ldx, Kin, M, recs, nl, pool_K, ptr(arg), ptr(gout), ldg, ptr(dX),
+                 X.shape[1], ptr(ws), nws, st)
         else:
             call('pcs_mlp_backward_deferred', ptr(X), ldx, Kin, M, recs, nl, pool_K, ptr(arg), ptr(gout), ldg,
-                 ptr(dX), ptr(ws), nws, st)
+                 ptr(dX), X.shape[1], ptr(ws), nws, st)
             # the lane still reads these: the caching allocator must not hand them out before it is done
             for t in (X, saved[1], saved[2], gout, ws, *([arg] if arg is not None else [])):
                 t.record_stream(lane)
             _queue_lane_join(dev)
         notify_grad_ready(params)
-        return (dX, None, None, None, None, *([None] * len(params)))
+        return (dX, None, None, None, None, None, *([None] * len(params)))
 
 
 def _edge_ws(B, N, C, Cout, backward, dev):
@@ -450,15 +456,34 @@ def edgeconv(x_rows: torch.Tensor, cin: int, idx: torch.Tensor, conv, bn, slope:
     return EdgeConvFn.apply(x_rows, idx.contiguous(), cin, slope, bn, conv.weight, bn.weight, bn.bias)
 
 
+def storage_alias(base: torch.Tensor, col0: int, ncol: int) -> torch.Tensor:
+    """Columns [col0, col0 + ncol) of the row-major (M, ld) buffer `base` as an (M, ncol)
+    tensor with row stride ld that shares base's storage WITHOUT being an autograd view of it:
+    several custom Functions can each write their output into their own column block of one
+    buffer (a zero-copy concatenation) without autograd's view+in-place checks firing."""
+    t = torch.empty(0, dtype=base.dtype, device=base.device)
+    t.set_(base.untyped_storage(), base.storage_offset() + col0, (base.shape[0], ncol), (base.stride(0), 1))
+    return t
+
+
+def _rows_ok(x: torch.Tensor) -> bool:
+    """(M, W) rows the engine reads in place: unit column stride, 16-B aligned rows, W % 4 == 0."""
+    return (x.dim() == 2 and x.stride(1) == 1 and x.stride(0) % 4 == 0 and x.stride(0) >= x.shape[1]
+            and x.shape[1] % 4 == 0 and x.data_ptr() % 16 == 0)
+
+
 def shared_mlp(x_rows: torch.Tensor, kin: int, convs, bns, act='relu', slope=0.0,
-               pool_k: int = 0) -> torch.Tensor:
-    """Run a conv/BN/act stack on rows.  x_rows (M, ld) with `kin` logical channels, ld % 4 == 0.
-    `act` / `slope` are one value for every layer or a sequence with one per layer
-    ('relu', 'lrelu', 'none')."""
+               pool_k: int = 0, out: torch.Tensor | None = None) -> torch.Tensor:
+    """Run a conv/BN/act stack on rows.  x_rows (M, W) with `kin` logical channels, W % 4 == 0,
+    dense or a column block of a wider buffer (row stride >= W).  `act` / `slope` are one value
+    for every layer or a sequence with one per layer ('relu', 'lrelu', 'none').  `out`: an
+    (M, cout) row block (storage_alias) the un-pooled activation is written into."""
     if not x_rows.is_cuda:
         raise RuntimeError('pcseg ops run only on the GPU (no CPU fallback); got a CPU tensor')
-    if x_rows.shape[1] % 4 or not x_rows.is_contiguous():
+    if not _rows_ok(x_rows):
         x_rows = pad_rows(x_rows[:, :kin])
+    if out is not None and (pool_k or not _rows_ok(out) or out.shape != (x_rows.shape[0], convs[-1].weight.shape[0])):
+        raise ValueError('shared_mlp: out must be an un-pooled (M, cout) row block')
     nl = len(convs)
     names = [act] * nl if isinstance(act, str) else list(act)
     slopes = [slope] * nl if isinstance(slope, (int, float)) else list(slope)
@@ -468,7 +493,7 @@ def shared_mlp(x_rows: torch.Tensor, kin: int, convs, bns, act='relu', slope=0.0
     params = []
     for conv, bn in zip(convs, bns):
         params += [conv.weight, conv.bias, bn.weight, bn.bias]
-    return SharedMLPFn.apply(x_rows, kin, pool_k, acts, list(bns), *params)
+    return SharedMLPFn.apply(x_rows, kin, pool_k, acts, list(bns), None if out is None else (out,), *params)
 
 
 class RowLinearFn(torch.autograd.Function):

@@ -17,7 +17,7 @@ import torch.nn.functional as F
 
 from . import ops
 from .common import SetAbstraction, FeaturePropagation, InvResMLP, UnitPointNet, GeometryPlan, GeometryPrefetch
-from .engine import shared_mlp, pad_rows, linear_rows, edgeconv, edgeconv_fused_ok
+from .engine import shared_mlp, pad_rows, linear_rows, edgeconv, edgeconv_fused_ok, storage_alias
 from .replay import active as _replay
 
 
@@ -189,9 +189,11 @@ class PointNeXt(GeometryPrefetch, nn.Module):
 
 
 # ------------------------------------------------------------------------- DGCNN
-def _seq_rows(x_rows: torch.Tensor, seq: nn.Sequential, kin: int | None = None) -> torch.Tensor:
-    """Conv1d(bias=False) -> BN1d -> LeakyReLU [-> Dropout] on rows (HIP shared-MLP engine)."""
-    y = shared_mlp(x_rows, kin or x_rows.shape[1], [seq[0]], [seq[1]], 'lrelu', seq[2].negative_slope, 0)
+def _seq_rows(x_rows: torch.Tensor, seq: nn.Sequential, kin: int | None = None,
+              out: torch.Tensor | None = None) -> torch.Tensor:
+    """Conv1d(bias=False) -> BN1d -> LeakyReLU [-> Dropout] on rows (HIP shared-MLP engine);
+    `out`: a row block the activation is written into (no Dropout after it)."""
+    y = shared_mlp(x_rows, kin or x_rows.shape[1], [seq[0]], [seq[1]], 'lrelu', seq[2].negative_slope, 0, out=out)
     if len(seq) > 3:
         y = seq[3](y)
     return y
@@ -254,15 +256,72 @@ class EdgeConv(nn.Module):
         return self.forward_points(x.transpose(1, 2).contiguous()).transpose(1, 2)
 
 
+class _CopyColumns(torch.autograd.Function):
+    """parts (B, N, C_i) copied side by side into the (B*N, sum C_i) row block dest[0]
+    (torch.cat(parts, dim=-1) of dgcnn.py:200 / :245, written into a wider buffer)."""
+
+    @staticmethod
+    def forward(ctx, dest, *parts):
+        out = dest[0]
+        off = 0
+        for p in parts:
+            c = p.shape[-1]
+            out[:, off:off + c].copy_(p.reshape(-1, c))
+            off += c
+        ctx.shapes = [p.shape for p in parts]
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        grads, off = [], 0
+        for shp in ctx.shapes:
+            c = shp[-1]
+            grads.append(g[:, off:off + c].view(shp))
+            off += c
+        return (None, *grads)
+
+
+class _ColumnConcat(torch.autograd.Function):
+    """torch.cat(blocks, dim=1) of row blocks that already sit side by side in one buffer
+    (equal row stride, consecutive columns): the result aliases them, nothing is copied; the
+    backward hands each block its column slice of the gradient (row-strided, read in place)."""
+
+    @staticmethod
+    def forward(ctx, *blocks):
+        first = blocks[0]
+        off = 0
+        for b in blocks:
+            if (b.data_ptr() != first.data_ptr() + 4 * off or b.stride(0) != first.stride(0) or b.stride(1) != 1
+                    or b.shape[0] != first.shape[0]):
+                raise RuntimeError('_ColumnConcat: blocks are not adjacent column blocks of one buffer')
+            off += b.shape[1]
+        ctx.widths = [b.shape[1] for b in blocks]
+        return storage_alias(first, 0, off)
+
+    @staticmethod
+    def backward(ctx, g):
+        grads, off = [], 0
+        for w in ctx.widths:
+            grads.append(g[:, off:off + w])
+            off += w
+        return tuple(grads)
+
+
 def _dgcnn_head(self, parts: list[torch.Tensor], B: int, N: int):
-    xc = torch.cat(parts, dim=-1)                      # (B, N, 320|384)
-    xr = xc.view(B * N, -1)
-    x5 = _seq_rows(xr, self.conv5)                      # (B*N, emb)
-    x6 = _seq_rows(torch.cat((xr, x5), dim=1), self.conv6)
+    # conv6 reads cat((x1..x4 [, colour], x5), 1) (dgcnn.py:203-206 / :248-251): one (B*N, 1408)
+    # buffer holds it -- the EdgeConv outputs are copied into its first columns, conv5 writes its
+    # activation straight into the rest, and the concatenation is an alias (no 0.7 GB copy)
+    M = B * N
+    cxr = sum(p.shape[-1] for p in parts)
+    emb = self.conv5[0].weight.shape[0]
+    H = torch.empty((M, cxr + emb), dtype=torch.float32, device=parts[0].device)
+    xr = _CopyColumns.apply((storage_alias(H, 0, cxr),), *parts)          # (B*N, 320|384), row stride 1344|1408
+    x5 = _seq_rows(xr, self.conv5, out=storage_alias(H, cxr, emb))        # (B*N, emb)
+    x6 = _seq_rows(_ColumnConcat.apply(xr, x5), self.conv6)
     x7 = _seq_rows(x6, self.conv7)
     logits = linear_rows(x7, self.conv8).view(B, N, -1)
     # the reference returns x5 as a contiguous (B, emb, N); a transposed view of
-    # the point-major tensor has the same shape and values without a 0.5 GB copy
+    # the point-major rows has the same shape and values without a 0.5 GB copy
     return logits, x5.view(B, N, -1).transpose(1, 2), None
 
 

@@ -222,16 +222,18 @@ typedef struct pcs_mlp_layer {
 int pcs_mlp_workspace(int M, int kin, int ldx, const pcs_mlp_layer* layers, int nl,
                       int pool_k, int backward, size_t* bytes);
 /* X (M x ldx rows, kin channels) -> out = pooled (M/pool_k x cout_L) + argmax u8
- * (pool_k > 0), or the activation (M x cout_L). */
+ * (pool_k > 0), or the activation (M x cout_L, row stride ldo; 0 = cout_L): a stack can
+ * write its activation straight into a column block of a wider buffer (DGCNN's conv5
+ * output inside the [x1..x4 | x5] concatenation conv6 reads, dgcnn.py:203-206). */
 int pcs_mlp_forward(const float* X, int ldx, int kin, int M, pcs_mlp_layer* layers,
-                    int nl, int pool_k, float* out, uint8_t* arg, void* workspace,
+                    int nl, int pool_k, float* out, int ldo, uint8_t* arg, void* workspace,
                     size_t ws_bytes, void* stream);
 /* gout = d loss / d out (same shape as out; row stride ldg, = cout_L when pooled);
- * accumulates every layer's dW/db/dgamma/dbeta; dX (M x ldx, nullable) = d loss / d X
- * (pad columns zeroed). */
+ * accumulates every layer's dW/db/dgamma/dbeta; dX (M x lddx, nullable; lddx 0 = ldx)
+ * = d loss / d X (pad columns zeroed). */
 int pcs_mlp_backward(const float* X, int ldx, int kin, int M,
                      const pcs_mlp_layer* layers, int nl, int pool_k,
-                     const uint8_t* arg, const float* gout, int ldg, float* dX,
+                     const uint8_t* arg, const float* gout, int ldg, float* dX, int lddx,
                      void* workspace, size_t ws_bytes, void* stream);
 /* The same, but the weight gradients are left running on the device's wgrad lane (a side
  * stream) after return, so they overlap the caller's next work.  Until
@@ -239,7 +241,7 @@ int pcs_mlp_backward(const float* X, int ldx, int kin, int M,
  * layers' Z/coef and the workspace must stay allocated (lane stream: pcs_wgrad_lane). */
 int pcs_mlp_backward_deferred(const float* X, int ldx, int kin, int M,
                               const pcs_mlp_layer* layers, int nl, int pool_k,
-                              const uint8_t* arg, const float* gout, int ldg, float* dX,
+                              const uint8_t* arg, const float* gout, int ldg, float* dX, int lddx,
                               void* workspace, size_t ws_bytes, void* stream);
 /* the current device's wgrad lane stream (null if none could be created) */
 int pcs_wgrad_lane(void** side_stream);
