@@ -108,6 +108,8 @@ static size_t max_partials(int M, int kin, const pcs_mlp_layer* L, int nl, int p
         const size_t c = (size_t)L[l].cout;
         m = std::max(m, 2 * c * (size_t)pcs_gemm_row_blocks(M, (int)c));
         if (backward) m = std::max(m, 2 * c * (size_t)pcs_gemm_row_blocks_dgrad(M, (int)c));
+        // a fused inner layer writes its input's BN-backward partials, one per fused block
+        if (backward && l > 0) m = std::max(m, 2 * (size_t)L[l].cin * (size_t)fused_bwd_grid(M));
     }
     if (backward) {
         const size_t c = (size_t)L[nl - 1].cout;
@@ -139,6 +141,8 @@ struct BwdScratch {
     size_t wg_bytes;
     char* wg0;             // the first layer's, when its wgrad runs on the caller's stream
     size_t wg0_bytes;
+    char* fw;              // fused inner layers' dW partials (caller's stream only)
+    size_t fw_bytes;
 };
 
 static size_t carve_backward(Carve& cv, int M, int kin, int ldx, const pcs_mlp_layer* L, int nl, int pool_k,
@@ -162,6 +166,11 @@ static size_t carve_backward(Carve& cv, int M, int kin, int ldx, const pcs_mlp_l
     s.wg = cv.take<char>(wg);
     s.wg0_bytes = L[0].dW ? wgrad_ws_bytes((int)L[0].cout, (int)L[0].cin, M) : 0;
     s.wg0 = cv.take<char>(s.wg0_bytes);
+    size_t fw = 0;
+    for (int l = 1; l < nl; ++l)
+        if (L[l].dW) fw = std::max(fw, fused_bwd_ws_bytes(M, (int)L[l].cout, (int)L[l].cin));
+    s.fw_bytes = fw;
+    s.fw = cv.take<char>(fw);
     s.dz = materialize_dz_of(L[nl - 1], M, true) ? cv.take<float>((size_t)M * (size_t)L[nl - 1].cout) : nullptr;
     if (out) *out = s;
     return cv.used;
@@ -406,7 +415,16 @@ static int mlp_backward(const float* X, int ldx, int kin, int M, const pcs_mlp_l
     for (int l = nl - 1; l >= 0; --l) {
         const pcs_mlp_layer& P = layers[l];
         const int C = (int)P.cout, Cin = (int)P.cin;
-        if (materialize_dz_of(P, M, l > 0 || dX) && S.dz_ok(l == nl - 1)) {
+        // a thin inner layer with a weight gradient: data + weight gradient in one launch
+        // (fused_bwd.hip) from one read of its rebuilt dZ, on the caller's stream
+        pcs_operand qop{};
+        if (l > 0) {
+            qop = bnbwd_op(nullptr, 0, layers[l - 1], nullptr, nullptr);
+            qop.data = layers[l - 1].Z;
+            qop.ld = Cin;
+        }
+        const bool fused = l > 0 && P.dW && fused_bwd_ok(M, C, Cin, (int)P.ldw, &xop, &qop);
+        if (!fused && materialize_dz_of(P, M, l > 0 || dX) && S.dz_ok(l == nl - 1)) {
             // the top layer's into its own buffer (gout is the caller's), inner ones in place
             // over the dA buffer the rebuilt operand reads
             float* dst = l == nl - 1 ? S.dz : const_cast<float*>(xop.data);
@@ -417,7 +435,9 @@ static int mlp_backward(const float* X, int ldx, int kin, int M, const pcs_mlp_l
         // stack's input needs no gradient): it then runs beside the lane's pending wgrads
         // instead of queueing behind them at the end of the backward
         const bool wg_here = l == 0 && !dX && nl > 1;
-        if (P.dW && wg_here) {
+        if (fused) {
+            // its wgrad is part of the fused launch below
+        } else if (P.dW && wg_here) {
             const pcs_operand y = plain_op(X, ldx);
             if (int e = pcs::wgrad_launch(&xop, C, &y, Cin, M, P.dW, P.db, S.wg0, S.wg0_bytes, stream)) return fail(e);
         } else if (P.dW) {
@@ -454,10 +474,18 @@ static int mlp_backward(const float* X, int ldx, int kin, int M, const pcs_mlp_l
         if (l > 0) {
             const pcs_mlp_layer& Q = layers[l - 1];
             float* dA = S.dA[da];
-            const int nbg = pcs_gemm_row_blocks_dgrad(M, Cin);
-            pcs_operand epi = bnbwd_op(nullptr, 0, Q, nullptr, nullptr);
-            if (int e = gemm_rows_ex(&xop, M, C, Bw, ldb, bt, nullptr, dA, Cin, Cin, nullptr, &epi, S.part, stream))
-                return fail(e);
+            int nbg;
+            if (fused) {
+                nbg = fused_bwd_grid(M);
+                if (int e = fused_bwd(&xop, C, &qop, Cin, P.W, (int)P.ldw, M, dA, Cin, S.part, P.dW, P.db, S.fw,
+                                      S.fw_bytes, st))
+                    return fail(e);
+            } else {
+                nbg = pcs_gemm_row_blocks_dgrad(M, Cin);
+                pcs_operand epi = bnbwd_op(nullptr, 0, Q, nullptr, nullptr);
+                if (int e = gemm_rows_ex(&xop, M, C, Bw, ldb, bt, nullptr, dA, Cin, Cin, nullptr, &epi, S.part, stream))
+                    return fail(e);
+            }
             pp = (pp + 1) % 3;
             const float* sq = Q.coef;
             if (int e = pcs_bn_bwd_finalize(S.part, nbg, Cin, M, sq, sq + 3 * Cin, Q.dgamma, Q.dbeta, S.kb[pp],

@@ -1,0 +1,314 @@
+// Fused backward of one thin shared-MLP layer: data gradient AND weight gradient from ONE
+// read of the layer's rebuilt dZ.
+//
+// Reference semantics: the autograd backward of conv1x1 -> BatchNorm(train) -> act
+// (MiniPointNet / UnitPointNet, models/utils/common.py:125-178), for an inner layer l of a
+// stack whose input is the previous layer's BN + activation:
+//   dA_{l-1} = dZ_l . W_l                 (M x CI; then BN-backward sums of layer l-1)
+//   dW_l    += dZ_l^T . act(BN(Z_{l-1}))  (C x CI),   db_l += column sums of dZ_l
+// The separate path (mlp.hip) runs these as two GEMMs -- the dgrad on the caller's stream,
+// the wgrad on the side lane -- and each rebuilds dZ (output gradient x act' and the BN
+// backward) from HBM: on the thin layers (C, CI <= 128 over 10^5..10^6 rows: PointNet++
+// SA1/SA2/SA3/FP1, PointNeXt) both are HBM-latency bound and the pair reads dZ's inputs
+// two or three times.  Here one workgroup stages a 64-row tile once:
+//   Zs = dZ tile (rebuilt on load, rows past M zeroed)     64 x C
+//   Xs = the previous layer's RAW pre-BN Z tile             64 x CI
+// and runs both MFMA products out of LDS:
+//   * dA tile = Zs . W with W's fragments held in registers for the whole launch (each wave
+//     owns one 32-wide column strip of dA), stored with the previous layer's BN-backward
+//     partial sums (sum dy, sum dy*xhat, dy = dA*act'(z*s+t), z read back from Xs) -- the
+//     epilogue of the dgrad GEMM;
+//   * dW += Zs^T . act(Xs*s + t): the activation is applied as the B fragment is read, so
+//     the raw z stays available for the epilogue; accumulators live across the block's
+//     tiles (persistent grid), one partial tile per block, summed in block order by
+//     wgrad_reduce_kernel (deterministic: no float atomics).
+// Every MFMA is v_mfma_f32_32x32x2_f32 (fp32 in, fp32 accumulate), so the results differ
+// from the two-GEMM path only in fp32 summation order.
+#include "mlp_common.hpp"
+
+namespace pcs {
+
+constexpr int FB_BM = 64;        // rows per tile
+constexpr int FB_BLOCKS_PER_CU = 2;
+
+struct FusedBwdArgs {
+    Operand x;            // layer l's dZ operand: BNBWD / POOLBWD (rebuilt on load) or PLAIN, C wide
+    Operand q;            // layer l-1: data = its pre-BN Z (M x CI, stride ld), s/t/mean/inv/slope
+    const float* W;       // layer l's weight, row-major C x CI (W[c * ldw + i])
+    int ldw;
+    int M;
+    float* dA;            // M x CI, row stride ldd
+    int ldd;
+    double* bstats;       // [2][CI][gridDim.x]: layer l-1's (sum dy, sum dy*xhat) per block
+    float* part;          // [gridDim.x][C][CI]: this block's dW partial
+    float* pdb;           // [gridDim.x][C]: this block's db partial (or null)
+};
+
+__device__ __forceinline__ int acc_row_of(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+// 256 threads, two blocks per CU: while one block stages its next tile (all of a tile's
+// loads in flight per thread chunk), the other runs its MFMAs.  (A 512-thread producer /
+// consumer variant with a double-buffered LDS tile, one block per CU, measured slower:
+// 145 vs 117 us isolated on the FP1 shape -- one consumer wave per SIMD does not keep the
+// MFMA pipe fed through its LDS fragment reads.)
+template <int C, int CI, int XM>
+__global__ __launch_bounds__(256, 2) void fused_bwd_kernel(FusedBwdArgs f) {
+    constexpr int BM = FB_BM;
+    constexpr int ZS = C + 2;                  // row stride = 2 (mod 64) banks: the dA fragment reads
+                                               // (32 rows x 2 k) hit 64 distinct banks
+    constexpr int XS = CI + 4;                 // float4-aligned rows (row reads only)
+    constexpr int NIT = CI / 32, NCT = C / 32;
+    constexpr int TW = NCT * NIT;              // 32 x 32 tiles of dW
+    constexpr int WPT = TW >= 4 ? TW / 4 : 1;  // dW tiles per wave
+    constexpr int WR = TW >= 4 ? 1 : 4 / TW;   // waves splitting one dW tile's rows
+    constexpr int NRT = NIT == 4 ? 2 : 1;      // dA row tiles per wave
+    static_assert(C % 32 == 0 && CI % 32 == 0 && C <= 128 && CI <= 128, "fused backward widths");
+    __shared__ float Zs[BM * ZS];
+    __shared__ __attribute__((aligned(16))) float Xs[BM * XS];
+    __shared__ double red[2][4][32];
+    __shared__ float wred[WR > 1 ? (WR - 1) * TW * 1024 : 1];   // per (row subset, tile)
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int h = lane >> 5, l32 = lane & 31;
+
+    // ---- data-gradient assignment: column strip a_ct, row tiles a_rt0 .. a_rt0 + NRT - 1
+    const int a_ct = NIT == 4 ? w : (NIT == 2 ? (w & 1) : 0);
+    const int a_rt0 = NIT == 4 ? 0 : (NIT == 2 ? (w >> 1) : (w & 1));
+    const bool a_on = NIT >= 2 || w < 2;
+    const int a_col = a_ct * 32 + l32;
+    float wf[C / 2];                           // wf[j] = W[2j + h][a_col]: B fragments of every k step
+#pragma unroll
+    for (int j = 0; j < C / 2; ++j) wf[j] = f.W[(size_t)(2 * j + h) * f.ldw + a_col];
+    // previous layer's BN at this lane's dA column (BN-backward epilogue)
+    const float es = f.q.s[a_col], et = f.q.t[a_col], em = f.q.mean[a_col], ei = f.q.inv[a_col];
+    const float qslope = f.q.slope;
+
+    // ---- weight-gradient assignment: tiles t = ct_c * NIT + ct_i.  TW >= 4: wave w takes
+    // t = w + 4u (all share ct_i = w % NIT); TW < 4: wave w takes t = w % TW over the row
+    // pairs p = w / TW (mod WR)
+    const int t_base = TW >= 4 ? w : (w % TW);
+    const int w_i = t_base % NIT;
+    const int wsub = TW >= 4 ? 0 : w / TW;
+    const int b_col = w_i * 32 + l32;
+    const float bs = f.q.s[b_col], bt = f.q.t[b_col];
+
+    f32x16 accW[WPT];
+#pragma unroll
+    for (int u = 0; u < WPT; ++u)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) accW[u][r] = 0.f;
+    double s1 = 0.0, s2 = 0.0;
+    float dbs = 0.f;
+
+    const int M = f.M;
+    const int tiles = (M + BM - 1) / BM;
+    for (int t = blockIdx.x; t < tiles; t += gridDim.x) {
+        const int m0 = t * BM;
+        __syncthreads();                       // the previous tile's reads of Zs / Xs are done
+        // ---- stage dZ: thread = one channel quad over rows r0 + j*RPP (one coefficient quad)
+        {
+            constexpr int CQ = C / 4, RPP = 256 / CQ, NJ = BM / RPP;
+            constexpr int CH = NJ < 4 ? NJ : 4;          // rows in flight per chunk (register budget)
+            const int cq = tid % CQ, r0 = tid / CQ;
+            Quad qd;
+            load_quad<XM>(f.x, 4 * cq, C, qd);
+#pragma unroll
+            for (int j0 = 0; j0 < NJ; j0 += CH) {
+                float4 v[CH], z[CH];
+                unsigned a[CH];
+#pragma unroll
+                for (int j = 0; j < CH; ++j) {
+                    const int rc = min(m0 + r0 + (j0 + j) * RPP, M - 1);
+                    load_raw<XM>(f.x, rc, 4 * cq, v[j], z[j], a[j]);
+                }
+#pragma unroll
+                for (int j = 0; j < CH; ++j) {
+                    const int r = r0 + (j0 + j) * RPP;
+                    float4 o = xform4<XM>(f.x, v[j], z[j], a[j], min(m0 + r, M - 1), qd, 4 * cq, C);
+                    if (m0 + r >= M) o = make_float4(0.f, 0.f, 0.f, 0.f);
+                    float* d = &Zs[r * ZS + 4 * cq];
+                    d[0] = o.x; d[1] = o.y; d[2] = o.z; d[3] = o.w;
+                }
+            }
+        }
+        // ---- stage the previous layer's raw Z (float4 rows)
+        {
+            constexpr int IQ = CI / 4, RPI = 256 / IQ, NJ = BM / RPI;
+            const int iq = tid % IQ, s0 = tid / IQ;
+            float4 xv[NJ];
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                const int rc = min(m0 + s0 + j * RPI, M - 1);
+                xv[j] = *reinterpret_cast<const float4*>(f.q.data + (size_t)rc * f.q.ld + 4 * iq);
+            }
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) *reinterpret_cast<float4*>(&Xs[(s0 + j * RPI) * XS + 4 * iq]) = xv[j];
+        }
+        __syncthreads();
+
+        // ---- dA tile(s) = Zs . W
+        if (a_on) {
+            f32x16 accA[NRT];
+#pragma unroll
+            for (int rt = 0; rt < NRT; ++rt)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) accA[rt][r] = 0.f;
+#pragma unroll
+            for (int j = 0; j < C / 2; ++j)
+#pragma unroll
+                for (int rt = 0; rt < NRT; ++rt) {
+                    const float a = Zs[((a_rt0 + rt) * 32 + l32) * ZS + 2 * j + h];
+                    accA[rt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, wf[j], accA[rt], 0, 0, 0);
+                }
+#pragma unroll
+            for (int rt = 0; rt < NRT; ++rt) {
+                const int rb = (a_rt0 + rt) * 32;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int row = rb + acc_row_of(r, h);
+                    const float v = accA[rt][r];
+                    if (m0 + row < M) {
+                        f.dA[(size_t)(m0 + row) * f.ldd + a_col] = v;
+                        const float z = Xs[row * XS + a_col];
+                        const float dy = v * dact_f(z * es + et, 0, qslope);
+                        const float xh = (z - em) * ei;
+                        s1 += (double)dy;
+                        s2 += (double)dy * (double)xh;
+                    }
+                }
+            }
+        }
+        // ---- dW += Zs^T . act(Xs*s + t)
+#pragma unroll 4
+        for (int pq = 0; pq < BM / 2 / WR; ++pq) {
+            const int r = 2 * (pq * WR + wsub) + h;
+            const float b = act_f(Xs[r * XS + b_col] * bs + bt, 0, qslope);
+#pragma unroll
+            for (int u = 0; u < WPT; ++u) {
+                const int ct_c = (t_base + 4 * u) / NIT;
+                const float a = Zs[r * ZS + ct_c * 32 + l32];
+                accW[u] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, accW[u], 0, 0, 0);
+            }
+        }
+        // ---- db: column sums of dZ (row order)
+        if (f.pdb && tid < C) {
+#pragma unroll 8
+            for (int r = 0; r < BM; ++r) dbs += Zs[r * ZS + tid];
+        }
+    }
+
+    // ---- previous layer's BN-backward partials: both lane halves, then the waves of a strip
+    s1 += __shfl_xor(s1, 32);
+    s2 += __shfl_xor(s2, 32);
+    if (lane < 32) {
+        red[0][w][l32] = a_on ? s1 : 0.0;
+        red[1][w][l32] = a_on ? s2 : 0.0;
+    }
+    __syncthreads();
+    if (tid < CI) {
+        const int ct = tid / 32, lc = tid % 32;
+        double a = 0.0, b = 0.0;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            const int vct = NIT == 4 ? v : (NIT == 2 ? (v & 1) : 0);
+            const bool von = NIT >= 2 || v < 2;
+            if (von && vct == ct) { a += red[0][v][lc]; b += red[1][v][lc]; }
+        }
+        f.bstats[(size_t)tid * gridDim.x + blockIdx.x] = a;
+        f.bstats[((size_t)CI + tid) * gridDim.x + blockIdx.x] = b;
+    }
+    if (f.pdb && tid < C) f.pdb[(size_t)blockIdx.x * C + tid] = dbs;
+    // ---- dW partial tile(s): waves splitting one tile's rows add theirs in wave order
+    float* part = f.part + (size_t)blockIdx.x * C * CI;
+    if constexpr (WR > 1) {
+        if (wsub > 0) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) wred[((wsub - 1) * TW + t_base) * 1024 + r * 64 + lane] = accW[0][r];
+        }
+        __syncthreads();
+        if (wsub == 0) {
+#pragma unroll
+            for (int s = 1; s < WR; ++s)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) accW[0][r] += wred[((s - 1) * TW + t_base) * 1024 + r * 64 + lane];
+        }
+    }
+    if (wsub == 0) {
+#pragma unroll
+        for (int u = 0; u < WPT; ++u) {
+            const int tt = t_base + 4 * u;
+            const int c0 = (tt / NIT) * 32, i0 = (tt % NIT) * 32;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) part[(size_t)(c0 + acc_row_of(r, h)) * CI + i0 + l32] = accW[u][r];
+        }
+    }
+}
+
+template <int C, int CI>
+static void launch_fused(dim3 grid, hipStream_t st, const FusedBwdArgs& a) {
+    switch (a.x.mode) {
+    case OP_PLAIN: hipLaunchKernelGGL((fused_bwd_kernel<C, CI, OP_PLAIN>), grid, dim3(256), 0, st, a); break;
+    case OP_BNBWD: hipLaunchKernelGGL((fused_bwd_kernel<C, CI, OP_BNBWD>), grid, dim3(256), 0, st, a); break;
+    default: hipLaunchKernelGGL((fused_bwd_kernel<C, CI, OP_POOLBWD>), grid, dim3(256), 0, st, a); break;
+    }
+}
+
+template <int C>
+static void launch_fused_ci(int CI, dim3 grid, hipStream_t st, const FusedBwdArgs& a) {
+    if (CI == 32) launch_fused<C, 32>(grid, st, a);
+    else if (CI == 64) launch_fused<C, 64>(grid, st, a);
+    else launch_fused<C, 128>(grid, st, a);
+}
+
+static bool fb_width(int c) { return c == 32 || c == 64 || c == 128; }
+
+bool fused_bwd_ok(int M, int C, int CI, int ldw, const pcs_operand* x, const pcs_operand* q) {
+    const int pol = fused_bwd_policy();
+    if (pol == 0 || (pol == 2 && M < (1 << 19))) return false;
+    if (M < 4 * FB_BM || !fb_width(C) || !fb_width(CI) || ldw % 4 != 0 || ldw < CI) return false;
+    if (!x || !q || x->mode == PCS_OP_BNACT || x->ld % 4 != 0 || x->ld < C) return false;
+    if (x->mode == PCS_OP_POOLBWD && (x->pool_k < 1 || M % x->pool_k != 0)) return false;
+    if (x->mode != PCS_OP_PLAIN && x->ldz % 4 != 0) return false;
+    return q->data && q->ld % 4 == 0 && q->ld >= CI && q->s && q->t && q->mean && q->inv;
+}
+
+int fused_bwd_grid(int M) {
+    const int tiles = (M + FB_BM - 1) / FB_BM;
+    return std::min(tiles, 256 * FB_BLOCKS_PER_CU);
+}
+
+size_t fused_bwd_ws_bytes(int M, int C, int CI) {
+    return (size_t)fused_bwd_grid(M) * ((size_t)C * CI + C) * sizeof(float) + 256;
+}
+
+int fused_bwd(const pcs_operand* x, int C, const pcs_operand* q, int CI, const float* W, int ldw, int M, float* dA,
+              int ldd, double* bstats, float* dW, float* db, void* ws, size_t ws_bytes, hipStream_t st) {
+    PCS_CHECK_ARG(fused_bwd_ok(M, C, CI, ldw, x, q), "fused_bwd: unsupported shape C=%d CI=%d M=%d", C, CI, M);
+    PCS_CHECK_ARG(dA && ldd >= CI && ldd % 4 == 0 && bstats && dW && W, "fused_bwd: bad output arguments");
+    PCS_CHECK_ARG(ws && ws_bytes >= fused_bwd_ws_bytes(M, C, CI), "fused_bwd: workspace too small");
+    const int G = fused_bwd_grid(M);
+    float* part = reinterpret_cast<float*>((reinterpret_cast<uintptr_t>(ws) + 255) & ~uintptr_t(255));
+    float* pdb = db ? part + (size_t)G * C * CI : nullptr;
+    FusedBwdArgs a{to_dev_operand(x), to_dev_operand(q), W, ldw, M, dA, ldd, bstats, part, pdb};
+    const dim3 grid(G);
+    auto launch = [=]() {
+        if (C == 32) launch_fused_ci<32>(CI, grid, st, a);
+        else if (C == 64) launch_fused_ci<64>(CI, grid, st, a);
+        else launch_fused_ci<128>(CI, grid, st, a);
+    };
+    int probe = -1;
+    if (probe_enabled()) {
+        char nm[80];
+        snprintf(nm, sizeof nm, "pcs::fused_bwd_kernel<%d, %d, %d>", C, CI, x->mode);
+        const double xb = x->mode == PCS_OP_POOLBWD ? 4.0 * M * C + 5.0 * (double)(M / x->pool_k) * C
+                                                   : 4.0 * M * C * (x->mode == PCS_OP_BNBWD ? 2 : 1);
+        probe = probe_start(nm, 4.0 * M * C * CI, xb + 8.0 * M * CI, st, launch);
+    }
+    launch();
+    probe_stop(probe, st);
+    wgrad_reduce_launch(part, G, (long long)C * CI, dW, pdb, C, db, st);
+    return launch_status("fused_bwd");
+}
+
+}  // namespace pcs

@@ -990,7 +990,7 @@ static int check_operand(const pcs_operand* o, int K, const char* who, const cha
     return 0;
 }
 
-static Operand to_dev(const pcs_operand* o) {
+Operand pcs::to_dev_operand(const pcs_operand* o) {
     Operand r{};
     if (!o) return r;
     r.data = o->data; r.ld = o->ld; r.mode = o->mode;
@@ -999,6 +999,24 @@ static Operand to_dev(const pcs_operand* o) {
     r.mean = o->mean; r.inv = o->inv; r.alpha = o->alpha; r.kb = o->kb;
     r.arg = o->arg; r.pool_k = o->pool_k;
     return r;
+}
+
+static Operand to_dev(const pcs_operand* o) { return to_dev_operand(o); }
+
+void pcs::wgrad_reduce_launch(const float* part, int splits, long long nk, float* dW, const float* pdb, int N,
+                              float* db, hipStream_t st) {
+    const long long blocks = (nk + kRedElems - 1) / kRedElems + (db ? (N + kRedElems - 1) / kRedElems : 0);
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, st, part, splits, nk, dW, pdb, N, db);
+}
+
+// A/B knob (scripts only): PCS_FUSED_BWD=0 off, 1 every thin inner layer, 2 (default) only
+// layers over >= 2^19 rows
+int pcs::fused_bwd_policy() {
+    static const int v = [] {
+        const char* e = getenv("PCS_FUSED_BWD");
+        return e && e[0] >= '0' && e[0] <= '2' ? e[0] - '0' : 2;
+    }();
+    return v;
 }
 
 // dZ (M x C, row stride ldo) = the BNBWD / POOLBWD transform of operand o, materialised: the

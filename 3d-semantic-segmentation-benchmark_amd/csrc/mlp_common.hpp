@@ -2,6 +2,7 @@
 // operand descriptors with their on-load transforms and the row-GEMM argument block.
 #pragma once
 
+#include <algorithm>
 #include <functional>
 
 #include "pcs_common.hpp"
@@ -168,5 +169,19 @@ void probe_stop(int idx, hipStream_t s);
 size_t wgrad_ws_bytes(int N, int K, int M);
 int wgrad_launch(const pcs_operand* x, int N, const pcs_operand* y, int K, int M, float* dW, float* db, void* ws,
                  size_t ws_bytes, void* stream);
+
+// device-side operand of an ABI operand (the activation folded into one slope)
+Operand to_dev_operand(const pcs_operand* o);
+// dW[e] += sum_s part[s][e] (e < nk), db[e] += sum_s pdb[s][e] (e < N; pdb/db nullable): fixed order
+void wgrad_reduce_launch(const float* part, int splits, long long nk, float* dW, const float* pdb, int N, float* db,
+                         hipStream_t st);
+// fused data + weight gradient of one thin inner layer (fused_bwd.hip): C = its width, CI = its
+// input width; q = the previous layer's pre-BN Z with its BN coefficients (s, t, mean, inv, act)
+int fused_bwd_policy();
+bool fused_bwd_ok(int M, int C, int CI, int ldw, const pcs_operand* x, const pcs_operand* q);
+int fused_bwd_grid(int M);
+size_t fused_bwd_ws_bytes(int M, int C, int CI);
+int fused_bwd(const pcs_operand* x, int C, const pcs_operand* q, int CI, const float* W, int ldw, int M, float* dA,
+              int ldd, double* bstats, float* dW, float* db, void* ws, size_t ws_bytes, hipStream_t st);
 
 }  // namespace pcs
