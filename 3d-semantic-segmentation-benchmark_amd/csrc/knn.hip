@@ -256,9 +256,14 @@ __device__ __forceinline__ float knn_select_row(float2* L, int nl, int c0, int c
 // A full segment flags the survivor as dropped; after the wave merges the flagged rows the
 // dropped survivors are re-appended.  Blocks of one cloud are mapped onto one XCD
 // (blockIdx round-robins over the 8 XCDs), so each XCD's L2 holds the clouds it works on.
-template <int F, int K, int WPB>
+// xx_pre (PRE): the squared norm of every point, precomputed by knn_sqnorm_kernel with the
+// same partial sums and the same final add as below, so the lists are bitwise the same; it
+// removes F multiply-adds per lane and tile (the candidate side recomputed every norm in every
+// wave that streams it)
+template <int F, int K, int WPB, bool PRE>
 __global__ __launch_bounds__(64 * WPB, 2) void knn_wave_kernel(const float* __restrict__ x, int B, int N, int rblocks,
-                                                            int* __restrict__ out_idx) {
+                                                            int* __restrict__ out_idx,
+                                                            const float* __restrict__ xx_pre) {
     constexpr bool MF = (F % 4 == 0);
     static_assert(MF || F == 3, "F must be 3 or a multiple of 4");
     constexpr int FH = MF ? F / 2 : 2;
@@ -314,6 +319,7 @@ __global__ __launch_bounds__(64 * WPB, 2) void knn_wave_kernel(const float* __re
         const float other = __shfl_xor(part, 32);
         xxq = h ? __fadd_rn(other, part) : __fadd_rn(part, other);
     }
+    if constexpr (PRE) xxq = xx_pre[(size_t)b * N + qr];
     float tau = -INFINITY;
     int cnt = 0, nl = 0;
 
@@ -325,9 +331,11 @@ __global__ __launch_bounds__(64 * WPB, 2) void knn_wave_kernel(const float* __re
     };
     // this lane's candidate (l32) of tile tt: features h*FH .. (F = 3: (x, y) | (z, 0))
     float4 cur[NQ], nxt[NQ];
-    auto fetch = [&](int tt, float4* dst) __attribute__((always_inline)) {
+    float cxx_cur = 0.f, cxx_nxt = 0.f;          // PRE: this lane's candidate's squared norm
+    auto fetch = [&](int tt, float4* dst, float& cxx) __attribute__((always_inline)) {
         const int c0 = tile_c0(tt);
         const int n = c0 + min(l32, N - c0 - 1);
+        if constexpr (PRE) cxx = xx_pre[(size_t)b * N + n];
         if constexpr (MF) {
             const float4* src = reinterpret_cast<const float4*>(X + (size_t)n * F + h * FH);
 #pragma unroll
@@ -337,11 +345,11 @@ __global__ __launch_bounds__(64 * WPB, 2) void knn_wave_kernel(const float* __re
             dst[0] = h ? make_float4(xr[2], 0.f, 0.f, 0.f) : make_float4(xr[0], xr[1], 0.f, 0.f);
         }
     };
-    fetch(0, cur);
+    fetch(0, cur, cxx_cur);
     for (int tt = 0; tt < ntile; ++tt) {
         const int c0 = tile_c0(tt);
         const int nc = min(KNN_TC, N - c0);
-        if (tt + 1 < ntile) fetch(tt + 1, nxt);
+        if (tt + 1 < ntile) fetch(tt + 1, nxt, cxx_nxt);
         float pd[16];
         {
             typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -351,7 +359,7 @@ __global__ __launch_bounds__(64 * WPB, 2) void knn_wave_kernel(const float* __re
                 const float vx = cur[0].x, vy = cur[0].y;
                 acc = __builtin_amdgcn_mfma_f32_32x32x2f32(vx, a[0], acc, 0, 0, 0);
                 acc = __builtin_amdgcn_mfma_f32_32x32x2f32(vy, a[1], acc, 0, 0, 0);
-                part = __fadd_rn(__fmul_rn(vx, vx), __fmul_rn(vy, vy));
+                if constexpr (!PRE) part = __fadd_rn(__fmul_rn(vx, vx), __fmul_rn(vy, vy));
             } else {
 #pragma unroll
                 for (int q = 0; q < NQ; ++q) {
@@ -361,27 +369,47 @@ __global__ __launch_bounds__(64 * WPB, 2) void knn_wave_kernel(const float* __re
                     acc = __builtin_amdgcn_mfma_f32_32x32x2f32(v.y, a[s + 1], acc, 0, 0, 0);
                     acc = __builtin_amdgcn_mfma_f32_32x32x2f32(v.z, a[s + 2], acc, 0, 0, 0);
                     acc = __builtin_amdgcn_mfma_f32_32x32x2f32(v.w, a[s + 3], acc, 0, 0, 0);
-                    part = __fadd_rn(part, __fmul_rn(v.x, v.x));
-                    part = __fadd_rn(part, __fmul_rn(v.y, v.y));
-                    part = __fadd_rn(part, __fmul_rn(v.z, v.z));
-                    part = __fadd_rn(part, __fmul_rn(v.w, v.w));
+                    if constexpr (!PRE) {
+                        part = __fadd_rn(part, __fmul_rn(v.x, v.x));
+                        part = __fadd_rn(part, __fmul_rn(v.y, v.y));
+                        part = __fadd_rn(part, __fmul_rn(v.z, v.z));
+                        part = __fadd_rn(part, __fmul_rn(v.w, v.w));
+                    }
                 }
             }
-            const float other = __shfl_xor(part, 32);
-            if (h == 0) s_cxx[w][l32] = __fadd_rn(part, other);
+            if constexpr (PRE) {
+                if (h == 0) s_cxx[w][l32] = cxx_cur;
+            } else {
+                const float other = __shfl_xor(part, 32);
+                if (h == 0) s_cxx[w][l32] = __fadd_rn(part, other);
+            }
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
                 const float inner = -2.f * acc[i];
                 pd[i] = __fsub_rn(__fsub_rn(-xxq, inner), s_cxx[w][acc_row(i, h)]);
             }
         }
-        unsigned dropped = 0;
+        // survivors of this tile (one bit per candidate slot); when no lane's segment can fill
+        // (the common case) they are appended without the overflow bookkeeping -- the same
+        // writes and counts as the general loop below, which handles a filling segment
+        unsigned pm = 0;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const bool p = acc_row(i, h) < nc && pd[i] >= tau;
-            sg[min(cnt, CAP)] = make_float2(pd[i], __int_as_float(c0 + acc_row(i, h)));
-            dropped |= (p && cnt >= CAP) ? (1u << i) : 0u;
-            cnt += (p && cnt < CAP) ? 1 : 0;
+        for (int i = 0; i < 16; ++i) pm |= (acc_row(i, h) < nc && pd[i] >= tau) ? (1u << i) : 0u;
+        unsigned dropped = 0;
+        if (!ballot(cnt + __builtin_popcount(pm) > CAP)) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                sg[cnt] = make_float2(pd[i], __int_as_float(c0 + acc_row(i, h)));
+                cnt += (pm >> i) & 1u;
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const bool p = (pm >> i) & 1u;
+                sg[min(cnt, CAP)] = make_float2(pd[i], __int_as_float(c0 + acc_row(i, h)));
+                dropped |= (p && cnt >= CAP) ? (1u << i) : 0u;
+                cnt += (p && cnt < CAP) ? 1 : 0;
+            }
         }
         const unsigned long long nm = ballot(dropped != 0 || cnt > CAP - PCS_KNN_SLACK);
         if (nm) {
@@ -407,6 +435,7 @@ __global__ __launch_bounds__(64 * WPB, 2) void knn_wave_kernel(const float* __re
         }
 #pragma unroll
         for (int q = 0; q < NQ; ++q) cur[q] = nxt[q];
+        cxx_cur = cxx_nxt;
     }
     for (int r = 0; r < 32; ++r) {
         const int c0n = (int)readlane_u((unsigned)cnt, r);
@@ -424,27 +453,57 @@ __global__ __launch_bounds__(64 * WPB, 2) void knn_wave_kernel(const float* __re
     }
 }
 
+// xx[b][n] = |x_n|^2 exactly as knn_wave_kernel forms it: two half-feature partial sums
+// (sequential fp32 multiply-adds, un-fused) added once (F = 3: (x^2 + y^2) + z^2)
+template <int F>
+__global__ __launch_bounds__(256) void knn_sqnorm_kernel(const float* __restrict__ x, long long P,
+                                                       float* __restrict__ xx) {
+    const long long p = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (p >= P) return;
+    const float* r = x + (size_t)p * F;
+    if constexpr (F % 4 == 0) {
+        constexpr int FH = F / 2;
+        float p0 = 0.f, p1 = 0.f;
+#pragma unroll
+        for (int s = 0; s < FH; ++s) p0 = __fadd_rn(p0, __fmul_rn(r[s], r[s]));
+#pragma unroll
+        for (int s = 0; s < FH; ++s) p1 = __fadd_rn(p1, __fmul_rn(r[FH + s], r[FH + s]));
+        xx[p] = __fadd_rn(p0, p1);
+    } else {
+        const float p0 = __fadd_rn(__fmul_rn(r[0], r[0]), __fmul_rn(r[1], r[1]));
+        const float p1 = __fadd_rn(__fmul_rn(r[2], r[2]), __fmul_rn(0.f, 0.f));
+        xx[p] = __fadd_rn(p0, p1);
+    }
+}
+
 template <int K>
 constexpr bool knn_tiled() { return (KNN_NMAX - K) / 2 - 1 >= 16; }
 
 template <int F, int K>
-static void launch_knn(const float* x, int B, int N, int* out, hipStream_t s) {
+static void launch_knn(const float* x, int B, int N, int* out, float* xx, hipStream_t s) {
     if constexpr (knn_tiled<K>()) {
         const int rb = (N + KNN_QROWS - 1) / KNN_QROWS;
-        hipLaunchKernelGGL((knn_wave_kernel<F, K, KNN_WAVES>), dim3(rb * B), dim3(64 * KNN_WAVES), 0, s, x, B, N, rb,
-                           out);
+        if (xx) {
+            const long long P = (long long)B * N;
+            hipLaunchKernelGGL((knn_sqnorm_kernel<F>), dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, x, P, xx);
+            hipLaunchKernelGGL((knn_wave_kernel<F, K, KNN_WAVES, true>), dim3(rb * B), dim3(64 * KNN_WAVES), 0, s, x, B,
+                               N, rb, out, (const float*)xx);
+        } else {
+            hipLaunchKernelGGL((knn_wave_kernel<F, K, KNN_WAVES, false>), dim3(rb * B), dim3(64 * KNN_WAVES), 0, s, x,
+                               B, N, rb, out, (const float*)nullptr);
+        }
         return;
     }
     hipLaunchKernelGGL((knn_kernel<F, K>), dim3((N + 255) / 256, B), dim3(256), 0, s, x, N, out);
 }
 
 template <int F>
-static int dispatch_k(const float* x, int B, int N, int k, int* out, hipStream_t s) {
+static int dispatch_k(const float* x, int B, int N, int k, int* out, float* xx, hipStream_t s) {
     switch (k) {
-        case 16: launch_knn<F, 16>(x, B, N, out, s); return 0;
-        case 20: launch_knn<F, 20>(x, B, N, out, s); return 0;
-        case 32: launch_knn<F, 32>(x, B, N, out, s); return 0;
-        case 40: launch_knn<F, 40>(x, B, N, out, s); return 0;
+        case 16: launch_knn<F, 16>(x, B, N, out, xx, s); return 0;
+        case 20: launch_knn<F, 20>(x, B, N, out, xx, s); return 0;
+        case 32: launch_knn<F, 32>(x, B, N, out, xx, s); return 0;
+        case 40: launch_knn<F, 40>(x, B, N, out, xx, s); return 0;
         default:
             set_error("pcs_knn: k=%d not instantiated (16, 20, 32, 40)", k);
             return (int)hipErrorInvalidValue;
@@ -453,9 +512,7 @@ static int dispatch_k(const float* x, int B, int N, int k, int* out, hipStream_t
 
 }  // namespace pcs
 
-// Reference: models/dgcnn/dgcnn.py:7-21.  x point-major (B, N, F) fp32; out (B, N, k) int32,
-// best first.  F in {3, 64}; k in {16, 20, 32, 40}.
-PCS_API int pcs_knn(const float* x, int B, int N, int F, int k, int32_t* out_idx, void* stream) {
+static int knn_run(const float* x, int B, int N, int F, int k, int32_t* out_idx, float* xx, void* stream) {
     using namespace pcs;
     PCS_CHECK_ARG(B >= 0 && N >= 1 && k >= 1 && k <= N, "pcs_knn: bad sizes B=%d N=%d k=%d", B, N, k);
     PCS_CHECK_ARG(x && out_idx, "pcs_knn: null pointer");
@@ -463,8 +520,8 @@ PCS_API int pcs_knn(const float* x, int B, int N, int F, int k, int32_t* out_idx
     hipStream_t s = as_stream(stream);
     int rc;
     switch (F) {
-        case 3: rc = dispatch_k<3>(x, B, N, k, out_idx, s); break;
-        case 64: rc = dispatch_k<64>(x, B, N, k, out_idx, s); break;
+        case 3: rc = dispatch_k<3>(x, B, N, k, out_idx, xx, s); break;
+        case 64: rc = dispatch_k<64>(x, B, N, k, out_idx, xx, s); break;
         default:
             set_error("pcs_knn: F=%d not instantiated (3, 64)", F);
             return (int)hipErrorInvalidValue;
@@ -473,4 +530,23 @@ PCS_API int pcs_knn(const float* x, int B, int N, int F, int k, int32_t* out_idx
     return launch_status("pcs_knn");
 }
 
+// Reference: models/dgcnn/dgcnn.py:7-21.  x point-major (B, N, F) fp32; out (B, N, k) int32,
+// best first.  F in {3, 64}; k in {16, 20, 32, 40}.
+PCS_API int pcs_knn(const float* x, int B, int N, int F, int k, int32_t* out_idx, void* stream) {
+    return knn_run(x, B, N, F, k, out_idx, nullptr, stream);
+}
 
+PCS_API int pcs_knn_workspace(int B, int N, size_t* bytes) {
+    PCS_CHECK_ARG(bytes && B >= 0 && N >= 0, "pcs_knn_workspace: bad arguments");
+    *bytes = (size_t)B * N * sizeof(float) + 256;
+    return 0;
+}
+
+// pcs_knn with a caller workspace (pcs_knn_workspace bytes): the squared norms are computed
+// once per point instead of once per point and streaming wave (same lists, fewer VALU ops)
+PCS_API int pcs_knn_ws(const float* x, int B, int N, int F, int k, int32_t* out_idx, void* ws, size_t ws_bytes,
+                       void* stream) {
+    PCS_CHECK_ARG(ws && ws_bytes >= (size_t)B * N * sizeof(float) + 256, "pcs_knn_ws: workspace too small");
+    float* xx = reinterpret_cast<float*>((reinterpret_cast<uintptr_t>(ws) + 255) & ~uintptr_t(255));
+    return knn_run(x, B, N, F, k, out_idx, xx, stream);
+}

@@ -71,7 +71,8 @@ def knn(x: torch.Tensor, k: int) -> torch.Tensor:
     x = _c(x.float())
     B, N, Fd = x.shape
     out = torch.empty((B, N, k), dtype=torch.int32, device=x.device)
-    call('pcs_knn', ptr(x), B, N, Fd, k, ptr(out), stream_ptr(x.device))
+    ws = torch.empty((B * N + 64,), dtype=torch.float32, device=x.device)    # per-point squared norms
+    call('pcs_knn_ws', ptr(x), B, N, Fd, k, ptr(out), ptr(ws), ws.numel() * 4, stream_ptr(x.device))
     return out
 
 

@@ -57,6 +57,11 @@ int pcs_knn_select(const float* query, const float* ref, int B, int N, int M,
  * F in {3,64}, k in {16,20,32,40}; out_idx (B,N,k) best first. */
 int pcs_knn(const float* x, int B, int N, int F, int k, int32_t* out_idx,
             void* stream);
+/* pcs_knn with a caller workspace of pcs_knn_workspace(B, N) bytes: the
+ * squared norms are computed once per point (same lists as pcs_knn). */
+int pcs_knn_workspace(int B, int N, size_t* bytes);
+int pcs_knn_ws(const float* x, int B, int N, int F, int k, int32_t* out_idx,
+               void* ws, size_t ws_bytes, void* stream);
 
 /* ---- gather / scatter --------------------------------------------------- */
 

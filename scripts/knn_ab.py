@@ -14,14 +14,24 @@ B, N, k = 32, 4096, 20
 pts, _, _ = make_batch(B, N, seed=3)
 xyz = pts[:, :, :3].contiguous().cuda()
 feat = torch.randn(B, N, 64, device='cuda')
+from pcseg._lib import call, ptr, stream_ptr  # noqa: E402
+
+
+def plain(x, k):      # pcs_knn: squared norms recomputed by every streaming wave
+    o = torch.empty((x.shape[0], x.shape[1], k), dtype=torch.int32, device=x.device)
+    call('pcs_knn', ptr(x), x.shape[0], x.shape[1], x.shape[2], k, ptr(o), stream_ptr(x.device))
+    return o
+
+
 for name, x in (('F=3', xyz), ('F=64', feat)):
-    out = ops.knn(x, k)
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(10):
-        again = ops.knn(x, k)
-    e1.record()
-    e1.synchronize()
-    print(f'{name}: {e0.elapsed_time(e1) / 10 * 1e3:8.1f} us  repeat bitwise-equal {torch.equal(out, again)}',
-          flush=True)
+    for path, fn in (('ws', ops.knn), ('plain', plain)):
+        out = fn(x, k)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(10):
+            again = fn(x, k)
+        e1.record()
+        e1.synchronize()
+        print(f'{name} {path}: {e0.elapsed_time(e1) / 10 * 1e3:8.1f} us  repeat bitwise-equal {torch.equal(out, again)}'
+              f'  equal to ws {torch.equal(out, ops.knn(x, k))}', flush=True)

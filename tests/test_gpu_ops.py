@@ -231,6 +231,20 @@ def test_dgcnn_knn_selection_exact_on_integer_grids(F_, lo, hi, N):
     assert torch.equal(got, exp)
 
 
+@pytest.mark.parametrize('F_', [3, 64])
+def test_dgcnn_knn_workspace_path_bitwise_equal(F_):
+    """pcs_knn_ws (squared norms precomputed once per point, the path ops.knn takes) gives
+    bitwise the same lists as pcs_knn (norms recomputed per streaming wave), B=4, N=4096."""
+    from pcseg._lib import call, ptr, stream_ptr
+    torch.manual_seed(F_)
+    x = (torch.randn(4, 4096, F_) if F_ == 64 else make_batch(4, 4096, seed=9)[0][:, :, :3].contiguous()).to(DEV)
+    a = torch.empty((4, 4096, 20), dtype=torch.int32, device=DEV)
+    call('pcs_knn', ptr(x), 4, 4096, F_, 20, ptr(a), stream_ptr(x.device))
+    b = ops.knn(x, 20)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+
+
 def test_dgcnn_knn_vs_reference_graph_at_4096(golden):
     """The xyz graph the reference itself built for BASELINE config 2's block size
     (tests/golden/model_dgcnn_color_4096.npz, knn0: B=2, N=4096, k=20)."""
