@@ -799,9 +799,10 @@ __global__ __launch_bounds__(256) void bn_act_kernel(const float* __restrict__ Z
         const int r = e / nq;
         const int c = 4 * (e - r * nq);
         const F4 z = ld4(Z + (size_t)r * ldz + c);
+        const F4 sv = ld4(s + c), tv = ld4(t + c);          // one quad load each (c % 4 == 0)
         F4 o;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) o.v[j] = act_f(z.v[j] * s[c + j] + t[c + j], act, slope);
+        for (int j = 0; j < 4; ++j) o.v[j] = act_f(z.v[j] * sv.v[j] + tv.v[j], act, slope);
         st4(out + (size_t)r * ldo + c, o);
     }
 }

@@ -215,6 +215,26 @@ class GeometryPrefetch:
     def prefetch_geometry(self, x: torch.Tensor) -> None:
         self._pcs_prefetched = (x, x._version, self._plan_for(self._coords_of(x)))
 
+    def prefetch_geometry_in_backward(self, x: torch.Tensor) -> None:
+        """Arm a prefetch for the NEXT forward: it hooks the gradient of a mid-network
+        activation (the input of the last FeaturePropagation) so that prefetch_geometry(x) is
+        enqueued from the backward, once the head's and FP1's backward GEMMs are already queued
+        on the GPU.  Enqueued between the loss and backward() instead, the ~25 Python-level
+        geometry launches leave the GPU idle: the forward has drained its queue by then."""
+        self._pcs_prefetch_armed = x
+
+    def _prefetch_point(self, t: torch.Tensor) -> torch.Tensor:
+        x = getattr(self, '_pcs_prefetch_armed', None)
+        if x is not None and torch.is_grad_enabled() and t.requires_grad:
+            self._pcs_prefetch_armed = None
+            dev = t.device
+
+            def hook(_grad, x=x):
+                with torch.cuda.device(dev):
+                    self.prefetch_geometry(x)
+            t.register_hook(hook)
+        return t
+
     def _geometry(self, x: torch.Tensor, coords: torch.Tensor) -> GeometryPlan:
         pf = getattr(self, '_pcs_prefetched', None)
         self._pcs_prefetched = None

@@ -56,7 +56,7 @@ class PointNetpp(GeometryPrefetch, nn.Module):
         c4, f4 = self.sa4(c3, f3, geo=geo.sa(4))
         f3 = self.fp4(c3, c4, f3, f4, geo=geo.fp(3))
         f2 = self.fp3(c2, c3, f2, f3, geo=geo.fp(2))
-        f1 = self.fp2(c1, c2, f1, f2, geo=geo.fp(1))
+        f1 = self._prefetch_point(self.fp2(c1, c2, f1, f2, geo=geo.fp(1)))
         f0 = self.fp1(c0, c1, None, f1, geo=geo.fp(0))
         return _head_rows(f0.reshape(B * N, -1), self.drop, self.conv).view(B, N, -1)
 
@@ -119,7 +119,7 @@ class PointNetppMSG(GeometryPrefetch, nn.Module):
             fs.append(f)
         f3 = self.fp4(cs[3], cs[4], fs[3], fs[4], geo=geo.fp(3))
         f2 = self.fp3(cs[2], cs[3], fs[2], f3, geo=geo.fp(2))
-        f1 = self.fp2(cs[1], cs[2], fs[1], f2, geo=geo.fp(1))
+        f1 = self._prefetch_point(self.fp2(cs[1], cs[2], fs[1], f2, geo=geo.fp(1)))
         f0 = self.fp1(cs[0], cs[1], None, f1, geo=geo.fp(0))
         return _head_rows(f0.reshape(B * N, -1), self.drop, self.conv).view(B, N, -1)
 
@@ -183,7 +183,7 @@ class PointNeXt(GeometryPrefetch, nn.Module):
         c4, f4 = self.irmlp4(c4, c4, f4, geo=geo.sa(4, 1)[1:])
         f3 = self.fp4(c3, c4, f3, f4, geo=geo.fp(3))
         f2 = self.fp3(c2, c3, f2, f3, geo=geo.fp(2))
-        f1 = self.fp2(c1, c2, f1, f2, geo=geo.fp(1))
+        f1 = self._prefetch_point(self.fp2(c1, c2, f1, f2, geo=geo.fp(1)))
         f0 = self.fp1(c0, c1, f0, f1, geo=geo.fp(0))
         return _head_rows(f0.reshape(B * N, -1), self.drop, self.conv).view(B, N, -1)
 

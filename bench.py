@@ -235,12 +235,17 @@ def run_workload(key, batch, npoints, args, world, rank, dev):
     lengths = lengths.to(dev)
     prefetch = hasattr(model, 'prefetch_geometry') and not args.no_prefetch and not use_graph
 
+    in_bwd = args.prefetch_point == 'backward'
+
     def step():
         grads.zero_grad()
-        loss = pcseg.masked_onehot_cross_entropy(logits_of(model(x)), lab, lengths)
-        if prefetch:
+        if prefetch and in_bwd:
             # pipelined input: the next batch's neighbour search (here the same resident
-            # blocks, fresh FPS starts) runs on the side stream under this backward
+            # blocks, fresh FPS starts) runs on the side stream under this backward,
+            # enqueued from a gradient hook once the first backward stages are queued
+            model.prefetch_geometry_in_backward(x)
+        loss = pcseg.masked_onehot_cross_entropy(logits_of(model(x)), lab, lengths)
+        if prefetch and not in_bwd:
             model.prefetch_geometry(x)
         loss.backward()
         grads.synchronize()
@@ -368,6 +373,9 @@ def main():
                     help='also time the dominant kernel\'s launches replayed back to back (rewrites outputs)')
     ap.add_argument('--graph', action='store_true',
                     help='capture one training step in a HIP graph and time its replays (N=1, no prefetch)')
+    ap.add_argument('--prefetch-point', choices=['backward', 'loss'], default='loss',
+                    help="where the next step's geometry is enqueued: between the loss and backward() (default) "
+                         "or from a gradient hook inside the backward (round 2 A/B: within noise, 5.50 vs 5.52 ms)")
     ap.add_argument('--no-prefetch', action='store_true',
                     help='do not enqueue the next step\'s FPS/ball-query/3-NN before this step\'s backward')
     ap.add_argument('--check-launch', action='store_true',

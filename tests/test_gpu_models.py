@@ -313,6 +313,31 @@ def test_prefetched_geometry_matches_inline(ctor):
     assert torch.equal(inline, again)
 
 
+@pytest.mark.parametrize('ctor', [lambda: pcseg.PointNetpp(14), lambda: pcseg.PointNeXt(14),
+                                  lambda: pcseg.PointNetppMSG(14)])
+def test_geometry_prefetched_from_backward_hook(ctor):
+    """prefetch_geometry_in_backward(x) (bench.py's default): the plan enqueued from the
+    gradient hook during the backward is the one the next forward(x) consumes, and it gives
+    the logits of an inline forward with the same FPS start draws."""
+    torch.manual_seed(0)
+    model = ctor().to(DEV).train()
+    dropout_off(model)
+    pts, _, _ = make_batch(2, 4096, seed=33)
+    x = pts.to(DEV)
+    torch.manual_seed(5)
+    ref = model(x).detach().clone()
+    torch.manual_seed(7)
+    model.prefetch_geometry_in_backward(x)
+    out = model(x)
+    assert getattr(model, '_pcs_prefetched', None) is None
+    torch.manual_seed(5)                       # the hook's FPS start draws
+    out.square().mean().backward()
+    torch.cuda.synchronize()
+    assert model._pcs_prefetched is not None and model._pcs_prefetched[0] is x
+    got = model(x).detach()
+    assert torch.equal(ref, got)
+
+
 def test_geometry_plan_copy_from_double_buffer():
     """GeometryPlan.copy_from (bench.py --graph's double-buffered geometry): after copying
     plan B into plan A's tensors, a forward that consumes A gives exactly the logits of a
