@@ -169,6 +169,7 @@ static size_t carve_backward(Carve& cv, int M, int kin, int ldx, const pcs_mlp_l
     size_t fw = 0;
     for (int l = 1; l < nl; ++l)
         if (L[l].dW) fw = std::max(fw, fused_bwd_ws_bytes(M, (int)L[l].cout, (int)L[l].cin));
+    if (L[0].dW && L[0].cin <= 32) fw = std::max(fw, fused_wgrad_ws_bytes(M, (int)L[0].cout, (int)L[0].cin));
     s.fw_bytes = fw;
     s.fw = cv.take<char>(fw);
     s.dz = materialize_dz_of(L[nl - 1], M, true) ? cv.take<float>((size_t)M * (size_t)L[nl - 1].cout) : nullptr;
@@ -437,6 +438,8 @@ static int mlp_backward(const float* X, int ldx, int kin, int M, const pcs_mlp_l
         const bool wg_here = l == 0 && !dX && nl > 1;
         if (fused) {
             // its wgrad is part of the fused launch below
+        } else if (P.dW && wg_here && fused_wgrad_ok(M, C, Cin, ldx, &xop)) {
+            if (int e = fused_wgrad(&xop, C, X, ldx, Cin, M, P.dW, P.db, S.fw, S.fw_bytes, st)) return fail(e);
         } else if (P.dW && wg_here) {
             const pcs_operand y = plain_op(X, ldx);
             if (int e = pcs::wgrad_launch(&xop, C, &y, Cin, M, P.dW, P.db, S.wg0, S.wg0_bytes, stream)) return fail(e);

@@ -40,8 +40,10 @@ struct FusedBwdArgs {
     float* dA;            // M x CI, row stride ldd
     int ldd;
     double* bstats;       // [2][CI][gridDim.x]: layer l-1's (sum dy, sum dy*xhat) per block
-    float* part;          // [gridDim.x][C][CI]: this block's dW partial
+    float* part;          // [gridDim.x][C][kp]: this block's dW partial (columns < kp)
     float* pdb;           // [gridDim.x][C]: this block's db partial (or null)
+    int kx;               // valid input columns (< CI: a stack's first layer, its raw input zero-padded)
+    int kp;               // dW row length (= kx)
 };
 
 __device__ __forceinline__ int acc_row_of(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
@@ -51,7 +53,9 @@ __device__ __forceinline__ int acc_row_of(int r, int h) { return (r & 3) + 8 * (
 // consumer variant with a double-buffered LDS tile, one block per CU, measured slower:
 // 145 vs 117 us isolated on the FP1 shape -- one consumer wave per SIMD does not keep the
 // MFMA pipe fed through its LDS fragment reads.)
-template <int C, int CI, int XM>
+// DA = false: weight gradient only (a stack's first layer, whose input needs no gradient):
+// the input is the plain raw rows (q.s == null: identity, no BN), kx <= CI columns.
+template <int C, int CI, int XM, bool DA>
 __global__ __launch_bounds__(256, 2) void fused_bwd_kernel(FusedBwdArgs f) {
     constexpr int BM = FB_BM;
     constexpr int ZS = C + 2;                  // row stride = 2 (mod 64) banks: the dA fragment reads
@@ -75,14 +79,17 @@ __global__ __launch_bounds__(256, 2) void fused_bwd_kernel(FusedBwdArgs f) {
     // ---- data-gradient assignment: column strip a_ct, row tiles a_rt0 .. a_rt0 + NRT - 1
     const int a_ct = NIT == 4 ? w : (NIT == 2 ? (w & 1) : 0);
     const int a_rt0 = NIT == 4 ? 0 : (NIT == 2 ? (w >> 1) : (w & 1));
-    const bool a_on = NIT >= 2 || w < 2;
+    const bool a_on = DA && (NIT >= 2 || w < 2);
     const int a_col = a_ct * 32 + l32;
-    float wf[C / 2];                           // wf[j] = W[2j + h][a_col]: B fragments of every k step
+    float wf[DA ? C / 2 : 1];                  // wf[j] = W[2j + h][a_col]: B fragments of every k step
+    float es = 0.f, et = 0.f, em = 0.f, ei = 0.f;
+    if constexpr (DA) {
 #pragma unroll
-    for (int j = 0; j < C / 2; ++j) wf[j] = f.W[(size_t)(2 * j + h) * f.ldw + a_col];
-    // previous layer's BN at this lane's dA column (BN-backward epilogue)
-    const float es = f.q.s[a_col], et = f.q.t[a_col], em = f.q.mean[a_col], ei = f.q.inv[a_col];
-    const float qslope = f.q.slope;
+        for (int j = 0; j < C / 2; ++j) wf[j] = f.W[(size_t)(2 * j + h) * f.ldw + a_col];
+        // previous layer's BN at this lane's dA column (BN-backward epilogue)
+        es = f.q.s[a_col]; et = f.q.t[a_col]; em = f.q.mean[a_col]; ei = f.q.inv[a_col];
+    }
+    const float qslope = DA ? f.q.slope : 1.f;
 
     // ---- weight-gradient assignment: tiles t = ct_c * NIT + ct_i.  TW >= 4: wave w takes
     // t = w + 4u (all share ct_i = w % NIT); TW < 4: wave w takes t = w % TW over the row
@@ -91,7 +98,7 @@ __global__ __launch_bounds__(256, 2) void fused_bwd_kernel(FusedBwdArgs f) {
     const int w_i = t_base % NIT;
     const int wsub = TW >= 4 ? 0 : w / TW;
     const int b_col = w_i * 32 + l32;
-    const float bs = f.q.s[b_col], bt = f.q.t[b_col];
+    const float bs = DA ? f.q.s[b_col] : 1.f, bt = DA ? f.q.t[b_col] : 0.f;   // !DA: identity
 
     f32x16 accW[WPT];
 #pragma unroll
@@ -137,10 +144,12 @@ __global__ __launch_bounds__(256, 2) void fused_bwd_kernel(FusedBwdArgs f) {
             constexpr int IQ = CI / 4, RPI = 256 / IQ, NJ = BM / RPI;
             const int iq = tid % IQ, s0 = tid / IQ;
             float4 xv[NJ];
+            const bool xin = DA || 4 * iq < f.kx;        // !DA: columns past the raw input are 0
 #pragma unroll
             for (int j = 0; j < NJ; ++j) {
                 const int rc = min(m0 + s0 + j * RPI, M - 1);
-                xv[j] = *reinterpret_cast<const float4*>(f.q.data + (size_t)rc * f.q.ld + 4 * iq);
+                xv[j] = xin ? *reinterpret_cast<const float4*>(f.q.data + (size_t)rc * f.q.ld + 4 * iq)
+                            : make_float4(0.f, 0.f, 0.f, 0.f);
             }
 #pragma unroll
             for (int j = 0; j < NJ; ++j) *reinterpret_cast<float4*>(&Xs[(s0 + j * RPI) * XS + 4 * iq]) = xv[j];
@@ -148,7 +157,7 @@ __global__ __launch_bounds__(256, 2) void fused_bwd_kernel(FusedBwdArgs f) {
         __syncthreads();
 
         // ---- dA tile(s) = Zs . W
-        if (a_on) {
+        if (DA && a_on) {
             f32x16 accA[NRT];
 #pragma unroll
             for (int rt = 0; rt < NRT; ++rt)
@@ -206,7 +215,7 @@ __global__ __launch_bounds__(256, 2) void fused_bwd_kernel(FusedBwdArgs f) {
         red[1][w][l32] = a_on ? s2 : 0.0;
     }
     __syncthreads();
-    if (tid < CI) {
+    if (DA && tid < CI) {
         const int ct = tid / 32, lc = tid % 32;
         double a = 0.0, b = 0.0;
 #pragma unroll
@@ -220,7 +229,7 @@ __global__ __launch_bounds__(256, 2) void fused_bwd_kernel(FusedBwdArgs f) {
     }
     if (f.pdb && tid < C) f.pdb[(size_t)blockIdx.x * C + tid] = dbs;
     // ---- dW partial tile(s): waves splitting one tile's rows add theirs in wave order
-    float* part = f.part + (size_t)blockIdx.x * C * CI;
+    float* part = f.part + (size_t)blockIdx.x * C * f.kp;
     if constexpr (WR > 1) {
         if (wsub > 0) {
 #pragma unroll
@@ -240,7 +249,8 @@ __global__ __launch_bounds__(256, 2) void fused_bwd_kernel(FusedBwdArgs f) {
             const int tt = t_base + 4 * u;
             const int c0 = (tt / NIT) * 32, i0 = (tt % NIT) * 32;
 #pragma unroll
-            for (int r = 0; r < 16; ++r) part[(size_t)(c0 + acc_row_of(r, h)) * CI + i0 + l32] = accW[u][r];
+            for (int r = 0; r < 16; ++r)
+                if (DA || i0 + l32 < f.kp) part[(size_t)(c0 + acc_row_of(r, h)) * f.kp + i0 + l32] = accW[u][r];
         }
     }
 }
@@ -248,9 +258,9 @@ __global__ __launch_bounds__(256, 2) void fused_bwd_kernel(FusedBwdArgs f) {
 template <int C, int CI>
 static void launch_fused(dim3 grid, hipStream_t st, const FusedBwdArgs& a) {
     switch (a.x.mode) {
-    case OP_PLAIN: hipLaunchKernelGGL((fused_bwd_kernel<C, CI, OP_PLAIN>), grid, dim3(256), 0, st, a); break;
-    case OP_BNBWD: hipLaunchKernelGGL((fused_bwd_kernel<C, CI, OP_BNBWD>), grid, dim3(256), 0, st, a); break;
-    default: hipLaunchKernelGGL((fused_bwd_kernel<C, CI, OP_POOLBWD>), grid, dim3(256), 0, st, a); break;
+    case OP_PLAIN: hipLaunchKernelGGL((fused_bwd_kernel<C, CI, OP_PLAIN, true>), grid, dim3(256), 0, st, a); break;
+    case OP_BNBWD: hipLaunchKernelGGL((fused_bwd_kernel<C, CI, OP_BNBWD, true>), grid, dim3(256), 0, st, a); break;
+    default: hipLaunchKernelGGL((fused_bwd_kernel<C, CI, OP_POOLBWD, true>), grid, dim3(256), 0, st, a); break;
     }
 }
 
@@ -259,6 +269,16 @@ static void launch_fused_ci(int CI, dim3 grid, hipStream_t st, const FusedBwdArg
     if (CI == 32) launch_fused<C, 32>(grid, st, a);
     else if (CI == 64) launch_fused<C, 64>(grid, st, a);
     else launch_fused<C, 128>(grid, st, a);
+}
+
+// weight gradient only, input width <= 32 (a stack's first layer over raw rows)
+template <int C>
+static void launch_wgrad_only(dim3 grid, hipStream_t st, const FusedBwdArgs& a) {
+    switch (a.x.mode) {
+    case OP_PLAIN: hipLaunchKernelGGL((fused_bwd_kernel<C, 32, OP_PLAIN, false>), grid, dim3(256), 0, st, a); break;
+    case OP_BNBWD: hipLaunchKernelGGL((fused_bwd_kernel<C, 32, OP_BNBWD, false>), grid, dim3(256), 0, st, a); break;
+    default: hipLaunchKernelGGL((fused_bwd_kernel<C, 32, OP_POOLBWD, false>), grid, dim3(256), 0, st, a); break;
+    }
 }
 
 static bool fb_width(int c) { return c == 32 || c == 64 || c == 128; }
@@ -290,7 +310,7 @@ int fused_bwd(const pcs_operand* x, int C, const pcs_operand* q, int CI, const f
     const int G = fused_bwd_grid(M);
     float* part = reinterpret_cast<float*>((reinterpret_cast<uintptr_t>(ws) + 255) & ~uintptr_t(255));
     float* pdb = db ? part + (size_t)G * C * CI : nullptr;
-    FusedBwdArgs a{to_dev_operand(x), to_dev_operand(q), W, ldw, M, dA, ldd, bstats, part, pdb};
+    FusedBwdArgs a{to_dev_operand(x), to_dev_operand(q), W, ldw, M, dA, ldd, bstats, part, pdb, CI, CI};
     const dim3 grid(G);
     auto launch = [=]() {
         if (C == 32) launch_fused_ci<32>(CI, grid, st, a);
@@ -309,6 +329,49 @@ int fused_bwd(const pcs_operand* x, int C, const pcs_operand* q, int CI, const f
     probe_stop(probe, st);
     wgrad_reduce_launch(part, G, (long long)C * CI, dW, pdb, C, db, st);
     return launch_status("fused_bwd");
+}
+
+bool fused_wgrad_ok(int M, int C, int kin, int ldx, const pcs_operand* x) {
+    const int pol = fused_bwd_policy();
+    if (pol == 0 || (pol == 2 && M < (1 << 19))) return false;
+    if (M < 4 * FB_BM || !fb_width(C) || kin < 1 || kin > 32 || ldx % 4 != 0 || ldx < kin) return false;
+    if (!x || x->mode == PCS_OP_BNACT || x->ld % 4 != 0 || x->ld < C) return false;
+    if (x->mode == PCS_OP_POOLBWD && (x->pool_k < 1 || M % x->pool_k != 0)) return false;
+    return x->mode == PCS_OP_PLAIN || x->ldz % 4 == 0;
+}
+
+size_t fused_wgrad_ws_bytes(int M, int C, int kin) {
+    return (size_t)fused_bwd_grid(M) * ((size_t)C * kin + C) * sizeof(float) + 256;
+}
+
+int fused_wgrad(const pcs_operand* x, int C, const float* X, int ldx, int kin, int M, float* dW, float* db, void* ws,
+                size_t ws_bytes, hipStream_t st) {
+    PCS_CHECK_ARG(fused_wgrad_ok(M, C, kin, ldx, x) && X && dW, "fused_wgrad: unsupported C=%d kin=%d M=%d", C, kin, M);
+    PCS_CHECK_ARG(ws && ws_bytes >= fused_wgrad_ws_bytes(M, C, kin), "fused_wgrad: workspace too small");
+    const int G = fused_bwd_grid(M);
+    float* part = reinterpret_cast<float*>((reinterpret_cast<uintptr_t>(ws) + 255) & ~uintptr_t(255));
+    float* pdb = db ? part + (size_t)G * C * kin : nullptr;
+    Operand q{};
+    q.data = X; q.ld = ldx; q.slope = 1.f;
+    FusedBwdArgs a{to_dev_operand(x), q, nullptr, 0, M, nullptr, 0, nullptr, part, pdb, kin, kin};
+    const dim3 grid(G);
+    auto launch = [=]() {
+        if (C == 32) launch_wgrad_only<32>(grid, st, a);
+        else if (C == 64) launch_wgrad_only<64>(grid, st, a);
+        else launch_wgrad_only<128>(grid, st, a);
+    };
+    int probe = -1;
+    if (probe_enabled()) {
+        char nm[80];
+        snprintf(nm, sizeof nm, "pcs::fused_bwd_kernel<%d, 32, %d, false>", C, x->mode);
+        const double xb = x->mode == PCS_OP_POOLBWD ? 4.0 * M * C + 5.0 * (double)(M / x->pool_k) * C
+                                                   : 4.0 * M * C * (x->mode == PCS_OP_BNBWD ? 2 : 1);
+        probe = probe_start(nm, 2.0 * M * C * kin, xb + 4.0 * M * kin, st, launch);
+    }
+    launch();
+    probe_stop(probe, st);
+    wgrad_reduce_launch(part, G, (long long)C * kin, dW, pdb, C, db, st);
+    return launch_status("fused_wgrad");
 }
 
 }  // namespace pcs

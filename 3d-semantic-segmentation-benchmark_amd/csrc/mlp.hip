@@ -911,7 +911,8 @@ static void gemm_tile(int M, int N, bool bwd, int* bm, int* bn) {
     static const T big[] = {{128, 128}, {64, 128}, {64, 64}, {32, 128}};
     static const T mid[] = {{128, 64}, {64, 64}};
     static const T mid64[] = {{64, 64}, {128, 64}};
-    // Data-gradient tiles by regime (same-box A/B, round 1): the thin, HBM-latency-bound
+    // Data-gradient tiles by regime (same-box A/B, round 1; round 2 re-check: 64 x 128 on the
+    // 128-wide PointNet++ layers, one A read instead of two, made the step 8 % slower): the thin, HBM-latency-bound
     // layers (PointNet++, EdgeConv) run best on 64 x 64 tiles (4 blocks per CU, more loads in
     // flight: PointNet++ step -1 %); the big MFMA-bound ones (DGCNN conv5-7: N >= 256 over
     // >= 64K rows) on the wide list despite its register pressure (DGCNN step -2 %).

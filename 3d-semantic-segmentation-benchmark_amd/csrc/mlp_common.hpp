@@ -183,5 +183,11 @@ int fused_bwd_grid(int M);
 size_t fused_bwd_ws_bytes(int M, int C, int CI);
 int fused_bwd(const pcs_operand* x, int C, const pcs_operand* q, int CI, const float* W, int ldw, int M, float* dA,
               int ldd, double* bstats, float* dW, float* db, void* ws, size_t ws_bytes, hipStream_t st);
+// the same kernel, weight gradient only, for a stack's first layer over raw rows X (M x kin,
+// stride ldx; kin <= 32): dW (C x kin) and db += ...
+bool fused_wgrad_ok(int M, int C, int kin, int ldx, const pcs_operand* x);
+size_t fused_wgrad_ws_bytes(int M, int C, int kin);
+int fused_wgrad(const pcs_operand* x, int C, const float* X, int ldx, int kin, int M, float* dW, float* db, void* ws,
+                size_t ws_bytes, hipStream_t st);
 
 }  // namespace pcs

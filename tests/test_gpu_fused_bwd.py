@@ -47,11 +47,13 @@ def _fp64_stack(mod, x, pool_k):
     yield a
 
 
-def _run(widths, cin, B, H, W, pool_k, seed):
+def _run(widths, cin, B, H, W, pool_k, seed, need_dx=True):
+    """need_dx=False: the stack's input takes no gradient (PointNet++ SA1's grouped rows), so
+    its first layer runs the weight-gradient-only form."""
     torch.manual_seed(seed)
     mod = pcseg.MiniPointNet(cin, widths).cuda().train()
     x = torch.randn(B, cin, H, W, dtype=torch.float32)
-    xg = x.cuda().requires_grad_()
+    xg = x.cuda().requires_grad_(need_dx)
     if pool_k:
         rows = xg.permute(0, 2, 3, 1).reshape(B * H * W, cin)
         out = mod.forward_rows(pcseg.engine.pad_rows(rows), cin, pool_k=pool_k)
@@ -62,7 +64,7 @@ def _run(widths, cin, B, H, W, pool_k, seed):
     torch.cuda.synchronize()
     grads = [(c.weight.grad.view(c.weight.shape[0], -1).cpu(), c.bias.grad.cpu(), n.weight.grad.cpu(),
               n.bias.grad.cpu()) for c, n in zip(mod.conv, mod.batch)]
-    return mod, x, gout, grads, xg.grad.cpu()
+    return mod, x, gout, grads, xg.grad.cpu() if need_dx else None
 
 
 def _rel(a, b):
@@ -80,9 +82,9 @@ CASES = [
 ]
 
 
-def check_vs_fp64(cin, widths, pool_k, B=2, H=80, W=32):
+def check_vs_fp64(cin, widths, pool_k, B=2, H=80, W=32, need_dx=True):
     """M = B*H*W rows (default 5120 = 80 row tiles)."""
-    mod, x, gout, grads, gx = _run(widths, cin, B, H, W, pool_k, seed=cin + len(widths))
+    mod, x, gout, grads, gx = _run(widths, cin, B, H, W, pool_k, seed=cin + len(widths), need_dx=need_dx)
     xd = x.double().requires_grad_()
     it = _fp64_stack(mod, xd, pool_k)
     params = [next(it) for _ in widths]
@@ -96,7 +98,8 @@ def check_vs_fp64(cin, widths, pool_k, B=2, H=80, W=32):
         assert _rel(dbe, ref[3].grad) < 1e-3, (l, 'dbeta', _rel(dbe, ref[3].grad))
         # pre-BN conv bias: analytically zero under training-mode BN; its fp32 value is noise
         assert float((db.double() - ref[1].grad).abs().max()) < 1e-3 * scale, (l, 'db')
-    assert _rel(gx, xd.grad) < 1e-3, ('dX', _rel(gx, xd.grad))
+    if need_dx:
+        assert _rel(gx, xd.grad) < 1e-3, ('dX', _rel(gx, xd.grad))
 
 
 def test_fused_backward_width_sweep_vs_fp64():
@@ -111,8 +114,9 @@ def test_fused_backward_width_sweep_vs_fp64():
 
 def test_fused_backward_default_policy_sa1_sized():
     """SA1 of PointNet++ at batch 16: 16 x 1024 centroids x 32 neighbours = 2^19 rows, widths
-    9 -> 32 -> 32 -> 64, pooled over 32 -- the layers the default policy fuses."""
-    check_vs_fp64(9, [32, 32, 64], 32, B=16, H=1024, W=32)
+    9 -> 32 -> 32 -> 64, pooled over 32 -- the layers the default policy fuses; the input takes
+    no gradient, as in the model, so the first layer runs the weight-gradient-only form."""
+    check_vs_fp64(9, [32, 32, 64], 32, B=16, H=1024, W=32, need_dx=False)
 
 
 def check_ragged_rows():
@@ -143,6 +147,9 @@ if __name__ == '__main__':        # the width sweep, run by test_fused_backward_
     for case in CASES:
         check_vs_fp64(*case)
         print('ok', case, flush=True)
+        if case[0] <= 32:                       # first layer: weight gradient only
+            check_vs_fp64(*case, need_dx=False)
+            print('ok (no dX)', case, flush=True)
     check_ragged_rows()
     check_bitwise_reproducible()
     print('fused sweep ok')
