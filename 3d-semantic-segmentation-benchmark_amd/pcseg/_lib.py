@@ -13,7 +13,8 @@ import threading
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, 'libpcseg.so')
+# PCS_LIB: another build of the library (A/B scripts only)
+LIB_PATH = os.environ.get('PCS_LIB') or os.path.join(_HERE, 'libpcseg.so')
 
 P = ctypes.c_void_p
 I32 = ctypes.c_int
