@@ -110,51 +110,72 @@ __global__ __launch_bounds__(256, 2) void fused_bwd_kernel(FusedBwdArgs f) {
 
     const int M = f.M;
     const int tiles = (M + BM - 1) / BM;
+    // staging: thread = one dZ channel quad over rows r0 + j*RPP (one coefficient quad) and
+    // one raw-input quad over rows s0 + j*RPI
+    constexpr int CQ = C / 4, RPP = 256 / CQ, NJ = BM / RPP;
+    constexpr int IQ = CI / 4, RPI = 256 / IQ, NJX = BM / RPI;
+    // PF: the narrow layers (SA1-sized, HBM-bound) hold the NEXT tile's raw loads in registers
+    // while the current tile's MFMAs run; the wide ones stage in chunks after the barrier
+    constexpr bool PF = C + CI <= 96;
+    constexpr int CH = PF ? NJ : (NJ < 4 ? NJ : 4);      // rows in flight per chunk
+    const int cq = tid % CQ, r0 = tid / CQ;
+    const int iq = tid % IQ, s0 = tid / IQ;
+    const bool xin = DA || 4 * iq < f.kx;                // !DA: columns past the raw input are 0
+    Quad qd;
+    load_quad<XM>(f.x, 4 * cq, C, qd);
+    float4 pv[CH], pz[CH], px[NJX];
+    unsigned pa[CH];
+    auto issue_dz = [&](int m0, int j0) __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < CH; ++j)
+            load_raw<XM>(f.x, min(m0 + r0 + (j0 + j) * RPP, M - 1), 4 * cq, pv[j], pz[j], pa[j]);
+    };
+    auto commit_dz = [&](int m0, int j0) __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+            const int r = r0 + (j0 + j) * RPP;
+            float4 o = xform4<XM>(f.x, pv[j], pz[j], pa[j], min(m0 + r, M - 1), qd, 4 * cq, C);
+            if (m0 + r >= M) o = make_float4(0.f, 0.f, 0.f, 0.f);
+            float* d = &Zs[r * ZS + 4 * cq];
+            d[0] = o.x; d[1] = o.y; d[2] = o.z; d[3] = o.w;
+        }
+    };
+    auto issue_x = [&](int m0) __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < NJX; ++j) {
+            const int rc = min(m0 + s0 + j * RPI, M - 1);
+            px[j] = xin ? *reinterpret_cast<const float4*>(f.q.data + (size_t)rc * f.q.ld + 4 * iq)
+                        : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    };
+    auto commit_x = [&]() __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < NJX; ++j) *reinterpret_cast<float4*>(&Xs[(s0 + j * RPI) * XS + 4 * iq]) = px[j];
+    };
+    if (PF && (int)blockIdx.x < tiles) {
+        issue_dz((int)blockIdx.x * BM, 0);
+        issue_x((int)blockIdx.x * BM);
+    }
     for (int t = blockIdx.x; t < tiles; t += gridDim.x) {
         const int m0 = t * BM;
         __syncthreads();                       // the previous tile's reads of Zs / Xs are done
-        // ---- stage dZ: thread = one channel quad over rows r0 + j*RPP (one coefficient quad)
-        {
-            constexpr int CQ = C / 4, RPP = 256 / CQ, NJ = BM / RPP;
-            constexpr int CH = NJ < 4 ? NJ : 4;          // rows in flight per chunk (register budget)
-            const int cq = tid % CQ, r0 = tid / CQ;
-            Quad qd;
-            load_quad<XM>(f.x, 4 * cq, C, qd);
+        if constexpr (PF) {
+            commit_dz(m0, 0);
+            commit_x();
+        } else {
 #pragma unroll
             for (int j0 = 0; j0 < NJ; j0 += CH) {
-                float4 v[CH], z[CH];
-                unsigned a[CH];
-#pragma unroll
-                for (int j = 0; j < CH; ++j) {
-                    const int rc = min(m0 + r0 + (j0 + j) * RPP, M - 1);
-                    load_raw<XM>(f.x, rc, 4 * cq, v[j], z[j], a[j]);
-                }
-#pragma unroll
-                for (int j = 0; j < CH; ++j) {
-                    const int r = r0 + (j0 + j) * RPP;
-                    float4 o = xform4<XM>(f.x, v[j], z[j], a[j], min(m0 + r, M - 1), qd, 4 * cq, C);
-                    if (m0 + r >= M) o = make_float4(0.f, 0.f, 0.f, 0.f);
-                    float* d = &Zs[r * ZS + 4 * cq];
-                    d[0] = o.x; d[1] = o.y; d[2] = o.z; d[3] = o.w;
-                }
+                issue_dz(m0, j0);
+                commit_dz(m0, j0);
             }
-        }
-        // ---- stage the previous layer's raw Z (float4 rows)
-        {
-            constexpr int IQ = CI / 4, RPI = 256 / IQ, NJ = BM / RPI;
-            const int iq = tid % IQ, s0 = tid / IQ;
-            float4 xv[NJ];
-            const bool xin = DA || 4 * iq < f.kx;        // !DA: columns past the raw input are 0
-#pragma unroll
-            for (int j = 0; j < NJ; ++j) {
-                const int rc = min(m0 + s0 + j * RPI, M - 1);
-                xv[j] = xin ? *reinterpret_cast<const float4*>(f.q.data + (size_t)rc * f.q.ld + 4 * iq)
-                            : make_float4(0.f, 0.f, 0.f, 0.f);
-            }
-#pragma unroll
-            for (int j = 0; j < NJ; ++j) *reinterpret_cast<float4*>(&Xs[(s0 + j * RPI) * XS + 4 * iq]) = xv[j];
+            issue_x(m0);
+            commit_x();
         }
         __syncthreads();
+        if (PF && t + (int)gridDim.x < tiles) {          // next tile's loads fly under this tile's MFMAs
+            issue_dz(m0 + (int)gridDim.x * BM, 0);
+            issue_x(m0 + (int)gridDim.x * BM);
+        }
 
         // ---- dA tile(s) = Zs . W
         if (DA && a_on) {
@@ -293,13 +314,16 @@ bool fused_bwd_ok(int M, int C, int CI, int ldw, const pcs_operand* x, const pcs
     return q->data && q->ld % 4 == 0 && q->ld >= CI && q->s && q->t && q->mean && q->inv;
 }
 
-int fused_bwd_grid(int M) {
+// persistent grid: 2 blocks per CU, 3 for the narrow prefetching layers (<= 194 VGPRs) and 4
+// for the weight-gradient-only form (<= 128 VGPRs): more tiles' loads in flight per CU
+int fused_bwd_grid(int M, int C, int CI, bool da) {
     const int tiles = (M + FB_BM - 1) / FB_BM;
-    return std::min(tiles, 256 * FB_BLOCKS_PER_CU);
+    const int per_cu = !da ? 4 : (C + CI <= 96 ? 3 : FB_BLOCKS_PER_CU);
+    return std::min(tiles, 256 * per_cu);
 }
 
 size_t fused_bwd_ws_bytes(int M, int C, int CI) {
-    return (size_t)fused_bwd_grid(M) * ((size_t)C * CI + C) * sizeof(float) + 256;
+    return (size_t)fused_bwd_grid(M, C, CI, true) * ((size_t)C * CI + C) * sizeof(float) + 256;
 }
 
 int fused_bwd(const pcs_operand* x, int C, const pcs_operand* q, int CI, const float* W, int ldw, int M, float* dA,
@@ -307,7 +331,7 @@ int fused_bwd(const pcs_operand* x, int C, const pcs_operand* q, int CI, const f
     PCS_CHECK_ARG(fused_bwd_ok(M, C, CI, ldw, x, q), "fused_bwd: unsupported shape C=%d CI=%d M=%d", C, CI, M);
     PCS_CHECK_ARG(dA && ldd >= CI && ldd % 4 == 0 && bstats && dW && W, "fused_bwd: bad output arguments");
     PCS_CHECK_ARG(ws && ws_bytes >= fused_bwd_ws_bytes(M, C, CI), "fused_bwd: workspace too small");
-    const int G = fused_bwd_grid(M);
+    const int G = fused_bwd_grid(M, C, CI, true);
     float* part = reinterpret_cast<float*>((reinterpret_cast<uintptr_t>(ws) + 255) & ~uintptr_t(255));
     float* pdb = db ? part + (size_t)G * C * CI : nullptr;
     FusedBwdArgs a{to_dev_operand(x), to_dev_operand(q), W, ldw, M, dA, ldd, bstats, part, pdb, CI, CI};
@@ -341,14 +365,14 @@ bool fused_wgrad_ok(int M, int C, int kin, int ldx, const pcs_operand* x) {
 }
 
 size_t fused_wgrad_ws_bytes(int M, int C, int kin) {
-    return (size_t)fused_bwd_grid(M) * ((size_t)C * kin + C) * sizeof(float) + 256;
+    return (size_t)fused_bwd_grid(M, C, 32, false) * ((size_t)C * kin + C) * sizeof(float) + 256;
 }
 
 int fused_wgrad(const pcs_operand* x, int C, const float* X, int ldx, int kin, int M, float* dW, float* db, void* ws,
                 size_t ws_bytes, hipStream_t st) {
     PCS_CHECK_ARG(fused_wgrad_ok(M, C, kin, ldx, x) && X && dW, "fused_wgrad: unsupported C=%d kin=%d M=%d", C, kin, M);
     PCS_CHECK_ARG(ws && ws_bytes >= fused_wgrad_ws_bytes(M, C, kin), "fused_wgrad: workspace too small");
-    const int G = fused_bwd_grid(M);
+    const int G = fused_bwd_grid(M, C, 32, false);
     float* part = reinterpret_cast<float*>((reinterpret_cast<uintptr_t>(ws) + 255) & ~uintptr_t(255));
     float* pdb = db ? part + (size_t)G * C * kin : nullptr;
     Operand q{};

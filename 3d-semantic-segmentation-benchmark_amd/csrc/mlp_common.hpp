@@ -179,7 +179,7 @@ void wgrad_reduce_launch(const float* part, int splits, long long nk, float* dW,
 // input width; q = the previous layer's pre-BN Z with its BN coefficients (s, t, mean, inv, act)
 int fused_bwd_policy();
 bool fused_bwd_ok(int M, int C, int CI, int ldw, const pcs_operand* x, const pcs_operand* q);
-int fused_bwd_grid(int M);
+int fused_bwd_grid(int M, int C, int CI, bool da);   // blocks = BN-backward partials
 size_t fused_bwd_ws_bytes(int M, int C, int CI);
 int fused_bwd(const pcs_operand* x, int C, const pcs_operand* q, int CI, const float* W, int ldw, int M, float* dA,
               int ldd, double* bstats, float* dW, float* db, void* ws, size_t ws_bytes, hipStream_t st);
