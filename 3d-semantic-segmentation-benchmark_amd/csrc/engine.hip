@@ -300,6 +300,8 @@ PCS_API int pcs_mlp_forward(const float* X, int ldx, int kin, int M, pcs_mlp_lay
                             float* out, int ldo, uint8_t* arg, void* ws, size_t ws_bytes, void* stream) {
     if (int e = check_layers(M, kin, ldx, layers, nl, pool_k, "pcs_mlp_forward")) return e;
     PCS_CHECK_ARG(X && out && (!pool_k || arg), "pcs_mlp_forward: null pointer");
+    PCS_CHECK_ARG(layers[nl - 1].drop_p == 0.0 || (!pool_k && layers[nl - 1].drop_p > 0.0 && layers[nl - 1].drop_p < 1.0),
+                  "pcs_mlp_forward: drop_p=%g (un-pooled top layer only, 0 <= p < 1)", layers[nl - 1].drop_p);
     const int CT = (int)layers[nl - 1].cout;
     if (ldo == 0) ldo = CT;
     PCS_CHECK_ARG(!pool_k ? (ldo >= CT && ldo % 4 == 0) : ldo == CT,
@@ -349,6 +351,9 @@ PCS_API int pcs_mlp_forward(const float* X, int ldx, int kin, int M, pcs_mlp_lay
     if (pool_k)
         return pcs_pool_fwd(T.Z, C, M / pool_k, pool_k, T.coef, T.coef + C, (int)T.act, (float)T.slope, out, arg,
                             stream);
+    if (T.drop_p > 0.0)
+        return bn_act_dropout(T.Z, C, M, C, T.coef, T.coef + C, (int)T.act, (float)T.slope, out, ldo, T.drop_p,
+                              (long long)T.drop_seed, st);
     return pcs_bn_act(T.Z, C, M, C, T.coef, T.coef + C, (int)T.act, (float)T.slope, out, ldo, stream);
 }
 

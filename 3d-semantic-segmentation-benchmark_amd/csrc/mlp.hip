@@ -807,6 +807,56 @@ __global__ __launch_bounds__(256) void bn_act_kernel(const float* __restrict__ Z
     }
 }
 
+// inverted-dropout keep test of element i (counter-based: splitmix64 finaliser of seed + i*phi)
+__device__ __forceinline__ bool dropout_keep(unsigned long long seed, unsigned long long i, unsigned thr) {
+    unsigned long long z = seed + i * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    return (unsigned)(z >> 32) >= thr;
+}
+
+// bn_act with the training-mode dropout that follows it fused in (no mask stored)
+__global__ __launch_bounds__(256) void bn_act_drop_kernel(const float* __restrict__ Z, int ldz, int total4, int nq,
+                                                          const float* __restrict__ s, const float* __restrict__ t,
+                                                          int act, float slope, float* __restrict__ out, int ldo,
+                                                          unsigned long long seed, unsigned thr, float scale) {
+    for (int e = blockIdx.x * 256 + threadIdx.x; e < total4; e += gridDim.x * 256) {
+        const int r = e / nq;
+        const int c = 4 * (e - r * nq);
+        const F4 z = ld4(Z + (size_t)r * ldz + c);
+        const F4 sv = ld4(s + c), tv = ld4(t + c);
+        const unsigned long long i0 = (unsigned long long)r * (4ull * nq) + c;
+        F4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float a = act_f(z.v[j] * sv.v[j] + tv.v[j], act, slope);
+            o.v[j] = dropout_keep(seed, i0 + j, thr) ? a * scale : 0.f;
+        }
+        st4(out + (size_t)r * ldo + c, o);
+    }
+}
+
+__global__ __launch_bounds__(256) void dropout_bwd_kernel(const float* __restrict__ g, int ldg, int total4, int nq,
+                                                          float* __restrict__ gi, int ldi, unsigned long long seed,
+                                                          unsigned thr, float scale) {
+    for (int e = blockIdx.x * 256 + threadIdx.x; e < total4; e += gridDim.x * 256) {
+        const int r = e / nq;
+        const int c = 4 * (e - r * nq);
+        const F4 v = ld4(g + (size_t)r * ldg + c);
+        const unsigned long long i0 = (unsigned long long)r * (4ull * nq) + c;
+        F4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o.v[j] = dropout_keep(seed, i0 + j, thr) ? v.v[j] * scale : 0.f;
+        st4(gi + (size_t)r * ldi + c, o);
+    }
+}
+
+static unsigned dropout_thr(double p) {
+    const double v = p * 4294967296.0;
+    return v >= 4294967295.0 ? 4294967295u : (unsigned)v;
+}
+
 void bn_finalize_launch(const double* part, int nb, int N, long long M, const float* gamma, const float* beta,
                         float eps, float momentum, float* run_mean, float* run_var, float* s, float* t, float* mean,
                         float* invstd, long long* nbt, hipStream_t st) {
@@ -1329,6 +1379,32 @@ PCS_API int pcs_pool_bwd_reduce(const float* dpool, const uint8_t* arg, const fl
     hipLaunchKernelGGL(pool_bwd_reduce_kernel, grid, dim3(256), 0, as_stream(stream), dpool, arg, Z, N, (int)G, K, s,
                        t, mean, inv, act, eff_slope(act, slope), gpb, part);
     return launch_status("pcs_pool_bwd_reduce");
+}
+
+int pcs::bn_act_dropout(const float* Z, int ldz, int M, int N, const float* s, const float* t, int act, float slope,
+                        float* out, int ldo, double p, long long seed, hipStream_t st) {
+    PCS_CHECK_ARG(M >= 0 && N >= 4 && N % 4 == 0 && ldz % 4 == 0 && ldo % 4 == 0 && p > 0.0 && p < 1.0,
+                  "bn_act_dropout: bad sizes or p=%g", p);
+    const long long total = (long long)M * N / 4;
+    PCS_CHECK_ARG(total < (1ll << 31), "bn_act_dropout: too many elements");
+    if (total == 0) return 0;
+    hipLaunchKernelGGL(bn_act_drop_kernel, dim3(ew_grid(total)), dim3(256), 0, st, Z, ldz, (int)total, N / 4, s, t, act,
+                       eff_slope(act, slope), out, ldo, (unsigned long long)seed, dropout_thr(p),
+                       (float)(1.0 / (1.0 - p)));
+    return launch_status("bn_act_dropout");
+}
+
+PCS_API int pcs_dropout_bwd(const float* gout, int ldg, int M, int N, double p, int64_t seed, float* gin, int ldi,
+                            void* stream) {
+    PCS_CHECK_ARG(M >= 0 && N >= 4 && N % 4 == 0 && ldg % 4 == 0 && ldi % 4 == 0 && p > 0.0 && p < 1.0,
+                  "pcs_dropout_bwd: bad sizes or p=%g", p);
+    PCS_CHECK_ARG(gout && gin, "pcs_dropout_bwd: null pointer");
+    const long long total = (long long)M * N / 4;
+    PCS_CHECK_ARG(total < (1ll << 31), "pcs_dropout_bwd: too many elements");
+    if (total == 0) return 0;
+    hipLaunchKernelGGL(dropout_bwd_kernel, dim3(ew_grid(total)), dim3(256), 0, as_stream(stream), gout, ldg, (int)total,
+                       N / 4, gin, ldi, (unsigned long long)seed, dropout_thr(p), (float)(1.0 / (1.0 - p)));
+    return launch_status("pcs_dropout_bwd");
 }
 
 PCS_API int pcs_bn_act(const float* Z, int ldz, int M, int N, const float* s, const float* t, int act, float slope,

@@ -175,6 +175,9 @@ Operand to_dev_operand(const pcs_operand* o);
 // dW[e] += sum_s part[s][e] (e < nk), db[e] += sum_s pdb[s][e] (e < N; pdb/db nullable): fixed order
 void wgrad_reduce_launch(const float* part, int splits, long long nk, float* dW, const float* pdb, int N, float* db,
                          hipStream_t st);
+// out = dropout_p(act(Z*s + t)) (pcs_mlp_layer.drop_p / drop_seed of a stack's top layer)
+int bn_act_dropout(const float* Z, int ldz, int M, int N, const float* s, const float* t, int act, float slope,
+                   float* out, int ldo, double p, long long seed, hipStream_t st);
 // fused data + weight gradient of one thin inner layer (fused_bwd.hip): C = its width, CI = its
 // input width; q = the previous layer's pre-BN Z with its BN coefficients (s, t, mean, inv, act)
 int fused_bwd_policy();

@@ -161,7 +161,7 @@ def _f32(shape, dev):
 
 
 # pcs_mlp_layer (include/pcseg.h): 24 little-endian 8-byte slots
-_REC = struct.Struct('<QqqqQQQQQQddqqdQQQQQQqqq')
+_REC = struct.Struct('<QqqqQQQQQQddqqdQQQQQQdqq')   # ... dW db dgamma dbeta drop_p drop_seed reserved
 _ws_cache: dict = {}
 
 
@@ -228,7 +228,7 @@ class SharedMLPFn(torch.autograd.Function):
     record per layer."""
 
     @staticmethod
-    def forward(ctx, X, Kin, pool_K, acts, bns, dest, *params):
+    def forward(ctx, X, Kin, pool_K, acts, bns, dest, drop, *params):
         dev = X.device
         st = stream_ptr(dev)
         lib = load()
@@ -269,7 +269,10 @@ class SharedMLPFn(torch.autograd.Function):
                           Zbuf.data_ptr() + 4 * M * off, coef.data_ptr() + 16 * off))
             off += C
             cin = C
-        recs = b''.join(_REC.pack(*f, 0, 0, 0, 0, 0, 0, 0) for f in fixed)
+        # drop = (p, seed): the training-mode Dropout after the stack, fused into its output
+        dp, dseed = drop if drop is not None else (0.0, 0)
+        recs = b''.join(_REC.pack(*f, 0, 0, 0, 0, dp if li == nl - 1 else 0.0, dseed if li == nl - 1 else 0, 0)
+                        for li, f in enumerate(fixed))
         CL = couts[-1]
         ldo = 0
         if pool_K:
@@ -302,6 +305,7 @@ class SharedMLPFn(torch.autograd.Function):
                 off += C
         ctx.save_for_backward(X, Zbuf, coef, *Wms, *([arg] if arg is not None else []))
         ctx.meta = (Kin, pool_K, nl, fixed, couts, arg is not None)
+        ctx.drop = drop
         ctx.params = params
         return out
 
@@ -321,6 +325,11 @@ class SharedMLPFn(torch.autograd.Function):
         if not (gout.dim() == 2 and gout.stride(1) == 1 and gout.stride(0) % 4 == 0 and gout.data_ptr() % 16 == 0
                 and (pool_K == 0 or gout.is_contiguous())):
             gout = gout.contiguous()
+        if ctx.drop is not None:       # the fused dropout's backward: the mask is recomputed from its seed
+            g2 = _f32((M, couts[-1]), dev)
+            call('pcs_dropout_bwd', ptr(gout), gout.stride(0), M, couts[-1], float(ctx.drop[0]), int(ctx.drop[1]),
+                 ptr(g2), couts[-1], st)
+            gout = g2
         ldg = gout.stride(0)
         recs = b''.join(_REC.pack(*f, _nz(grad_target(params[4 * li])), _nz(grad_target(params[4 * li + 1])),
                                   _nz(grad_target(params[4 * li + 2])), _nz(grad_target(params[4 * li + 3])), 0, 0, 0)
@@ -343,7 +352,7 @@ class SharedMLPFn(torch.autograd.Function):
                 t.record_stream(lane)
             _queue_lane_join(dev)
         notify_grad_ready(params)
-        return (dX, None, None, None, None, None, *([None] * len(params)))
+        return (dX, None, None, None, None, None, None, *([None] * len(params)))
 
 
 def _edge_ws(B, N, C, Cout, backward, dev):
@@ -473,11 +482,13 @@ def _rows_ok(x: torch.Tensor) -> bool:
 
 
 def shared_mlp(x_rows: torch.Tensor, kin: int, convs, bns, act='relu', slope=0.0,
-               pool_k: int = 0, out: torch.Tensor | None = None) -> torch.Tensor:
+               pool_k: int = 0, out: torch.Tensor | None = None, dropout: tuple | None = None) -> torch.Tensor:
     """Run a conv/BN/act stack on rows.  x_rows (M, W) with `kin` logical channels, W % 4 == 0,
     dense or a column block of a wider buffer (row stride >= W).  `act` / `slope` are one value
     for every layer or a sequence with one per layer ('relu', 'lrelu', 'none').  `out`: an
-    (M, cout) row block (storage_alias) the un-pooled activation is written into."""
+    (M, cout) row block (storage_alias) the un-pooled activation is written into.  `dropout` =
+    (p, seed): a training-mode nn.Dropout(p) after the stack, fused into its output
+    (pcs_mlp_layer.drop_p; backward pcs_dropout_bwd recomputes the mask from the seed)."""
     if not x_rows.is_cuda:
         raise RuntimeError('pcseg ops run only on the GPU (no CPU fallback); got a CPU tensor')
     if not _rows_ok(x_rows):
@@ -493,7 +504,9 @@ def shared_mlp(x_rows: torch.Tensor, kin: int, convs, bns, act='relu', slope=0.0
     params = []
     for conv, bn in zip(convs, bns):
         params += [conv.weight, conv.bias, bn.weight, bn.bias]
-    return SharedMLPFn.apply(x_rows, kin, pool_k, acts, list(bns), None if out is None else (out,), *params)
+    if dropout is not None and (pool_k or not 0.0 < float(dropout[0]) < 1.0):
+        raise ValueError('shared_mlp: dropout needs an un-pooled output and 0 < p < 1')
+    return SharedMLPFn.apply(x_rows, kin, pool_k, acts, list(bns), None if out is None else (out,), dropout, *params)
 
 
 class RowLinearFn(torch.autograd.Function):

@@ -193,8 +193,14 @@ def _seq_rows(x_rows: torch.Tensor, seq: nn.Sequential, kin: int | None = None,
               out: torch.Tensor | None = None) -> torch.Tensor:
     """Conv1d(bias=False) -> BN1d -> LeakyReLU [-> Dropout] on rows (HIP shared-MLP engine);
     `out`: a row block the activation is written into (no Dropout after it)."""
-    y = shared_mlp(x_rows, kin or x_rows.shape[1], [seq[0]], [seq[1]], 'lrelu', seq[2].negative_slope, 0, out=out)
-    if len(seq) > 3:
+    drop = None
+    if len(seq) > 3 and seq[3].training and 0.0 < seq[3].p < 1.0 and out is None:
+        # training-mode Dropout fused into the stack's output (one 64-bit mask seed per call,
+        # from torch's CPU generator: reproducible under torch.manual_seed, no device sync)
+        drop = (float(seq[3].p), int(torch.randint(0, 2 ** 62, (1,)).item()))
+    y = shared_mlp(x_rows, kin or x_rows.shape[1], [seq[0]], [seq[1]], 'lrelu', seq[2].negative_slope, 0, out=out,
+                   dropout=drop)
+    if len(seq) > 3 and drop is None:
         y = seq[3](y)
     return y
 

@@ -194,6 +194,14 @@ int pcs_pool_bwd_reduce(const float* dpool, const uint8_t* arg, const float* Z,
                         int N, long long G, int K, const float* s,
                         const float* t, const float* mean, const float* inv,
                         int act, float slope, double* part, void* stream);
+/* nn.Dropout(p) in training mode after a stack's activation (dgcnn.py:206-207 conv6 /
+ * conv7): element (r, c) of an M x N output is kept when a counter-based hash of
+ * (seed, r*N + c) clears p (same Bernoulli(1-p) keep / 1/(1-p) scale as torch's, a
+ * different random stream); the forward is fused into the stack's output (drop_p /
+ * drop_seed of its top layer), the mask is recomputed here, never stored:
+ * gin (ldi) = gout (ldg) * keep / (1 - p). */
+int pcs_dropout_bwd(const float* gout, int ldg, int M, int N, double p, int64_t seed,
+                    float* gin, int ldi, void* stream);
 /* out (M x N, ldo) = act(Z*s + t) */
 int pcs_bn_act(const float* Z, int ldz, int M, int N, const float* s,
                const float* t, int act, float slope, float* out, int ldo,
@@ -220,7 +228,9 @@ typedef struct pcs_mlp_layer {
     int64_t use_batch, act; double slope;
     float* Z; float* coef;
     float* dW; float* db; float* dgamma; float* dbeta;
-    int64_t reserved[3];
+    double drop_p;        /* top layer, un-pooled: inverted dropout of the output (0 = none) */
+    int64_t drop_seed;    /* its mask: pcs_dropout_keep(seed, row * cout + col) */
+    int64_t reserved;
 } pcs_mlp_layer;
 
 /* workspace bytes of pcs_mlp_forward (backward = 0) or pcs_mlp_backward (1) */

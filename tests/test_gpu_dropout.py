@@ -1,0 +1,75 @@
+"""Training-mode Dropout fused into a shared-MLP stack's output (DGCNN conv6 / conv7,
+reference models/dgcnn/dgcnn.py:196-207: Conv1d -> BatchNorm1d -> LeakyReLU -> Dropout).
+
+The mask comes from a counter-based hash of (seed, element) instead of torch's Philox
+stream, so it is checked by its properties: every output is either 0 or exactly
+activation / (1 - p); the kept fraction is 1 - p; one seed gives one mask, another seed a
+different one; and the backward (pcs_dropout_bwd, mask recomputed) equals the stack's
+backward fed with the masked, scaled gradient -- bitwise, as the engine is deterministic."""
+import pytest
+import torch
+import torch.nn as nn
+
+import pcseg
+from pcseg.engine import shared_mlp
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda'
+
+
+def _stack(cin=64, cout=128, seed=0):
+    torch.manual_seed(seed)
+    return nn.Sequential(nn.Conv1d(cin, cout, 1, bias=False), nn.BatchNorm1d(cout),
+                         nn.LeakyReLU(negative_slope=0.2)).to(DEV).train()
+
+
+def _run(seq, x, dropout):
+    return shared_mlp(x, x.shape[1], [seq[0]], [seq[1]], 'lrelu', 0.2, 0, dropout=dropout)
+
+
+@pytest.mark.parametrize('p', [0.5, 0.2])
+def test_fused_dropout_forward_properties(p):
+    seq = _stack()
+    x = torch.randn(65536, 64, device=DEV)
+    y0 = _run(seq, x, None).detach()
+    y = _run(seq, x, (p, 1234)).detach()
+    scale = torch.tensor(1.0 / (1.0 - p), dtype=torch.float32)
+    kept = y != 0
+    assert torch.equal(y[kept], y0[kept] * scale.to(DEV))
+    frac = float(kept.float().mean())
+    assert abs(frac - (1.0 - p)) < 0.005, frac
+    again = _run(seq, x, (p, 1234)).detach()
+    assert torch.equal(y, again)
+    other = _run(seq, x, (p, 99)).detach()
+    assert not torch.equal(y != 0, other != 0)
+
+
+def test_fused_dropout_backward_matches_masked_gradient():
+    p, seed = 0.5, 777
+    seq_a, seq_b = _stack(seed=3), _stack(seed=3)
+    x = torch.randn(32768, 64, device=DEV)
+    g = torch.randn(32768, 128, device=DEV)
+    y0 = _run(seq_b, x, None)
+    y = _run(seq_a, x, (p, seed))
+    kept = ((y != 0) | (y0 == 0)).float()
+    y.backward(g)
+    y0.backward(g * kept * 2.0)
+    torch.cuda.synchronize()
+    for a, b in zip(seq_a.parameters(), seq_b.parameters()):
+        assert torch.equal(a.grad, b.grad)
+
+
+def test_dgcnn_head_uses_fused_dropout():
+    """DGCNNWithColor in training mode runs its conv6 / conv7 dropout inside the engine (no
+    torch dropout kernel), and a seeded step is reproducible."""
+    def step():
+        torch.manual_seed(0)
+        m = pcseg.DGCNNWithColor(num_classes=13, k=20).to(DEV).train()
+        torch.manual_seed(1)
+        x = torch.randn(2, 6, 1024, device=DEV)
+        out = m(x)[0]
+        out.square().mean().backward()
+        return out.detach(), m.conv6[0].weight.grad.clone()
+    o1, g1 = step()
+    o2, g2 = step()
+    assert torch.equal(o1, o2) and torch.equal(g1, g2)
