@@ -1407,6 +1407,28 @@ PCS_API int pcs_dropout_bwd(const float* gout, int ldg, int M, int N, double p, 
     return launch_status("pcs_dropout_bwd");
 }
 
+__global__ __launch_bounds__(256) void copy_cols_kernel(const float* __restrict__ src, int lds, int total4, int nq,
+                                                       float* __restrict__ dst, int ldd) {
+    for (int e = blockIdx.x * 256 + threadIdx.x; e < total4; e += gridDim.x * 256) {
+        const int r = e / nq;
+        const int c = 4 * (e - r * nq);
+        st4(dst + (size_t)r * ldd + c, ld4(src + (size_t)r * lds + c));
+    }
+}
+
+PCS_API int pcs_copy_cols(const float* src, int lds, int M, int C, float* dst, int ldd, void* stream) {
+    PCS_CHECK_ARG(M >= 0 && C >= 4 && C % 4 == 0 && lds % 4 == 0 && ldd % 4 == 0 && lds >= C && ldd >= C,
+                  "pcs_copy_cols: bad sizes M=%d C=%d lds=%d ldd=%d", M, C, lds, ldd);
+    PCS_CHECK_ARG(src && dst && (reinterpret_cast<uintptr_t>(src) & 15) == 0 && (reinterpret_cast<uintptr_t>(dst) & 15) == 0,
+                  "pcs_copy_cols: null or unaligned pointer");
+    const long long total = (long long)M * C / 4;
+    PCS_CHECK_ARG(total < (1ll << 31), "pcs_copy_cols: too many elements");
+    if (total == 0) return 0;
+    hipLaunchKernelGGL(copy_cols_kernel, dim3(ew_grid(total)), dim3(256), 0, as_stream(stream), src, lds, (int)total,
+                       C / 4, dst, ldd);
+    return launch_status("pcs_copy_cols");
+}
+
 PCS_API int pcs_bn_act(const float* Z, int ldz, int M, int N, const float* s, const float* t, int act, float slope,
                        float* out, int ldo, void* stream) {
     PCS_CHECK_ARG(M >= 0 && N >= 4 && N % 4 == 0 && ldz % 4 == 0 && ldo % 4 == 0, "pcs_bn_act: bad sizes");

@@ -42,6 +42,7 @@ SIGNATURES = {
     'pcs_knn': [P, I32, I32, I32, I32, P, P],
     'pcs_knn_workspace': [I32, I32, P],
     'pcs_dropout_bwd': [P, I32, I32, I32, ctypes.c_double, I64, P, I32, P],
+    'pcs_copy_cols': [P, I32, I32, I32, P, I32, P],
     'pcs_knn_ws': [P, I32, I32, I32, I32, P, P, ctypes.c_size_t, P],
     'pcs_group_fwd': [P, P, P, P, I32, I32, I32, I32, I32, F32, I32, P, I32, P],
     'pcs_maxk_fwd': [P, I64, I32, I32, P, P, P],

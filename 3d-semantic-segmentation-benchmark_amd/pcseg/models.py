@@ -19,6 +19,7 @@ from . import ops
 from .common import SetAbstraction, FeaturePropagation, InvResMLP, UnitPointNet, GeometryPlan, GeometryPrefetch
 from .engine import shared_mlp, pad_rows, linear_rows, edgeconv, edgeconv_fused_ok, storage_alias
 from .replay import active as _replay
+from ._lib import call, ptr, stream_ptr
 
 
 def _head_rows(x_rows: torch.Tensor, drop: nn.Module, conv: nn.Module) -> torch.Tensor:
@@ -272,7 +273,15 @@ class _CopyColumns(torch.autograd.Function):
         off = 0
         for p in parts:
             c = p.shape[-1]
-            out[:, off:off + c].copy_(p.reshape(-1, c))
+            src = p.reshape(-1, c)
+            blk = out[:, off:off + c]
+            if (src.stride(1) == 1 and src.stride(0) % 4 == 0 and c % 4 == 0 and out.stride(0) % 4 == 0
+                    and src.data_ptr() % 16 == 0 and blk.data_ptr() % 16 == 0):
+                # one float4 copy kernel per block (torch's strided copy_ runs at ~2 TB/s)
+                call('pcs_copy_cols', ptr(src), src.stride(0), src.shape[0], c, ptr(blk), out.stride(0),
+                     stream_ptr(out.device))
+            else:
+                blk.copy_(src)
             off += c
         ctx.shapes = [p.shape for p in parts]
         return out

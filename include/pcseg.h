@@ -202,6 +202,10 @@ int pcs_pool_bwd_reduce(const float* dpool, const uint8_t* arg, const float* Z,
  * gin (ldi) = gout (ldg) * keep / (1 - p). */
 int pcs_dropout_bwd(const float* gout, int ldg, int M, int N, double p, int64_t seed,
                     float* gin, int ldi, void* stream);
+/* dst (M x C, row stride ldd) = src (M x C, row stride lds): a row block copied into
+ * columns of a wider buffer (DGCNN's cat(x1..x4, colour) into the head's (B*N, 1408)
+ * buffer, dgcnn.py:200 / :245); float4 rows, 16-B aligned pointers, C, lds, ldd % 4 == 0. */
+int pcs_copy_cols(const float* src, int lds, int M, int C, float* dst, int ldd, void* stream);
 /* out (M x N, ldo) = act(Z*s + t) */
 int pcs_bn_act(const float* Z, int ldz, int M, int N, const float* s,
                const float* t, int act, float slope, float* out, int ldo,
