@@ -284,8 +284,9 @@ class UnitPointNet(nn.Module):
             self.batch.append(nn.BatchNorm1d(m))
             prev = m
 
-    def forward_rows(self, x: torch.Tensor, kin: int | None = None) -> torch.Tensor:
-        return shared_mlp(x, kin or x.shape[1], self.conv, self.batch, 'relu', 0.0, 0)
+    def forward_rows(self, x: torch.Tensor, kin: int | None = None, dropout: tuple | None = None) -> torch.Tensor:
+        """dropout = (p, seed): a training-mode Dropout after the stack, fused into its output."""
+        return shared_mlp(x, kin or x.shape[1], self.conv, self.batch, 'relu', 0.0, 0, dropout=dropout)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         B, Cin, N = x.shape
@@ -335,8 +336,9 @@ class FeaturePropagation(nn.Module):
         self.point_net = UnitPointNet(in_channels, mlps)
 
     def forward(self, coords_1: torch.Tensor, coords_2: torch.Tensor, features_1: torch.Tensor | None,
-                features_2: torch.Tensor, geo: tuple | None = None) -> torch.Tensor:
-        """geo = (3-NN idx, squared dist) precomputed by a GeometryPlan, else computed here."""
+                features_2: torch.Tensor, geo: tuple | None = None, dropout: tuple | None = None) -> torch.Tensor:
+        """geo = (3-NN idx, squared dist) precomputed by a GeometryPlan, else computed here;
+        dropout = (p, seed): the model head's training-mode Dropout, fused into the MLP output."""
         B, N, _ = coords_1.shape
         inv = None
         if geo is None:
@@ -348,7 +350,7 @@ class FeaturePropagation(nn.Module):
             idx, dist = geo[0], geo[1]
             inv = geo[2] if len(geo) > 2 else None
         rows = ops.interp_cat_rows(features_1, features_2, idx, dist, inv)
-        return self.point_net.forward_rows(rows).view(B, N, -1)
+        return self.point_net.forward_rows(rows, dropout=dropout).view(B, N, -1)
 
 
 class InvResMLP(nn.Module):

@@ -22,8 +22,16 @@ from .replay import active as _replay
 from ._lib import call, ptr, stream_ptr
 
 
-def _head_rows(x_rows: torch.Tensor, drop: nn.Module, conv: nn.Module) -> torch.Tensor:
-    return linear_rows(drop(x_rows), conv)
+def _head_rows(x_rows: torch.Tensor, drop: nn.Module | None, conv: nn.Module) -> torch.Tensor:
+    return linear_rows(drop(x_rows) if drop is not None else x_rows, conv)
+
+
+def _fused_dropout(drop: nn.Module):
+    """(p, seed) for a training-mode Dropout the engine fuses into the preceding stack's output
+    (one 64-bit mask seed from torch's CPU generator), else None."""
+    if drop.training and 0.0 < drop.p < 1.0:
+        return float(drop.p), int(torch.randint(0, 2 ** 62, (1,)).item())
+    return None
 
 
 class PointNetpp(GeometryPrefetch, nn.Module):
@@ -58,8 +66,9 @@ class PointNetpp(GeometryPrefetch, nn.Module):
         f3 = self.fp4(c3, c4, f3, f4, geo=geo.fp(3))
         f2 = self.fp3(c2, c3, f2, f3, geo=geo.fp(2))
         f1 = self._prefetch_point(self.fp2(c1, c2, f1, f2, geo=geo.fp(1)))
-        f0 = self.fp1(c0, c1, None, f1, geo=geo.fp(0))
-        return _head_rows(f0.reshape(B * N, -1), self.drop, self.conv).view(B, N, -1)
+        dz = _fused_dropout(self.drop)       # the head's Dropout, fused into FP1's output
+        f0 = self.fp1(c0, c1, None, f1, geo=geo.fp(0), dropout=dz)
+        return _head_rows(f0.reshape(B * N, -1), None if dz else self.drop, self.conv).view(B, N, -1)
 
 
 class PointNetppMSG(GeometryPrefetch, nn.Module):
@@ -121,8 +130,9 @@ class PointNetppMSG(GeometryPrefetch, nn.Module):
         f3 = self.fp4(cs[3], cs[4], fs[3], fs[4], geo=geo.fp(3))
         f2 = self.fp3(cs[2], cs[3], fs[2], f3, geo=geo.fp(2))
         f1 = self._prefetch_point(self.fp2(cs[1], cs[2], fs[1], f2, geo=geo.fp(1)))
-        f0 = self.fp1(cs[0], cs[1], None, f1, geo=geo.fp(0))
-        return _head_rows(f0.reshape(B * N, -1), self.drop, self.conv).view(B, N, -1)
+        dz = _fused_dropout(self.drop)       # the head's Dropout, fused into FP1's output
+        f0 = self.fp1(cs[0], cs[1], None, f1, geo=geo.fp(0), dropout=dz)
+        return _head_rows(f0.reshape(B * N, -1), None if dz else self.drop, self.conv).view(B, N, -1)
 
 
 class PointNeXt(GeometryPrefetch, nn.Module):
@@ -185,8 +195,9 @@ class PointNeXt(GeometryPrefetch, nn.Module):
         f3 = self.fp4(c3, c4, f3, f4, geo=geo.fp(3))
         f2 = self.fp3(c2, c3, f2, f3, geo=geo.fp(2))
         f1 = self._prefetch_point(self.fp2(c1, c2, f1, f2, geo=geo.fp(1)))
-        f0 = self.fp1(c0, c1, f0, f1, geo=geo.fp(0))
-        return _head_rows(f0.reshape(B * N, -1), self.drop, self.conv).view(B, N, -1)
+        dz = _fused_dropout(self.drop)       # the head's Dropout, fused into FP1's output
+        f0 = self.fp1(c0, c1, f0, f1, geo=geo.fp(0), dropout=dz)
+        return _head_rows(f0.reshape(B * N, -1), None if dz else self.drop, self.conv).view(B, N, -1)
 
 
 # ------------------------------------------------------------------------- DGCNN
@@ -194,11 +205,8 @@ def _seq_rows(x_rows: torch.Tensor, seq: nn.Sequential, kin: int | None = None,
               out: torch.Tensor | None = None) -> torch.Tensor:
     """Conv1d(bias=False) -> BN1d -> LeakyReLU [-> Dropout] on rows (HIP shared-MLP engine);
     `out`: a row block the activation is written into (no Dropout after it)."""
-    drop = None
-    if len(seq) > 3 and seq[3].training and 0.0 < seq[3].p < 1.0 and out is None:
-        # training-mode Dropout fused into the stack's output (one 64-bit mask seed per call,
-        # from torch's CPU generator: reproducible under torch.manual_seed, no device sync)
-        drop = (float(seq[3].p), int(torch.randint(0, 2 ** 62, (1,)).item()))
+    # training-mode Dropout fused into the stack's output
+    drop = _fused_dropout(seq[3]) if len(seq) > 3 and out is None else None
     y = shared_mlp(x_rows, kin or x_rows.shape[1], [seq[0]], [seq[1]], 'lrelu', seq[2].negative_slope, 0, out=out,
                    dropout=drop)
     if len(seq) > 3 and drop is None:

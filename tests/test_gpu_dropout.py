@@ -73,3 +73,24 @@ def test_dgcnn_head_uses_fused_dropout():
     o1, g1 = step()
     o2, g2 = step()
     assert torch.equal(o1, o2) and torch.equal(g1, g2)
+
+
+@pytest.mark.parametrize('ctor', [lambda: pcseg.PointNetpp(14), lambda: pcseg.PointNetppMSG(14)])
+def test_pointnet2_head_dropout_fused_and_reproducible(ctor):
+    """PointNet++'s head Dropout (PointNetpp.py:44-45: drop -> conv) runs fused into FP1's
+    output in training mode: the step is finite and, seeded, bitwise reproducible (the mask
+    seed comes from torch's CPU generator)."""
+    from pcseg.synthetic import make_batch
+
+    def step():
+        torch.manual_seed(0)
+        m = ctor().to(DEV).train()
+        pts, _, _ = make_batch(2, 2048, seed=4)
+        torch.manual_seed(1)
+        out = m(pts.to(DEV))
+        out.square().mean().backward()
+        return out.detach(), m.conv.weight.grad.clone()
+    o1, g1 = step()
+    o2, g2 = step()
+    assert torch.isfinite(o1).all()
+    assert torch.equal(o1, o2) and torch.equal(g1, g2)
