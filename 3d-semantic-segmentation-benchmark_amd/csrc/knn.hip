@@ -116,7 +116,7 @@ __global__ __launch_bounds__(256) void knn_kernel(const float* __restrict__ x, i
 constexpr int KNN_TC = 32;      // candidates per tile
 constexpr int KNN_WAVES = 4;
 constexpr int KNN_QROWS = 32 * KNN_WAVES;
-constexpr int KNN_NMAX = 60;    // LDS items per row: top-k list + one survivor segment per lane half
+constexpr int KNN_NMAX = 64;    // LDS items per row: top-k list + one survivor segment per lane half (<= 64: one per lane in a merge)
 constexpr int KNN_RS = KNN_NMAX;       // row stride in items
 #ifndef PCS_KNN_SLACK
 #define PCS_KNN_SLACK 0         // merge early when a segment has fewer free slots (0: only on overflow;
