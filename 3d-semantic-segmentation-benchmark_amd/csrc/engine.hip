@@ -276,6 +276,8 @@ static int check_layers(int M, int kin, int ldx, const pcs_mlp_layer* L, int nl,
         PCS_CHECK_ARG(L[l].use_batch || (L[l].run_mean && L[l].run_var),
                       "%s: layer %d: eval-mode BatchNorm needs running statistics", who, l);
         PCS_CHECK_ARG(L[l].act >= 0 && L[l].act <= 2, "%s: layer %d: act=%lld", who, l, (long long)L[l].act);
+        PCS_CHECK_ARG(L[l].bwd_fuse >= PCS_BWD_FUSE_DEFAULT && L[l].bwd_fuse <= PCS_BWD_FUSE_ALL,
+                      "%s: layer %d: bwd_fuse=%lld", who, l, (long long)L[l].bwd_fuse);
         cin = (int)L[l].cout;
     }
     return 0;
@@ -430,7 +432,8 @@ static int mlp_backward(const float* X, int ldx, int kin, int M, const pcs_mlp_l
             qop.data = layers[l - 1].Z;
             qop.ld = Cin;
         }
-        const bool fused = l > 0 && P.dW && fused_bwd_ok(M, C, Cin, (int)P.ldw, &xop, &qop);
+        const bool fused = l > 0 && P.dW && fused_bwd_wanted((int)P.bwd_fuse, M) &&
+                           fused_bwd_ok(M, C, Cin, (int)P.ldw, &xop, &qop);
         if (!fused && materialize_dz_of(P, M, l > 0 || dX) && S.dz_ok(l == nl - 1)) {
             // the top layer's into its own buffer (gout is the caller's), inner ones in place
             // over the dA buffer the rebuilt operand reads
@@ -444,7 +447,7 @@ static int mlp_backward(const float* X, int ldx, int kin, int M, const pcs_mlp_l
         const bool wg_here = l == 0 && !dX && nl > 1;
         if (fused) {
             // its wgrad is part of the fused launch below
-        } else if (P.dW && wg_here && fused_wgrad_ok(M, C, Cin, ldx, &xop)) {
+        } else if (P.dW && wg_here && fused_bwd_wanted((int)P.bwd_fuse, M) && fused_wgrad_ok(M, C, Cin, ldx, &xop)) {
             if (int e = fused_wgrad(&xop, C, X, ldx, Cin, M, P.dW, P.db, S.fw, S.fw_bytes, st)) return fail(e);
         } else if (P.dW && wg_here) {
             const pcs_operand y = plain_op(X, ldx);

@@ -304,9 +304,16 @@ static void launch_wgrad_only(dim3 grid, hipStream_t st, const FusedBwdArgs& a) 
 
 static bool fb_width(int c) { return c == 32 || c == 64 || c == 128; }
 
+// the per-layer policy (pcs_mlp_layer.bwd_fuse): by default only layers over >= 2^19 rows (SA1:
+// HBM-bound, the fused launch beats the dgrad + lane wgrad pair there); on the 128-wide layers
+// the overlapped pair is faster
+bool fused_bwd_wanted(int policy, int M) {
+    if (policy == PCS_BWD_FUSE_OFF) return false;
+    return policy == PCS_BWD_FUSE_ALL || M >= (1 << 19);
+}
+
+// shape / operand eligibility of the fused kernel (the policy is the caller's decision)
 bool fused_bwd_ok(int M, int C, int CI, int ldw, const pcs_operand* x, const pcs_operand* q) {
-    const int pol = fused_bwd_policy();
-    if (pol == 0 || (pol == 2 && M < (1 << 19))) return false;
     if (M < 4 * FB_BM || !fb_width(C) || !fb_width(CI) || ldw % 4 != 0 || ldw < CI) return false;
     if (!x || !q || x->mode == PCS_OP_BNACT || x->ld % 4 != 0 || x->ld < C) return false;
     if (x->mode == PCS_OP_POOLBWD && (x->pool_k < 1 || M % x->pool_k != 0)) return false;
@@ -356,8 +363,6 @@ int fused_bwd(const pcs_operand* x, int C, const pcs_operand* q, int CI, const f
 }
 
 bool fused_wgrad_ok(int M, int C, int kin, int ldx, const pcs_operand* x) {
-    const int pol = fused_bwd_policy();
-    if (pol == 0 || (pol == 2 && M < (1 << 19))) return false;
     if (M < 4 * FB_BM || !fb_width(C) || kin < 1 || kin > 32 || ldx % 4 != 0 || ldx < kin) return false;
     if (!x || x->mode == PCS_OP_BNACT || x->ld % 4 != 0 || x->ld < C) return false;
     if (x->mode == PCS_OP_POOLBWD && (x->pool_k < 1 || M % x->pool_k != 0)) return false;

@@ -1061,16 +1061,6 @@ void pcs::wgrad_reduce_launch(const float* part, int splits, long long nk, float
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, st, part, splits, nk, dW, pdb, N, db);
 }
 
-// A/B knob (scripts only): PCS_FUSED_BWD=0 off, 1 every thin inner layer, 2 (default) only
-// layers over >= 2^19 rows
-int pcs::fused_bwd_policy() {
-    static const int v = [] {
-        const char* e = getenv("PCS_FUSED_BWD");
-        return e && e[0] >= '0' && e[0] <= '2' ? e[0] - '0' : 2;
-    }();
-    return v;
-}
-
 // dZ (M x C, row stride ldo) = the BNBWD / POOLBWD transform of operand o, materialised: the
 // same load_quad / load_raw / xform4 the GEMM loaders apply, so the values are bitwise those
 // the GEMMs would rebuild on load.  Wide layers read dZ once per column tile of their data /

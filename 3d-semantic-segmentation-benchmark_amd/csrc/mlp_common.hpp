@@ -180,7 +180,9 @@ int bn_act_dropout(const float* Z, int ldz, int M, int N, const float* s, const 
                    float* out, int ldo, double p, long long seed, hipStream_t st);
 // fused data + weight gradient of one thin inner layer (fused_bwd.hip): C = its width, CI = its
 // input width; q = the previous layer's pre-BN Z with its BN coefficients (s, t, mean, inv, act)
-int fused_bwd_policy();
+// policy = pcs_mlp_layer.bwd_fuse of the layer: PCS_BWD_FUSE_DEFAULT (only layers over >= 2^19
+// rows), PCS_BWD_FUSE_OFF, PCS_BWD_FUSE_ALL (every eligible layer)
+bool fused_bwd_wanted(int policy, int M);
 bool fused_bwd_ok(int M, int C, int CI, int ldw, const pcs_operand* x, const pcs_operand* q);
 int fused_bwd_grid(int M, int C, int CI, bool da);   // blocks = BN-backward partials
 size_t fused_bwd_ws_bytes(int M, int C, int CI);

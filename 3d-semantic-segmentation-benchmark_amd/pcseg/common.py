@@ -240,7 +240,8 @@ class GeometryPrefetch:
         self._pcs_prefetched = None
         if pf is not None and pf[0] is x and pf[1] == x._version:
             return pf[2]
-        return self._plan_for(coords)
+        # the inverse maps serve only the backward of the gathers: none under no_grad (eval)
+        return self._plan_for(coords, inverse=torch.is_grad_enabled())
 
     @staticmethod
     def _coords_of(x: torch.Tensor) -> torch.Tensor:
@@ -260,10 +261,11 @@ class MiniPointNet(nn.Module):
             self.conv.append(nn.Conv2d(prev, m, (1, 1)))
             self.batch.append(nn.BatchNorm2d(m))
             prev = m
+        self.bwd_fuse = 0           # backward kernel choice (pcseg.engine.set_bwd_fuse)
 
     def forward_rows(self, x: torch.Tensor, kin: int | None = None, pool_k: int = 0) -> torch.Tensor:
         """rows (M, ld) -> (M, C_L), or (M/pool_k, C_L) max-pooled over consecutive groups of pool_k rows."""
-        return shared_mlp(x, kin or x.shape[1], self.conv, self.batch, 'relu', 0.0, pool_k)
+        return shared_mlp(x, kin or x.shape[1], self.conv, self.batch, 'relu', 0.0, pool_k, bwd_fuse=self.bwd_fuse)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         B, Cin, H, W = x.shape
@@ -283,10 +285,12 @@ class UnitPointNet(nn.Module):
             self.conv.append(nn.Conv1d(prev, m, 1))
             self.batch.append(nn.BatchNorm1d(m))
             prev = m
+        self.bwd_fuse = 0           # backward kernel choice (pcseg.engine.set_bwd_fuse)
 
     def forward_rows(self, x: torch.Tensor, kin: int | None = None, dropout: tuple | None = None) -> torch.Tensor:
         """dropout = (p, seed): a training-mode Dropout after the stack, fused into its output."""
-        return shared_mlp(x, kin or x.shape[1], self.conv, self.batch, 'relu', 0.0, 0, dropout=dropout)
+        return shared_mlp(x, kin or x.shape[1], self.conv, self.batch, 'relu', 0.0, 0, dropout=dropout,
+                          bwd_fuse=self.bwd_fuse)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         B, Cin, N = x.shape

@@ -149,17 +149,28 @@ class DistributedBlockSampler:
     an epoch are disjoint and together cover every block (the reference's
     DataLoader(shuffle=True) draws one uniform permutation per epoch for its single
     process, block_datasets.py:166-173).  `shuffle=False` keeps the block order.
+
+    `pad=False` (evaluation): no wrap padding and no dropping -- rank r takes entries r,
+    r + world, ... of the permutation, so the shards have uneven lengths (they differ by at
+    most one) and every block is evaluated exactly once across ranks, as the reference's
+    single-process test loader does; a padded shard would count some blocks twice in
+    aggregated metrics.
     """
 
     def __init__(self, num_blocks: int, rank: int | None = None, world: int | None = None, shuffle: bool = True,
-                 seed: int = 0, drop_last: bool = False):
+                 seed: int = 0, drop_last: bool = False, pad: bool = True):
         self.n = int(num_blocks)
         self.rank, self.world = _dist_rank_world(rank, world)
         if not 0 <= self.rank < self.world:
             raise ValueError(f'rank {self.rank} out of range for world size {self.world}')
-        self.shuffle, self.seed, self.drop_last = shuffle, int(seed), drop_last
+        if drop_last and not pad:
+            raise ValueError('DistributedBlockSampler: drop_last and pad=False exclude each other')
+        self.shuffle, self.seed, self.drop_last, self.pad = shuffle, int(seed), drop_last, pad
         self.epoch = 0
-        self.per_rank = self.n // self.world if drop_last else -(-self.n // self.world)
+        if not pad:
+            self.per_rank = len(range(self.rank, self.n, self.world))
+        else:
+            self.per_rank = self.n // self.world if drop_last else -(-self.n // self.world)
 
     def set_epoch(self, epoch: int) -> None:
         self.epoch = int(epoch)
@@ -170,6 +181,8 @@ class DistributedBlockSampler:
             perm = torch.randperm(self.n, generator=g).tolist()
         else:
             perm = list(range(self.n))
+        if not self.pad:
+            return perm
         total = self.per_rank * self.world
         if total > self.n:                                  # wrap-pad so every rank gets per_rank blocks
             perm = (perm * (-(-total // max(self.n, 1))))[:total]
@@ -223,15 +236,16 @@ def create_block_dataloaders(data_dir: str, test_areas, train_batch_size: int = 
     whose blocks are resident in HBM (`DeviceBlockStore`) and whose batches are assembled
     on the device.  `num_workers` is accepted for signature compatibility (no host workers
     are needed).  Under torch.distributed (or explicit rank/world) each loader yields only
-    this rank's shard (`DistributedBlockSampler`)."""
+    this rank's shard (`DistributedBlockSampler`): the train shards are padded to equal
+    length, the test shards are not (every test block is evaluated exactly once)."""
     del num_workers
     areas = {1, 2, 3, 4, 5, 6}
     test_areas = set(test_areas)
     out = []
-    for inc, bs, samp, shuf in ((areas - test_areas, train_batch_size, train_sampling, train_shuffle),
-                                (test_areas, test_batch_size, test_sampling, test_shuffle)):
+    for inc, bs, samp, shuf, pad in ((areas - test_areas, train_batch_size, train_sampling, train_shuffle, True),
+                                     (test_areas, test_batch_size, test_sampling, test_shuffle, False)):
         store = DeviceBlockStore(data_dir, inc, sampling=samp, device=device)
-        sampler = DistributedBlockSampler(len(store), rank, world, shuffle=shuf, seed=seed)
+        sampler = DistributedBlockSampler(len(store), rank, world, shuffle=shuf, seed=seed, pad=pad)
         out.append(DeviceBlockLoader(store, bs, sampler, seed=seed))
     return out[0], out[1]
 

@@ -5,16 +5,18 @@ gradient all-reduce after backward.  Gradients live in 
 fp32 buffer (every `param.grad` is a view into it), split into a few
 contiguous buckets that are all-reduced as soon as autograd has produced every
 gradient in them -- overlapping the collective with the rest of backward on
-RCCL's own stream.  BatchNorm statistics stay local per rank (DDP's default;
-the reference has no SyncBN); parameters and buffers are broadcast from rank 0
-once.
+RCCL's own stream.  BatchNorm statistics are computed locally per rank (DDP's
+default; the reference has no SyncBN); parameters are broadcast from rank 0 once and,
+as DDP's `broadcast_buffers=True` does, rank 0's buffers (BN running statistics) are
+broadcast to every rank at the start of each training forward -- coalesced into one
+flat buffer per dtype, so that is one or two collectives per step.
 """
 from __future__ import annotations
 
 import torch
 import torch.distributed as dist
 
-from .engine import wgrad_lane
+from .engine import wgrad_lane, lane_join
 
 
 def broadcast_model(model: torch.nn.Module, src: int = 0) -> None:
@@ -29,10 +31,40 @@ def _align(n: int) -> int:
     return (n + 63) // 64 * 64
 
 
+class FlatBuffers:
+    """Every buffer of a model (BN running mean / var, num_batches_tracked) rebound as a view
+    of one flat tensor per dtype, so rank 0's buffers reach every rank in one broadcast per
+    dtype (DDP `broadcast_buffers` semantics).  The HIP engine updates running statistics in
+    place through their pointers, which the views keep."""
+
+    def __init__(self, model: torch.nn.Module):
+        groups: dict = {}
+        for mod in model.modules():
+            for name, b in mod._buffers.items():
+                if b is not None:
+                    groups.setdefault(b.dtype, []).append((mod, name, b))
+        self.flats = []
+        for dtype, items in groups.items():
+            flat = torch.empty(sum(b.numel() for _, _, b in items), dtype=dtype, device=items[0][2].device)
+            off = 0
+            for mod, name, b in items:
+                n = b.numel()
+                view = flat[off:off + n].view_as(b)
+                view.copy_(b)
+                mod._buffers[name] = view
+                off += n
+            self.flats.append(flat)
+
+    def broadcast(self, src: int = 0) -> None:
+        for f in self.flats:
+            dist.broadcast(f, src)
+
+
 class FlatGradAllReduce:
     """Flat gradient buffer + bucketed, backward-overlapped all-reduce (mean)."""
 
-    def __init__(self, model: torch.nn.Module, bucket_bytes: int = 4 << 20, overlap: bool = True):
+    def __init__(self, model: torch.nn.Module, bucket_bytes: int = 4 << 20, overlap: bool = True,
+                 broadcast_buffers: bool = True):
         self.params = [p for p in model.parameters() if p.requires_grad]
         # every parameter (and its gradient) starts on a 256-B boundary of the flat buffers: the
         # wide GEMMs stage weights by 16-B LDS-DMA and take only aligned operands
@@ -63,6 +95,11 @@ class FlatGradAllReduce:
         self._seen: set[int] = set()
         self._handles: list = []
         self.overlap = overlap and self.world > 1
+        self.buffers = None
+        if broadcast_buffers and self.world > 1 and any(True for _ in model.buffers()):
+            # DDP broadcast_buffers: rank 0's buffers at the start of every training forward
+            self.buffers = FlatBuffers(model)
+            model.register_forward_pre_hook(self._pre_forward)
         self.attach()
         if self.overlap:
             for p in self.params:
@@ -70,6 +107,10 @@ class FlatGradAllReduce:
                 # gradients the HIP engine writes in place call _pcs_grad_ready instead
                 p.register_post_accumulate_grad_hook(self._hook)
                 p._pcs_grad_ready = self._hook
+
+    def _pre_forward(self, module, inputs) -> None:
+        if module.training and torch.is_grad_enabled():
+            self.buffers.broadcast()
 
     def attach(self) -> None:
         """(Re)bind every param.grad to its view of the flat buffer."""
@@ -112,6 +153,8 @@ class FlatGradAllReduce:
 
     def synchronize(self) -> None:
         """Finish all bucket reductions and average (call before optimizer.step())."""
+        if self.flat.is_cuda:
+            lane_join(self.flat.device)      # every deferred weight gradient is written
         if self.world == 1:
             return
         if self.overlap:

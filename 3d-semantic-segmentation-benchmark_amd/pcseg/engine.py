@@ -169,9 +169,12 @@ _ws_cache: dict = {}
 # A stack's weight gradients run on the device's wgrad lane (a native side stream).  With
 # pcs_mlp_backward_deferred they keep running after the stack's backward returns, under the
 # next autograd nodes, and one join per backward pass (an autograd engine callback) makes
-# the caller's stream wait for them before anything reads the gradients.
+# the caller's stream wait for them before anything reads the gradients (FlatAdam.step and
+# FlatGradAllReduce.synchronize join again, unconditionally).
 _lanes: dict = {}
-_join_queued: set = set()
+_join_queued: dict = {}      # device index -> autograd graph task whose backward has a join queued
+
+BWD_FUSE = {'default': 0, 'off': 1, 'all': 2}   # pcs_mlp_layer.bwd_fuse (include/pcseg.h)
 
 
 def wgrad_lane(dev: torch.device):
@@ -186,13 +189,18 @@ def wgrad_lane(dev: torch.device):
 
 
 def _queue_lane_join(dev: torch.device) -> None:
+    """Queue one lane join at the end of the CURRENT backward pass (graph task).  The dedup is
+    keyed on the graph task id: if a backward raises after queueing, its final callbacks never
+    run, and the next backward (a new task id) still queues its own join."""
     idx = dev.index if dev.index is not None else torch.cuda.current_device()
-    if idx in _join_queued:
+    task = torch._C._current_graph_task_id()
+    if task >= 0 and _join_queued.get(idx) == task:
         return
-    _join_queued.add(idx)
+    _join_queued[idx] = task
 
     def join():
-        _join_queued.discard(idx)
+        if _join_queued.get(idx) == task:
+            del _join_queued[idx]
         with torch.cuda.device(idx):
             call('pcs_wgrad_lane_join', stream_ptr(torch.device('cuda', idx)))
     torch.autograd.Variable._execution_engine.queue_callback(join)
@@ -202,6 +210,16 @@ def lane_join(dev: torch.device) -> None:
     """Make the current stream wait for every weight gradient pending on the device's lane."""
     with torch.cuda.device(dev):
         call('pcs_wgrad_lane_join', stream_ptr(dev))
+
+
+def set_bwd_fuse(module: torch.nn.Module, policy: str = 'default') -> None:
+    """Per-module backward kernel choice of every shared-MLP stack under `module`
+    (pcs_mlp_layer.bwd_fuse): 'default' fuses a thin layer's data + weight gradient into one
+    launch only over >= 2^19 rows, 'off' never, 'all' for every eligible layer."""
+    v = BWD_FUSE[policy]
+    for m in module.modules():
+        if hasattr(m, 'bwd_fuse'):
+            m.bwd_fuse = v
 
 
 def _workspace(lib, key, M, kin, ldx, recs, nl, pool_k, backward):
@@ -228,7 +246,7 @@ class SharedMLPFn(torch.autograd.Function):
     record per layer."""
 
     @staticmethod
-    def forward(ctx, X, Kin, pool_K, acts, bns, dest, drop, *params):
+    def forward(ctx, X, Kin, pool_K, acts, bns, dest, drop, bwd_fuse, *params):
         dev = X.device
         st = stream_ptr(dev)
         lib = load()
@@ -271,7 +289,8 @@ class SharedMLPFn(torch.autograd.Function):
             cin = C
         # drop = (p, seed): the training-mode Dropout after the stack, fused into its output
         dp, dseed = drop if drop is not None else (0.0, 0)
-        recs = b''.join(_REC.pack(*f, 0, 0, 0, 0, dp if li == nl - 1 else 0.0, dseed if li == nl - 1 else 0, 0)
+        recs = b''.join(_REC.pack(*f, 0, 0, 0, 0, dp if li == nl - 1 else 0.0, dseed if li == nl - 1 else 0,
+                                  bwd_fuse)
                         for li, f in enumerate(fixed))
         CL = couts[-1]
         ldo = 0
@@ -306,6 +325,7 @@ class SharedMLPFn(torch.autograd.Function):
         ctx.save_for_backward(X, Zbuf, coef, *Wms, *([arg] if arg is not None else []))
         ctx.meta = (Kin, pool_K, nl, fixed, couts, arg is not None)
         ctx.drop = drop
+        ctx.bwd_fuse = bwd_fuse
         ctx.params = params
         return out
 
@@ -332,7 +352,8 @@ class SharedMLPFn(torch.autograd.Function):
             gout = g2
         ldg = gout.stride(0)
         recs = b''.join(_REC.pack(*f, _nz(grad_target(params[4 * li])), _nz(grad_target(params[4 * li + 1])),
-                                  _nz(grad_target(params[4 * li + 2])), _nz(grad_target(params[4 * li + 3])), 0, 0, 0)
+                                  _nz(grad_target(params[4 * li + 2])), _nz(grad_target(params[4 * li + 3])), 0, 0,
+                                  ctx.bwd_fuse)
                         for li, f in enumerate(fixed))
         dX = None
         if ctx.needs_input_grad[0]:
@@ -352,7 +373,7 @@ class SharedMLPFn(torch.autograd.Function):
                 t.record_stream(lane)
             _queue_lane_join(dev)
         notify_grad_ready(params)
-        return (dX, None, None, None, None, None, None, *([None] * len(params)))
+        return (dX, None, None, None, None, None, None, None, *([None] * len(params)))
 
 
 def _edge_ws(B, N, C, Cout, backward, dev):
@@ -482,13 +503,15 @@ def _rows_ok(x: torch.Tensor) -> bool:
 
 
 def shared_mlp(x_rows: torch.Tensor, kin: int, convs, bns, act='relu', slope=0.0,
-               pool_k: int = 0, out: torch.Tensor | None = None, dropout: tuple | None = None) -> torch.Tensor:
+               pool_k: int = 0, out: torch.Tensor | None = None, dropout: tuple | None = None,
+               bwd_fuse: int = 0) -> torch.Tensor:
     """Run a conv/BN/act stack on rows.  x_rows (M, W) with `kin` logical channels, W % 4 == 0,
     dense or a column block of a wider buffer (row stride >= W).  `act` / `slope` are one value
     for every layer or a sequence with one per layer ('relu', 'lrelu', 'none').  `out`: an
     (M, cout) row block (storage_alias) the un-pooled activation is written into.  `dropout` =
     (p, seed): a training-mode nn.Dropout(p) after the stack, fused into its output
-    (pcs_mlp_layer.drop_p; backward pcs_dropout_bwd recomputes the mask from the seed)."""
+    (pcs_mlp_layer.drop_p; backward pcs_dropout_bwd recomputes the mask from the seed).
+    `bwd_fuse`: the stack's backward kernel choice (BWD_FUSE values, pcs_mlp_layer.bwd_fuse)."""
     if not x_rows.is_cuda:
         raise RuntimeError('pcseg ops run only on the GPU (no CPU fallback); got a CPU tensor')
     if not _rows_ok(x_rows):
@@ -506,7 +529,8 @@ def shared_mlp(x_rows: torch.Tensor, kin: int, convs, bns, act='relu', slope=0.0
         params += [conv.weight, conv.bias, bn.weight, bn.bias]
     if dropout is not None and (pool_k or not 0.0 < float(dropout[0]) < 1.0):
         raise ValueError('shared_mlp: dropout needs an un-pooled output and 0 < p < 1')
-    return SharedMLPFn.apply(x_rows, kin, pool_k, acts, list(bns), None if out is None else (out,), dropout, *params)
+    return SharedMLPFn.apply(x_rows, kin, pool_k, acts, list(bns), None if out is None else (out,), dropout,
+                             int(bwd_fuse), *params)
 
 
 class RowLinearFn(torch.autograd.Function):

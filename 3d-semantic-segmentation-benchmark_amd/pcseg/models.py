@@ -28,8 +28,10 @@ def _head_rows(x_rows: torch.Tensor, drop: nn.Module | None, conv: nn.Module) ->
 
 def _fused_dropout(drop: nn.Module):
     """(p, seed) for a training-mode Dropout the engine fuses into the preceding stack's output
-    (one 64-bit mask seed from torch's CPU generator), else None."""
-    if drop.training and 0.0 < drop.p < 1.0:
+    (one 64-bit mask seed from torch's CPU generator), else None.  Under HIP-graph capture the
+    seed would be baked into the graph as a kernel argument (every replay the same mask), so
+    there the module's own nn.Dropout runs instead: torch's Philox offset advances per replay."""
+    if drop.training and 0.0 < drop.p < 1.0 and not torch.cuda.is_current_stream_capturing():
         return float(drop.p), int(torch.randint(0, 2 ** 62, (1,)).item())
     return None
 
@@ -50,8 +52,9 @@ class PointNetpp(GeometryPrefetch, nn.Module):
         self.drop = nn.Dropout(0.5)
         self.conv = nn.Conv1d(128, part_classes, 1)
 
-    def _plan_for(self, c0):
-        return GeometryPlan(c0, [(sa.C, [(sa.radius, sa.K, False)]) for sa in (self.sa1, self.sa2, self.sa3, self.sa4)])
+    def _plan_for(self, c0, inverse=True):
+        return GeometryPlan(c0, [(sa.C, [(sa.radius, sa.K, False)]) for sa in (self.sa1, self.sa2, self.sa3, self.sa4)],
+                            inverse=inverse)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         B, N, _ = x.shape
@@ -105,8 +108,9 @@ class PointNetppMSG(GeometryPrefetch, nn.Module):
         self.drop = nn.Dropout(0.5)
         self.conv = nn.Conv1d(128, part_classes, 1)
 
-    def _plan_for(self, c0):
-        return GeometryPlan(c0, [(br[0].C, [(sa.radius, sa.K, False) for sa in br]) for br in self.levels])
+    def _plan_for(self, c0, inverse=True):
+        return GeometryPlan(c0, [(br[0].C, [(sa.radius, sa.K, False) for sa in br]) for br in self.levels],
+                            inverse=inverse)
 
     def _sa_level(self, branches, coords, feats, geo, level):
         C = branches[0].C
@@ -167,14 +171,14 @@ class PointNeXt(GeometryPrefetch, nn.Module):
         self.drop = nn.Dropout(0.5)
         self.conv = nn.Conv1d(fp1, part_classes, 1)
 
-    def _plan_for(self, c0):
+    def _plan_for(self, c0, inverse=True):
         def q(m, on_self):
             return (m.radius, m.K, on_self)
         return GeometryPlan(c0, [
             (self.sa1.C, [q(self.sa1, False), q(self.irmlp1, True)]),
             (self.sa2.C, [q(self.sa2, False), q(self.irmlp2, True), q(self.irmlp2_1, True)]),
             (self.sa3.C, [q(self.sa3, False), q(self.irmlp3, True)]),
-            (self.sa4.C, [q(self.sa4, False), q(self.irmlp4, True)])])
+            (self.sa4.C, [q(self.sa4, False), q(self.irmlp4, True)])], inverse=inverse)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         B, N, Cin = x.shape

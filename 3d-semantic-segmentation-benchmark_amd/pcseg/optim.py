@@ -15,6 +15,7 @@ import math
 import torch
 
 from ._lib import call, ptr, stream_ptr
+from .engine import lane_join
 
 
 class FlatAdam:
@@ -46,6 +47,11 @@ class FlatAdam:
         bc1 = 1 - b1 ** self.t
         step = -(self.lr / bc1)
         bc2_sqrt = math.sqrt(1 - b2 ** self.t)
+        if self.flat.is_cuda:
+            # the engine's deferred weight gradients are joined at the end of every backward; join
+            # again here so no path (e.g. a backward that raised before its final callbacks ran)
+            # lets the update read partial gradients
+            lane_join(self.flat.device)
         call('pcs_adam', ptr(self.flat), ptr(self.grads.flat), ptr(self.exp_avg), ptr(self.exp_avg_sq),
              self.flat.numel(), 1 - b1, b2, 1 - b2, step, bc2_sqrt, self.eps, self.weight_decay,
              stream_ptr(self.flat.device))

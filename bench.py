@@ -222,6 +222,7 @@ def run_workload(key, batch, npoints, args, world, rank, dev):
     name, ctor, kind, _, _, cfg = WORKLOADS[key]
     torch.manual_seed(0)
     model = ctor(pcseg).to(dev).train()     # PyTorch default init (random weights)
+    pcseg.engine.set_bwd_fuse(model, args.bwd_fuse)
     broadcast_model(model)
     grads = FlatGradAllReduce(model)
     use_graph = args.graph and world == 1
@@ -378,6 +379,8 @@ def main():
                          "or from a gradient hook inside the backward (round 2 A/B: within noise, 5.50 vs 5.52 ms)")
     ap.add_argument('--no-prefetch', action='store_true',
                     help='do not enqueue the next step\'s FPS/ball-query/3-NN before this step\'s backward')
+    ap.add_argument('--bwd-fuse', choices=['default', 'off', 'all'], default='default',
+                    help='backward kernel choice of the shared-MLP stacks (pcs_mlp_layer.bwd_fuse; A/B runs)')
     ap.add_argument('--check-launch', action='store_true',
                     help='launcher self-test: each rank joins a gloo group, prints its env as JSON, exits (no GPU)')
     args = ap.parse_args()

@@ -234,8 +234,16 @@ typedef struct pcs_mlp_layer {
     float* dW; float* db; float* dgamma; float* dbeta;
     double drop_p;        /* top layer, un-pooled: inverted dropout of the output (0 = none) */
     int64_t drop_seed;    /* its mask: pcs_dropout_keep(seed, row * cout + col) */
-    int64_t reserved;
+    int64_t bwd_fuse;     /* backward kernel choice for this layer (a per-call field, no
+                           * process-global switch): PCS_BWD_FUSE_DEFAULT fuses the data +
+                           * weight gradient of a thin layer into one launch only over >= 2^19
+                           * rows, _OFF never, _ALL for every eligible layer (same results to
+                           * fp32 rounding; tests / A-B runs) */
 } pcs_mlp_layer;
+
+#define PCS_BWD_FUSE_DEFAULT 0
+#define PCS_BWD_FUSE_OFF 1
+#define PCS_BWD_FUSE_ALL 2
 
 /* workspace bytes of pcs_mlp_forward (backward = 0) or pcs_mlp_backward (1) */
 int pcs_mlp_workspace(int M, int kin, int ldx, const pcs_mlp_layer* layers, int nl,

@@ -187,6 +187,23 @@ def test_sampler_shards_partition_each_epoch(n, world, drop_last):
     assert list(s0) != e0 or n <= world
 
 
+@pytest.mark.parametrize('n,world', [(13, 2), (12, 4), (3, 4), (10, 3)])
+def test_eval_sampler_shards_have_no_duplicates(n, world):
+    """pad=False (the test loader's sampler): the union of the ranks' shards is every block
+    exactly once, shard lengths differ by at most one."""
+    for shuffle in (False, True):
+        shards = []
+        for r in range(world):
+            s = D.DistributedBlockSampler(n, rank=r, world=world, seed=11, shuffle=shuffle, pad=False)
+            shards.append(list(s))
+            assert len(shards[-1]) == len(s)
+        flat = [i for sh in shards for i in sh]
+        assert sorted(flat) == list(range(n))
+        assert max(map(len, shards)) - min(map(len, shards)) <= 1
+    with pytest.raises(ValueError):
+        D.DistributedBlockSampler(n, rank=0, world=world, drop_last=True, pad=False)
+
+
 def _sampler_worker(rank, world, port, n, out):
     import torch.distributed as dist
     os.environ['MASTER_ADDR'] = '127.0.0.1'
@@ -222,3 +239,38 @@ def test_sampler_world2_gloo_disjoint_and_covering():
         assert set(a[0].tolist()).isdisjoint(a[1].tolist())
         assert sorted(a.reshape(-1).tolist()) == list(range(n))
     assert not torch.equal(out[0][0], out[0][1])             # a fresh permutation per epoch
+
+
+def _eval_shard_worker(rank, world, port, n, out):
+    import torch.distributed as dist
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        s = D.DistributedBlockSampler(n, seed=5, pad=False)
+        mine = torch.tensor(list(s), dtype=torch.int64)
+        sizes = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+        dist.all_gather(sizes, torch.tensor([mine.numel()]))
+        width = int(max(sizes))
+        padded = torch.full((width,), -1, dtype=torch.int64)
+        padded[:mine.numel()] = mine
+        got = [torch.zeros_like(padded) for _ in range(world)]
+        dist.all_gather(got, padded)
+        out[rank] = torch.stack(got)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_eval_shards_world2_gloo_cover_each_block_once():
+    """The test loader's shards over a world-2 gloo group: no block is evaluated twice."""
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as sk:
+        sk.bind(('127.0.0.1', 0))
+        port = sk.getsockname()[1]
+    n, world = 11, 2
+    out = mp.Manager().dict()
+    mp.spawn(_eval_shard_worker, args=(world, port, n, out), nprocs=world, join=True)
+    allb = out[0].reshape(-1)
+    allb = allb[allb >= 0]
+    assert sorted(allb.tolist()) == list(range(n))

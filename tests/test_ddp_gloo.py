@@ -197,3 +197,60 @@ def test_flat_grad_allreduce_world2_engine_on_gpu(overlap):
         p.join(timeout=600)
     print('DDPOUT', dict(out), flush=True)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+
+
+def _buffers_worker(rank, world, port, out, broadcast_buffers):
+    """DDP broadcast_buffers: rank 0's BN running statistics reach every rank at the start of a
+    training forward, then each rank updates them with its OWN batch statistics."""
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    torch.set_num_threads(1)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        torch.manual_seed(0)
+        model = torch.nn.Sequential(torch.nn.Linear(4, 8), torch.nn.BatchNorm1d(8)).train()
+        broadcast_model(model)
+        with torch.no_grad():                   # rank-dependent buffers after the initial broadcast
+            model[1].running_mean.fill_(float(rank + 1))
+            model[1].running_var.fill_(float(2 * rank + 1))
+            model[1].num_batches_tracked.fill_(5 * rank)
+        grads = FlatGradAllReduce(model, overlap=True, broadcast_buffers=broadcast_buffers)
+        x = torch.randn(16, 4, generator=torch.Generator().manual_seed(rank))
+        with torch.no_grad():
+            z = model[0](x)
+        bm, bv = z.mean(0), z.var(0, unbiased=True)
+        grads.zero_grad()
+        model(x).square().sum().backward()
+        grads.synchronize()
+        src = 0 if broadcast_buffers else rank
+        exp_mean = 0.9 * float(src + 1) + 0.1 * bm
+        exp_var = 0.9 * float(2 * src + 1) + 0.1 * bv
+        assert torch.allclose(model[1].running_mean, exp_mean, atol=1e-6), (model[1].running_mean, exp_mean)
+        assert torch.allclose(model[1].running_var, exp_var, atol=1e-6)
+        assert int(model[1].num_batches_tracked) == 5 * src + 1
+        # state_dict still names the rebound buffers and loads into them in place
+        sd = model.state_dict()
+        assert torch.equal(sd['1.running_mean'], model[1].running_mean)
+        # an eval forward does not broadcast
+        model.eval()
+        with torch.no_grad():
+            model(x)
+        out[rank] = float(model[1].running_mean[0])
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('broadcast_buffers', [True, False])
+def test_broadcast_buffers_world2(broadcast_buffers):
+    world = 2
+    ctx = mp.get_context('spawn')
+    out = ctx.Manager().dict()
+    port = _free_port()
+    procs = [ctx.Process(target=_buffers_worker, args=(r, world, port, out, broadcast_buffers))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    assert len(out) == world

@@ -94,3 +94,32 @@ def test_pointnet2_head_dropout_fused_and_reproducible(ctor):
     o2, g2 = step()
     assert torch.isfinite(o1).all()
     assert torch.equal(o1, o2) and torch.equal(g1, g2)
+
+
+def test_dropout_masks_differ_between_graph_replays():
+    """A training step captured in a HIP graph: the Dropout after a DGCNN head stack must draw a
+    new mask on every replay (the fused path's host-drawn seed would be baked into the graph,
+    so under capture the module's nn.Dropout runs -- torch's Philox offset advances per replay)."""
+    from pcseg.models import _seq_rows
+    torch.manual_seed(0)
+    seq = nn.Sequential(nn.Conv1d(64, 128, 1, bias=False), nn.BatchNorm1d(128), nn.LeakyReLU(negative_slope=0.2),
+                        nn.Dropout(0.5)).to(DEV).train()
+    x = torch.randn(8192, 64, device=DEV)
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        for _ in range(2):
+            _seq_rows(x, seq)
+    torch.cuda.current_stream().wait_stream(side)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        y = _seq_rows(x, seq)
+    g.replay()
+    a = y.detach().clone()
+    g.replay()
+    b = y.detach().clone()
+    torch.cuda.synchronize()
+    za, zb = a == 0, b == 0
+    assert not torch.equal(za, zb)
+    for z in (za, zb):
+        assert abs(float(z.float().mean()) - 0.5) < 0.01

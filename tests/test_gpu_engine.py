@@ -247,3 +247,122 @@ def test_stack_pooling_matches_max_of_activation(K, act):
     scale = max(float(q.grad.abs().max()) for q in list(c2.parameters()) + list(b2.parameters()))
     for p, q in zip(list(c1.parameters()) + list(b1.parameters()), list(c2.parameters()) + list(b2.parameters())):
         assert float((p.grad - q.grad).abs().max()) <= 1e-5 * scale
+
+
+# ---------------------------------------------------------------- DGCNN conv5-7 at BASELINE config 2
+# B = 32 x N = 4096 -> M = 131 072 rows (models/dgcnn/dgcnn.py:188-207, colour model: x_cat 384,
+# emb 1024, conv6 input 1408): the LDS-DMA wide GEMMs of gemm_big.hip, each identified by the
+# launch probe's kernel name, against an fp64 product on the GPU.
+def _rel_dev(a, b):
+    return float((a.double() - b).norm() / b.norm().clamp_min(1e-30))
+
+
+WIDE = [  # M, K (contraction), N (outputs), ldc, BN statistics, kernel the dispatch must pick
+    (131072, 1024, 384, 1408, False, 'pcs::gemm_nt_kernel<128, 4, 2, false>'),   # conv5 dgrad into the head buffer
+    (131072, 512, 1408, 1408, False, 'pcs::gemm_nt_kernel<128, 4, 2, false>'),   # conv6 dgrad
+    (131072, 256, 512, 512, False, 'pcs::gemm_nt_kernel<256, 2, 4, false>'),     # conv7 dgrad
+    (131072, 384, 1024, 1408, True, 'pcs::gemm_nt_kernel<256, 2, 4, true>'),     # conv5 forward
+    (131072, 1408, 512, 512, True, 'pcs::gemm_nt_kernel<256, 2, 4, true>'),      # conv6 forward
+    (65601, 64, 300, 300, False, 'pcs::gemm_nt_kernel<128, 4, 2, false>'),       # ragged M and N
+    (65601, 96, 512, 516, True, 'pcs::gemm_nt_kernel<256, 2, 4, true>'),         # ragged M, stats
+]
+
+
+@pytest.mark.parametrize('M,K,N,ldc,stats,kernel', WIDE)
+def test_wide_gemm_nt_vs_fp64(M, K, N, ldc, stats, kernel):
+    from pcseg.engine import KernelProbe
+    g = torch.Generator(device=DEV).manual_seed(M + 3 * K + 7 * N)
+    A = torch.randn(M, K, device=DEV, generator=g)
+    W = torch.randn(N, K, device=DEV, generator=g) / math.sqrt(K)
+    bias = torch.randn(N, device=DEV, generator=g) if stats else None
+    C = torch.full((M, ldc), float('nan'), device=DEV)
+    part = None
+    if stats:
+        nb = load().pcs_gemm_row_blocks(M, N)
+        assert nb == load().pcs_gemm_nt_row_tiles(M)
+        part = torch.empty(2, N, nb, dtype=torch.float64, device=DEV)
+    with KernelProbe() as kp:
+        gemm_rows(operand(A, K), M, K, W, K, bias, C, ldc, N, part, st=stream_ptr(torch.device(DEV)))
+    assert [r[0] for r in kp.records()] == [kernel]
+    ref = A.double() @ W.double().t()
+    if bias is not None:
+        ref += bias.double()
+    tol = 2e-6 * math.sqrt(K)
+    assert _rel_dev(C[:, :N], ref) <= tol
+    assert torch.isnan(C[:, N:]).all()                      # the row stride's pad columns are not written
+    if stats:
+        sums = part.sum(-1)
+        assert _rel_dev(sums[0], ref.sum(0)) <= tol + 1e-6
+        assert _rel_dev(sums[1], (ref * ref).sum(0)) <= tol
+
+
+WIDE_W = [  # M rows, N (dZ channels), K (input channels), Y operand mode, kernel the dispatch must pick
+    (131072, 256, 512, OP_PLAIN, 'pcs::wgrad_nt_kernel<128, 4, 2>'),            # conv7 weight gradient
+    (131072, 1024, 384, OP_PLAIN, 'pcs::wgrad_kernel<128, 128, 0, 0, 1>'),      # conv5 (row-split wgrad)
+    (131072, 512, 1408, OP_PLAIN, 'pcs::wgrad_kernel<128, 128, 0, 0, 1>'),      # conv6
+    (131072, 256, 512, OP_BNACT, 'pcs::wgrad_kernel<128, 128, 0, 1, 1>'),       # conv7 over a BN+act input
+    (65568, 256, 256, OP_PLAIN, 'pcs::wgrad_nt_kernel<128, 4, 2>'),             # M % 32 == 0, not a split multiple
+]
+
+
+@pytest.mark.parametrize('M,N,K,ymode,kernel', WIDE_W)
+def test_wide_wgrad_vs_fp64(M, N, K, ymode, kernel):
+    """dW = dZ^T . X for the wide layers (no bias: conv5-7 have bias=False), plain dZ (the
+    materialised top-layer gradient), fp64 reference on the GPU; deterministic."""
+    from pcseg.engine import KernelProbe
+    g = torch.Generator(device=DEV).manual_seed(M + 11 * N + 5 * K + ymode)
+    x = Xform(OP_PLAIN, M, N, ld4(N), 0.2, 0, g)
+    y = Xform(ymode, M, K, ld4(K), 0.2, 0, g)
+    st = stream_ptr(torch.device(DEV))
+    dW = torch.zeros(N, K, device=DEV)
+    with KernelProbe() as kp:
+        wgrad(x.op(), N, y.op(), K, M, dW, None, st)
+    names = [r[0] for r in kp.records()]
+    assert names == [kernel], names
+    ref = x.value().t() @ y.value()
+    assert _rel_dev(dW, ref) <= 3e-5
+    dW2 = torch.zeros(N, K, device=DEV)
+    wgrad(x.op(), N, y.op(), K, M, dW2, None, st)
+    assert torch.equal(dW, dW2)
+
+
+def test_lane_join_after_a_backward_that_raised(monkeypatch):
+    """A backward that raises after a deferred stack backward queued its wgrad-lane join never
+    runs its final callbacks; the next backward (a new graph task) must queue and run its own
+    join, and its gradients must be those of a clean run."""
+    import pcseg
+    import pcseg.engine as E
+    joins = []
+    orig = E.call
+
+    def counting(name, *a):
+        if name == 'pcs_wgrad_lane_join':
+            joins.append(1)
+        return orig(name, *a)
+    monkeypatch.setattr(E, 'call', counting)
+
+    class Boom(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, t):
+            return t.clone()
+
+        @staticmethod
+        def backward(ctx, gr):
+            raise RuntimeError('boom')
+
+    torch.manual_seed(3)
+    mods = [pcseg.MiniPointNet(32, [64, 64]).to(DEV).train() for _ in range(2)]
+    mods[1].load_state_dict(mods[0].state_dict())
+    x = torch.randn(8192, 32, device=DEV, requires_grad=True)
+    y = mods[0].forward_rows(Boom.apply(x), 32)
+    with pytest.raises(RuntimeError, match='boom'):
+        y.square().sum().backward()
+    torch.cuda.synchronize()
+    n0 = len(joins)
+    for m in mods:
+        m.zero_grad(set_to_none=True)
+        m.forward_rows(x.detach(), 32).square().sum().backward()
+    torch.cuda.synchronize()
+    assert len(joins) >= n0 + 2                             # both backwards joined the lane
+    for (k, a), (_, b) in zip(mods[0].named_parameters(), mods[1].named_parameters()):
+        assert torch.equal(a.grad, b.grad), k

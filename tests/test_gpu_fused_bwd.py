@@ -7,11 +7,10 @@ row count, and for bitwise reproducibility.
 
 The engine's default policy fuses only layers over >= 2^19 rows (SA1-sized: there the fused
 launch beats the dgrad + side-lane wgrad pair, PointNet++ step -1.2 %; on the smaller 128-wide
-layers the overlapped pair is faster).  So the width sweep runs in a child process with
-PCS_FUSED_BWD=1 (every thin inner layer fused), and one SA1-sized stack checks the default
-policy in this process."""
+layers the overlapped pair is faster).  So the width sweep sets the per-layer policy
+(pcs_mlp_layer.bwd_fuse, pcseg.engine.set_bwd_fuse) to 'all' (every thin inner layer fused),
+and one SA1-sized stack checks the default policy."""
 import os
-import subprocess
 import sys
 
 import pytest
@@ -47,11 +46,12 @@ def _fp64_stack(mod, x, pool_k):
     yield a
 
 
-def _run(widths, cin, B, H, W, pool_k, seed, need_dx=True):
+def _run(widths, cin, B, H, W, pool_k, seed, need_dx=True, fuse='all'):
     """need_dx=False: the stack's input takes no gradient (PointNet++ SA1's grouped rows), so
     its first layer runs the weight-gradient-only form."""
     torch.manual_seed(seed)
     mod = pcseg.MiniPointNet(cin, widths).cuda().train()
+    pcseg.engine.set_bwd_fuse(mod, fuse)
     x = torch.randn(B, cin, H, W, dtype=torch.float32)
     xg = x.cuda().requires_grad_(need_dx)
     if pool_k:
@@ -82,9 +82,10 @@ CASES = [
 ]
 
 
-def check_vs_fp64(cin, widths, pool_k, B=2, H=80, W=32, need_dx=True):
+def check_vs_fp64(cin, widths, pool_k, B=2, H=80, W=32, need_dx=True, fuse='all'):
     """M = B*H*W rows (default 5120 = 80 row tiles)."""
-    mod, x, gout, grads, gx = _run(widths, cin, B, H, W, pool_k, seed=cin + len(widths), need_dx=need_dx)
+    mod, x, gout, grads, gx = _run(widths, cin, B, H, W, pool_k, seed=cin + len(widths), need_dx=need_dx,
+                                   fuse=fuse)
     xd = x.double().requires_grad_()
     it = _fp64_stack(mod, xd, pool_k)
     params = [next(it) for _ in widths]
@@ -102,27 +103,44 @@ def check_vs_fp64(cin, widths, pool_k, B=2, H=80, W=32, need_dx=True):
         assert _rel(gx, xd.grad) < 1e-3, ('dX', _rel(gx, xd.grad))
 
 
-def test_fused_backward_width_sweep_vs_fp64():
-    """Every width pair, the pooled / plain top layers, ragged rows and reproducibility, with
-    every thin inner layer fused (child process, PCS_FUSED_BWD=1)."""
-    env = dict(os.environ, PCS_FUSED_BWD='1')
-    r = subprocess.run([sys.executable, os.path.abspath(__file__)], env=env, capture_output=True, text=True,
-                       timeout=600)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
-    assert 'fused sweep ok' in r.stdout
+@pytest.mark.parametrize('case', CASES, ids=[f'{c[0]}-{"x".join(map(str, c[1]))}-{c[2]}' for c in CASES])
+def test_fused_backward_width_sweep_vs_fp64(case):
+    """Every width pair and the pooled / plain top layers with every thin inner layer fused
+    (bwd_fuse = 'all'); first layers of <= 32 channels also in the weight-gradient-only form."""
+    check_vs_fp64(*case)
+    if case[0] <= 32:
+        check_vs_fp64(*case, need_dx=False)
+
+
+def test_fused_backward_ragged_and_bitwise():
+    check_ragged_rows()
+    check_bitwise_reproducible()
+
+
+def test_bwd_fuse_policy_is_per_call():
+    """Two stacks in one process with different policies: the 'all' stack's backward runs the
+    fused kernel, the 'off' stack's does not (no process-global switch)."""
+    from pcseg.engine import KernelProbe
+    names = {}
+    for fuse in ('all', 'off'):
+        with KernelProbe() as kp:
+            _run([64, 64], 64, 2, 40, 32, 0, seed=3, fuse=fuse)
+        names[fuse] = {r[0] for r in kp.records()}
+    assert any('fused_bwd_kernel' in n for n in names['all']), names['all']
+    assert not any('fused_bwd_kernel' in n for n in names['off']), names['off']
 
 
 def test_fused_backward_default_policy_sa1_sized():
     """SA1 of PointNet++ at batch 16: 16 x 1024 centroids x 32 neighbours = 2^19 rows, widths
     9 -> 32 -> 32 -> 64, pooled over 32 -- the layers the default policy fuses; the input takes
     no gradient, as in the model, so the first layer runs the weight-gradient-only form."""
-    check_vs_fp64(9, [32, 32, 64], 32, B=16, H=1024, W=32, need_dx=False)
+    check_vs_fp64(9, [32, 32, 64], 32, B=16, H=1024, W=32, need_dx=False, fuse='default')
 
 
 def check_ragged_rows():
     """M not a multiple of the 64-row tile: the last tile's missing rows contribute nothing."""
     B, H, W = 1, 2051, 1
-    mod, x, gout, grads, gx = _run([64, 64], 64, B, H, W, 0, seed=5)
+    mod, x, gout, grads, gx = _run([64, 64], 64, B, H, W, 0, seed=5)   # 64 x 64 inner layer fused
     xd = x.double().requires_grad_()
     it = _fp64_stack(mod, xd, 0)
     params = [next(it) for _ in range(2)]
@@ -141,15 +159,3 @@ def check_bitwise_reproducible():
         for ta, tb in zip(ga, gb):
             assert torch.equal(ta, tb)
     assert torch.equal(a[4], b[4])
-
-
-if __name__ == '__main__':        # the width sweep, run by test_fused_backward_width_sweep_vs_fp64
-    for case in CASES:
-        check_vs_fp64(*case)
-        print('ok', case, flush=True)
-        if case[0] <= 32:                       # first layer: weight gradient only
-            check_vs_fp64(*case, need_dx=False)
-            print('ok (no dX)', case, flush=True)
-    check_ragged_rows()
-    check_bitwise_reproducible()
-    print('fused sweep ok')

@@ -245,6 +245,25 @@ def test_dgcnn_three_way_all_tensors():
                                 chfirst=True), 'dgcnn')
 
 
+@pytest.mark.timeout(1200)
+def test_dgcnn_color_three_way_wide_regime_b16():
+    """BASELINE config 2's dispatch: B = 16 x N = 4096 gives M = 65 536 rows, the regime in which
+    DGCNN's conv5-7 run on the LDS-DMA wide GEMMs (gemm_big.hip) -- the data gradients of conv5 /
+    conv6 on gemm_nt_kernel<128, 4, 2, false>, conv7's on <256, 2, 4, false>, conv7's weight
+    gradient on wgrad_nt_kernel.  Every tensor three-way against the oracle (the reference
+    algorithm, dgcnn.py:165-257) on the oracle's own kNN graphs (replayed)."""
+    from pcseg.engine import KernelProbe
+    with KernelProbe() as kp:
+        rows = three_way(lambda: pcseg.DGCNNWithColor(14), lambda: R.DGCNNWithColor(14), 16, 4096, 111,
+                         chfirst=True)
+    names = {r[0] for r in kp.records()}
+    for k in ('pcs::gemm_nt_kernel<128, 4, 2, false>', 'pcs::gemm_nt_kernel<256, 2, 4, false>',
+              'pcs::gemm_nt_kernel<256, 2, 4, true>', 'pcs::wgrad_nt_kernel<128, 4, 2>'):
+        assert k in names, (k, sorted(names))
+    print('wide kernels exercised:', sorted(n for n in names if '_nt_' in n))
+    _assert_three_way(rows, 'dgcnn B=16 (M = 65536)')
+
+
 def test_dgcnn_xyz_three_way_all_tensors():
     """The xyz-only DGCNN (dgcnn.py:80-162) with a 6-channel input (it keeps xyz, :134-137)."""
     _assert_three_way(three_way(lambda: pcseg.DGCNN(13), lambda: R.DGCNN(13), 2, 1024, 110, chfirst=True,
