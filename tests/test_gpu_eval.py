@@ -55,9 +55,9 @@ def calibrated(ref_ctor, seed):
     bns = [m for m in ref.modules() if isinstance(m, torch.nn.modules.batchnorm._BatchNorm)]
     for m in bns:
         m.momentum = 1.0
-    cal, _, _ = make_batch(2, 2048, seed=seed + 1)
+    cal, _, _ = make_batch(6, 2048, seed=seed + 1)       # 6 samples: the TNet BN1d layers see a batch of 6
     ref.train()
-    with torch.no_grad(), R.replay(R.Replay(fps_starts=[torch.tensor([5, 9], dtype=torch.int32)] * 4)):
+    with torch.no_grad(), R.replay(R.Replay(fps_starts=[torch.tensor([5, 9, 1, 7, 3, 2], dtype=torch.int32)] * 4)):
         ref(cal)
     g = torch.Generator().manual_seed(seed + 2)
     with torch.no_grad():
