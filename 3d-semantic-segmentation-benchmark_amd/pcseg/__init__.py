@@ -12,7 +12,7 @@ from .models import (PointNetpp, PointNetppMSG, PointNeXt, EdgeConv, DGCNN, DGCN
                      TNet, PointNetEncoder, PointNetSeg, knn, get_graph_feature)
 from .loss import masked_onehot_cross_entropy
 from .replay import Replay, replay
-from . import metrics, inference
+from . import metrics, inference, graphs
 
 __all__ = ['sample', 'group', 'reduce', 'interpolate', 'MiniPointNet', 'UnitPointNet', 'SetAbstraction',
            'FeaturePropagation', 'InvResMLP', 'PointNetpp', 'PointNetppMSG', 'PointNeXt', 'EdgeConv', 'DGCNN',

@@ -20,6 +20,7 @@ P = ctypes.c_void_p
 I32 = ctypes.c_int
 I64 = ctypes.c_longlong
 F32 = ctypes.c_float
+F64 = ctypes.c_double
 
 
 class Operand(ctypes.Structure):
@@ -101,6 +102,7 @@ SIGNATURES = {
     'pcs_pad_onehot': [P, I32, P, P, P, I32, I32, I32, P, P, P],
     # optimizer
     'pcs_adam': [P, P, P, P, I64, F32, F32, F32, F32, F32, F32, F32, P],
+    'pcs_adam_dev': [P, P, P, P, I64, F32, F32, F32, F64, F64, F64, F32, F32, P, P],
     # loss
     'pcs_masked_ce_blocks': [I32, I32],
     'pcs_masked_ce': [P, I32, P, I32, I32, P, I32, I32, I32, P, P, P, P],

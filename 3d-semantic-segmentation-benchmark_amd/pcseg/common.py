@@ -24,11 +24,11 @@ def _fps_start(B: int, N: int, device) -> torch.Tensor:
     return torch.randint(0, N, (B,), dtype=torch.int, device=device)
 
 
-def sample_indices(coords: torch.Tensor, C: int):
-    """FPS -> (idx (B,C) int32, centroid coords (B,C,3))."""
+def sample_indices(coords: torch.Tensor, C: int, out=None):
+    """FPS -> (idx (B,C) int32, centroid coords (B,C,3)); out = (idx, centroids) to write into."""
     B, N, _ = coords.shape
     start = _fps_start(B, N, coords.device)
-    idx, cent = ops.fps(coords, C, start)
+    idx, cent = ops.fps(coords, C, start, out=out)
     rp = _replay()
     if rp is not None:
         rp.rec_fps_starts.append(start.detach().cpu())
@@ -41,8 +41,8 @@ def sample(coords: torch.Tensor, C: int) -> torch.Tensor:
     return sample_indices(coords, C)[1]
 
 
-def _ball(cent, coords, r, K):
-    idx = ops.ball_query(cent, coords, r, K)
+def _ball(cent, coords, r, K, out=None):
+    idx = ops.ball_query(cent, coords, r, K, out=out)
     rp = _replay()
     if rp is not None:
         rp.rec_group_idx.append(idx.detach().cpu())
@@ -110,7 +110,10 @@ class GeometryPlan:
     reference's sequence.  Consumers wait on the per-level event before reading.
     """
 
-    def __init__(self, coords: torch.Tensor, levels, interp: bool = True, inverse: bool = True):
+    def __init__(self, coords: torch.Tensor, levels, interp: bool = True, inverse: bool = True,
+                 into: 'GeometryPlan | None' = None):
+        """into: a plan of the same structure whose tensors this one writes into (no allocation:
+        the double-buffered plans of a HIP-graph-captured training step, pcseg.graphs)."""
         dev = coords.device
         main = torch.cuda.current_stream(dev)
         side = side_stream(dev)
@@ -119,16 +122,20 @@ class GeometryPlan:
         self.balls, self.events, self.nn = [], [], []
         made = []
         self.inverse = inverse
+        self.fps_idx = []
         with torch.cuda.stream(side):
             prev = coords
-            for C, queries in levels:
-                _, cent = sample_indices(prev, C)
+            for lv, (C, queries) in enumerate(levels):
+                fo = (into.fps_idx[lv], into.coords[lv + 1]) if into is not None else None
+                fidx, cent = sample_indices(prev, C, out=fo)
+                self.fps_idx.append(fidx)
                 bl = []
-                for r, K, on_self in queries:
+                for q, (r, K, on_self) in enumerate(queries):
                     src = cent if on_self else prev
-                    idx = _ball(cent, src, r, K)
+                    ib, iv = into.balls[lv][q] if into is not None else (None, None)
+                    idx = _ball(cent, src, r, K, out=ib)
                     # inverse map for the atomic-free backward of the feature gather
-                    inv = ops.inverse_index(idx, src.shape[1]) if inverse else None
+                    inv = ops.inverse_index(idx, src.shape[1], out=iv) if inverse else None
                     bl.append((idx, inv))
                     made += [idx, *(inv or ())]
                 ev = torch.cuda.Event()
@@ -136,16 +143,18 @@ class GeometryPlan:
                 self.coords.append(cent)
                 self.balls.append(bl)
                 self.events.append(ev)
-                made.append(cent)
+                made += [fidx, cent]
                 prev = cent
             if interp:
                 nn_ = []
                 for lv in range(len(levels) - 1, -1, -1):      # FP_L ... FP_1, the reference's order
-                    idx, dist = ops.knn_select(self.coords[lv], self.coords[lv + 1], 3)
+                    no = into.nn[lv] if into is not None else (None, None, None)
+                    idx, dist = ops.knn_select(self.coords[lv], self.coords[lv + 1], 3,
+                                               out=(no[0], no[1]) if into is not None else None)
                     rp = _replay()
                     if rp is not None:
                         rp.rec_interp_idx.append(idx.detach().cpu())
-                    inv = ops.inverse_index(idx, self.coords[lv + 1].shape[1]) if inverse else None
+                    inv = ops.inverse_index(idx, self.coords[lv + 1].shape[1], out=no[2]) if inverse else None
                     nn_.append((idx, dist, inv))
                     made += [idx, dist, *(inv or ())]
                 self.nn = nn_[::-1]                             # nn[lv] pairs level lv with lv + 1
@@ -212,8 +221,9 @@ class GeometryPrefetch:
     query / 3-NN of the next batch overlap that backward.  The next forward with
     the same, unmodified tensor consumes it; anything else recomputes."""
 
-    def prefetch_geometry(self, x: torch.Tensor) -> None:
-        self._pcs_prefetched = (x, x._version, self._plan_for(self._coords_of(x)))
+    def prefetch_geometry(self, x: torch.Tensor, into: GeometryPlan | None = None) -> None:
+        """into: write the plan into an existing plan's tensors (see GeometryPlan)."""
+        self._pcs_prefetched = (x, x._version, self._plan_for(self._coords_of(x), into=into))
 
     def prefetch_geometry_in_backward(self, x: torch.Tensor) -> None:
         """Arm a prefetch for the NEXT forward: it hooks the gradient of a mid-network

@@ -52,9 +52,9 @@ class PointNetpp(GeometryPrefetch, nn.Module):
         self.drop = nn.Dropout(0.5)
         self.conv = nn.Conv1d(128, part_classes, 1)
 
-    def _plan_for(self, c0, inverse=True):
+    def _plan_for(self, c0, inverse=True, into=None):
         return GeometryPlan(c0, [(sa.C, [(sa.radius, sa.K, False)]) for sa in (self.sa1, self.sa2, self.sa3, self.sa4)],
-                            inverse=inverse)
+                            inverse=inverse, into=into)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         B, N, _ = x.shape
@@ -108,9 +108,9 @@ class PointNetppMSG(GeometryPrefetch, nn.Module):
         self.drop = nn.Dropout(0.5)
         self.conv = nn.Conv1d(128, part_classes, 1)
 
-    def _plan_for(self, c0, inverse=True):
+    def _plan_for(self, c0, inverse=True, into=None):
         return GeometryPlan(c0, [(br[0].C, [(sa.radius, sa.K, False) for sa in br]) for br in self.levels],
-                            inverse=inverse)
+                            inverse=inverse, into=into)
 
     def _sa_level(self, branches, coords, feats, geo, level):
         C = branches[0].C
@@ -171,14 +171,14 @@ class PointNeXt(GeometryPrefetch, nn.Module):
         self.drop = nn.Dropout(0.5)
         self.conv = nn.Conv1d(fp1, part_classes, 1)
 
-    def _plan_for(self, c0, inverse=True):
+    def _plan_for(self, c0, inverse=True, into=None):
         def q(m, on_self):
             return (m.radius, m.K, on_self)
         return GeometryPlan(c0, [
             (self.sa1.C, [q(self.sa1, False), q(self.irmlp1, True)]),
             (self.sa2.C, [q(self.sa2, False), q(self.irmlp2, True), q(self.irmlp2_1, True)]),
             (self.sa3.C, [q(self.sa3, False), q(self.irmlp3, True)]),
-            (self.sa4.C, [q(self.sa4, False), q(self.irmlp4, True)])], inverse=inverse)
+            (self.sa4.C, [q(self.sa4, False), q(self.irmlp4, True)])], inverse=inverse, into=into)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         B, N, Cin = x.shape

@@ -27,40 +27,50 @@ def radius_sq_f32(r: float) -> float:
 
 
 # ------------------------------------------------------------------ neighbour search (no grad)
-def fps(xyz: torch.Tensor, C: int, start: torch.Tensor):
-    """xyz (B,N,3) -> (idx (B,C) int32, centroids (B,C,3))."""
+def _out(out, shape, dtype, dev):
+    """`out` (a preallocated tensor of that shape / dtype, e.g. a graph-resident buffer) or a new one."""
+    if out is None:
+        return torch.empty(shape, dtype=dtype, device=dev)
+    if tuple(out.shape) != tuple(shape) or out.dtype != dtype or not out.is_contiguous():
+        raise ValueError(f'out: expected a contiguous {dtype} tensor of shape {tuple(shape)}, got {out.dtype} '
+                         f'{tuple(out.shape)}')
+    return out
+
+
+def fps(xyz: torch.Tensor, C: int, start: torch.Tensor, out=None):
+    """xyz (B,N,3) -> (idx (B,C) int32, centroids (B,C,3)); out = (idx, centroids) to write into."""
     check_cuda(xyz)
     xyz = _c(xyz.float())
     B, N, _ = xyz.shape
     start = _c(start.to(device=xyz.device, dtype=torch.int32))
-    idx = torch.empty((B, C), dtype=torch.int32, device=xyz.device)
-    cent = torch.empty((B, C, 3), dtype=torch.float32, device=xyz.device)
+    idx = _out(out[0] if out else None, (B, C), torch.int32, xyz.device)
+    cent = _out(out[1] if out else None, (B, C, 3), torch.float32, xyz.device)
     call('pcs_fps', ptr(xyz), B, N, C, ptr(start), ptr(idx), ptr(cent), stream_ptr(xyz.device))
     return idx, cent
 
 
-def ball_query(cent: torch.Tensor, xyz: torch.Tensor, r: float, K: int) -> torch.Tensor:
+def ball_query(cent: torch.Tensor, xyz: torch.Tensor, r: float, K: int, out=None) -> torch.Tensor:
     check_cuda(cent, xyz)
     cent, xyz = _c(cent.float()), _c(xyz.float())
     B, C, _ = cent.shape
     N = xyz.shape[1]
     if K > N:
         raise RuntimeError(f'selected index k out of range (K={K} > N={N})')
-    out = torch.empty((B, C, K), dtype=torch.int32, device=xyz.device)
+    out = _out(out, (B, C, K), torch.int32, xyz.device)
     call('pcs_ball_query', ptr(cent), ptr(xyz), B, C, N, radius_sq_f32(r), K, ptr(out), stream_ptr(xyz.device))
     return out
 
 
-def knn_select(query: torch.Tensor, ref: torch.Tensor, k: int = 3):
-    """(idx (B,N,k) int32, squared dist (B,N,k)) of the k nearest ref points."""
+def knn_select(query: torch.Tensor, ref: torch.Tensor, k: int = 3, out=None):
+    """(idx (B,N,k) int32, squared dist (B,N,k)) of the k nearest ref points; out = (idx, dist)."""
     check_cuda(query, ref)
     query, ref = _c(query.float()), _c(ref.float())
     B, N, _ = query.shape
     M = ref.shape[1]
     if k > M:
         raise RuntimeError(f'selected index k out of range (k={k} > M={M})')
-    idx = torch.empty((B, N, k), dtype=torch.int32, device=query.device)
-    dist = torch.empty((B, N, k), dtype=torch.float32, device=query.device)
+    idx = _out(out[0] if out else None, (B, N, k), torch.int32, query.device)
+    dist = _out(out[1] if out else None, (B, N, k), torch.float32, query.device)
     call('pcs_knn_select', ptr(query), ptr(ref), B, N, M, k, ptr(idx), ptr(dist), stream_ptr(query.device))
     return idx, dist
 
@@ -76,10 +86,10 @@ def knn(x: torch.Tensor, k: int) -> torch.Tensor:
     return out
 
 
-def inverse_index(idx: torch.Tensor, targets: int):
+def inverse_index(idx: torch.Tensor, targets: int, out=None):
     """CSR inverse of a neighbour table idx (B, S, k) int32 with values in [0, targets):
     (offsets (B*targets+1,), entries (B*S*k,)) int32 -- the slots reading each source point,
-    ascending.  Feeds the atomic-free, fixed-order gather backward."""
+    ascending.  Feeds the atomic-free, fixed-order gather backward.  out = (offsets, entries)."""
     check_cuda(idx)
     idx = _c(idx.to(torch.int32))
     B = idx.shape[0]
@@ -90,8 +100,8 @@ def inverse_index(idx: torch.Tensor, targets: int):
     if rc:
         raise RuntimeError(lib.pcs_last_error().decode())
     ws = torch.empty(max(int(need.value), 1), dtype=torch.uint8, device=idx.device)
-    offsets = torch.empty(B * targets + 1, dtype=torch.int32, device=idx.device)
-    entries = torch.empty(B * per, dtype=torch.int32, device=idx.device)
+    offsets = _out(out[0] if out else None, (B * targets + 1,), torch.int32, idx.device)
+    entries = _out(out[1] if out else None, (B * per,), torch.int32, idx.device)
     call('pcs_inverse_index', ptr(idx), B, per, targets, ptr(offsets), ptr(entries), ptr(ws), int(need.value),
          stream_ptr(idx.device))
     return offsets, entries

@@ -6,11 +6,11 @@ FlatAdam moves the parameters into a second flat buffer with the same layout (ev
 an optimizer step is a single memory-bound kernel instead of torch.optim.Adam's
 ~10 foreach launches per parameter group.  Same update and fp32 operation order as
 torch.optim.Adam's default path (the reference trains with Adam, lr 1e-3:
-Training/train_model.py:263, models/dgcnn/train.py:79).
+Training/train_model.py:263, models/dgcnn/train.py:79).  The step count lives on the device
+(pcs_adam_dev derives the bias corrections there), so a training step captured in a HIP
+graph (pcseg.graphs) replays with the right corrections.
 """
 from __future__ import annotations
-
-import math
 
 import torch
 
@@ -35,23 +35,24 @@ class FlatAdam:
                 p.data = self.flat[off:off + n].view_as(p)
         self.exp_avg = torch.zeros_like(self.flat)
         self.exp_avg_sq = torch.zeros_like(self.flat)
-        self.t = 0
+        # {int64 t; float step; float bc2_sqrt} (pcs_adam_dev)
+        self.state = torch.zeros(2, dtype=torch.int64, device=self.flat.device)
 
     def zero_grad(self, set_to_none: bool = False) -> None:
         self.grads.zero_grad()
 
+    @property
+    def t(self) -> int:
+        """Steps taken (a device read: synchronises)."""
+        return int(self.state[0])
+
     @torch.no_grad()
     def step(self) -> None:
-        self.t += 1
         b1, b2 = self.betas
-        bc1 = 1 - b1 ** self.t
-        step = -(self.lr / bc1)
-        bc2_sqrt = math.sqrt(1 - b2 ** self.t)
-        if self.flat.is_cuda:
-            # the engine's deferred weight gradients are joined at the end of every backward; join
-            # again here so no path (e.g. a backward that raised before its final callbacks ran)
-            # lets the update read partial gradients
-            lane_join(self.flat.device)
-        call('pcs_adam', ptr(self.flat), ptr(self.grads.flat), ptr(self.exp_avg), ptr(self.exp_avg_sq),
-             self.flat.numel(), 1 - b1, b2, 1 - b2, step, bc2_sqrt, self.eps, self.weight_decay,
+        # the engine's deferred weight gradients are joined at the end of every backward; join
+        # again here so no path (e.g. a backward that raised before its final callbacks ran)
+        # lets the update read partial gradients
+        lane_join(self.flat.device)
+        call('pcs_adam_dev', ptr(self.flat), ptr(self.grads.flat), ptr(self.exp_avg), ptr(self.exp_avg_sq),
+             self.flat.numel(), 1 - b1, b2, 1 - b2, self.lr, b1, b2, self.eps, self.weight_decay, ptr(self.state),
              stream_ptr(self.flat.device))

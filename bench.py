@@ -226,15 +226,12 @@ def run_workload(key, batch, npoints, args, world, rank, dev):
     broadcast_model(model)
     grads = FlatGradAllReduce(model)
     use_graph = args.graph and world == 1
-    if use_graph:      # graph replays need device-side step counters
-        opt = torch.optim.Adam(model.parameters(), lr=1e-3, capturable=True)
-    else:              # one HIP launch over the flat parameter / gradient buffers
-        opt = FlatAdam(grads, lr=1e-3)
+    opt = FlatAdam(grads, lr=1e-3)          # one HIP launch; step count on the device (capturable)
     pts, labels, lengths = make_batch(batch, npoints, seed=1000 * 2 + rank)
     x = model_input(pts.to(dev), kind)
     lab = (labels.float() if kind == 'chfirst6' else labels).to(dev)
     lengths = lengths.to(dev)
-    prefetch = hasattr(model, 'prefetch_geometry') and not args.no_prefetch and not use_graph
+    prefetch = hasattr(model, 'prefetch_geometry') and not args.no_prefetch
 
     in_bwd = args.prefetch_point == 'backward'
 
@@ -255,48 +252,15 @@ def run_workload(key, batch, npoints, args, world, rank, dev):
 
     eager_step = step
     if use_graph:
-        graph_prefetch = hasattr(model, 'prefetch_geometry') and not args.no_prefetch
-        side = torch.cuda.Stream(dev)
-        side.wait_stream(torch.cuda.current_stream(dev))
-        with torch.cuda.stream(side):
-            for _ in range(max(args.warmup, 2)):
-                step()
-            plan = None
-            if graph_prefetch:
-                # double-buffered geometry: the captured forward reads `plan`; the captured
-                # prefetch computes the next step's plan under the backward and the step ends
-                # by copying it into `plan` (a few MB of indices), ready for the next replay
-                model.prefetch_geometry(x)
-                plan = model._pcs_prefetched[2]
-                torch.cuda.synchronize(dev)
-                plan.settle()
-        torch.cuda.current_stream(dev).wait_stream(side)
-
-        def graph_body():
-            if plan is not None:
-                model._pcs_prefetched = (x, x._version, plan)
-            grads.zero_grad()
-            loss = pcseg.masked_onehot_cross_entropy(logits_of(model(x)), lab, lengths)
-            nxt = None
-            if plan is not None:
-                model.prefetch_geometry(x)
-                nxt = model._pcs_prefetched[2]
-            loss.backward()
-            grads.synchronize()
-            opt.step()
-            if nxt is not None:
-                plan.copy_from(nxt)
-                model._pcs_prefetched = None
-            return loss
-
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            static_loss = graph_body()
-        prefetch = plan is not None
+        # the whole step in two alternating HIP graphs (pcseg.graphs.CapturedStep): one
+        # hipGraphLaunch per step; the next step's geometry still runs under the backward
+        from pcseg.graphs import CapturedStep
+        cs = CapturedStep(model, x, lab, lengths, grads, opt, pcseg.masked_onehot_cross_entropy, logits_of,
+                          warmup=2, prefetch=not args.no_prefetch)
+        prefetch = cs.prefetch
 
         def step():
-            graph.replay()
-            return static_loss
+            return cs.step()
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
@@ -373,7 +337,8 @@ def main():
     ap.add_argument('--roofline-replay', action='store_true',
                     help='also time the dominant kernel\'s launches replayed back to back (rewrites outputs)')
     ap.add_argument('--graph', action='store_true',
-                    help='capture one training step in a HIP graph and time its replays (N=1, no prefetch)')
+                    help='capture the training step in HIP graphs (pcseg.graphs.CapturedStep) and time its replays '
+                         '(N=1 only; multi-GPU steps run eagerly)')
     ap.add_argument('--prefetch-point', choices=['backward', 'loss'], default='loss',
                     help="where the next step's geometry is enqueued: between the loss and backward() (default) "
                          "or from a gradient hook inside the backward (round 2 A/B: within noise, 5.50 vs 5.52 ms)")

@@ -394,6 +394,13 @@ int pcs_gather_blocks(const float* points, const uint8_t* labels,
 int pcs_adam(float* p, const float* g, float* m, float* v, long long n, float beta1_w,
              float beta2, float beta2_w, float step, float bc2_sqrt, float eps,
              float weight_decay, void* stream);
+/* pcs_adam with the step count on the device (graph-capturable: a captured step replays
+ * correctly): state = 16 B of zero-initialised device memory {int64 t; float coef[2]}; each
+ * call does t += 1 and the bias corrections step = -lr / (1 - beta1^t), bc2_sqrt =
+ * sqrt(1 - beta2^t) in double on the device (the host path's arithmetic), then the update. */
+int pcs_adam_dev(float* p, const float* g, float* m, float* v, long long n, float beta1_w,
+                 float beta2_f, float beta2_w, double lr, double beta1, double beta2, float eps,
+                 float weight_decay, long long* state, void* stream);
 
 /* ---- loss ---------------------------------------------------------------- */
 
