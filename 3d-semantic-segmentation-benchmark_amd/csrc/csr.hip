@@ -317,6 +317,9 @@ PCS_API int pcs_inverse_index(const int32_t* idx, int B, int per_batch, int targ
                   ws_bytes, inv_ws_bytes(n, T));
     hipStream_t s = as_stream(stream);
     int32_t* scratch = static_cast<int32_t*>(workspace);
+    // algorithmic bytes of the map (both kernels): idx read, entries + offsets written
+    ProbeScope pr(s, 0.0, 8.0 * (double)n + 4.0 * (double)(T + 1),
+                  targets <= kInvLdsTargets ? "pcs::inverse_index+sort<true>" : "pcs::inverse_index+sort<false>");
     int* gcnt = reinterpret_cast<int*>(static_cast<char*>(workspace) + ((size_t)n * 4 + 255) / 256 * 256);
     if (targets <= kInvLdsTargets) {
         static const hipError_t attr = hipFuncSetAttribute(
@@ -341,6 +344,9 @@ PCS_API int pcs_group_bwd_csr(const float* grad_out, int ld_gout, const int32_t*
     const long long total = (long long)B * N * D, targets = (long long)B * N;
     PCS_CHECK_ARG(total < (1ll << 31), "pcs_group_bwd_csr: too many elements");
     PCS_CHECK_ARG(grad_out && offsets && entries && grad_feats, "pcs_group_bwd_csr: null pointer");
+    // algorithmic bytes (SURVEY.md 8(d) group bwd): the D gradient columns of every grouped row
+    // read once, the source gradient written, the map read
+    ProbeScope pr(as_stream(stream), 0.0, 8.0 * (double)total + 4.0 * (double)(targets + 1), "pcs::group_bwd_csr_kernel");
     hipLaunchKernelGGL(group_bwd_csr_kernel, dim3((unsigned)((targets + 3) / 4)), dim3(256), 0, as_stream(stream),
                        grad_out, ld_gout, offsets, entries, (int)targets, D, grad_feats);
     return launch_status("pcs_group_bwd_csr");
@@ -354,6 +360,7 @@ PCS_API int pcs_interp_bwd_csr(const float* grad_out, int ld_gout, int col_off, 
     const long long total = (long long)B * M * D, targets = (long long)B * M;
     PCS_CHECK_ARG(total < (1ll << 31), "pcs_interp_bwd_csr: too many elements");
     PCS_CHECK_ARG(grad_out && dist && offsets && entries && grad_pts, "pcs_interp_bwd_csr: null pointer");
+    ProbeScope pr(as_stream(stream), 0.0, 8.0 * (double)total + 4.0 * (double)(targets + 1), "pcs::interp_bwd_csr_kernel");
     hipLaunchKernelGGL(interp_bwd_csr_kernel, dim3((unsigned)((targets + 3) / 4)), dim3(256), 0, as_stream(stream),
                        grad_out, ld_gout, col_off, dist, offsets, entries, (int)targets, D, grad_pts);
     return launch_status("pcs_interp_bwd_csr");

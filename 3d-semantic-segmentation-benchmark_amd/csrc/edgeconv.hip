@@ -281,7 +281,13 @@ PCS_API int pcs_edgeconv_fwd(const float* X, int ldx, int C, const int32_t* idx,
         return e;
     double* part = static_cast<double*>(workspace);
     const int nb = fwd_blocks(G, Cout);
-    hipLaunchKernelGGL(edgeconv_fwd_kernel, dim3(nb), dim3(256), 0, st, Y, PQ, idx, N, k, Cout, G, pz, pa, S, part);
+    {
+        // compulsory bytes: Y, Q and idx read once, (max z, min z, S) fp32 + 2 argmax u8 written;
+        // flops: the k edge values (2 adds) and BN sums (3) per (point, channel)
+        ProbeScope pr(st, 5.0 * (double)G * k * Cout, 4.0 * (double)G * (2.0 * Cout + k) + 14.0 * (double)G * Cout,
+                      "pcs::edgeconv_fwd_kernel");
+        hipLaunchKernelGGL(edgeconv_fwd_kernel, dim3(nb), dim3(256), 0, st, Y, PQ, idx, N, k, Cout, G, pz, pa, S, part);
+    }
     bn_finalize_launch(part, nb, Cout, G * k, gamma, beta, eps, momentum, run_mean, run_var, coef, coef + Cout,
                        coef + 2 * Cout, coef + 3 * Cout, num_batches, st);
     return pool_finalize(pz, pa, G, Cout, coef, coef + Cout, ACT_LRELU, slope, out, arg, st);
@@ -325,8 +331,13 @@ PCS_API int pcs_edgeconv_bwd(const float* X, int ldx, int C, const int32_t* csr_
     const unsigned eg = (unsigned)std::min<long long>((GN + 255) / 256, 65536);
     hipLaunchKernelGGL(edgeconv_bwd_center_kernel, dim3(eg), dim3(256), 0, st, dout, pz, S, G, Cout, k, coef, kBC,
                        slope, D, Gd);
-    hipLaunchKernelGGL(edgeconv_bwd_gather_kernel, dim3((unsigned)((G + 3) / 4)), dim3(256), 0, st, Y, Q, D, arg,
-                       csr_off, csr_ent, G, Cout, k, coef, kBC, Gd);
+    {
+        // compulsory bytes: Y, Q, D, arg and the inverse map read once, the (dY | dP) rows written
+        ProbeScope pr(st, 0.0, 4.0 * (double)G * Cout * 3 + (double)G * Cout + 4.0 * (double)G * (k + 1) +
+                                   8.0 * (double)G * Cout, "pcs::edgeconv_bwd_gather_kernel");
+        hipLaunchKernelGGL(edgeconv_bwd_gather_kernel, dim3((unsigned)((G + 3) / 4)), dim3(256), 0, st, Y, Q, D, arg,
+                           csr_off, csr_ent, G, Cout, k, coef, kBC, Gd);
+    }
     if (int e = launch_status("pcs_edgeconv_bwd")) return e;
     // dW (as 2Cout x C) += G^T X ;  dX = G W_int
     const pcs_operand ga = plain(Gd, 2 * Cout);

@@ -261,7 +261,14 @@ PCS_API int pcs_fps(const float* xyz, int B, int N, int C, const int32_t* start,
     // threads per cloud by size (round-1 sweep)
     const int blk = N <= 256 ? 64 : (N <= 2048 ? 256 : (N <= 8192 ? 512 : 1024));
     const int ppt = (N + blk - 1) / blk;
-#define PCS_FPS_CASE(BL, PP) if (blk == BL && ppt <= PP) { launch_fps<BL, PP>(xyz, B, N, C, start, out_idx, out_xyz, s); } else
+    // algorithmic: C serial steps over N points per cloud (8 fp32 flops per distance + update);
+    // the cloud read once, C (index, xyz) written.  A latency-bound chain: see DESIGN.md 3.1
+    const double flops = 8.0 * B * (double)N * C, bytes = (double)B * (12.0 * N + 16.0 * C);
+#define PCS_FPS_CASE(BL, PP)                                                                    \
+    if (blk == BL && ppt <= PP) {                                                               \
+        ProbeScope pr(s, flops, bytes, "pcs::fps_kernel<%d, %d>", BL, PP);                     \
+        launch_fps<BL, PP>(xyz, B, N, C, start, out_idx, out_xyz, s);                           \
+    } else
     PCS_FPS_CASE(64, 1) PCS_FPS_CASE(64, 2) PCS_FPS_CASE(64, 4) PCS_FPS_CASE(64, 8)
     PCS_FPS_CASE(256, 1) PCS_FPS_CASE(256, 2) PCS_FPS_CASE(256, 4) PCS_FPS_CASE(256, 8) PCS_FPS_CASE(256, 16)
     PCS_FPS_CASE(512, 2) PCS_FPS_CASE(512, 4) PCS_FPS_CASE(512, 8) PCS_FPS_CASE(512, 16)

@@ -196,6 +196,11 @@ PCS_API int pcs_group_fwd(const float* xyz, const float* feats, const float* cen
     const long long total = (long long)B * C * K * ld_out;
     if (total == 0) return 0;
     if (ld_out % 4 == 0 && (uintptr_t)out % 16 == 0) {
+        // algorithmic bytes (SURVEY.md 8(d) group fwd): source points + centroids + idx read once,
+        // the grouped rows written
+        ProbeScope pr(as_stream(stream), 0.0,
+                      4.0 * ((double)B * N * (3 + D) + 3.0 * B * C + (double)B * C * K) + 4.0 * (double)total,
+                      "pcs::group_fwd_q_kernel");
         hipLaunchKernelGGL(group_fwd_q_kernel, grid_for(total / 4), dim3(256), 0, as_stream(stream), xyz, feats,
                            centroids, idx, C, N, K, D, r, normalize, out, ld_out / 4, total / 4);
         return launch_status("pcs_group_fwd");
@@ -272,6 +277,11 @@ PCS_API int pcs_interp_cat_fwd(const float* f1, int D1, const float* pts, const 
     PCS_CHECK_ARG(((uintptr_t)out | (uintptr_t)pts | (uintptr_t)f1) % 16 == 0, "pcs_interp_cat_fwd: 16-B alignment");
     const long long total = (long long)B * N * ((D1 + D2) / 4);
     if (total == 0) return 0;
+    // algorithmic bytes (SURVEY.md 8(d) interp fwd): coarse features + skip + (idx, dist) read
+    // once, the concatenated rows written
+    ProbeScope pr(as_stream(stream), 9.0 * (double)B * N * D2,
+                  4.0 * ((double)B * M * D2 + (double)B * N * D1 + 6.0 * B * N + (double)B * N * (D1 + D2)),
+                  "pcs::interp_cat_q_kernel");
     hipLaunchKernelGGL(interp_cat_q_kernel, grid_for(total), dim3(256), 0, as_stream(stream), f1, D1, pts, idx, dist,
                        N, M, D2, out, ld_out / 4, total);
     return launch_status("pcs_interp_cat_fwd");

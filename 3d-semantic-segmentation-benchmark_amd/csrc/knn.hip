@@ -486,6 +486,10 @@ static void launch_knn(const float* x, int B, int N, int* out, float* xx, hipStr
         if (xx) {
             const long long P = (long long)B * N;
             hipLaunchKernelGGL((knn_sqnorm_kernel<F>), dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, x, P, xx);
+            // algorithmic: the N x N inner-product tile per cloud (2F flops per pair, the
+            // reference's bmm), x read + the k-lists written
+            ProbeScope pr(s, 2.0 * F * (double)N * N * B, 4.0 * (double)B * N * (F + K), "pcs::knn_wave_kernel<%d, %d, %d, true>",
+                          F, K, KNN_WAVES);
             hipLaunchKernelGGL((knn_wave_kernel<F, K, KNN_WAVES, true>), dim3(rb * B), dim3(64 * KNN_WAVES), 0, s, x, B,
                                N, rb, out, (const float*)xx);
         } else {

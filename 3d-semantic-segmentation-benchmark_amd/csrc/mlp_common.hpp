@@ -161,10 +161,7 @@ const char* wgrad_nt_name(int N, int K, int M);
 // monotone in z, so this is max_k act(s*z_k + t) with its first argmax
 int pool_finalize(const float* pz, const unsigned char* pa, long long G, int N, const float* s, const float* t,
                   int act, float slope, float* out, unsigned char* arg, hipStream_t st);
-// engine launch probe (probe.cpp)
-bool probe_enabled();
-int probe_start(const char* name, double flops, double bytes, hipStream_t s, std::function<void()> relaunch);
-void probe_stop(int idx, hipStream_t s);
+// engine launch probe: probe_enabled / probe_start / probe_stop (pcs_common.hpp, probe.cpp)
 // weight gradient with deterministic partials: workspace bytes for (N, K, M), and the launch
 size_t wgrad_ws_bytes(int N, int K, int M);
 int wgrad_launch(const pcs_operand* x, int N, const pcs_operand* y, int K, int M, float* dW, float* db, void* ws,

@@ -8,15 +8,44 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <stdarg.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <string.h>
+
+#include <functional>
 
 #include "../../include/pcseg.h"   // the ABI this library implements (prototype check)
 
 #define PCS_API extern "C" __attribute__((visibility("default")))
 
 namespace pcs {
+
+// ------------------------------------------------------------ launch probe (probe.cpp)
+// While enabled (pcs_probe_begin .. pcs_probe_end), a launch bracketed by probe_start /
+// probe_stop is timed by two HIP events on its own stream and recorded with the kernel
+// name as rocprofv3 reports it and its algorithmic flops / bytes (bench.py's roofline).
+bool probe_enabled();
+int probe_start(const char* name, double flops, double bytes, hipStream_t s, std::function<void()> relaunch);
+void probe_stop(int idx, hipStream_t s);
+
+// scoped form for single-launch entry points: the name is formatted only while probing
+struct ProbeScope {
+    int idx = -1;
+    hipStream_t s;
+    ProbeScope(hipStream_t st, double flops, double bytes, const char* fmt, ...) : s(st) {
+        if (!probe_enabled()) return;
+        char nm[128];
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(nm, sizeof nm, fmt, ap);
+        va_end(ap);
+        idx = probe_start(nm, flops, bytes, st, {});
+    }
+    ~ProbeScope() { probe_stop(idx, s); }
+    ProbeScope(const ProbeScope&) = delete;
+    ProbeScope& operator=(const ProbeScope&) = delete;
+};
 
 // ------------------------------------------------------------ error plumbing
 void set_error(const char* fmt, ...);

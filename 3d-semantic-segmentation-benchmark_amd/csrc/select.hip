@@ -478,8 +478,13 @@ static int run_select(Geo g, hipStream_t s, const char* what) {
     const bool heap_path = (long long)g.K * 64 <= g.N;
     const bool stage = g.N <= kStageMaxPoints;
     const size_t xyz_lds = stage ? ((size_t)g.N * 12 + 15) / 16 * 16 : 0;
+    // algorithmic work per launch: R x N un-fused distances (8 flops each) per cloud; bytes =
+    // both point sets read once + the neighbour lists written (SURVEY.md 8(d) neighbour-op model)
+    const double flops = 8.0 * g.B * (double)g.R * g.N;
+    const double bytes = 12.0 * g.B * ((double)g.N + g.R) + 4.0 * g.B * (double)g.R * g.K * (g.out_dist ? 2 : 1);
     if (heap_path && g.K == 3 && !g.use_radius) {
         const dim3 grid((g.R + 255) / 256, g.B);
+        ProbeScope pr(s, flops, bytes, "pcs::three_nn_kernel<%s>", stage ? "true" : "false");
         if (stage) hipLaunchKernelGGL(three_nn_kernel<true>, grid, dim3(256), xyz_lds, s, g);
         else hipLaunchKernelGGL(three_nn_kernel<false>, grid, dim3(256), 0, s, g);
         return launch_status(what);
@@ -490,6 +495,7 @@ static int run_select(Geo g, hipStream_t s, const char* what) {
         const int waves = (g.R + rows_per_wave - 1) / rows_per_wave;
         constexpr int wpb = kHeapBlock / kWave;
         const dim3 grid((waves + wpb - 1) / wpb, g.B);
+        ProbeScope pr(s, flops, bytes, "pcs::heap_select_kernel<%s>", stage ? "true" : "false");
         if (stage) hipLaunchKernelGGL(heap_select_kernel<true>, grid, dim3(kHeapBlock), xyz_lds, s, g, rows_per_wave);
         else hipLaunchKernelGGL(heap_select_kernel<false>, grid, dim3(kHeapBlock), 0, s, g, rows_per_wave);
         return launch_status(what);
@@ -503,6 +509,7 @@ static int run_select(Geo g, hipStream_t s, const char* what) {
     while (wpb > 1 && xyz_lds + wpb * row_lds > 64 * 1024) wpb >>= 1;
     const dim3 grid((waves + wpb - 1) / wpb, g.B);
     const size_t lds = xyz_lds + wpb * row_lds;
+    ProbeScope pr(s, flops, bytes, "pcs::intro_select_kernel<%s>", stage ? "true" : "false");
     if (stage) hipLaunchKernelGGL(intro_select_kernel<true>, grid, dim3(64 * wpb), lds, s, g, rows_per_wave);
     else hipLaunchKernelGGL(intro_select_kernel<false>, grid, dim3(64 * wpb), lds, s, g, rows_per_wave);
     return launch_status(what);

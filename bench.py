@@ -55,6 +55,8 @@ WORKLOADS = {
                  'PointNet seg, 4096 pts, batch 32/GPU (configs[0] model on the GPU)'),
 }
 METRIC = 'points/sec fwd+bwd, 4096-pt S3DIS blocks, PointNet++/DGCNN @1/2/4/8 GPU'
+# CPU baseline batch per workload: a bounded sample of the same workload, ~5-6 s per CPU step
+CPU_BATCH = {'pointnetpp': 32, 'dgcnn': 8, 'pointnetpp_msg': 16, 'pointnext': 2, 'pointnet': 16}
 HBM_PEAK_GBS = 8000.0           # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP32_PEAK_TFLOPS = 157.3        # fp32 MFMA dense (= fp32 vector) peak
 RIDGE = FP32_PEAK_TFLOPS * 1e12 / (HBM_PEAK_GBS * 1e9)     # flop / byte
@@ -111,8 +113,8 @@ def cpu_baseline_worker(args):
     t0 = time.perf_counter()
     step()
     warm = time.perf_counter() - t0
-    # timed steps: as many as fit in ~cpu_budget seconds (at least 2)
-    n = max(2, min(args.cpu_steps, int(args.cpu_budget / max(warm, 1e-3))))
+    # timed steps: cpu_steps (>= 5 by default), fewer only past ~cpu_budget seconds, at least 3
+    n = max(3, min(args.cpu_steps, int(args.cpu_budget / max(warm, 1e-3))))
     times = []
     for _ in range(n):
         t0 = time.perf_counter()
@@ -126,19 +128,29 @@ def cpu_baseline_worker(args):
                                 f'{n} steps ({sum(times):.1f} s timed)'}))
 
 
-def run_cpu_baseline(args, key, batch, npoints):
-    aff, phys = host_cpu_info()
-    # the box's CPU share for one GPU is 16 threads (OMP_NUM_THREADS there); nproc shows the whole host
-    threads = args.cpu_threads or min(aff, int(os.environ.get('OMP_NUM_THREADS', '16') or 16), 16)
+def _cpu_run(args, key, batch, npoints, threads):
     env = dict(os.environ, HIP_VISIBLE_DEVICES='', CUDA_VISIBLE_DEVICES='', OMP_NUM_THREADS=str(threads))
     cmd = [sys.executable, os.path.abspath(__file__), '--cpu-baseline-worker', '--model', key,
-           '--npoints', str(npoints), '--cpu-batch', str(args.cpu_batch or batch), '--cpu-steps',
+           '--npoints', str(npoints), '--cpu-batch', str(batch), '--cpu-steps',
            str(args.cpu_steps), '--cpu-threads', str(threads), '--cpu-budget', str(args.cpu_budget)]
     try:
         out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=900, check=True).stdout
-        res = json.loads(out.strip().splitlines()[-1])
+        return json.loads(out.strip().splitlines()[-1])
     except Exception as e:  # noqa: BLE001 -- the baseline is informative, never fatal
-        res = {'value': None, 'unit': 'points/s', 'cores': threads, 'kind': 'port', 'sample': f'failed: {e}'}
+        return {'value': None, 'unit': 'points/s', 'cores': threads, 'kind': 'port', 'sample': f'failed: {e}'}
+
+
+def run_cpu_baseline(args, key, batch, npoints):
+    """The oracle on the host's CPU share (16 threads on the GPU box: OMP_NUM_THREADS there) and,
+    beside it, on every physical core of the host; >= cpu_steps timed steps each on a bounded
+    batch (CPU_BATCH: about 30 s per run)."""
+    aff, phys = host_cpu_info()
+    share = args.cpu_threads or min(aff, int(os.environ.get('OMP_NUM_THREADS', '16') or 16), 16)
+    cb = args.cpu_batch or min(batch, CPU_BATCH.get(key, batch))
+    res = _cpu_run(args, key, cb, npoints, share)
+    full = min(aff, phys) if phys else aff
+    if not args.cpu_threads and full > share:
+        res['all_physical_cores'] = _cpu_run(args, key, cb, npoints, full)
     res['host_cpus_visible'] = aff
     res['host_physical_cores'] = phys
     return res
@@ -159,13 +171,35 @@ def pmc_traffic(kernel, key, batch, npoints):
     return None, None
 
 
+def _kernel_entry(name, n, fl, by, sec):
+    """Roofline of one kernel from its summed in-step launches."""
+    intensity = fl / by if by else float('inf')
+    bound = 'mfma' if intensity >= RIDGE else 'hbm'
+    tf, gbs = fl / sec / 1e12, by / sec / 1e9
+    achieved, peak, unit = (tf, FP32_PEAK_TFLOPS, 'TFLOP/s') if bound == 'mfma' else (gbs, HBM_PEAK_GBS, 'GB/s')
+    # fp32 compute on gfx950: the MFMA and the vector ALU share the 157.3 TF peak; the neighbour
+    # search kernels (FPS, ball query, 3-NN) are VALU kernels, the engine GEMMs and kNN MFMA ones
+    unit_kind = 'valu' if any(k in name for k in ('fps_kernel', 'select_kernel', 'three_nn')) else \
+        ('mfma' if any(k in name for k in ('gemm', 'wgrad', 'fused_bwd', 'knn_wave')) else 'memory')
+    return {'kernel': name, 'bound': bound, 'achieved': round(achieved, 2), 'peak': peak, 'unit': unit,
+            'frac': round(achieved / peak, 4), 'compute_unit': unit_kind, 'launches_per_step': n,
+            'avg_launch_us': round(sec / n * 1e6, 2), 'in_step_ms': round(sec * 1e3, 3),
+            'algo_flops_per_launch': round(fl / n), 'algo_bytes_per_launch': round(by / n),
+            'arith_intensity_flop_per_byte': round(intensity, 2) if by else None,
+            'achieved_tflops': round(tf, 2), 'frac_of_fp32_peak': round(tf / FP32_PEAK_TFLOPS, 4),
+            'achieved_hbm_gbs': round(gbs, 1), 'frac_of_hbm_peak': round(gbs / HBM_PEAK_GBS, 4)}
+
+
 def kernel_roofline(step, dev, key, batch, npoints, replay=False):
-    """One more training step with every engine GEMM launch bracketed by HIP events on its
-    stream (pcseg.engine.KernelProbe).  The step is enqueued behind a 50 ms spin on the main
-    stream, so the GPU runs the whole step back to back (as it does in the GPU-bound timed
-    loop) and the event pairs time the kernels, not host-enqueue gaps.  The dominant kernel
-    is the variant with the largest summed in-step time; `achieved` = its algorithmic flops
-    (2*M*K*N per launch) or bytes over that in-step time."""
+    """One more training step with every probed HIP launch -- engine GEMMs, FPS, ball query,
+    3-NN, kNN, gathers, inverse maps, EdgeConv -- bracketed by HIP events on its own stream
+    (csrc/probe.cpp).  The step is enqueued behind a 50 ms spin on the main stream, so the GPU
+    runs the whole step back to back (as it does in the GPU-bound timed loop) and the event
+    pairs time the kernels, not host-enqueue gaps.  The dominant kernel is the one with the
+    largest summed in-step time over ALL streams; `achieved` = its algorithmic flops or bytes
+    (per-launch models in DESIGN.md section 3) over that time.  Also returned: the largest
+    kernel on the critical path's engine (`critical_path_gemm`), the top kernels, and the flops
+    the probed launches execute per sample (`executed_gflop_per_step`)."""
     import torch
     from pcseg.engine import KernelProbe
     from pcseg._lib import call, stream_ptr
@@ -175,39 +209,53 @@ def kernel_roofline(step, dev, key, batch, npoints, replay=False):
         step()
     summ = kp.summary()
     torch.cuda.synchronize(dev)
-    name, (n, fl, by, sec) = max(summ.items(), key=lambda kv: kv[1][3])
-    intensity = fl / by
-    bound = 'mfma' if intensity >= RIDGE else 'hbm'
-    tf, gbs = fl / sec / 1e12, by / sec / 1e9
-    achieved, peak, unit = (tf, FP32_PEAK_TFLOPS, 'TFLOP/s') if bound == 'mfma' else (gbs, HBM_PEAK_GBS, 'GB/s')
+    ranked = sorted(summ.items(), key=lambda kv: -kv[1][3])
+    name, (n, fl, by, sec) = ranked[0]
+    out = _kernel_entry(name, n, fl, by, sec)
     traffic, src = pmc_traffic(name, key, batch, npoints)
-    all_fl = sum(v[1] for v in summ.values())
-    all_sec = sum(v[3] for v in summ.values())
-    out = {'kernel': name, 'bound': bound, 'achieved': round(achieved, 2), 'peak': peak, 'unit': unit,
-           'frac': round(achieved / peak, 4), 'traffic': traffic, 'traffic_unit': 'bytes/launch',
-           'traffic_source': src, 'launches_per_step': n, 'avg_launch_us': round(sec / n * 1e6, 2),
-           'timing': 'in-step HIP events, step enqueued behind a spin (no host gaps)',
-           'algo_flops_per_launch': round(fl / n), 'algo_bytes_per_launch': round(by / n),
-           'arith_intensity_flop_per_byte': round(intensity, 2),
-           'achieved_tflops': round(tf, 2), 'frac_of_fp32_mfma_peak': round(tf / FP32_PEAK_TFLOPS, 4),
-           'achieved_hbm_gbs': round(gbs, 1), 'frac_of_hbm_peak': round(gbs / HBM_PEAK_GBS, 4),
-           'all_engine_gemms_in_step': {'tflops': round(all_fl / all_sec / 1e12, 2),
-                                        'ms_per_step': round(all_sec * 1e3, 3),
-                                        'launches': sum(v[0] for v in summ.values())}}
+    out.update({'traffic': traffic, 'traffic_unit': 'bytes/launch', 'traffic_source': src,
+                'timing': 'in-step HIP events, step enqueued behind a spin (no host gaps)'})
+    gemms = [kv for kv in ranked if any(k in kv[0] for k in ('gemm', 'wgrad', 'fused_bwd'))]
+    if gemms and gemms[0][0] != name:
+        g, (gn, gfl, gby, gsec) = gemms[0]
+        cg = _kernel_entry(g, gn, gfl, gby, gsec)
+        cg['traffic'], cg['traffic_source'] = pmc_traffic(g, key, batch, npoints)
+        out['critical_path_gemm'] = cg
+    out['top_kernels'] = [{k: v for k, v in _kernel_entry(nm, *vals).items()
+                           if k in ('kernel', 'in_step_ms', 'launches_per_step', 'frac', 'unit', 'compute_unit')}
+                          for nm, vals in ranked[:8]]
+    mf = [v for k, v in summ.items() if any(t in k for t in ('gemm', 'wgrad', 'fused_bwd', 'knn_wave'))]
+    out['executed_gflop_per_step'] = round(sum(v[1] for v in mf) / 1e9, 2)      # MFMA work only
+    out['all_engine_gemms_in_step'] = {
+        'tflops': round(sum(v[1] for _, v in gemms) / max(sum(v[3] for _, v in gemms), 1e-12) / 1e12, 2),
+        'ms_per_step': round(sum(v[3] for _, v in gemms) * 1e3, 3), 'launches': sum(v[0] for _, v in gemms)}
     if replay:      # isolated back-to-back replay of the recorded launches (rewrites outputs: last)
-        rs = kp.replay(name, reps=20)
-        out['isolated_replay'] = {'avg_launch_us': round(rs * 1e6, 2), 'tflops': round(fl / n / rs / 1e12, 2)}
+        try:
+            rs = kp.replay(name, reps=20)
+            out['isolated_replay'] = {'avg_launch_us': round(rs * 1e6, 2), 'tflops': round(fl / n / rs / 1e12, 2)}
+        except RuntimeError as e:       # single-launch probes of the non-engine kernels keep no relaunch
+            out['isolated_replay'] = f'n/a: {e}'
     return out
 
 
-def step_roofline(key, npoints, batch, ms):
-    """Whole-step fraction of the fp32 MFMA roofline with the reference algorithm's flop count."""
+def step_roofline(key, npoints, batch, ms, roof=None):
+    """Whole-step fraction of the fp32 peak with the reference algorithm's flop count and, when
+    the probe ran, with the flops the build executes (the fused EdgeConv / algebraic rewrites
+    execute fewer than the reference algorithm: SURVEY.md 8(d))."""
     gf = ALGO_GFLOP_PER_SAMPLE.get((key, npoints))
     if gf is None:
         return None
     tf = gf * batch / (ms * 1e-3) / 1e3
-    return {'algo_gflop_per_sample': gf, 'achieved_tflops_per_gpu': round(tf, 2),
-            'frac_of_fp32_peak': round(tf / FP32_PEAK_TFLOPS, 4)}
+    out = {'algo_gflop_per_sample': gf, 'achieved_tflops_per_gpu': round(tf, 2),
+           'frac_of_fp32_peak': round(tf / FP32_PEAK_TFLOPS, 4)}
+    if roof and roof.get('executed_gflop_per_step'):
+        eg = roof['executed_gflop_per_step'] / batch
+        etf = eg * batch / (ms * 1e-3) / 1e3
+        out['executed'] = {'gflop_per_sample': round(eg, 3), 'tflops_per_gpu': round(etf, 2),
+                           'frac_of_fp32_peak': round(etf / FP32_PEAK_TFLOPS, 4),
+                           'source': 'sum of the probed MFMA launches\' algorithmic flops (engine GEMMs, '
+                                     'fused backward, kNN distance tiles) in one step'}
+    return out
 
 
 # ----------------------------------------------------------------------------- one workload
@@ -291,7 +339,7 @@ def run_workload(key, batch, npoints, args, world, rank, dev):
                       'baseline_config': cfg, 'model': name, 'global_batch': world * batch, 'npoints': npoints,
                       'parallelism': f'dp{world}', 'geometry_prefetch': prefetch, 'hip_graph': use_graph},
            'host_enqueue_ms_per_step': round(t_host / args.steps * 1e3, 3),
-           'roofline': roof, 'step_roofline': step_roofline(key, npoints, batch, ms)}
+           'roofline': roof, 'step_roofline': step_roofline(key, npoints, batch, ms, roof)}
     del model, grads, opt
     torch.cuda.empty_cache()
     return res
@@ -330,7 +378,7 @@ def main():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-batch', type=int, default=0, help='CPU baseline batch (default: the GPU batch)')
     ap.add_argument('--cpu-steps', type=int, default=5)
-    ap.add_argument('--cpu-budget', type=float, default=12.0, help='seconds of timed CPU steps per workload')
+    ap.add_argument('--cpu-budget', type=float, default=40.0, help='seconds of timed CPU steps per workload')
     ap.add_argument('--cpu-threads', type=int, default=0)
     ap.add_argument('--cpu-baseline-worker', action='store_true')
     ap.add_argument('--no-roofline', action='store_true')
