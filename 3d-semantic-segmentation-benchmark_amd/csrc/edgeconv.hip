@@ -37,8 +37,16 @@ __global__ __launch_bounds__(256) void edgeconv_fwd_kernel(const float* __restri
     const int slot = threadIdx.x / tq;
     const int c = 4 * (threadIdx.x - slot * tq);
     double s1[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0};
+    // XCD-aware point order: blocks b, b + 8, ... share an XCD (dispatch round-robin; speed
+    // only), so XCD x takes the contiguous range [x Gx, (x+1) Gx) of points and its blocks sweep
+    // it together, pb points each per pass: at any time an XCD gathers the Y rows of about one
+    // cloud (1 MB at N = 4096, Cout = 64), which its 4 MB L2 holds
+    const int nx = gridDim.x % 8 == 0 ? 8 : 1;
+    const int xcd = blockIdx.x % nx, lb = blockIdx.x / nx, nl = gridDim.x / nx;
+    const long long Gx = (G + nx - 1) / nx;
+    const long long gx0 = (long long)xcd * Gx, gx1 = min(G, gx0 + Gx);
     if (slot < pb) {
-        for (long long g = (long long)blockIdx.x * pb + slot; g < G; g += (long long)gridDim.x * pb) {
+        for (long long g = gx0 + (long long)lb * pb + slot; g < gx1; g += (long long)nl * pb) {
             const long long cloud = (g / N) * N;
             const float4 yi = *reinterpret_cast<const float4*>(Y + g * Cout + c);
             const float4 pi = *reinterpret_cast<const float4*>(PQ + g * Cout + c);
@@ -171,7 +179,12 @@ __global__ __launch_bounds__(256) void edgeconv_bwd_gather_kernel(const float* _
                                                                   int Cout, int k, const float* __restrict__ coef,
                                                                   const float* __restrict__ kBC,
                                                                   float* __restrict__ Gd) {
-    const long long m = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    // XCD-aware order (bijective remap of the 1-D grid, speed only): XCD x takes a contiguous
+    // run of target points, so the D / Q / arg rows its waves gather stay within ~one cloud
+    const int nwg = gridDim.x, bid = blockIdx.x;
+    const int q8 = nwg / 8, r8 = nwg % 8, xcd = bid % 8;
+    const int tb = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+    const long long m = (long long)tb * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (m >= G) return;
     const int a = off[m], zend = off[m + 1];
@@ -228,7 +241,8 @@ static pcs_operand plain(const float* p, int ld) {
 static int fwd_blocks(long long G, int Cout) {
     const long long pb = 256 / (Cout / 4);
     const long long need = (G + pb - 1) / pb;
-    return (int)std::min<long long>(kEdgeFwdBlocks, std::max<long long>(need, 1));
+    const long long nb = std::min<long long>(kEdgeFwdBlocks, std::max<long long>(need, 1));
+    return (int)(nb >= 8 ? (nb + 7) / 8 * 8 : nb);         // a multiple of 8: the XCD-aware order
 }
 
 static const int kEdgeRedRows = 512;

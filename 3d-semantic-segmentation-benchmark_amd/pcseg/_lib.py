@@ -135,15 +135,31 @@ def load() -> ctypes.CDLL:
     return _lib
 
 
+_raw_stream = torch._C._cuda_getCurrentRawStream
+
+
 def stream_ptr(device: torch.device | None = None) -> int:
-    return torch.cuda.current_stream(device).cuda_stream
+    """hipStream_t of the current stream of `device` (a torch.device, an index or None = the
+    current device), without building a torch.cuda.Stream object (host enqueue cost)."""
+    if device is None:
+        idx = torch.cuda.current_device()
+    elif isinstance(device, int):
+        idx = device
+    else:
+        idx = device.index if device.index is not None else torch.cuda.current_device()
+    return _raw_stream(idx)
+
+
+_fns: dict = {}
 
 
 def call(name: str, *args) -> None:
-    lib = load()
-    rc = getattr(lib, name)(*args)
+    fn = _fns.get(name)
+    if fn is None:
+        fn = _fns[name] = getattr(load(), name)
+    rc = fn(*args)
     if rc != 0:
-        raise RuntimeError(f'{name} failed ({rc}): {lib.pcs_last_error().decode(errors="replace")}')
+        raise RuntimeError(f'{name} failed ({rc}): {load().pcs_last_error().decode(errors="replace")}')
 
 
 def ptr(t: torch.Tensor | None) -> int | None:

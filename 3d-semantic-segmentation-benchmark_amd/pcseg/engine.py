@@ -238,6 +238,24 @@ def _nz(p) -> int:
     return 0 if p is None else p.data_ptr()
 
 
+def _workspace_probe(lib, key, M, Kin, ldx, params, bns, nl, pool_K, couts, acts):
+    """pcs_mlp_workspace for a stack (sizes only: the records carry non-null placeholder pointers)."""
+    recs = []
+    cin = Kin
+    for li in range(nl):
+        W = params[4 * li]
+        C = couts[li]
+        ldw = W.reshape(C, -1).shape[1]
+        if ldw % 4 and li > 0:
+            ldw = ld4(ldw)
+        bn = bns[li]
+        use_batch = bn.training or bn.running_mean is None
+        recs.append(_REC.pack(16, ldw, cin, C, 0, 0, 0, 16, 16, 0, 0.0, 1e-5, int(use_batch), acts[li][0],
+                              acts[li][1], 16, 16, 0, 0, 0, 0, 0.0, 0, 0))
+        cin = C
+    return _workspace(lib, key, M, Kin, ldx, b''.join(recs), nl, pool_K, 0)
+
+
 class SharedMLPFn(torch.autograd.Function):
     """rows X (M, ld) with Kin logical channels -> pooled (M/pool_K, C_L) or activation (M, C_L).
 
@@ -255,8 +273,17 @@ class SharedMLPFn(torch.autograd.Function):
         nl = len(bns)
         couts = [params[4 * li].shape[0] for li in range(nl)]
         tot = sum(couts)
-        Zbuf = _f32((M * tot,), dev)
-        coef = _f32((4 * tot,), dev)
+        key = (M, Kin, ldx, tuple(couts), pool_K, 0)
+        nws = _ws_cache.get(key)
+        # ONE allocation per stack call: [pre-BN Z of every layer | BN coefficients | workspace]
+        zc = M * tot + 4 * tot
+        wsoff = (zc + 63) // 64 * 64                      # 256-B aligned workspace
+        buf = _f32((wsoff + ((nws or 0) + 3) // 4,), dev) if nws is not None else None
+        if buf is None:                                   # first call with this shape: size the workspace
+            nws = _workspace_probe(lib, key, M, Kin, ldx, params, bns, nl, pool_K, couts, acts)
+            buf = _f32((wsoff + (nws + 3) // 4,), dev)
+        Zbuf = buf[:M * tot]
+        coef = buf[M * tot:zc]
         Wms, fixed = [], []
         off, cin = 0, Kin
         for li in range(nl):
@@ -306,10 +333,8 @@ class SharedMLPFn(torch.autograd.Function):
         else:
             out = _f32((M, CL), dev)
             arg = None
-        key = (M, Kin, ldx, tuple(couts), pool_K, 0)
-        nws = _workspace(lib, key, M, Kin, ldx, recs, nl, pool_K, 0)
-        ws = torch.empty((nws,), dtype=torch.uint8, device=dev)
-        call('pcs_mlp_forward', ptr(X), ldx, Kin, M, recs, nl, pool_K, ptr(out), ldo, ptr(arg), ptr(ws), nws, st)
+        call('pcs_mlp_forward', ptr(X), ldx, Kin, M, recs, nl, pool_K, ptr(out), ldo, ptr(arg),
+             buf.data_ptr() + 4 * wsoff, nws, st)
         if arg is not None:
             record_pool_arg(arg)
         if recording():

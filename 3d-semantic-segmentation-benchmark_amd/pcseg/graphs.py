@@ -36,7 +36,10 @@ class CapturedStep:
     it before the next step)."""
 
     def __init__(self, model, x, labels, lengths, grads, opt, loss_fn, logits_of=None, warmup: int = 2,
-                 prefetch: bool = True):
+                 prefetch: bool = True, geometry: str = 'graph'):
+        """geometry: 'graph' -- the next step's neighbour search is captured with the step (one
+        launch per step); 'eager' -- it is enqueued eagerly on the side stream after each replay
+        (the graphs then hold the main-stream work and the wgrad lane only)."""
         if grads.world != 1:
             raise RuntimeError('CapturedStep: single process only (multi-GPU steps run eagerly)')
         self.model, self.x, self.labels, self.lengths = model, x, labels, lengths
@@ -45,6 +48,9 @@ class CapturedStep:
         dev = x.device
         self.dev = dev
         self.prefetch = prefetch and hasattr(model, 'prefetch_geometry')
+        if geometry not in ('graph', 'eager'):
+            raise ValueError(f"geometry must be 'graph' or 'eager', got {geometry!r}")
+        self.geo_eager = self.prefetch and geometry == 'eager'
         main = torch.cuda.current_stream(dev)
         warm = torch.cuda.Stream(dev)
         warm.wait_stream(main)
@@ -71,6 +77,11 @@ class CapturedStep:
             self.losses.append(loss)
         torch.cuda.synchronize(dev)
         self.k = 0
+        if self.geo_eager:
+            self.prev_done = torch.cuda.Event()
+            self.geo_ready = [torch.cuda.Event(), torch.cuda.Event()]
+            for e in self.geo_ready:
+                e.record(main)
 
     def _eager_step(self):
         self.grads.zero_grad()
@@ -86,7 +97,7 @@ class CapturedStep:
             m._pcs_prefetched = (x, x._version, self.plans[k])
         self.grads.zero_grad()
         loss = self.loss_fn(self.logits_of(m(x)), self.labels, self.lengths)
-        if self.prefetch:
+        if self.prefetch and not self.geo_eager:
             # the other buffer's geometry for the next replay, under this backward
             m.prefetch_geometry(x, into=self.plans[1 - k])
         loss.backward()
@@ -94,12 +105,26 @@ class CapturedStep:
         self.opt.step()
         if self.prefetch:
             m._pcs_prefetched = None
-        # join every side stream the step forked (geometry; the wgrad lane joins in backward)
-        torch.cuda.current_stream(self.dev).wait_stream(side_stream(self.dev))
+        if self.prefetch and not self.geo_eager:
+            # join the geometry stream the captured prefetch forked (the wgrad lane joins in backward)
+            torch.cuda.current_stream(self.dev).wait_stream(side_stream(self.dev))
         return loss
 
     def step(self) -> torch.Tensor:
         k = self.k
+        if not self.geo_eager:
+            self.graphs[k].replay()
+            self.k = (k + 1) % len(self.graphs)
+            return self.losses[k]
+        main = torch.cuda.current_stream(self.dev)
+        side = side_stream(self.dev)
+        self.prev_done.record(main)                 # the previous replay (the last reader of plan 1-k)
+        main.wait_event(self.geo_ready[k])          # this replay's plan, computed under the last one
         self.graphs[k].replay()
-        self.k = (k + 1) % len(self.graphs)
+        side.wait_event(self.prev_done)
+        with torch.cuda.stream(side):
+            self.model.prefetch_geometry(self.x, into=self.plans[1 - k])
+            self.geo_ready[1 - k].record(side)
+        self.model._pcs_prefetched = None
+        self.k = 1 - k
         return self.losses[k]

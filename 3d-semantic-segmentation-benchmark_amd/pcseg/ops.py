@@ -91,18 +91,26 @@ def inverse_index(idx: torch.Tensor, targets: int, out=None):
     (offsets (B*targets+1,), entries (B*S*k,)) int32 -- the slots reading each source point,
     ascending.  Feeds the atomic-free, fixed-order gather backward.  out = (offsets, entries)."""
     check_cuda(idx)
-    idx = _c(idx.to(torch.int32))
+    if idx.dtype != torch.int32:
+        idx = idx.to(torch.int32)
+    idx = _c(idx)
     B = idx.shape[0]
     per = idx[0].numel()
-    lib = _lib.load()
-    need = ctypes.c_size_t(0)
-    rc = lib.pcs_inverse_index_workspace(B * per, B * targets, ctypes.byref(need))
-    if rc:
-        raise RuntimeError(lib.pcs_last_error().decode())
-    ws = torch.empty(max(int(need.value), 1), dtype=torch.uint8, device=idx.device)
-    offsets = _out(out[0] if out else None, (B * targets + 1,), torch.int32, idx.device)
-    entries = _out(out[1] if out else None, (B * per,), torch.int32, idx.device)
-    call('pcs_inverse_index', ptr(idx), B, per, targets, ptr(offsets), ptr(entries), ptr(ws), int(need.value),
+    n, T = B * per, B * targets
+    # pcs_inverse_index_workspace: the scatter scratch (n ints, 256-B aligned) + T counters
+    nws = (n * 4 + 255) // 256 * 256 + T * 4
+    if out is None:
+        # one int32 allocation: [offsets (T+1) | entries (n) | workspace], 256-B aligned parts
+        o_ent = (T + 1 + 63) // 64 * 64
+        o_ws = (o_ent + n + 63) // 64 * 64
+        buf = torch.empty(o_ws + nws // 4, dtype=torch.int32, device=idx.device)
+        offsets, entries, wsp = buf[:T + 1], buf[o_ent:o_ent + n], buf.data_ptr() + 4 * o_ws
+    else:
+        offsets = _out(out[0], (T + 1,), torch.int32, idx.device)
+        entries = _out(out[1], (n,), torch.int32, idx.device)
+        ws = torch.empty(nws, dtype=torch.uint8, device=idx.device)
+        wsp = ws.data_ptr()
+    call('pcs_inverse_index', ptr(idx), B, per, targets, ptr(offsets), ptr(entries), wsp, nws,
          stream_ptr(idx.device))
     return offsets, entries
 

@@ -304,7 +304,7 @@ def run_workload(key, batch, npoints, args, world, rank, dev):
         # hipGraphLaunch per step; the next step's geometry still runs under the backward
         from pcseg.graphs import CapturedStep
         cs = CapturedStep(model, x, lab, lengths, grads, opt, pcseg.masked_onehot_cross_entropy, logits_of,
-                          warmup=2, prefetch=not args.no_prefetch)
+                          warmup=2, prefetch=not args.no_prefetch, geometry=args.graph_geometry)
         prefetch = cs.prefetch
 
         def step():
@@ -392,6 +392,8 @@ def main():
                          "or from a gradient hook inside the backward (round 2 A/B: within noise, 5.50 vs 5.52 ms)")
     ap.add_argument('--no-prefetch', action='store_true',
                     help='do not enqueue the next step\'s FPS/ball-query/3-NN before this step\'s backward')
+    ap.add_argument('--graph-geometry', choices=['graph', 'eager'], default='graph',
+                    help="--graph: capture the next step's neighbour search too, or enqueue it eagerly per step")
     ap.add_argument('--bwd-fuse', choices=['default', 'off', 'all'], default='default',
                     help='backward kernel choice of the shared-MLP stacks (pcs_mlp_layer.bwd_fuse; A/B runs)')
     ap.add_argument('--check-launch', action='store_true',
