@@ -257,6 +257,76 @@ __global__ __launch_bounds__(256) void interp_bwd_csr_kernel(const float* __rest
     }
 }
 
+// The same for D = 64 V (V = 2, 4: FP1 / FP2-4 of PointNet++): one pass over the slot list,
+// each lane owning V consecutive channels (float2 / float4 loads of a 16-B aligned row run), so
+// the list, the distances and the IDW coefficients are read once instead of D / 64 times.
+// Same per-term rounding and per-channel fp64 summation order as the kernel above.
+template <int V>
+__global__ __launch_bounds__(256) void interp_bwd_csr_vec_kernel(const float* __restrict__ gout, int ld, int col_off,
+                                                                 const float* __restrict__ dist,
+                                                                 const int32_t* __restrict__ off,
+                                                                 const int32_t* __restrict__ ent, int targets,
+                                                                 float* __restrict__ gpts) {
+    typedef float fv __attribute__((ext_vector_type(V)));
+    constexpr int D = 64 * V;
+    const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (t >= targets) return;
+    const int a = off[t], z = off[t + 1];
+    double acc[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) acc[v] = 0.0;
+    const float* g0 = gout + col_off + V * lane;
+    for (int base = a; base < z; base += 64) {
+        const int n = min(64, z - base);
+        int row = 0;
+        float nrm = 1.f, wj = 0.f;
+        if (lane < n) {
+            const int s = ent[base + lane];
+            row = s / 3;
+            const int j = s - 3 * row;
+            const float w0 = 1.0f / (dist[(size_t)row * 3 + 0] + 1e-9f);
+            const float w1 = 1.0f / (dist[(size_t)row * 3 + 1] + 1e-9f);
+            const float w2 = 1.0f / (dist[(size_t)row * 3 + 2] + 1e-9f);
+            nrm = (w0 + w1) + w2;
+            wj = j == 0 ? w0 : (j == 1 ? w1 : w2);
+        }
+        auto term = [&](int e, fv& out) {
+            const int r = __builtin_amdgcn_readlane(row, e);
+            const float nv = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(nrm), e));
+            const float wv = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wj), e));
+            const fv gv = *reinterpret_cast<const fv*>(g0 + (size_t)r * ld);
+#pragma unroll
+            for (int v = 0; v < V; ++v) out[v] = (gv[v] / nv) * wv;
+        };
+        int e = 0;
+        for (; e + 4 <= n; e += 4) {
+            fv t0, t1, t2, t3;
+            term(e, t0);
+            term(e + 1, t1);
+            term(e + 2, t2);
+            term(e + 3, t3);
+#pragma unroll
+            for (int v = 0; v < V; ++v) {
+                acc[v] += (double)t0[v];
+                acc[v] += (double)t1[v];
+                acc[v] += (double)t2[v];
+                acc[v] += (double)t3[v];
+            }
+        }
+        for (; e < n; ++e) {
+            fv t0;
+            term(e, t0);
+#pragma unroll
+            for (int v = 0; v < V; ++v) acc[v] += (double)t0[v];
+        }
+    }
+    fv o;
+#pragma unroll
+    for (int v = 0; v < V; ++v) o[v] = (float)acc[v];
+    *reinterpret_cast<fv*>(gpts + (size_t)t * D + V * lane) = o;
+}
+
 // get_graph_feature backward (dgcnn.py:41-53, rows [x_j - x_i, x_i] of stride ld): point t's
 // gradient = sum_j (g_b[t,j] - g_a[t,j]) over its own k rows, plus g_a of every edge row
 // whose neighbour is t (its inverse-map list, ascending).  One wave per point, lanes over
@@ -360,9 +430,20 @@ PCS_API int pcs_interp_bwd_csr(const float* grad_out, int ld_gout, int col_off, 
     const long long total = (long long)B * M * D, targets = (long long)B * M;
     PCS_CHECK_ARG(total < (1ll << 31), "pcs_interp_bwd_csr: too many elements");
     PCS_CHECK_ARG(grad_out && dist && offsets && entries && grad_pts, "pcs_interp_bwd_csr: null pointer");
-    ProbeScope pr(as_stream(stream), 0.0, 8.0 * (double)total + 4.0 * (double)(targets + 1), "pcs::interp_bwd_csr_kernel");
-    hipLaunchKernelGGL(interp_bwd_csr_kernel, dim3((unsigned)((targets + 3) / 4)), dim3(256), 0, as_stream(stream),
-                       grad_out, ld_gout, col_off, dist, offsets, entries, (int)targets, D, grad_pts);
+    const dim3 grid((unsigned)((targets + 3) / 4));
+    const bool al = ld_gout % 4 == 0 && col_off % 4 == 0 && ((uintptr_t)grad_out | (uintptr_t)grad_pts) % 16 == 0;
+    const int V = al && (D == 128 || D == 256) ? D / 64 : 1;
+    ProbeScope pr(as_stream(stream), 0.0, 8.0 * (double)total + 4.0 * (double)(targets + 1),
+                  V == 1 ? "pcs::interp_bwd_csr_kernel" : "pcs::interp_bwd_csr_vec_kernel<%d>", V);
+    if (V == 2)
+        hipLaunchKernelGGL(interp_bwd_csr_vec_kernel<2>, grid, dim3(256), 0, as_stream(stream), grad_out, ld_gout,
+                           col_off, dist, offsets, entries, (int)targets, grad_pts);
+    else if (V == 4)
+        hipLaunchKernelGGL(interp_bwd_csr_vec_kernel<4>, grid, dim3(256), 0, as_stream(stream), grad_out, ld_gout,
+                           col_off, dist, offsets, entries, (int)targets, grad_pts);
+    else
+        hipLaunchKernelGGL(interp_bwd_csr_kernel, grid, dim3(256), 0, as_stream(stream), grad_out, ld_gout, col_off,
+                           dist, offsets, entries, (int)targets, D, grad_pts);
     return launch_status("pcs_interp_bwd_csr");
 }
 

@@ -517,39 +517,52 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(Operand xo, int N, Operan
 
 // dW[e] += sum_{s < splits} part[s][e] (e < nk) and db[e] += sum_s pdb[s][e] (e < N, the
 // blocks past dW's): the weight and bias gradients from the wgrad's per-split partials.
-// 16 elements per block, 16 threads per element: thread g sums splits g, g + 16, ... (fp64,
-// 4 interleaved accumulators), then the 16 thread sums are added in order through LDS -- a
-// fixed summation tree, so the result is reproducible bit for bit.
-constexpr int kRedElems = 16, kRedGroups = 16;
+// 64 elements per block as 16 lanes x float4, so one wave instruction reads four 256-B runs
+// (splits g .. g+3 of the same 64 elements); the block's 16 lane groups take splits g, g + 16,
+// ... (fp64, two interleaved accumulators), then the 16 group sums are added in group order
+// through LDS -- a fixed summation tree, so the result is reproducible bit for bit.
+// (Round 2's 16-element blocks read 64-B runs: ~18 us per FP1-sized reduce, ~1.8 TB/s.)
+constexpr int kRedElems = 64, kRedGroups = 16;
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, int splits, long long nk,
                                                            float* __restrict__ dW, const float* __restrict__ pdb,
                                                            int N, float* __restrict__ db) {
     __shared__ double red[kRedGroups][kRedElems];
-    const int el = threadIdx.x % kRedElems, g = threadIdx.x / kRedElems;
+    const int q = threadIdx.x & 15, g = threadIdx.x >> 4;
     const long long wblocks = (nk + kRedElems - 1) / kRedElems;
     const bool bias = blockIdx.x >= wblocks;
     const float* src = bias ? pdb : part;
     float* out = bias ? db : dW;
     const long long n = bias ? N : nk;
-    const long long e = (bias ? blockIdx.x - wblocks : (long long)blockIdx.x) * kRedElems + el;
-    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
-    if (e < n) {
+    const long long eb = (bias ? blockIdx.x - wblocks : (long long)blockIdx.x) * kRedElems;
+    const long long e0 = eb + 4 * q;
+    double a[4] = {0.0, 0.0, 0.0, 0.0}, b[4] = {0.0, 0.0, 0.0, 0.0};
+    if (n % 4 == 0 && e0 + 3 < n) {          // rows of n floats: 16-B aligned float4 runs
         int sp = g;
-        for (; sp + 3 * kRedGroups < splits; sp += 4 * kRedGroups) {
-            a0 += (double)src[(size_t)sp * n + e];
-            a1 += (double)src[(size_t)(sp + kRedGroups) * n + e];
-            a2 += (double)src[(size_t)(sp + 2 * kRedGroups) * n + e];
-            a3 += (double)src[(size_t)(sp + 3 * kRedGroups) * n + e];
+        for (; sp + kRedGroups < splits; sp += 2 * kRedGroups) {
+            const float4 v = *reinterpret_cast<const float4*>(src + (size_t)sp * n + e0);
+            const float4 w = *reinterpret_cast<const float4*>(src + (size_t)(sp + kRedGroups) * n + e0);
+            a[0] += (double)v.x; a[1] += (double)v.y; a[2] += (double)v.z; a[3] += (double)v.w;
+            b[0] += (double)w.x; b[1] += (double)w.y; b[2] += (double)w.z; b[3] += (double)w.w;
         }
-        for (; sp < splits; sp += kRedGroups) a0 += (double)src[(size_t)sp * n + e];
-    }
-    red[g][el] = (a0 + a1) + (a2 + a3);
-    __syncthreads();
-    if (g == 0 && e < n) {
-        double a = red[0][el];
+        if (sp < splits) {
+            const float4 v = *reinterpret_cast<const float4*>(src + (size_t)sp * n + e0);
+            a[0] += (double)v.x; a[1] += (double)v.y; a[2] += (double)v.z; a[3] += (double)v.w;
+        }
+    } else {
 #pragma unroll
-        for (int i = 1; i < kRedGroups; ++i) a += red[i][el];
-        out[e] = (float)((double)out[e] + a);
+        for (int j = 0; j < 4; ++j)
+            if (e0 + j < n)
+                for (int sp = g; sp < splits; sp += kRedGroups) a[j] += (double)src[(size_t)sp * n + e0 + j];
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) red[g][4 * q + j] = a[j] + b[j];
+    __syncthreads();
+    if (threadIdx.x < kRedElems && eb + threadIdx.x < n) {
+        double sum = red[0][threadIdx.x];
+#pragma unroll
+        for (int i = 1; i < kRedGroups; ++i) sum += red[i][threadIdx.x];
+        const long long e = eb + threadIdx.x;
+        out[e] = (float)((double)out[e] + sum);
     }
 }
 

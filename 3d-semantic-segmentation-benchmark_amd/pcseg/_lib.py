@@ -23,6 +23,19 @@ F32 = ctypes.c_float
 F64 = ctypes.c_double
 
 
+QMAX = 4     # PCS_GEO_MAX_QUERIES
+
+
+class GeoLevel(ctypes.Structure):
+    """pcs_geo_level (include/pcseg.h): one level of a native geometry plan."""
+    _fields_ = [('C', ctypes.c_int64), ('nq', ctypes.c_int64), ('r2', ctypes.c_double * QMAX),
+                ('K', ctypes.c_int64 * QMAX), ('on_self', ctypes.c_int64 * QMAX),
+                ('fps_idx', ctypes.c_void_p), ('cent', ctypes.c_void_p), ('ball', ctypes.c_void_p * QMAX),
+                ('ball_off', ctypes.c_void_p * QMAX), ('ball_ent', ctypes.c_void_p * QMAX),
+                ('nn_idx', ctypes.c_void_p), ('nn_dist', ctypes.c_void_p), ('nn_off', ctypes.c_void_p),
+                ('nn_ent', ctypes.c_void_p), ('event', ctypes.c_void_p)]
+
+
 class Operand(ctypes.Structure):
     """pcs_operand (include/pcseg.h): an engine GEMM operand and its on-load transform."""
     _fields_ = [('data', P), ('ld', ctypes.c_int), ('mode', ctypes.c_int),
@@ -102,6 +115,8 @@ SIGNATURES = {
     'pcs_pad_onehot': [P, I32, P, P, P, I32, I32, I32, P, P, P],
     # optimizer
     'pcs_adam': [P, P, P, P, I64, F32, F32, F32, F32, F32, F32, F32, P],
+    'pcs_geometry_plan_workspace': [I32, I32, P, I32, I32, I32, P],
+    'pcs_geometry_plan': [P, I32, I32, P, P, I32, I32, I32, P, P, ctypes.c_size_t, P],
     'pcs_adam_dev': [P, P, P, P, I64, F32, F32, F32, F64, F64, F64, F32, F32, P, P],
     # loss
     'pcs_masked_ce_blocks': [I32, I32],

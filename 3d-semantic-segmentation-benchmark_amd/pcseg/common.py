@@ -12,6 +12,7 @@ import torch.nn as nn
 
 from . import ops
 from .engine import shared_mlp, pad_rows
+from ._lib import call, stream_ptr
 from .replay import active as _replay
 
 
@@ -84,6 +85,27 @@ def interpolate(points: torch.Tensor, coords_1: torch.Tensor, coords_2: torch.Te
 
 # --------------------------------------------------------------------------- geometry on a side stream
 _side_streams: dict = {}
+_plan_ws: dict = {}          # native geometry plan workspace bytes per plan structure
+_events: dict = {}           # device -> ring of event sets for the native plans
+
+
+def _event_set(dev, side, L):
+    """L + 1 torch events (per level + after the 3-NN) from a small per-device ring, created and
+    recorded once so that their raw handles exist; the native plan re-records them.  A plan's
+    waits are enqueued by the forward that consumes it, before the ring comes round again."""
+    key = dev.index if dev.index is not None else torch.cuda.current_device()
+    ring = _events.get(key)
+    if ring is None or len(ring[0][0]) < L + 1:
+        sets = []
+        for _ in range(4):
+            evs = [torch.cuda.Event() for _ in range(max(L, 6) + 1)]
+            for e in evs:
+                e.record(side)
+            sets.append(evs)
+        ring = _events[key] = [sets, 0]
+    sets, i = ring
+    ring[1] = (i + 1) % len(sets)
+    return sets[i]
 
 
 def side_stream(device) -> torch.cuda.Stream:
@@ -123,6 +145,10 @@ class GeometryPlan:
         made = []
         self.inverse = inverse
         self.fps_idx = []
+        if _replay() is None:
+            # one native call (pcs_geometry_plan): same kernels, same order, same RNG draws
+            self._build_native(coords, levels, interp, inverse, into, main, side)
+            return
         with torch.cuda.stream(side):
             prev = coords
             for lv, (C, queries) in enumerate(levels):
@@ -166,6 +192,100 @@ class GeometryPlan:
             coords.record_stream(side)
             for t in made:
                 t.record_stream(main)
+
+    def _build_native(self, coords, levels, interp, inverse, into, main, side):
+        import ctypes
+        from ._lib import GeoLevel, QMAX
+        dev = coords.device
+        if coords.dtype != torch.float32 or not coords.is_contiguous():
+            coords = coords.float().contiguous()
+            self.coords[0] = coords
+        B, N, _ = coords.shape
+        L = len(levels)
+        if L > 6 or any(len(q) > QMAX for _, q in levels):
+            raise ValueError('GeometryPlan: at most 6 levels of at most 4 ball queries')
+        recs = (GeoLevel * L)()
+        sizes = []                       # every output, int32 units, in a fixed order
+        prev = N
+        for l, (C, queries) in enumerate(levels):
+            r = recs[l]
+            r.C, r.nq = C, len(queries)
+            sizes += [B * C, B * C * 3]
+            for q, (rad, K, on_self) in enumerate(queries):
+                r.r2[q] = ops.radius_sq_f32(rad)
+                r.K[q], r.on_self[q] = K, int(bool(on_self))
+                src = C if on_self else prev
+                sizes += [B * C * K] + ([B * src + 1, B * C * K] if inverse else [])
+            if interp:
+                sizes += [B * prev * 3, B * prev * 3] + ([B * C + 1, B * prev * 3] if inverse else [])
+            prev = C
+        key = (B, N, tuple((C, tuple(qs)) for C, qs in levels), bool(interp), bool(inverse))
+        nws = _plan_ws.get(key)
+        if nws is None:
+            out = ctypes.c_size_t(0)
+            call('pcs_geometry_plan_workspace', B, N, recs, L, int(interp), int(inverse), ctypes.byref(out))
+            nws = _plan_ws[key] = int(out.value)
+        offs, o = [], 0
+        for n in sizes:
+            offs.append(o)
+            o += (n + 63) // 64 * 64
+        wso = o
+        buf = torch.empty(wso + (nws + 3) // 4 if into is None else (nws + 3) // 4, dtype=torch.int32, device=dev)
+        parts = iter(zip(offs, sizes))
+        evs = _event_set(dev, side, L)
+
+        def take():
+            off, n = next(parts)
+            return buf[off:off + n]
+        prev = N
+        for l, (C, queries) in enumerate(levels):
+            r = recs[l]
+            if into is None:
+                fidx, cent = take().view(B, C), take().view(torch.float32).view(B, C, 3)
+            else:
+                fidx, cent = into.fps_idx[l], into.coords[l + 1]
+            r.fps_idx, r.cent = fidx.data_ptr(), cent.data_ptr()
+            bl = []
+            for q, (rad, K, on_self) in enumerate(queries):
+                src = C if on_self else prev
+                if into is None:
+                    idx = take().view(B, C, K)
+                    inv = (take(), take()) if inverse else None
+                else:
+                    idx, inv = into.balls[l][q]
+                r.ball[q] = idx.data_ptr()
+                if inv is not None:
+                    r.ball_off[q], r.ball_ent[q] = inv[0].data_ptr(), inv[1].data_ptr()
+                bl.append((idx, inv))
+            if interp:
+                if into is None:
+                    nidx, ndist = take().view(B, prev, 3), take().view(torch.float32).view(B, prev, 3)
+                    ninv = (take(), take()) if inverse else None
+                else:
+                    nidx, ndist, ninv = into.nn[l]
+                r.nn_idx, r.nn_dist = nidx.data_ptr(), ndist.data_ptr()
+                if ninv is not None:
+                    r.nn_off, r.nn_ent = ninv[0].data_ptr(), ninv[1].data_ptr()
+                self.nn.append((nidx, ndist, ninv))
+            r.event = evs[l].cuda_event
+            self.fps_idx.append(fidx)
+            self.coords.append(cent)
+            self.balls.append(bl)
+            self.events.append(evs[l])
+            prev = C
+        if interp:
+            self.nn_event = evs[L]
+        with torch.cuda.stream(side):
+            # the FPS starts: one torch.randint per level, as sample_indices draws them
+            npts = [N] + [C for C, _ in levels[:-1]]
+            starts = torch.stack([_fps_start(B, n, dev) for n in npts])
+            call('pcs_geometry_plan', coords.data_ptr(), B, N, starts.data_ptr(), recs, L, int(interp),
+                 int(inverse), evs[L].cuda_event if interp else None, buf.data_ptr() + 4 * (wso if into is None else 0),
+                 nws, stream_ptr(dev))
+        if not torch.cuda.is_current_stream_capturing():
+            coords.record_stream(side)
+            if into is None:
+                buf.record_stream(main)
 
     @staticmethod
     def _wait(ev):

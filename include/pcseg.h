@@ -63,6 +63,40 @@ int pcs_knn_workspace(int B, int N, size_t* bytes);
 int pcs_knn_ws(const float* x, int B, int N, int F, int k, int32_t* out_idx,
                void* ws, size_t ws_bytes, void* stream);
 
+/* ---- geometry plan of a PointNet++-family forward --------------------------
+ * One call enqueues, on one stream and in this order, every neighbour structure of a
+ * forward: per level l, FPS of the previous level's points (level 0: coords) down to C
+ * centroids (pcs_fps, start = starts[l*B + b]), then its nq ball queries (pcs_ball_query
+ * against the previous level's points, or the centroids themselves when on_self -- the
+ * InvResMLP grouping, models/utils/common.py:288) with their inverse maps
+ * (pcs_inverse_index, when inverse), then `event` is recorded (nullable); after all
+ * levels, when interp, the 3-NN of each FeaturePropagation from level L-1 down to 0
+ * (pcs_knn_select of level l-1's points (coords for l = 0) among level l's centroids, and
+ * its inverse map), then nn_event.  Same kernels and arguments as the per-op calls:
+ * bitwise the same plan.  Outputs caller-owned; the inverse maps share one workspace of
+ * pcs_geometry_plan_workspace bytes.  Replaces pcseg.common.GeometryPlan's ~20 calls. */
+#define PCS_GEO_MAX_LEVELS 6
+#define PCS_GEO_MAX_QUERIES 4
+typedef struct pcs_geo_level {
+    int64_t C, nq;
+    double r2[PCS_GEO_MAX_QUERIES];      /* float32(r*r) of each query */
+    int64_t K[PCS_GEO_MAX_QUERIES];
+    int64_t on_self[PCS_GEO_MAX_QUERIES];
+    int32_t* fps_idx;                     /* (B, C) */
+    float* cent;                          /* (B, C, 3) */
+    int32_t* ball[PCS_GEO_MAX_QUERIES];  /* (B, C, K[q]) */
+    int32_t* ball_off[PCS_GEO_MAX_QUERIES];  /* (B * targets + 1) */
+    int32_t* ball_ent[PCS_GEO_MAX_QUERIES];  /* (B * C * K[q]) */
+    int32_t* nn_idx; float* nn_dist;      /* (B, N_{l-1}, 3): the FeaturePropagation 3-NN into level l */
+    int32_t* nn_off; int32_t* nn_ent;     /* its inverse map (B * C + 1), (B * N_{l-1} * 3) */
+    void* event;                          /* hipEvent_t recorded after the level's FPS + ball queries */
+} pcs_geo_level;
+int pcs_geometry_plan_workspace(int B, int N, const pcs_geo_level* levels, int L, int interp,
+                                int inverse, size_t* bytes);
+int pcs_geometry_plan(const float* coords, int B, int N, const int32_t* starts,
+                      const pcs_geo_level* levels, int L, int interp, int inverse, void* nn_event,
+                      void* workspace, size_t ws_bytes, void* stream);
+
 /* ---- gather / scatter --------------------------------------------------- */
 
 /* models/utils/common.py:62-71: out (B*C*K, 3+D) rows

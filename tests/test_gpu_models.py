@@ -357,6 +357,40 @@ def test_geometry_prefetched_from_backward_hook(ctor):
     assert torch.equal(ref, got)
 
 
+@pytest.mark.parametrize('ctor', [lambda: pcseg.PointNetpp(14), lambda: pcseg.PointNeXt(14),
+                                  lambda: pcseg.PointNetppMSG(14)], ids=['pointnetpp', 'pointnext', 'msg'])
+@pytest.mark.parametrize('inverse', [True, False])
+def test_native_geometry_plan_equals_python_plan(ctor, inverse):
+    """pcs_geometry_plan (one native call, csrc/geometry.hip) against the per-op Python plan
+    (taken under a replay context): same FPS draws, so every FPS index list, centroid, ball
+    table, 3-NN table and inverse map must be bitwise equal; also when written into another
+    plan's tensors (the graph-mode double buffer)."""
+    model = ctor().to(DEV)
+    pts, _, _ = make_batch(3, 4096, seed=41)
+    x = pts.to(DEV)
+    c0 = model._coords_of(x)
+    torch.manual_seed(9)
+    nat = model._plan_for(c0, inverse=inverse)
+    torch.manual_seed(9)
+    with pcseg.replay(pcseg.Replay()):
+        py = model._plan_for(c0, inverse=inverse)
+    torch.cuda.synchronize()
+    ta, tb = nat.tensors(), py.tensors()
+    assert len(ta) == len(tb) and len(nat.fps_idx) == len(py.fps_idx)
+    for a, b in zip(ta + nat.fps_idx, tb + py.fps_idx):
+        assert a.shape == b.shape and a.dtype == b.dtype and torch.equal(a, b)
+    torch.manual_seed(10)
+    other = model._plan_for(c0, inverse=inverse)
+    torch.cuda.synchronize()
+    other.settle()
+    torch.manual_seed(9)
+    again = model._plan_for(c0, inverse=inverse, into=other)
+    torch.cuda.synchronize()
+    assert all(a.data_ptr() == b.data_ptr() for a, b in zip(again.tensors()[1:], other.tensors()[1:]))
+    for a, b in zip(other.tensors()[1:] + other.fps_idx, tb[1:] + py.fps_idx):
+        assert torch.equal(a, b)
+
+
 def test_geometry_plan_copy_from_double_buffer():
     """GeometryPlan.copy_from (bench.py --graph's double-buffered geometry): after copying
     plan B into plan A's tensors, a forward that consumes A gives exactly the logits of a

@@ -335,8 +335,10 @@ def test_inverse_index_and_group_bwd_csr(B, N, C, K, r):
     assert torch.equal(g1, fb.grad)
 
 
-def test_interp_bwd_csr_with_and_without_forward_map():
-    B, N, M, D1, D2 = 2, 4096, 1024, 8, 64
+@pytest.mark.parametrize('D2', [64, 128, 256])
+def test_interp_bwd_csr_with_and_without_forward_map(D2):
+    """D2 = 128 / 256 take the channel-vector kernel (one list pass, float2 / float4 lanes)."""
+    B, N, M, D1 = 2, 4096, 1024, 8
     c1 = cloud(B, N, seed=42).to(DEV)
     c2 = c1[:, :M].contiguous()
     idx, dist = ops.knn_select(c1, c2, 3)
@@ -351,6 +353,15 @@ def test_interp_bwd_csr_with_and_without_forward_map():
     (ya * w).sum().backward()
     (yb * w).sum().backward()
     assert torch.equal(f2a.grad, f2b.grad)
+    # against the fp64 sum of the fp32 terms (g / norm) * w_j, list (= slot) order, rounded once
+    d = dist.double().cpu().float()
+    wts = 1.0 / (d + 1e-9)
+    nrm = (wts[..., 0] + wts[..., 1]) + wts[..., 2]
+    g = w.cpu().view(B, N, D1 + D2)[:, :, D1:]
+    terms = (g.unsqueeze(2) / nrm[..., None, None]) * wts[..., None]          # (B, N, 3, D2) fp32
+    ref = torch.zeros(B, M, D2, dtype=torch.float64)
+    ref.scatter_add_(1, idx.long().cpu().reshape(B, N * 3, 1).expand(-1, -1, D2), terms.reshape(B, N * 3, D2).double())
+    assert torch.equal(f2b.grad.cpu(), ref.float())
 
 
 @pytest.mark.parametrize('B,S,k,targets,kind', [(3, 500, 7, 1000, 'random'), (2, 1024, 32, 4096, 'same'),
