@@ -11,7 +11,7 @@ import torch
 import torch.nn as nn
 
 from . import ops
-from .engine import shared_mlp, pad_rows
+from .engine import shared_mlp, pad_rows, module_cache
 from ._lib import call, stream_ptr
 from .replay import active as _replay
 
@@ -395,7 +395,8 @@ class MiniPointNet(nn.Module):
 
     def forward_rows(self, x: torch.Tensor, kin: int | None = None, pool_k: int = 0) -> torch.Tensor:
         """rows (M, ld) -> (M, C_L), or (M/pool_k, C_L) max-pooled over consecutive groups of pool_k rows."""
-        return shared_mlp(x, kin or x.shape[1], self.conv, self.batch, 'relu', 0.0, pool_k, bwd_fuse=self.bwd_fuse)
+        return shared_mlp(x, kin or x.shape[1], self.conv, self.batch, 'relu', 0.0, pool_k, bwd_fuse=self.bwd_fuse,
+                          cache=module_cache(self))
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         B, Cin, H, W = x.shape
@@ -420,7 +421,7 @@ class UnitPointNet(nn.Module):
     def forward_rows(self, x: torch.Tensor, kin: int | None = None, dropout: tuple | None = None) -> torch.Tensor:
         """dropout = (p, seed): a training-mode Dropout after the stack, fused into its output."""
         return shared_mlp(x, kin or x.shape[1], self.conv, self.batch, 'relu', 0.0, 0, dropout=dropout,
-                          bwd_fuse=self.bwd_fuse)
+                          bwd_fuse=self.bwd_fuse, cache=module_cache(self))
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         B, Cin, N = x.shape

@@ -212,6 +212,14 @@ def lane_join(dev: torch.device) -> None:
         call('pcs_wgrad_lane_join', stream_ptr(dev))
 
 
+def module_cache(m: torch.nn.Module) -> dict:
+    """The per-module dict shared_mlp keeps a stack's static layer records in (host cost)."""
+    c = m.__dict__.get('_pcs_cache')
+    if c is None:
+        c = m.__dict__['_pcs_cache'] = {}
+    return c
+
+
 def set_bwd_fuse(module: torch.nn.Module, policy: str = 'default') -> None:
     """Per-module backward kernel choice of every shared-MLP stack under `module`
     (pcs_mlp_layer.bwd_fuse): 'default' fuses a thin layer's data + weight gradient into one
@@ -236,6 +244,52 @@ def _workspace(lib, key, M, kin, ldx, recs, nl, pool_k, backward):
 
 def _nz(p) -> int:
     return 0 if p is None else p.data_ptr()
+
+
+_STATIC = struct.Struct('<QqqqQQQQQQddqqd')     # pcs_mlp_layer fields W .. slope
+_DYN = struct.Struct('<QQQQQQdqq')               # Z coef dW db dgamma dbeta drop_p drop_seed bwd_fuse
+assert _STATIC.size + _DYN.size == _REC.size
+
+
+def _layer_statics(Kin, bns, acts, params, couts, dev):
+    """([static record bytes per layer], [weight matrices as the kernels read them], cacheable):
+    the pcs_mlp_layer fields that do not change from call to call.  Not cacheable when a weight
+    needs a padded copy (refreshed every call) or a BN momentum is None (cumulative average)."""
+    statics, Wms = [], []
+    cacheable = True
+    cin = Kin
+    for li, bn in enumerate(bns):
+        W, b, g, be = params[4 * li:4 * li + 4]
+        C = couts[li]
+        if C % 4:
+            raise ValueError(f'engine: layer width {C} must be a multiple of 4')
+        Wm = W.reshape(C, -1)
+        if Wm.shape[1] % 4 and li > 0:    # 16-B weight rows (the pad columns are zero)
+            Wp = torch.zeros((C, ld4(Wm.shape[1])), dtype=torch.float32, device=dev)
+            Wp[:, :Wm.shape[1]] = Wm
+            Wm = Wp
+            cacheable = False
+        elif not Wm.is_contiguous():        # (an unpadded first layer is read as is)
+            Wm = Wm.contiguous()
+            cacheable = False
+        Wms.append(Wm)
+        use_batch = bn.training or bn.running_mean is None
+        track = use_batch and bn.training and bn.track_running_stats and bn.running_mean is not None
+        momentum = 0.0
+        if track:
+            if bn.momentum is None:
+                cacheable = False
+                momentum = 1.0 / float(bn.num_batches_tracked + 1)
+            else:
+                momentum = bn.momentum
+        rm = bn.running_mean if (track or not use_batch) else None
+        rv = bn.running_var if (track or not use_batch) else None
+        nbt = bn.num_batches_tracked if track else None
+        act, slope = acts[li]
+        statics.append(_STATIC.pack(Wm.data_ptr(), Wm.shape[1], cin, C, _nz(b), _nz(g), _nz(be), _nz(rm), _nz(rv),
+                                    _nz(nbt), float(momentum), float(bn.eps), int(use_batch), act, slope))
+        cin = C
+    return statics, Wms, cacheable
 
 
 def _workspace_probe(lib, key, M, Kin, ldx, params, bns, nl, pool_K, couts, acts):
@@ -264,7 +318,7 @@ class SharedMLPFn(torch.autograd.Function):
     record per layer."""
 
     @staticmethod
-    def forward(ctx, X, Kin, pool_K, acts, bns, dest, drop, bwd_fuse, *params):
+    def forward(ctx, X, Kin, pool_K, acts, bns, dest, drop, bwd_fuse, cache, *params):
         dev = X.device
         st = stream_ptr(dev)
         lib = load()
@@ -284,41 +338,30 @@ class SharedMLPFn(torch.autograd.Function):
             buf = _f32((wsoff + (nws + 3) // 4,), dev)
         Zbuf = buf[:M * tot]
         coef = buf[M * tot:zc]
-        Wms, fixed = [], []
-        off, cin = 0, Kin
-        for li in range(nl):
-            W, b, g, be = params[4 * li:4 * li + 4]
-            bn = bns[li]
-            C = couts[li]
-            if C % 4:
-                raise ValueError(f'engine: layer width {C} must be a multiple of 4')
-            Wm = W.reshape(C, -1)
-            if Wm.shape[1] % 4 and li > 0:    # 16-B weight rows (the pad columns are zero)
-                Wp = torch.zeros((C, ld4(Wm.shape[1])), dtype=torch.float32, device=dev)
-                Wp[:, :Wm.shape[1]] = Wm
-                Wm = Wp
-            elif not Wm.is_contiguous():        # (an unpadded first layer is read as is)
-                Wm = Wm.contiguous()
-            Wms.append(Wm)
-            use_batch = bn.training or bn.running_mean is None
-            track = use_batch and bn.training and bn.track_running_stats and bn.running_mean is not None
-            momentum = 0.0
-            if track:
-                momentum = bn.momentum if bn.momentum is not None else 1.0 / float(bn.num_batches_tracked + 1)
-            rm = bn.running_mean if (track or not use_batch) else None
-            rv = bn.running_var if (track or not use_batch) else None
-            nbt = bn.num_batches_tracked if track else None
-            act, slope = acts[li]
-            fixed.append((Wm.data_ptr(), Wm.shape[1], cin, C, _nz(b), _nz(g), _nz(be), _nz(rm), _nz(rv), _nz(nbt),
-                          float(momentum), float(bn.eps), int(use_batch), act, slope,
-                          Zbuf.data_ptr() + 4 * M * off, coef.data_ptr() + 16 * off))
+        # the per-layer static record fields (W .. slope): cached on the calling module (`cache`,
+        # e.g. a MiniPointNet's dict) while the parameters' storage and the BN modes are unchanged
+        ent = None
+        if cache is not None:
+            key = (Kin, acts, tuple(bn.training for bn in bns), tuple(_nz(p) for p in params))
+            ent = cache.get('static')
+            if ent is not None and ent[0] != key:
+                ent = None
+        if ent is None:
+            statics, Wms, cacheable = _layer_statics(Kin, bns, acts, params, couts, dev)
+            if cache is not None and cacheable:
+                cache['static'] = (key, statics, Wms)
+        else:
+            statics, Wms = ent[1], ent[2]
+        zc_ptr, cf_ptr = Zbuf.data_ptr(), coef.data_ptr()
+        zptrs, off = [], 0
+        for C in couts:
+            zptrs.append((zc_ptr + 4 * M * off, cf_ptr + 16 * off))
             off += C
-            cin = C
         # drop = (p, seed): the training-mode Dropout after the stack, fused into its output
         dp, dseed = drop if drop is not None else (0.0, 0)
-        recs = b''.join(_REC.pack(*f, 0, 0, 0, 0, dp if li == nl - 1 else 0.0, dseed if li == nl - 1 else 0,
-                                  bwd_fuse)
-                        for li, f in enumerate(fixed))
+        recs = b''.join(statics[li] + _DYN.pack(zp, cp, 0, 0, 0, 0, dp if li == nl - 1 else 0.0,
+                                                  dseed if li == nl - 1 else 0, bwd_fuse)
+                        for li, (zp, cp) in enumerate(zptrs))
         CL = couts[-1]
         ldo = 0
         if pool_K:
@@ -348,7 +391,7 @@ class SharedMLPFn(torch.autograd.Function):
                     record_act_mask(Z * cf[:C] + cf[C:] > 0)
                 off += C
         ctx.save_for_backward(X, Zbuf, coef, *Wms, *([arg] if arg is not None else []))
-        ctx.meta = (Kin, pool_K, nl, fixed, couts, arg is not None)
+        ctx.meta = (Kin, pool_K, nl, statics, zptrs, couts, arg is not None)
         ctx.drop = drop
         ctx.bwd_fuse = bwd_fuse
         ctx.params = params
@@ -356,7 +399,7 @@ class SharedMLPFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gout):
-        Kin, pool_K, nl, fixed, couts, has_arg = ctx.meta
+        Kin, pool_K, nl, statics, zptrs, couts, has_arg = ctx.meta
         saved = ctx.saved_tensors
         X = saved[0]
         arg = saved[3 + nl] if has_arg else None
@@ -376,10 +419,11 @@ class SharedMLPFn(torch.autograd.Function):
                  ptr(g2), couts[-1], st)
             gout = g2
         ldg = gout.stride(0)
-        recs = b''.join(_REC.pack(*f, _nz(grad_target(params[4 * li])), _nz(grad_target(params[4 * li + 1])),
-                                  _nz(grad_target(params[4 * li + 2])), _nz(grad_target(params[4 * li + 3])), 0, 0,
-                                  ctx.bwd_fuse)
-                        for li, f in enumerate(fixed))
+        recs = b''.join(statics[li] + _DYN.pack(zp, cp, _nz(grad_target(params[4 * li])),
+                                                  _nz(grad_target(params[4 * li + 1])),
+                                                  _nz(grad_target(params[4 * li + 2])),
+                                                  _nz(grad_target(params[4 * li + 3])), 0.0, 0, ctx.bwd_fuse)
+                        for li, (zp, cp) in enumerate(zptrs))
         dX = None
         if ctx.needs_input_grad[0]:
             dX = _f32((M, X.shape[1]), dev)       # dense, X's width (its pad columns zeroed)
@@ -398,7 +442,7 @@ class SharedMLPFn(torch.autograd.Function):
                 t.record_stream(lane)
             _queue_lane_join(dev)
         notify_grad_ready(params)
-        return (dX, None, None, None, None, None, None, None, *([None] * len(params)))
+        return (dX, None, None, None, None, None, None, None, None, *([None] * len(params)))
 
 
 def _edge_ws(B, N, C, Cout, backward, dev):
@@ -529,14 +573,16 @@ def _rows_ok(x: torch.Tensor) -> bool:
 
 def shared_mlp(x_rows: torch.Tensor, kin: int, convs, bns, act='relu', slope=0.0,
                pool_k: int = 0, out: torch.Tensor | None = None, dropout: tuple | None = None,
-               bwd_fuse: int = 0) -> torch.Tensor:
+               bwd_fuse: int = 0, cache: dict | None = None) -> torch.Tensor:
     """Run a conv/BN/act stack on rows.  x_rows (M, W) with `kin` logical channels, W % 4 == 0,
     dense or a column block of a wider buffer (row stride >= W).  `act` / `slope` are one value
     for every layer or a sequence with one per layer ('relu', 'lrelu', 'none').  `out`: an
     (M, cout) row block (storage_alias) the un-pooled activation is written into.  `dropout` =
     (p, seed): a training-mode nn.Dropout(p) after the stack, fused into its output
     (pcs_mlp_layer.drop_p; backward pcs_dropout_bwd recomputes the mask from the seed).
-    `bwd_fuse`: the stack's backward kernel choice (BWD_FUSE values, pcs_mlp_layer.bwd_fuse)."""
+    `bwd_fuse`: the stack's backward kernel choice (BWD_FUSE values, pcs_mlp_layer.bwd_fuse).
+    `cache`: a dict owned by the calling module, where the stack's static layer records are
+    kept between calls (host enqueue cost)."""
     if not x_rows.is_cuda:
         raise RuntimeError('pcseg ops run only on the GPU (no CPU fallback); got a CPU tensor')
     if not _rows_ok(x_rows):
@@ -555,7 +601,7 @@ def shared_mlp(x_rows: torch.Tensor, kin: int, convs, bns, act='relu', slope=0.0
     if dropout is not None and (pool_k or not 0.0 < float(dropout[0]) < 1.0):
         raise ValueError('shared_mlp: dropout needs an un-pooled output and 0 < p < 1')
     return SharedMLPFn.apply(x_rows, kin, pool_k, acts, list(bns), None if out is None else (out,), dropout,
-                             int(bwd_fuse), *params)
+                             int(bwd_fuse), cache, *params)
 
 
 class RowLinearFn(torch.autograd.Function):

@@ -17,7 +17,7 @@ import torch.nn.functional as F
 
 from . import ops
 from .common import SetAbstraction, FeaturePropagation, InvResMLP, UnitPointNet, GeometryPlan, GeometryPrefetch
-from .engine import shared_mlp, pad_rows, linear_rows, edgeconv, edgeconv_fused_ok, storage_alias
+from .engine import shared_mlp, pad_rows, linear_rows, edgeconv, edgeconv_fused_ok, storage_alias, module_cache
 from .replay import active as _replay
 from ._lib import call, ptr, stream_ptr
 
@@ -212,7 +212,7 @@ def _seq_rows(x_rows: torch.Tensor, seq: nn.Sequential, kin: int | None = None,
     # training-mode Dropout fused into the stack's output
     drop = _fused_dropout(seq[3]) if len(seq) > 3 and out is None else None
     y = shared_mlp(x_rows, kin or x_rows.shape[1], [seq[0]], [seq[1]], 'lrelu', seq[2].negative_slope, 0, out=out,
-                   dropout=drop)
+                   dropout=drop, cache=module_cache(seq))
     if len(seq) > 3 and drop is None:
         y = seq[3](y)
     return y
