@@ -180,6 +180,15 @@ __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(GemmArgs g) {
         // keep the next slab's loads in flight: nothing that consumes them may be
         // scheduled above the MFMAs of this slab
         __builtin_amdgcn_sched_barrier(0);
+        // two-level fp32 accumulation (tiles with <= 2 MFMA blocks per wave, whose second set of
+        // accumulators fits the register budget; the 4-block 128 x 128 tile would spill): the
+        // slab's 16 MFMA steps (32 k) go into a fresh accumulator that is then added to the
+        // tile's running sum, so an output element sees 16 + K/32 roundings instead of K/2 (one
+        // per MFMA step).  Over K = 512 .. 2048 (the data gradients of the wide layers) that is
+        // 2-3x less rounding error in dX, the CPU reference's sgemm level
+        // (scripts/diag/stack_grad_error.py); the cost is 16 VALU adds per 16 MFMAs.
+        constexpr bool TWO = TM * TN <= 2;
+        f32x16 sacc[TWO ? TM : 1][TWO ? TN : 1];
 #pragma unroll
         for (int qq = 0; qq < 4; ++qq) {
             float4 a[TM], b[TN];
@@ -195,11 +204,19 @@ __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(GemmArgs g) {
             for (int i = 0; i < TM; ++i)
 #pragma unroll
                 for (int j = 0; j < TN; ++j) {
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].x, b[j].x, acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].y, b[j].y, acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].z, b[j].z, acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].w, b[j].w, acc[i][j], 0, 0, 0);
+                    f32x16& d = TWO ? sacc[TWO ? i : 0][TWO ? j : 0] : acc[i][j];
+                    const f32x16 c0 = {};
+                    d = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].x, b[j].x, (TWO && qq == 0) ? c0 : d, 0, 0, 0);
+                    d = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].y, b[j].y, d, 0, 0, 0);
+                    d = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].z, b[j].z, d, 0, 0, 0);
+                    d = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].w, b[j].w, d, 0, 0, 0);
                 }
+        }
+        if constexpr (TWO) {
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) acc[i][j] += sacc[TWO ? i : 0][TWO ? j : 0];
         }
         __builtin_amdgcn_sched_barrier(0);
         if (ks == nk - 1) {

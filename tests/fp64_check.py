@@ -187,4 +187,11 @@ def report(rows, rtol=1e-3, factor=10.0, floor=1e-3):
         lines.append(f'{cl[name] or "FAIL":9s} gpu/truth {rel:9.2e}  cpu32/truth {ec / n if n else 0.0:9.2e}  {name}')
     counts = {k: sum(v == k for v in cl.values()) for k in ('rel', 'ref-noise', 'floor', None)}
     lines.append(f'clauses: {counts}')
+    w = [(eg / ec if ec else float('inf'), eg / n if n else 0.0, name) for name, eg, ec, n, *_ in rows
+         if is_weight(name) and n]
+    if w:
+        ratio = max(w)
+        rel = max(w, key=lambda t: t[1])
+        lines.append(f'worst weight: gpu/cpu32 error ratio {ratio[0]:.2f} ({ratio[2]}), '
+                     f'gpu/truth {rel[1]:.2e} ({rel[2]})')
     return '\n'.join(lines)
