@@ -15,6 +15,13 @@
 // whose segments fill is merged by a ballot quickselect (no sort); the final merge ranks
 // the survivors (larger pd first, ties to the lower index).  The scan starts at the wave's
 // own tile, so spatially ordered clouds tighten the thresholds early.
+// Seeded threshold (pcs_knn_seeded): DGCNN's graphs 2-4 are built on features of the previous
+// EdgeConv, whose neighbour lists are mostly still near in the new space (15-17 of 20 shared
+// on the synthetic blocks).  The k-th best distance among any k candidates is a lower bound of
+// the row's true k-th best, so each row starts its scan with the threshold of its previous
+// neighbours (minus a rounding margin): about 30-45 survivors per row instead of ~180, and
+// the running merges almost vanish.  The lists are the same as unseeded: every true top-k
+// candidate still passes the (lower) threshold.
 // knn_kernel (k = 40): one thread per query row with a sorted register list.
 #include "pcs_common.hpp"
 
@@ -260,10 +267,13 @@ __device__ __forceinline__ float knn_select_row(float2* L, int nl, int c0, int c
 // same partial sums and the same final add as below, so the lists are bitwise the same; it
 // removes F multiply-adds per lane and tile (the candidate side recomputed every norm in every
 // wave that streams it)
-template <int F, int K, int WPB, bool PRE>
+// seeds (SEEDED, nullable): (B, N, ks) candidate lists whose k-th best bounds each row's
+// threshold from the start (rows with out-of-range or repeated seeds, or ks < K, start at -inf)
+template <int F, int K, int WPB, bool PRE, bool SEEDED>
 __global__ __launch_bounds__(64 * WPB, 2) void knn_wave_kernel(const float* __restrict__ x, int B, int N, int rblocks,
                                                             int* __restrict__ out_idx,
-                                                            const float* __restrict__ xx_pre) {
+                                                            const float* __restrict__ xx_pre,
+                                                            const int* __restrict__ seeds, int ks) {
     constexpr bool MF = (F % 4 == 0);
     static_assert(MF || F == 3, "F must be 3 or a multiple of 4");
     constexpr int FH = MF ? F / 2 : 2;
@@ -321,6 +331,41 @@ __global__ __launch_bounds__(64 * WPB, 2) void knn_wave_kernel(const float* __re
     }
     if constexpr (PRE) xxq = xx_pre[(size_t)b * N + qr];
     float tau = -INFINITY;
+    if constexpr (SEEDED) {
+        static_assert(MF && PRE, "seeded threshold: F % 4 == 0 with precomputed norms");
+        // the k-th best pd among the row's seeds (here: the minimum over k of them).  The scan's
+        // pd comes from an MFMA dot in another summation order: the margin 2^-14 (|x_q|^2 + |x_s|^2)
+        // covers that (|dot error| <= ~F u sum|x_q x_s| <= 64 u (|x_q|^2 + |x_s|^2) / 2)
+        const int* sr = seeds + ((size_t)b * N + qr) * ks;
+        float t0 = INFINITY;
+        bool ok = ks >= K;
+        int prev[K];
+        const int nsd = ks < K ? 0 : K;
+        for (int j = 0; j < nsd; ++j) {
+            const int sj = sr[j];
+            ok = ok && sj >= 0 && sj < N;
+            const int sc = (sj >= 0 && sj < N) ? sj : 0;
+#pragma unroll
+            for (int u = 0; u < K; ++u) ok = ok && !(u < j && prev[u] == sc);
+#pragma unroll
+            for (int u = 0; u < K; ++u) prev[u] = u == j ? sc : prev[u];
+            const float4* src = reinterpret_cast<const float4*>(X + (size_t)sc * F + h * FH);
+            float part = 0.f;
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                const float4 v = src[q];
+                part = __fmaf_rn(a[4 * q], v.x, part);
+                part = __fmaf_rn(a[4 * q + 1], v.y, part);
+                part = __fmaf_rn(a[4 * q + 2], v.z, part);
+                part = __fmaf_rn(a[4 * q + 3], v.w, part);
+            }
+            const float dot = __fadd_rn(part, __shfl_xor(part, 32));
+            const float cx = xx_pre[(size_t)b * N + sc];
+            const float pd = __fsub_rn(__fsub_rn(-xxq, -2.f * dot), cx);
+            t0 = fminf(t0, __fsub_rn(pd, ldexpf(__fadd_rn(xxq, cx), -14)));
+        }
+        tau = ok ? t0 : -INFINITY;
+    }
     int cnt = 0, nl = 0;
 
     const int ntile = (N + KNN_TC - 1) / KNN_TC;
@@ -480,7 +525,7 @@ template <int K>
 constexpr bool knn_tiled() { return (KNN_NMAX - K) / 2 - 1 >= 16; }
 
 template <int F, int K>
-static void launch_knn(const float* x, int B, int N, int* out, float* xx, hipStream_t s) {
+static void launch_knn(const float* x, int B, int N, int* out, float* xx, const int* seeds, int ks, hipStream_t s) {
     if constexpr (knn_tiled<K>()) {
         const int rb = (N + KNN_QROWS - 1) / KNN_QROWS;
         if (xx) {
@@ -488,13 +533,22 @@ static void launch_knn(const float* x, int B, int N, int* out, float* xx, hipStr
             hipLaunchKernelGGL((knn_sqnorm_kernel<F>), dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, x, P, xx);
             // algorithmic: the N x N inner-product tile per cloud (2F flops per pair, the
             // reference's bmm), x read + the k-lists written
+            if constexpr (F % 4 == 0) {
+                if (seeds) {
+                    ProbeScope pr(s, 2.0 * F * (double)N * N * B, 4.0 * (double)B * N * (F + K),
+                                  "pcs::knn_wave_kernel<%d, %d, %d, true, seeded>", F, K, KNN_WAVES);
+                    hipLaunchKernelGGL((knn_wave_kernel<F, K, KNN_WAVES, true, true>), dim3(rb * B),
+                                       dim3(64 * KNN_WAVES), 0, s, x, B, N, rb, out, (const float*)xx, seeds, ks);
+                    return;
+                }
+            }
             ProbeScope pr(s, 2.0 * F * (double)N * N * B, 4.0 * (double)B * N * (F + K), "pcs::knn_wave_kernel<%d, %d, %d, true>",
                           F, K, KNN_WAVES);
-            hipLaunchKernelGGL((knn_wave_kernel<F, K, KNN_WAVES, true>), dim3(rb * B), dim3(64 * KNN_WAVES), 0, s, x, B,
-                               N, rb, out, (const float*)xx);
+            hipLaunchKernelGGL((knn_wave_kernel<F, K, KNN_WAVES, true, false>), dim3(rb * B), dim3(64 * KNN_WAVES), 0, s,
+                               x, B, N, rb, out, (const float*)xx, (const int*)nullptr, 0);
         } else {
-            hipLaunchKernelGGL((knn_wave_kernel<F, K, KNN_WAVES, false>), dim3(rb * B), dim3(64 * KNN_WAVES), 0, s, x,
-                               B, N, rb, out, (const float*)nullptr);
+            hipLaunchKernelGGL((knn_wave_kernel<F, K, KNN_WAVES, false, false>), dim3(rb * B), dim3(64 * KNN_WAVES), 0,
+                               s, x, B, N, rb, out, (const float*)nullptr, (const int*)nullptr, 0);
         }
         return;
     }
@@ -502,12 +556,13 @@ static void launch_knn(const float* x, int B, int N, int* out, float* xx, hipStr
 }
 
 template <int F>
-static int dispatch_k(const float* x, int B, int N, int k, int* out, float* xx, hipStream_t s) {
+static int dispatch_k(const float* x, int B, int N, int k, int* out, float* xx, const int* seeds, int ks,
+                      hipStream_t s) {
     switch (k) {
-        case 16: launch_knn<F, 16>(x, B, N, out, xx, s); return 0;
-        case 20: launch_knn<F, 20>(x, B, N, out, xx, s); return 0;
-        case 32: launch_knn<F, 32>(x, B, N, out, xx, s); return 0;
-        case 40: launch_knn<F, 40>(x, B, N, out, xx, s); return 0;
+        case 16: launch_knn<F, 16>(x, B, N, out, xx, seeds, ks, s); return 0;
+        case 20: launch_knn<F, 20>(x, B, N, out, xx, seeds, ks, s); return 0;
+        case 32: launch_knn<F, 32>(x, B, N, out, xx, seeds, ks, s); return 0;
+        case 40: launch_knn<F, 40>(x, B, N, out, xx, seeds, ks, s); return 0;
         default:
             set_error("pcs_knn: k=%d not instantiated (16, 20, 32, 40)", k);
             return (int)hipErrorInvalidValue;
@@ -516,7 +571,8 @@ static int dispatch_k(const float* x, int B, int N, int k, int* out, float* xx, 
 
 }  // namespace pcs
 
-static int knn_run(const float* x, int B, int N, int F, int k, int32_t* out_idx, float* xx, void* stream) {
+static int knn_run(const float* x, int B, int N, int F, int k, int32_t* out_idx, float* xx, const int32_t* seeds,
+                   int ks, void* stream) {
     using namespace pcs;
     PCS_CHECK_ARG(B >= 0 && N >= 1 && k >= 1 && k <= N, "pcs_knn: bad sizes B=%d N=%d k=%d", B, N, k);
     PCS_CHECK_ARG(x && out_idx, "pcs_knn: null pointer");
@@ -524,8 +580,8 @@ static int knn_run(const float* x, int B, int N, int F, int k, int32_t* out_idx,
     hipStream_t s = as_stream(stream);
     int rc;
     switch (F) {
-        case 3: rc = dispatch_k<3>(x, B, N, k, out_idx, xx, s); break;
-        case 64: rc = dispatch_k<64>(x, B, N, k, out_idx, xx, s); break;
+        case 3: rc = dispatch_k<3>(x, B, N, k, out_idx, xx, nullptr, 0, s); break;
+        case 64: rc = dispatch_k<64>(x, B, N, k, out_idx, xx, seeds, ks, s); break;
         default:
             set_error("pcs_knn: F=%d not instantiated (3, 64)", F);
             return (int)hipErrorInvalidValue;
@@ -537,7 +593,7 @@ static int knn_run(const float* x, int B, int N, int F, int k, int32_t* out_idx,
 // Reference: models/dgcnn/dgcnn.py:7-21.  x point-major (B, N, F) fp32; out (B, N, k) int32,
 // best first.  F in {3, 64}; k in {16, 20, 32, 40}.
 PCS_API int pcs_knn(const float* x, int B, int N, int F, int k, int32_t* out_idx, void* stream) {
-    return knn_run(x, B, N, F, k, out_idx, nullptr, stream);
+    return knn_run(x, B, N, F, k, out_idx, nullptr, nullptr, 0, stream);
 }
 
 PCS_API int pcs_knn_workspace(int B, int N, size_t* bytes) {
@@ -552,5 +608,17 @@ PCS_API int pcs_knn_ws(const float* x, int B, int N, int F, int k, int32_t* out_
                        void* stream) {
     PCS_CHECK_ARG(ws && ws_bytes >= (size_t)B * N * sizeof(float) + 256, "pcs_knn_ws: workspace too small");
     float* xx = reinterpret_cast<float*>((reinterpret_cast<uintptr_t>(ws) + 255) & ~uintptr_t(255));
-    return knn_run(x, B, N, F, k, out_idx, xx, stream);
+    return knn_run(x, B, N, F, k, out_idx, xx, nullptr, 0, stream);
+}
+
+// pcs_knn_ws whose rows start from the threshold of a previous neighbour list (seeds (B, N, ks)
+// int32, e.g. the previous EdgeConv's graph): the same lists, fewer survivors to merge.  Any
+// seeds are safe -- a row whose seeds are out of range, repeated or fewer than k is searched
+// unseeded.  Seeding applies to F = 64 (F = 3 ignores the seeds).
+PCS_API int pcs_knn_seeded(const float* x, int B, int N, int F, int k, const int32_t* seeds, int ks, int32_t* out_idx,
+                           void* ws, size_t ws_bytes, void* stream) {
+    PCS_CHECK_ARG(ws && ws_bytes >= (size_t)B * N * sizeof(float) + 256, "pcs_knn_seeded: workspace too small");
+    PCS_CHECK_ARG(seeds && ks >= 1, "pcs_knn_seeded: null seeds or ks < 1");
+    float* xx = reinterpret_cast<float*>((reinterpret_cast<uintptr_t>(ws) + 255) & ~uintptr_t(255));
+    return knn_run(x, B, N, F, k, out_idx, xx, seeds, ks, stream);
 }

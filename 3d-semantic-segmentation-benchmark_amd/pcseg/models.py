@@ -254,22 +254,28 @@ class EdgeConv(nn.Module):
 
     def forward_points(self, xp: torch.Tensor) -> torch.Tensor:
         """xp point-major (B, N, C) -> (B, N, Cout)."""
+        return self.forward_graph(xp)[0]
+
+    def forward_graph(self, xp: torch.Tensor, seeds: torch.Tensor | None = None):
+        """(output (B, N, Cout), this layer's kNN graph (B, N, k) int32).  seeds: the previous
+        EdgeConv's graph -- its neighbours' distances in this layer's feature space bound the
+        search threshold from the start (same graph, less merge work)."""
         B, N, _ = xp.shape
         rp = _replay()
         if rp is not None and rp.knn_idx:
             idx = rp.knn_idx.pop(0).to(device=xp.device, dtype=torch.int32).contiguous()
         else:
-            idx = ops.knn(xp, self.k)
+            idx = ops.knn(xp, self.k, seeds=seeds)
         if rp is not None:
             rp.rec_knn_idx.append(idx.detach().cpu())
         C = xp.shape[2]
         if edgeconv_fused_ok(self.conv[0], self.conv[1], C):
             pooled = edgeconv(xp.reshape(B * N, C), C, idx, self.conv[0], self.conv[1], self.conv[2].negative_slope)
-            return pooled.view(B, N, -1)
+            return pooled.view(B, N, -1), idx
         rows = ops.edge_rows(xp, idx)
         pooled = shared_mlp(rows, 2 * C, [self.conv[0]], [self.conv[1]], 'lrelu',
                             self.conv[2].negative_slope, pool_k=self.k)
-        return pooled.view(B, N, -1)
+        return pooled.view(B, N, -1), idx
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         return self.forward_points(x.transpose(1, 2).contiguous()).transpose(1, 2)
@@ -378,10 +384,10 @@ class DGCNN(nn.Module):
         B, _, N = x.shape
         xyz = x[:, :3, :] if x.size(1) == 6 else x
         xp = xyz.transpose(1, 2).contiguous()
-        x1 = self.conv1.forward_points(xp)
-        x2 = self.conv2.forward_points(x1)
-        x3 = self.conv3.forward_points(x2)
-        x4 = self.conv4.forward_points(x3)
+        x1, g = self.conv1.forward_graph(xp)
+        x2, g = self.conv2.forward_graph(x1, g)
+        x3, g = self.conv3.forward_graph(x2, g)
+        x4, _ = self.conv4.forward_graph(x3, g)
         return _dgcnn_head(self, [x1, x2, x3, x4], B, N)
 
 
@@ -411,10 +417,10 @@ class DGCNNWithColor(nn.Module):
         xp = x.transpose(1, 2)                           # (B, N, 6) view of the (B,6,N) input
         xyz = xp[:, :, :3].contiguous()
         rgb = xp[:, :, 3:6].contiguous()
-        x1 = self.conv1.forward_points(xyz)
-        x2 = self.conv2.forward_points(x1)
-        x3 = self.conv3.forward_points(x2)
-        x4 = self.conv4.forward_points(x3)
+        x1, g = self.conv1.forward_graph(xyz)
+        x2, g = self.conv2.forward_graph(x1, g)
+        x3, g = self.conv3.forward_graph(x2, g)
+        x4, _ = self.conv4.forward_graph(x3, g)
         color = _seq_rows(pad_rows(rgb.view(B * N, 3)), self.color_conv, 3).view(B, N, -1)
         return _dgcnn_head(self, [x1, x2, x3, x4, color], B, N)
 

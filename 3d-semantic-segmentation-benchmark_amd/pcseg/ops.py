@@ -75,13 +75,22 @@ def knn_select(query: torch.Tensor, ref: torch.Tensor, k: int = 3, out=None):
     return idx, dist
 
 
-def knn(x: torch.Tensor, k: int) -> torch.Tensor:
-    """DGCNN feature-space kNN; x point-major (B,N,F) -> idx (B,N,k) int32."""
+def knn(x: torch.Tensor, k: int, seeds: torch.Tensor | None = None) -> torch.Tensor:
+    """DGCNN feature-space kNN; x point-major (B,N,F) -> idx (B,N,k) int32.  seeds (B,N,ks)
+    int32 (the previous graph) only speed the search up: the lists are the same."""
     check_cuda(x)
     x = _c(x.float())
     B, N, Fd = x.shape
     out = torch.empty((B, N, k), dtype=torch.int32, device=x.device)
     ws = torch.empty((B * N + 64,), dtype=torch.float32, device=x.device)    # per-point squared norms
+    if seeds is not None:
+        if seeds.dtype != torch.int32 or seeds.shape[:2] != (B, N) or seeds.device != x.device:
+            raise ValueError(f'knn seeds must be int32 (B, N, ks) on {x.device}, got {seeds.dtype} '
+                             f'{tuple(seeds.shape)} on {seeds.device}')
+        seeds = _c(seeds)
+        call('pcs_knn_seeded', ptr(x), B, N, Fd, k, ptr(seeds), seeds.shape[2], ptr(out), ptr(ws), ws.numel() * 4,
+             stream_ptr(x.device))
+        return out
     call('pcs_knn_ws', ptr(x), B, N, Fd, k, ptr(out), ptr(ws), ws.numel() * 4, stream_ptr(x.device))
     return out
 

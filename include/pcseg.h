@@ -62,6 +62,13 @@ int pcs_knn(const float* x, int B, int N, int F, int k, int32_t* out_idx,
 int pcs_knn_workspace(int B, int N, size_t* bytes);
 int pcs_knn_ws(const float* x, int B, int N, int F, int k, int32_t* out_idx,
                void* ws, size_t ws_bytes, void* stream);
+/* pcs_knn_ws whose rows start from the threshold of a previous neighbour list
+ * (seeds (B,N,ks) int32: DGCNN's previous EdgeConv graph, dgcnn.py:183-189 feeding
+ * get_graph_feature at :29-56): the same lists as pcs_knn, fewer survivors to merge.
+ * Rows whose seeds are out of range, repeated or fewer than k search unseeded; F = 3
+ * ignores the seeds. */
+int pcs_knn_seeded(const float* x, int B, int N, int F, int k, const int32_t* seeds,
+                   int ks, int32_t* out_idx, void* ws, size_t ws_bytes, void* stream);
 
 /* ---- geometry plan of a PointNet++-family forward --------------------------
  * One call enqueues, on one stream and in this order, every neighbour structure of a

@@ -45,17 +45,17 @@ for m, tag in ((ref32, 'r32'), (ref64, 'r64')):
         getattr(m, name).register_forward_hook(grab(tag))
 # product: wrap forward_points / _seq_rows outputs
 prod_out = []
-orig_fp = PM.EdgeConv.forward_points
+orig_fg = PM.EdgeConv.forward_graph
 
 
-def fp(self, xp):
-    o = orig_fp(self, xp)
+def fg(self, xp, seeds=None):
+    o, idx = orig_fg(self, xp, seeds)
     o.retain_grad()
     prod_out.append(o)
-    return o
+    return o, idx
 
 
-PM.EdgeConv.forward_points = fp
+PM.EdgeConv.forward_graph = fg
 orig_seq = PM._seq_rows
 
 

@@ -36,7 +36,11 @@ def timeit(fn):
 
 # (name, R = contraction, N = outputs, kind)
 SHAPES = [('conv5.fwd', 384, 1024), ('conv6.fwd', 1408, 512), ('conv7.fwd', 512, 256),
-          ('conv5.dgrad', 1024, 384), ('conv6.dgrad', 512, 1408), ('conv7.dgrad', 256, 512)]
+          ('conv5.dgrad', 1024, 384), ('conv6.dgrad', 512, 1408), ('conv7.dgrad', 256, 512),
+          # the same data gradients with N padded to a multiple of 256 (256-wide tiles)
+          ('conv5.dgrad256', 1024, 512), ('conv6.dgrad256', 512, 1536)]
+if os.environ.get('NT_ONLY'):
+    SHAPES = [s for s in SHAPES if s[0].startswith(tuple(os.environ['NT_ONLY'].split(',')))]
 for name, R, N in SHAPES:
     A = torch.randn(M, R, device=dev)
     B = torch.randn(N, R, device=dev) / R ** 0.5

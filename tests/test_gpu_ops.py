@@ -245,6 +245,56 @@ def test_dgcnn_knn_workspace_path_bitwise_equal(F_):
     assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize('k', [16, 20, 32])
+def test_dgcnn_knn_seeded_bitwise_equal(k):
+    """pcs_knn_seeded (rows start from the threshold of a previous neighbour list) gives
+    bitwise the same lists as the unseeded search, whatever the seeds: the previous graph of a
+    perturbed cloud (the DGCNN case), random seeds, seeds with repeats / out-of-range entries
+    (those rows search unseeded), too few seeds, and exact ties on integer features."""
+    g = torch.Generator().manual_seed(k)
+    B, N = 2, 4096
+    x = torch.randn(B, N, 64, generator=g).to(DEV)
+    base = ops.knn(x, k)
+    near = ops.knn((x + 0.3 * torch.randn(B, N, 64, generator=g).to(DEV)).contiguous(), k)
+    rnd = torch.randint(0, N, (B, N, k), generator=g, dtype=torch.int32).to(DEV)
+    bad = near.clone()
+    bad[:, ::3, 1] = bad[:, ::3, 0]            # repeats
+    bad[:, 1::3, 2] = N + 5                    # out of range
+    bad[:, 2::7, 3] = -1
+    for seeds in (near, rnd, bad, near[:, :, :k - 1].contiguous(), base):
+        assert torch.equal(ops.knn(x, k, seeds=seeds), base)
+    xi = torch.randint(-2, 3, (B, N, 64), generator=g).float().to(DEV)
+    bi = ops.knn(xi, k)
+    assert torch.equal(ops.knn(xi, k, seeds=ops.knn((xi + 0.5).contiguous(), k)), bi)
+    assert torch.equal(ops.knn(xi, k, seeds=bi), bi)
+
+
+def test_dgcnn_model_seeded_graphs_equal_unseeded():
+    """DGCNNWithColor's graphs 2-4 (seeded by the previous graph) equal the unseeded search on
+    the same features (B=2, N=4096)."""
+    torch.manual_seed(0)
+    m = pcseg.DGCNNWithColor(14).to(DEV).train()
+    pts, _, _ = make_batch(2, 4096, seed=31)
+    x = pts[:, :, :6].contiguous().transpose(1, 2).to(DEV)
+    feats, graphs = [], []
+    orig = pcseg.models.EdgeConv.forward_graph
+
+    def rec(self, xp, seeds=None):
+        out, idx = orig(self, xp, seeds)
+        feats.append(xp.detach().clone())
+        graphs.append(idx)
+        return out, idx
+    pcseg.models.EdgeConv.forward_graph = rec
+    try:
+        with torch.no_grad():
+            m(x)
+    finally:
+        pcseg.models.EdgeConv.forward_graph = orig
+    assert len(graphs) == 4
+    for f, gidx in zip(feats[1:], graphs[1:]):
+        assert torch.equal(gidx, ops.knn(f, 20))
+
+
 def test_dgcnn_knn_vs_reference_graph_at_4096(golden):
     """The xyz graph the reference itself built for BASELINE config 2's block size
     (tests/golden/model_dgcnn_color_4096.npz, knn0: B=2, N=4096, k=20)."""
