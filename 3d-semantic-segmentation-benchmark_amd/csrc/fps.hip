@@ -30,21 +30,29 @@ __device__ __forceinline__ unsigned dpp_u(unsigned v) {
 }
 
 // wave-wide max / min of an unsigned value, result wave-uniform: DPP inside 16-lane
-// rows (quad xor1, quad xor2, half-row mirror, row mirror) + v_readlane of the four
-// row results.  No LDS round trips.
+// rows (quad xor1, quad xor2, half-row mirror, row mirror), then row_bcast:15 / row_bcast:31
+// fold the four row results into lane 63, read with one v_readlane.  No LDS round trips.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ unsigned dpp_old(unsigned old, unsigned v) {
+    return (unsigned)__builtin_amdgcn_update_dpp((int)old, (int)v, CTRL, ROWS, 0xF, false);
+}
 __device__ __forceinline__ unsigned wave_umax(unsigned v) {
     v = max(v, dpp_u<0xB1>(v));
     v = max(v, dpp_u<0x4E>(v));
     v = max(v, dpp_u<0x141>(v));
     v = max(v, dpp_u<0x140>(v));
-    return max(max(readlane_u(v, 0), readlane_u(v, 16)), max(readlane_u(v, 32), readlane_u(v, 48)));
+    v = max(v, dpp_old<0x142, 0xA>(0u, v));       // row_bcast:15 -> rows 1, 3
+    v = max(v, dpp_old<0x143, 0xC>(0u, v));       // row_bcast:31 -> rows 2, 3
+    return readlane_u(v, 63);
 }
 __device__ __forceinline__ unsigned wave_umin(unsigned v) {
-    v = min(v, dpp_u<0xB1>(v));
-    v = min(v, dpp_u<0x4E>(v));
-    v = min(v, dpp_u<0x141>(v));
-    v = min(v, dpp_u<0x140>(v));
-    return min(min(readlane_u(v, 0), readlane_u(v, 16)), min(readlane_u(v, 32), readlane_u(v, 48)));
+    v = min(v, dpp_old<0xB1, 0xF>(~0u, v));
+    v = min(v, dpp_old<0x4E, 0xF>(~0u, v));
+    v = min(v, dpp_old<0x141, 0xF>(~0u, v));
+    v = min(v, dpp_old<0x140, 0xF>(~0u, v));
+    v = min(v, dpp_old<0x142, 0xA>(~0u, v));
+    v = min(v, dpp_old<0x143, 0xC>(~0u, v));
+    return readlane_u(v, 63);
 }
 
 constexpr int kFpsLdsOut = 2048;   // centroids buffered in LDS (written once at the end)
@@ -68,40 +76,77 @@ __device__ unsigned long long g_fps_stamps[8];
 #endif
 
 constexpr int kFpsLdsCloud = 8192;   // clouds up to this size keep a coordinate copy in LDS
+// Width (in float bit steps) of the near-tie window below a maximum.  Every float whose
+// correctly rounded sqrt equals sqrt_cr(M) lies within 6 bit steps below M (a sqrt bucket
+// spans at most 4 ulps of its binade, twice that in the binade below), so the window is a
+// superset of the reference's tie class; 16 leaves margin.
+constexpr unsigned kFpsWin = 16u;
 
-// One step per loop iteration:
-//  1. each thread folds the new distances into its squared running minima and takes
-//     its local max (squared);
-//  2. wave max M* (exact, as float bits) -> S = sqrtf(M*) and lo = the smallest
-//     float whose sqrt rounds to S (wave-uniform, sqrts in parallel);
-//  3. the wave's candidate = lowest point index with best >= lo, i.e. the lowest
-//     index among ALL its points whose reference distance sqrt(best) equals S;
-//  4. lane 0 of every wave publishes (S, index) in one LDS slot; after the barrier
-//     lane l of every wave reads slot l and the waves redo the (max S, min index)
-//     reduction with DPP -- no serial compare chain -- and fetch the winner's
-//     coordinates from the LDS copy of the cloud.
-// This is exactly the reference's "first index of max(sqrt distances)".
-template <int BLOCK, int PPT>
+// Per step (one loop iteration):
+//  1. each thread folds the new distances into its squared running minima (float bits) and
+//     takes its local max;
+//  2. wave max mw (DPP chain), then the lowest index whose value lies in the window
+//     [mw - kFpsWin, mw] together with a flag "its value is not mw" -- one key (idx<<1 | flag),
+//     one wave-min chain; lane 0 publishes (mw + 1, key) in one 8-B LDS slot;
+//  3. after the barrier, lanes 0..NW-1 hold the slots: the block max M*, and the FAST PATH holds
+//     when every slot in M*'s window has exactly M* and a clear flag.  Then no point other than
+//     those with value M* lies in the window, all points of the reference's tie class (same
+//     sqrt_cr as M*) have value exactly M*, and the winner -- the reference's first index of the
+//     max sqrt distance -- is the lowest published index among the M* slots (one short DPP
+//     chain over NW lanes).  No sqrt and no double arithmetic on that path.
+//  4. otherwise (a near-tie somewhere in the window: rare) every wave recomputes its exact key
+//     -- (sqrt_cr(mw), lowest index with a value whose sqrt_cr is that) -- and the block takes the
+//     (max sqrt, min index) slot after a second barrier.  All waves see the same slots, so all
+//     take the same path.
+// The winner's coordinates come from the LDS copy of the cloud (SoA, ds_read) when it fits.
+template <int NW>
+__device__ __forceinline__ unsigned slot_umax(unsigned v) {
+    // lanes 0..NW-1 (NW = 4, 8 or 16) end with the max over them
+    v = max(v, dpp_u<0xB1>(v));
+    v = max(v, dpp_u<0x4E>(v));
+    if constexpr (NW >= 8) v = max(v, dpp_u<0x141>(v));
+    if constexpr (NW >= 16) v = max(v, dpp_u<0x140>(v));
+    return readlane_u(v, 0);
+}
+template <int NW>
+__device__ __forceinline__ unsigned slot_umin(unsigned v) {
+    v = min(v, dpp_u<0xB1>(v));
+    v = min(v, dpp_u<0x4E>(v));
+    if constexpr (NW >= 8) v = min(v, dpp_u<0x141>(v));
+    if constexpr (NW >= 16) v = min(v, dpp_u<0x140>(v));
+    return readlane_u(v, 0);
+}
+
+// the smallest float whose correctly rounded sqrt is S (S > 0): the first float above the exact
+// (double) square of the midpoint between S and its lower neighbour (a float's sqrt is never
+// exactly a midpoint)
+__device__ __forceinline__ unsigned sqrt_class_lo(float S) {
+    if (!(S > 0.f)) return 0u;
+    const double mid = 0.5 * ((double)S + (double)__uint_as_float(__float_as_uint(S) - 1u));
+    const double m2 = mid * mid;
+    float f = (float)m2;
+    if ((double)f <= m2) f = __uint_as_float(__float_as_uint(f) + 1u);
+    return __float_as_uint(f);
+}
+
+template <int BLOCK, int PPT, bool LDSC>
 __global__ __launch_bounds__(BLOCK) void fps_kernel(const float* __restrict__ xyz, int N, int C,
                                                     const int* __restrict__ start, int* __restrict__ out_idx,
                                                     float* __restrict__ out_xyz) {
     constexpr int NW = BLOCK / kWave;
-    static_assert(NW <= 64, "one slot per lane");
-    __shared__ __attribute__((aligned(16))) uint2 s_key[2][NW];   // (sqrt bits + 1, index); 0 = empty
+    static_assert(NW == 1 || NW == 4 || NW == 8 || NW == 16, "slot reduction width");
+    __shared__ __attribute__((aligned(16))) uint2 s_slot[2][NW];   // (mw + 1, idx<<1 | flag); 0 = empty wave
+    __shared__ __attribute__((aligned(16))) uint2 s_key[NW];       // slow path: (sqrt bits + 1, index)
     // Per-step global stores would make every __syncthreads wait for them (the
     // barrier's fence drains vmcnt): keep the picked centroids in LDS instead.
     __shared__ float4 s_out[kFpsLdsOut];
-    __shared__ float s_cloud[3 * kFpsLdsCloud];
+    __shared__ float s_px[LDSC ? kFpsLdsCloud : 1], s_py[LDSC ? kFpsLdsCloud : 1], s_pz[LDSC ? kFpsLdsCloud : 1];
     const bool lds_out = C <= kFpsLdsOut;
-    const bool lds_cloud = N <= kFpsLdsCloud;
 
     const int b = blockIdx.x;
     const int t = threadIdx.x;
     const int w = t >> 6, lane = t & 63;
     const float* P = xyz + (size_t)b * N * 3;
-
-    if (lds_cloud)
-        for (int e = t; e < 3 * N; e += BLOCK) s_cloud[e] = P[e];
 
     // running minima as float BITS: the squared distances are >= +0 (never -0 or NaN), so
     // unsigned min/max order them exactly like fminf/fmaxf, with no canonicalising op.
@@ -117,6 +162,11 @@ __global__ __launch_bounds__(BLOCK) void fps_kernel(const float* __restrict__ xy
             py[j] = P[3 * p + 1];
             pz[j] = P[3 * p + 2];
             best[j] = 0x7f800000u;
+            if constexpr (LDSC) {
+                s_px[p] = px[j];
+                s_py[p] = py[j];
+                s_pz[p] = pz[j];
+            }
         } else {
             px[j] = py[j] = pz[j] = 0.f;
             best[j] = 0u;
@@ -126,7 +176,7 @@ __global__ __launch_bounds__(BLOCK) void fps_kernel(const float* __restrict__ xy
     int far = start[b];
     far = far < 0 ? 0 : (far >= N ? N - 1 : far);
     float cx = P[3 * far + 0], cy = P[3 * far + 1], cz = P[3 * far + 2];
-    if (lds_cloud) __syncthreads();
+    if constexpr (LDSC) __syncthreads();
 
 #ifdef PCS_FPS_STAMPS
     unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -175,45 +225,58 @@ __global__ __launch_bounds__(BLOCK) void fps_kernel(const float* __restrict__ xy
             }
         }
         FPS_STAMP(1);
+        // M + 1 never wraps (M <= +inf bits); 0 marks a wave with only padding slots
         const unsigned wk = wave_umax(M + 1u);
+        const unsigned mw = wk - 1u;
         FPS_STAMP(2);
-        const int buf = i & 1;
-        if (wk != 0) {
-            const unsigned mb = wk - 1u;
-            const float Mw = __uint_as_float(mb);
-            const float S = sqrt_cr(Mw);
-            // lo = the smallest float whose correctly rounded sqrt is S: the first float above
-            // the square of the midpoint between S and its lower neighbour (exact in double;
-            // a float's sqrt is never exactly a midpoint)
-            float lo = 0.f;
-            if (S > 0.f) {
-                const double mid = 0.5 * ((double)S + (double)__uint_as_float(__float_as_uint(S) - 1u));
-                const double m2 = mid * mid;
-                float f = (float)m2;
-                if ((double)f <= m2) f = __uint_as_float(__float_as_uint(f) + 1u);
-                lo = f;
-            }
-            unsigned cand = 0xFFFFFFFFu;
+        // window [mw - kFpsWin, mw]; an all-padding wave (wk == 0) matches nothing (best <= +inf bits)
+        const unsigned wlo = wk == 0u ? 0xFFFFFFFFu : (mw > kFpsWin ? mw - kFpsWin : 0u);
+        unsigned ci = 0xFFFFFFFFu, cv = 0u;   // lowest window index of this thread and its value
 #pragma unroll
-            for (int j = PPT - 1; j >= 0; --j)
-                cand = best[j] >= __float_as_uint(lo) ? (unsigned)(j * BLOCK + t) : cand;
-            FPS_STAMP(3);
-            const unsigned widx = wave_umin(cand);
-            FPS_STAMP(4);
-            if (lane == 0) s_key[buf][w] = make_uint2(__float_as_uint(S) + 1u, widx);
-        } else if (lane == 0) {
-            s_key[buf][w] = make_uint2(0u, 0xFFFFFFFFu);
+        for (int j = PPT - 1; j >= 0; --j) {
+            const bool in = best[j] >= wlo;
+            ci = in ? (unsigned)(j * BLOCK + t) : ci;
+            cv = in ? best[j] : cv;
         }
+        // no candidate: 0xFFFFFFFE / 0xFFFFFFFF, above every real key
+        const unsigned key = (ci << 1) | (cv != mw ? 1u : 0u);
+        FPS_STAMP(3);
+        const unsigned wkey = wave_umin(key);
+        FPS_STAMP(4);
+        const int buf = i & 1;
+        if (lane == 0) s_slot[buf][w] = make_uint2(wk, wkey);
         FPS_STAMP(5);
         __syncthreads();
         FPS_STAMP(6);
-        const uint2 k2 = lane < NW ? s_key[buf][lane] : make_uint2(0u, 0xFFFFFFFFu);
-        const unsigned bs = wave_umax(k2.x);
-        far = (int)wave_umin(k2.x == bs ? k2.y : 0xFFFFFFFFu);
-        if (lds_cloud) {
-            cx = s_cloud[3 * far + 0];
-            cy = s_cloud[3 * far + 1];
-            cz = s_cloud[3 * far + 2];
+        const uint2 sl = lane < NW ? s_slot[buf][lane] : make_uint2(0u, 0xFFFFFFFFu);
+        const unsigned Ms = NW == 1 ? readlane_u(sl.x, 0) : slot_umax<NW>(sl.x);
+        const unsigned slo = Ms > kFpsWin + 1u ? Ms - kFpsWin : 1u;
+        const bool near = sl.x >= slo && (sl.x != Ms || (sl.y & 1u));
+        const unsigned fk = NW == 1 ? readlane_u(sl.y, 0) : slot_umin<NW>(sl.x == Ms ? sl.y : 0xFFFFFFFFu);
+        if (__builtin_expect(ballot(near) == 0ull, 1)) {
+            far = (int)(fk >> 1);
+        } else {
+            // exact keys: the wave's max sqrt S and the lowest index whose value has that sqrt
+            unsigned kx = 0u, ky = 0xFFFFFFFFu;
+            if (wk != 0u) {
+                const float S = sqrt_cr(__uint_as_float(mw));
+                const unsigned lo = sqrt_class_lo(S);
+                unsigned cand = 0xFFFFFFFFu;
+#pragma unroll
+                for (int j = PPT - 1; j >= 0; --j) cand = best[j] >= lo ? (unsigned)(j * BLOCK + t) : cand;
+                kx = __float_as_uint(S) + 1u;
+                ky = wave_umin(cand);
+            }
+            if (lane == 0) s_key[w] = make_uint2(kx, ky);
+            __syncthreads();
+            const uint2 k2 = lane < NW ? s_key[lane] : make_uint2(0u, 0xFFFFFFFFu);
+            const unsigned bs = NW == 1 ? readlane_u(k2.x, 0) : slot_umax<NW>(k2.x);
+            far = (int)(NW == 1 ? readlane_u(k2.y, 0) : slot_umin<NW>(k2.x == bs ? k2.y : 0xFFFFFFFFu));
+        }
+        if constexpr (LDSC) {
+            cx = s_px[far];
+            cy = s_py[far];
+            cz = s_pz[far];
         } else {
             cx = P[3 * far + 0];
             cy = P[3 * far + 1];
@@ -244,7 +307,12 @@ __global__ __launch_bounds__(BLOCK) void fps_kernel(const float* __restrict__ xy
 template <int BLOCK, int PPT>
 static void launch_fps(const float* xyz, int B, int N, int C, const int* start, int* out_idx, float* out_xyz,
                        hipStream_t s) {
-    hipLaunchKernelGGL((fps_kernel<BLOCK, PPT>), dim3(B), dim3(BLOCK), 0, s, xyz, N, C, start, out_idx, out_xyz);
+    if (N <= kFpsLdsCloud)
+        hipLaunchKernelGGL((fps_kernel<BLOCK, PPT, true>), dim3(B), dim3(BLOCK), 0, s, xyz, N, C, start, out_idx,
+                           out_xyz);
+    else
+        hipLaunchKernelGGL((fps_kernel<BLOCK, PPT, false>), dim3(B), dim3(BLOCK), 0, s, xyz, N, C, start, out_idx,
+                           out_xyz);
 }
 
 }  // namespace pcs
@@ -259,14 +327,21 @@ PCS_API int pcs_fps(const float* xyz, int B, int N, int C, const int32_t* start,
     if (B == 0) return 0;
     hipStream_t s = as_stream(stream);
     // threads per cloud by size (round-1 sweep)
-    const int blk = N <= 256 ? 64 : (N <= 2048 ? 256 : (N <= 8192 ? 512 : 1024));
+#ifndef PCS_FPS_BLK2K
+#define PCS_FPS_BLK2K 256
+#endif
+#ifndef PCS_FPS_BLK8K
+#define PCS_FPS_BLK8K 512
+#endif
+    const int blk = N <= 256 ? 64 : (N <= 2048 ? PCS_FPS_BLK2K : (N <= 8192 ? PCS_FPS_BLK8K : 1024));
     const int ppt = (N + blk - 1) / blk;
     // algorithmic: C serial steps over N points per cloud (8 fp32 flops per distance + update);
     // the cloud read once, C (index, xyz) written.  A latency-bound chain: see DESIGN.md 3.1
     const double flops = 8.0 * B * (double)N * C, bytes = (double)B * (12.0 * N + 16.0 * C);
 #define PCS_FPS_CASE(BL, PP)                                                                    \
     if (blk == BL && ppt <= PP) {                                                               \
-        ProbeScope pr(s, flops, bytes, "pcs::fps_kernel<%d, %d>", BL, PP);                     \
+        ProbeScope pr(s, flops, bytes, "pcs::fps_kernel<%d, %d, %s>", BL, PP,                 \
+                      N <= kFpsLdsCloud ? "true" : "false");                                    \
         launch_fps<BL, PP>(xyz, B, N, C, start, out_idx, out_xyz, s);                           \
     } else
     PCS_FPS_CASE(64, 1) PCS_FPS_CASE(64, 2) PCS_FPS_CASE(64, 4) PCS_FPS_CASE(64, 8)

@@ -30,7 +30,7 @@ namespace pcs {
 // ------------------------------------------------------------------ row GEMM
 // C[M x N] = T(A)[M x K] . B[K x N],  B[k][n] = W[n*ldw + k]  (W row-major N x K).
 //
-// 256 threads = 4 waves in a WM x WN grid; each wave owns TM x TN 32x32 MFMA tiles.
+// WM x WN waves (4 or 8: 256 or 512 threads); each wave owns TM x TN 32x32 MFMA tiles.
 // K is consumed in 32-deep slabs staged through a double-buffered LDS ring with the
 // next slab's global loads in flight (registers) while the current slab is computed.
 // Inside a slab the k order is permuted so that lane half h takes k = 16h + s
@@ -55,13 +55,14 @@ __device__ __forceinline__ int lds_swz(int c) { return ((c >> 3) & 7) << 2; }
 constexpr int EPI_STATS = 1, EPI_BWD = 2, EPI_POOL = 4, EPI_GENERIC = 8;
 
 template <int BM, int BN, int WM, int WN, int AM, bool BT, int EPI>
-__global__ __launch_bounds__(256, 2) void gemm_rows_kernel(GemmArgs g) {
+__global__ __launch_bounds__(WM * WN * 64, 2) void gemm_rows_kernel(GemmArgs g) {
+    constexpr int NT = WM * WN * 64;
     constexpr int WTM = BM / WM, WTN = BN / WN;
     constexpr int TM = WTM / 32, TN = WTN / 32;
-    constexpr int AV = BM * GBK / 4 / 256;
-    constexpr int BV = (BN * GBK / 4 + 255) / 256;
-    constexpr bool kBFull = (BN * GBK / 4) % 256 == 0;     // every thread owns BV whole B quads
-    static_assert(WM * WN == 4 && TM >= 1 && TN >= 1 && AV >= 1, "tile");
+    constexpr int AV = BM * GBK / 4 / NT;
+    constexpr int BV = (BN * GBK / 4 + NT - 1) / NT;
+    constexpr bool kBFull = (BN * GBK / 4) % NT == 0;     // every thread owns BV whole B quads
+    static_assert((WM * WN == 4 || WM * WN == 8) && TM >= 1 && TN >= 1 && AV >= 1, "tile");
     __shared__ __attribute__((aligned(16))) float As[2][BM][GLDK];
     __shared__ __attribute__((aligned(16))) float Bs[2][BN][GLDK];
     __shared__ double red[2][WM][BN];
@@ -92,12 +93,12 @@ __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(GemmArgs g) {
         load_quad<AM>(g.a, gk, g.K, q);
 #pragma unroll
         for (int it = 0; it < AV; ++it) {
-            const int gr = min(m0 + ((it * 256 + tid) >> 3), g.M - 1);
+            const int gr = min(m0 + ((it * NT + tid) >> 3), g.M - 1);
             load_raw<AM>(g.a, gr, gkc, ra[it], rz[it], rg[it]);
         }
 #pragma unroll
         for (int it = 0; it < BV; ++it) {
-            const int e = it * 256 + tid;
+            const int e = it * NT + tid;
             if constexpr (BT) {
                 const int gk = min(k0 + e / (BN / 4), g.K - 1);
                 const int gn = min(n0 + 4 * (e % (BN / 4)), ldw_last);
@@ -123,13 +124,13 @@ __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(GemmArgs g) {
         const int gk = k0 + 4 * (tid & 7);
 #pragma unroll
         for (int it = 0; it < AV; ++it) {
-            const int r = (it * 256 + tid) >> 3;
+            const int r = (it * NT + tid) >> 3;
             *reinterpret_cast<float4*>(&As[buf][r][4 * (tid & 7)]) =
                 xform4<AM>(g.a, ra[it], rz[it], rg[it], min(m0 + r, g.M - 1), q, gk, g.K);
         }
 #pragma unroll
         for (int it = 0; it < BV; ++it) {
-            const int e = it * 256 + tid;
+            const int e = it * NT + tid;
             if constexpr (BT) {
                 const int kk = e / (BN / 4), n = 4 * (e % (BN / 4));
                 const float4 v = k0 + kk < g.K ? rb[it] : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -336,7 +337,7 @@ __global__ __launch_bounds__(256, 2) void gemm_rows_kernel(GemmArgs g) {
         }
         __syncthreads();
         double* out = want_stats ? g.stats : g.bstats;
-        for (int c = tid; c < BN; c += 256) {
+        for (int c = tid; c < BN; c += NT) {
             const int col = n0 + c;
             if (col < g.N) {
                 double a = 0.0, b = 0.0;
@@ -911,7 +912,7 @@ static void launch_gemm(const GemmArgs& g, int gx, bool bt, hipStream_t s) {
     const dim3 grid(gx, (g.N + BN - 1) / BN);
     const int e = (g.stats ? EPI_STATS : 0) | (g.bstats ? EPI_BWD : 0) | (g.pool_k ? EPI_POOL : 0);
 #define PCS_GEMM(AMODE, BTV, EPIV) \
-    hipLaunchKernelGGL((gemm_rows_kernel<BM, BN, WM, WN, AMODE, BTV, EPIV>), grid, dim3(256), 0, s, g)
+    hipLaunchKernelGGL((gemm_rows_kernel<BM, BN, WM, WN, AMODE, BTV, EPIV>), grid, dim3(WM * WN * 64), 0, s, g)
     if (bt) {   // data-gradient GEMMs: dZ operand (rebuilt on load) or a plain / materialised one
         switch (g.a.mode) {
 #define PCS_BT(AMODE) \
@@ -986,7 +987,7 @@ using namespace pcs;
 // gives >= 2 blocks per CU (256 CUs), else the one with the most blocks
 // bwd: the data-gradient GEMM (k-major W, or an A rebuilt from dZ: BNBWD / POOLBWD), with a
 // heavier operand transform and BN-backward epilogue; its tile policy is below
-static void gemm_tile(int M, int N, bool bwd, int* bm, int* bn) {
+static void gemm_tile(int M, int N, bool bwd, int* bm, int* bn, int* nt = nullptr) {
     struct T { int bm, bn; };
     static const T big[] = {{128, 128}, {64, 128}, {64, 64}, {32, 128}};
     static const T mid[] = {{128, 64}, {64, 64}};
@@ -996,6 +997,10 @@ static void gemm_tile(int M, int N, bool bwd, int* bm, int* bn) {
     // layers (PointNet++, EdgeConv) run best on 64 x 64 tiles (4 blocks per CU, more loads in
     // flight: PointNet++ step -1 %); the big MFMA-bound ones (DGCNN conv5-7: N >= 256 over
     // >= 64K rows) on the wide list despite its register pressure (DGCNN step -2 %).
+    // Round 3: outputs wider than 64 on the thin layers take a 64 x 128 tile on EIGHT waves
+    // (512 threads, each wave the 32 x 32 block of the 64 x 64 tile): the rebuilt dZ slab is
+    // loaded and transformed once for 128 output columns instead of once per 64.
+    if (nt) *nt = 256;
     bool wide;
     const T* c;
     if (!bwd) {
@@ -1003,6 +1008,12 @@ static void gemm_tile(int M, int N, bool bwd, int* bm, int* bn) {
         c = wide ? big : mid;
     } else {
         wide = N > 64 && N >= 256 && M >= 65536;
+#ifndef PCS_DGRAD256
+        if (!wide && N > 64 && nt) {
+            *bm = 64; *bn = 128; *nt = 512;
+            return;
+        }
+#endif
         c = wide ? big : mid64;
     }
     const int nc = wide ? 4 : 2;
@@ -1018,11 +1029,13 @@ static void gemm_tile(int M, int N, bool bwd, int* bm, int* bn) {
 // Persistent grid of the row GEMM: as many row blocks per column tile as fit on the chip
 // at once (LDS-limited blocks per CU x 256 CUs), each walking its row tiles with the next
 // tile's first slab prefetched under the current tile's epilogue.
-static int gemm_grid_x(int M, int N, int bm, int bn) {
+static int gemm_grid_x(int M, int N, int bm, int bn, int nt = 256) {
     const int mtiles = (M + bm - 1) / bm;
     const int lds = 4 * (bm + bn) * 2 * GLDK + 16 * bn;         // As + Bs + red (bytes)
     int per_cu = (160 * 1024) / lds;
-    per_cu = per_cu < 1 ? 1 : (per_cu > 4 ? 4 : per_cu);
+    // 512-thread tiles use > 128 VGPRs: 2 waves per SIMD, one block per CU
+    const int cap = nt == 512 ? 1 : 4;
+    per_cu = per_cu < 1 ? 1 : (per_cu > cap ? cap : per_cu);
     const int ntiles = (N + bn - 1) / bn;
     const int slots = (256 * per_cu + ntiles - 1) / ntiles;
     if (mtiles <= slots) return mtiles;
@@ -1031,8 +1044,9 @@ static int gemm_grid_x(int M, int N, int bm, int bn) {
 }
 
 // wave grid of a row-GEMM tile (mirrors the launch table in pcs_gemm_rows)
-static void gemm_waves(int bm, int bn, int* wm, int* wn) {
-    if (bn == 32 || (bm == 128 && bn == 64)) { *wm = 4; *wn = 1; }
+static void gemm_waves(int bm, int bn, int nt, int* wm, int* wn) {
+    if (nt == 512) { *wm = 2; *wn = 4; }
+    else if (bn == 32 || (bm == 128 && bn == 64)) { *wm = 4; *wn = 1; }
     else if (bm == 32) { *wm = 1; *wn = 4; }
     else { *wm = 2; *wn = 2; }
 }
@@ -1049,9 +1063,9 @@ static double operand_bytes(const pcs_operand& o, int M, int K) {
 // the operand needs an on-load transform), so the partial count depends on (M, N) only.
 static int row_blocks(int M, int N, bool bwd) {
     if (!bwd && gemm_nt_regime(M, N)) return gemm_nt_row_tiles(M);
-    int bm, bn;
-    gemm_tile(M, N, bwd, &bm, &bn);
-    return gemm_grid_x(M, N, bm, bn);
+    int bm, bn, nt;
+    gemm_tile(M, N, bwd, &bm, &bn, &nt);
+    return gemm_grid_x(M, N, bm, bn, nt);
 }
 
 PCS_API int pcs_gemm_row_blocks(int M, int N) { return row_blocks(M, N, false); }
@@ -1174,9 +1188,9 @@ int pcs::gemm_rows_ex(const pcs_operand* a, int M, int K, const float* W, int ld
     int probe = -1;
     if (probe_enabled()) {
         char nm[96];
-        int bm, bn, wm, wn;
-        gemm_tile(M, N, a->mode >= PCS_OP_BNBWD || bt, &bm, &bn);
-        gemm_waves(bm, bn, &wm, &wn);
+        int bm, bn, nt, wm, wn;
+        gemm_tile(M, N, a->mode >= PCS_OP_BNBWD || bt, &bm, &bn, &nt);
+        gemm_waves(bm, bn, nt, &wm, &wn);
         snprintf(nm, sizeof nm, "pcs::gemm_rows_kernel<%d, %d, %d, %d, %d, %s, %d>", bm, bn, wm, wn, a->mode,
                  bt ? "true" : "false", gemm_epi(a->mode, bt != 0, stats != nullptr, bstats != nullptr, pool_k != 0));
         const double bytes = operand_bytes(*a, M, K) + 4.0 * M * N * (bstats ? 2 : 1);
@@ -1186,13 +1200,14 @@ int pcs::gemm_rows_ex(const pcs_operand* a, int M, int K, const float* W, int ld
             gemm_rows_ex(&ac, M, K, W, ldw, bt, bias, C, ldc, N, stats, he ? &ec : nullptr, bstats, stream);
         });
     }
-    int bm, bn;
+    int bm, bn, nt;
     const bool bwd = a->mode >= PCS_OP_BNBWD || bt;
-    gemm_tile(M, N, bwd, &bm, &bn);
+    gemm_tile(M, N, bwd, &bm, &bn, &nt);
     // stats partials: one per row block as row_blocks() counts them (<= the row tiles: persistent)
-    const int gx = (stats || bstats) ? row_blocks(M, N, bwd) : gemm_grid_x(M, N, bm, bn);
+    const int gx = (stats || bstats) ? row_blocks(M, N, bwd) : gemm_grid_x(M, N, bm, bn, nt);
     const bool b = bt != 0;
-    if (bn == 32) launch_gemm<128, 32, 4, 1>(g, gx, b, s);
+    if (nt == 512) launch_gemm<64, 128, 2, 4>(g, gx, b, s);
+    else if (bn == 32) launch_gemm<128, 32, 4, 1>(g, gx, b, s);
     else if (bm == 128 && bn == 64) launch_gemm<128, 64, 4, 1>(g, gx, b, s);
     else if (bm == 128) launch_gemm<128, 128, 2, 2>(g, gx, b, s);
     else if (bm == 64 && bn == 128) launch_gemm<64, 128, 2, 2>(g, gx, b, s);
@@ -1239,8 +1254,8 @@ static void wgrad_plan(int N, int K, int M, int* BO, int* BI, int* splits, int* 
 int pcs::dz_passes(int M, int C, int cin, bool dgrad, bool wgrad) {
     int n = 0;
     if (dgrad) {
-        int bm, bn;
-        gemm_tile(M, cin, true, &bm, &bn);
+        int bm, bn, nt;
+        gemm_tile(M, cin, true, &bm, &bn, &nt);
         n += (cin + bn - 1) / bn;
     }
     if (wgrad) {

@@ -116,10 +116,13 @@ def cpu_baseline_worker(args):
     # timed steps: cpu_steps (>= 5 by default), fewer only past ~cpu_budget seconds, at least 3
     n = max(3, min(args.cpu_steps, int(args.cpu_budget / max(warm, 1e-3))))
     times = []
-    for _ in range(n):
+    for i in range(n):
         t0 = time.perf_counter()
         step()
         times.append(time.perf_counter() - t0)
+        # progress on stderr (a silent minute reads as a hang to the GPU box's watchdog)
+        print(f'[bench] cpu baseline {name} {torch.get_num_threads()} threads: step {i + 1}/{n} '
+              f'{times[-1]:.2f} s', file=sys.stderr, flush=True)
     med = statistics.median(times)
     print(json.dumps({'value': args.cpu_batch * args.npoints / med, 'unit': 'points/s',
                       'cores': torch.get_num_threads(), 'kind': 'port',
@@ -134,7 +137,8 @@ def _cpu_run(args, key, batch, npoints, threads):
            '--npoints', str(npoints), '--cpu-batch', str(batch), '--cpu-steps',
            str(args.cpu_steps), '--cpu-threads', str(threads), '--cpu-budget', str(args.cpu_budget)]
     try:
-        out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=900, check=True).stdout
+        print(f'[bench] cpu baseline {key} on {threads} threads', file=sys.stderr, flush=True)
+        out = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, text=True, timeout=900, check=True).stdout
         return json.loads(out.strip().splitlines()[-1])
     except Exception as e:  # noqa: BLE001 -- the baseline is informative, never fatal
         return {'value': None, 'unit': 'points/s', 'cores': threads, 'kind': 'port', 'sample': f'failed: {e}'}
@@ -268,6 +272,8 @@ def run_workload(key, batch, npoints, args, world, rank, dev):
     from pcseg.synthetic import make_batch
 
     name, ctor, kind, _, _, cfg = WORKLOADS[key]
+    print(f'[bench] {name}: batch {batch} x {npoints} pts, {args.warmup} warm-up + {args.steps} timed steps',
+          file=sys.stderr, flush=True)
     torch.manual_seed(0)
     model = ctor(pcseg).to(dev).train()     # PyTorch default init (random weights)
     pcseg.engine.set_bwd_fuse(model, args.bwd_fuse)

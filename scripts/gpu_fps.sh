@@ -1,4 +1,4 @@
-# FPS A/B (indices must match) + stamps + the FPS tests.
+# FPS A/B (indices must match the previous library's) + stamps + the FPS tests.
 set -u
 cd "$GRAFT_REPO_ROOT"; tag=${1:-fps}; out=gpurun_out/$tag; mkdir -p $out
 export TMPDIR=/tmp
