@@ -384,12 +384,24 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(Operand xo, int N, Operan
     const int wi = wave % WGI, wo = (wave / WGI) % WGO, wr = wave / (WGI * WGO);
     const int h = lane >> 5, l32 = lane & 31;
     const int tiles_i = (K + BI - 1) / BI;
-    const int n0 = (blockIdx.y / tiles_i) * BO;
-    const int k0 = (blockIdx.y % tiles_i) * BI;
-    const int rb = blockIdx.x * rows_per_block;
+    // XCD-aware order (a bijective remap of the (split, tile) grid, speed only): workgroups are
+    // dispatched round-robin over the 8 XCDs in linear-id order, so XCD x takes a contiguous run
+    // of remapped ids, tile-fastest -- the tiles of one row split (the same X / Y rows) run
+    // together on one XCD and share its L2 instead of each fetching the rows from HBM
+    const int lin = blockIdx.x + blockIdx.y * gridDim.x;
+#ifndef PCS_WGRAD_LINEAR
+    const int nwg = gridDim.x * gridDim.y, q8 = nwg / 8, r8 = nwg % 8, xcd = lin % 8;
+    const int rt = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + lin / 8;
+#else
+    const int rt = blockIdx.y + blockIdx.x * gridDim.y;     // A/B builds only: the round-2 order
+#endif
+    const int sp = rt / gridDim.y, ti = rt - sp * gridDim.y;
+    const int n0 = (ti / tiles_i) * BO;
+    const int k0 = (ti % tiles_i) * BI;
+    const int rb = sp * rows_per_block;
     const int re = min(M, rb + rows_per_block);
     const bool do_db = (pdb != nullptr) && (k0 == 0);
-    float* __restrict__ tile_part = part + (size_t)blockIdx.x * N * K;
+    float* __restrict__ tile_part = part + (size_t)sp * N * K;
 
     // Transposed LDS stores without bank conflicts: each 32-lane half stores 4 rows x 8
     // channel quads, and the row index is XOR-swizzled in 4-row groups by the channel
@@ -528,7 +540,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(Operand xo, int N, Operan
             float a = 0.f;
 #pragma unroll
             for (int gi = 0; gi < 256 / (BO / 4); ++gi) a += dbs[gi][tid];
-            pdb[(size_t)blockIdx.x * N + n0 + tid] = a;
+            pdb[(size_t)sp * N + n0 + tid] = a;
         }
     }
 }
@@ -997,9 +1009,10 @@ static void gemm_tile(int M, int N, bool bwd, int* bm, int* bn, int* nt = nullpt
     // layers (PointNet++, EdgeConv) run best on 64 x 64 tiles (4 blocks per CU, more loads in
     // flight: PointNet++ step -1 %); the big MFMA-bound ones (DGCNN conv5-7: N >= 256 over
     // >= 64K rows) on the wide list despite its register pressure (DGCNN step -2 %).
-    // Round 3: outputs wider than 64 on the thin layers take a 64 x 128 tile on EIGHT waves
-    // (512 threads, each wave the 32 x 32 block of the 64 x 64 tile): the rebuilt dZ slab is
-    // loaded and transformed once for 128 output columns instead of once per 64.
+    // Round 3 re-check: a 64 x 128 tile on EIGHT waves (512 threads, each wave the 32 x 32 block
+    // of the 64 x 64 tile; the rebuilt dZ slab loaded and transformed once per 128 output columns
+    // instead of once per 64) made the PointNet++ step 1-2 % slower (same-box A/B, 2 rounds):
+    // kept as an option of the kernel (WM x WN = 8), off in the policy.
     if (nt) *nt = 256;
     bool wide;
     const T* c;
@@ -1008,7 +1021,7 @@ static void gemm_tile(int M, int N, bool bwd, int* bm, int* bn, int* nt = nullpt
         c = wide ? big : mid;
     } else {
         wide = N > 64 && N >= 256 && M >= 65536;
-#ifndef PCS_DGRAD256
+#ifdef PCS_DGRAD512
         if (!wide && N > 64 && nt) {
             *bm = 64; *bn = 128; *nt = 512;
             return;
@@ -1206,8 +1219,11 @@ int pcs::gemm_rows_ex(const pcs_operand* a, int M, int K, const float* W, int ld
     // stats partials: one per row block as row_blocks() counts them (<= the row tiles: persistent)
     const int gx = (stats || bstats) ? row_blocks(M, N, bwd) : gemm_grid_x(M, N, bm, bn, nt);
     const bool b = bt != 0;
+#ifdef PCS_DGRAD512
     if (nt == 512) launch_gemm<64, 128, 2, 4>(g, gx, b, s);
-    else if (bn == 32) launch_gemm<128, 32, 4, 1>(g, gx, b, s);
+    else
+#endif
+    if (bn == 32) launch_gemm<128, 32, 4, 1>(g, gx, b, s);
     else if (bm == 128 && bn == 64) launch_gemm<128, 64, 4, 1>(g, gx, b, s);
     else if (bm == 128) launch_gemm<128, 128, 2, 2>(g, gx, b, s);
     else if (bm == 64 && bn == 128) launch_gemm<64, 128, 2, 2>(g, gx, b, s);

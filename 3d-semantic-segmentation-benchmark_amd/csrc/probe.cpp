@@ -115,6 +115,15 @@ PCS_API int pcs_probe_get(int i, char* name, int cap, double* flops, double* byt
     return 0;
 }
 
+// record i's stream (the hipStream_t its launch was enqueued on, as void*)
+PCS_API int pcs_probe_stream(int i, void** stream) {
+    std::lock_guard<std::mutex> g(g_probe_mu);
+    PCS_CHECK_ARG(i >= 0 && i < (int)g_probe.size() && stream, "pcs_probe_stream: index %d of %zu", i,
+                  g_probe.size());
+    *stream = reinterpret_cast<void*>(g_probe[i].stream);
+    return 0;
+}
+
 // Re-issue every recorded launch of kernel `name` back to back, `reps` times (after one
 // untimed pass), between two events on their stream: the average duration of one launch
 // with the queue kept full, the figure rocprofv3 --stats reports as AverageNs for that

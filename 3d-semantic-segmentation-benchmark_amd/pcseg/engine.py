@@ -87,15 +87,19 @@ class KernelProbe:
         self.n = load().pcs_probe_end()
         return False
 
-    def records(self):
-        """[(name, flops, bytes, seconds)] (waits for the launches)."""
-        lib = load()
+    def records(self, with_stream: bool = False):
+        """[(name, flops, bytes, seconds[, stream handle])] (waits for the launches)."""
         out = []
         buf = ctypes.create_string_buffer(128)
         fl, by, ms = ctypes.c_double(), ctypes.c_double(), ctypes.c_float()
+        sp = ctypes.c_void_p()
         for i in range(self.n):
             call('pcs_probe_get', i, buf, 128, ctypes.byref(fl), ctypes.byref(by), ctypes.byref(ms))
-            out.append((buf.value.decode(), fl.value, by.value, ms.value * 1e-3))
+            rec = (buf.value.decode(), fl.value, by.value, ms.value * 1e-3)
+            if with_stream:
+                call('pcs_probe_stream', i, ctypes.byref(sp))
+                rec += (sp.value or 0,)
+            out.append(rec)
         return out
 
     def replay(self, name: str, reps: int = 20) -> float:
@@ -105,10 +109,13 @@ class KernelProbe:
         call('pcs_probe_replay', name.encode(), reps, ctypes.byref(us), ctypes.byref(n))
         return us.value * 1e-6
 
-    def summary(self):
-        """{kernel: (launches, flops, bytes, seconds)} (synchronises)."""
+    def summary(self, stream=None, exclude: bool = False):
+        """{kernel: (launches, flops, bytes, seconds)} (synchronises); with `stream` (a raw
+        handle) only the launches on that stream, or with exclude=True only the others."""
         out = {}
-        for name, fl, by, sec in self.records():
+        for name, fl, by, sec, sh in self.records(with_stream=True):
+            if stream is not None and (sh == stream) == exclude:
+                continue
             n, f, b, t = out.get(name, (0, 0, 0, 0.0))
             out[name] = (n + 1, f + fl, b + by, t + sec)
         return out

@@ -200,31 +200,35 @@ def kernel_roofline(step, dev, key, batch, npoints, replay=False):
     (csrc/probe.cpp).  The step is enqueued behind a 50 ms spin on the main stream, so the GPU
     runs the whole step back to back (as it does in the GPU-bound timed loop) and the event
     pairs time the kernels, not host-enqueue gaps.  The dominant kernel is the one with the
-    largest summed in-step time over ALL streams; `achieved` = its algorithmic flops or bytes
-    (per-launch models in DESIGN.md section 3) over that time.  Also returned: the largest
-    kernel on the critical path's engine (`critical_path_gemm`), the top kernels, and the flops
-    the probed launches execute per sample (`executed_gflop_per_step`)."""
+    largest summed in-step time on the step's own stream -- the critical path: the side
+    streams (the next step's geometry, the wgrad lane) run under it; `achieved` = its
+    algorithmic flops or bytes (per-launch models in DESIGN.md section 3) over that time.  Also
+    returned: the largest side-stream kernel (`largest_side_stream_kernel`, e.g. PointNet++'s
+    prefetched FPS), the top kernels over all streams, and the flops the probed launches
+    execute per sample (`executed_gflop_per_step`)."""
     import torch
     from pcseg.engine import KernelProbe
     from pcseg._lib import call, stream_ptr
     torch.cuda.synchronize(dev)
-    call('pcs_spin', 50000, stream_ptr(dev))
+    main = stream_ptr(dev)
+    call('pcs_spin', 50000, main)
     with KernelProbe() as kp:
         step()
     summ = kp.summary()
+    crit = kp.summary(stream=int(main))
+    side = kp.summary(stream=int(main), exclude=True)
     torch.cuda.synchronize(dev)
     ranked = sorted(summ.items(), key=lambda kv: -kv[1][3])
-    name, (n, fl, by, sec) = ranked[0]
+    name, (n, fl, by, sec) = sorted(crit.items(), key=lambda kv: -kv[1][3])[0]
     out = _kernel_entry(name, n, fl, by, sec)
     traffic, src = pmc_traffic(name, key, batch, npoints)
     out.update({'traffic': traffic, 'traffic_unit': 'bytes/launch', 'traffic_source': src,
+                'selection': 'largest summed in-step time among the launches on the step\'s own stream',
                 'timing': 'in-step HIP events, step enqueued behind a spin (no host gaps)'})
+    if side:
+        sn, sv = sorted(side.items(), key=lambda kv: -kv[1][3])[0]
+        out['largest_side_stream_kernel'] = _kernel_entry(sn, *sv)
     gemms = [kv for kv in ranked if any(k in kv[0] for k in ('gemm', 'wgrad', 'fused_bwd'))]
-    if gemms and gemms[0][0] != name:
-        g, (gn, gfl, gby, gsec) = gemms[0]
-        cg = _kernel_entry(g, gn, gfl, gby, gsec)
-        cg['traffic'], cg['traffic_source'] = pmc_traffic(g, key, batch, npoints)
-        out['critical_path_gemm'] = cg
     out['top_kernels'] = [{k: v for k, v in _kernel_entry(nm, *vals).items()
                            if k in ('kernel', 'in_step_ms', 'launches_per_step', 'frac', 'unit', 'compute_unit')}
                           for nm, vals in ranked[:8]]
