@@ -283,9 +283,12 @@ class GeometryPlan:
                  int(inverse), evs[L].cuda_event if interp else None, buf.data_ptr() + 4 * (wso if into is None else 0),
                  nws, stream_ptr(dev))
         if not torch.cuda.is_current_stream_capturing():
+            # buf is allocated on the main stream and WRITTEN by the side stream: a plan that is
+            # dropped unread (a stale prefetch) must not hand buf back to the main stream's pool
+            # while the side stream's kernels still write it
             coords.record_stream(side)
             if into is None:
-                buf.record_stream(main)
+                buf.record_stream(side)
 
     @staticmethod
     def _wait(ev):
