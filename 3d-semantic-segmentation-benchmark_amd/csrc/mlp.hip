@@ -1251,7 +1251,10 @@ static void wgrad_plan(int N, int K, int M, int* BO, int* BI, int* splits, int* 
     *BO = N > 64 ? 128 : 64;
     *BI = K > 64 ? 128 : 64;
     const int tiles = ((N + *BO - 1) / *BO) * ((K + *BI - 1) / *BI);
-    const int target = 2.0 * M * N * K >= 1.6e10 ? 2048 : 1024;
+#ifndef PCS_WGRAD_BLOCKS
+#define PCS_WGRAD_BLOCKS 1024
+#endif
+    const int target = 2.0 * M * N * K >= 1.6e10 ? 2048 : PCS_WGRAD_BLOCKS;
     int sp = (target + tiles - 1) / tiles;
     // the partial tiles (sp x N x K floats, written once and read once by the reduce) stay
     // below half the operands' bytes M x (N + K), as long as >= 512 blocks remain

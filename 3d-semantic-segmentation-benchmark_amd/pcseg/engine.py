@@ -237,6 +237,17 @@ def set_bwd_fuse(module: torch.nn.Module, policy: str = 'default') -> None:
             m.bwd_fuse = v
 
 
+def set_edge_inverse(module: torch.nn.Module, where: str = 'side') -> None:
+    """Where every fused EdgeConv under `module` builds its backward's inverse kNN map: 'side'
+    (default: on the side stream during the forward) or 'backward' (on the caller's stream when
+    the backward needs it)."""
+    if where not in ('side', 'backward'):
+        raise ValueError(f"edge inverse must be 'side' or 'backward', got {where!r}")
+    for m in module.modules():
+        if hasattr(m, 'edge_inverse'):
+            m.edge_inverse = where
+
+
 def _workspace(lib, key, M, kin, ldx, recs, nl, pool_k, backward):
     n = _ws_cache.get(key)
     if n is None:
@@ -470,7 +481,7 @@ class EdgeConvFn(torch.autograd.Function):
     (csrc/edgeconv.hip); the backward gathers over the CSR inverse of idx."""
 
     @staticmethod
-    def forward(ctx, X, idx, C, slope, bn, W, gamma, beta):
+    def forward(ctx, X, idx, C, slope, bn, W, gamma, beta, inverse_side=True):
         dev = X.device
         st = stream_ptr(dev)
         B, N, k = idx.shape
@@ -497,7 +508,7 @@ class EdgeConvFn(torch.autograd.Function):
         if recording():
             record_act_mask(out > 0)          # LeakyReLU keeps the sign: out > 0 <=> y > 0 at the argmax
         ctx.inv = None
-        if any(ctx.needs_input_grad):
+        if inverse_side and any(ctx.needs_input_grad):
             # the backward's inverse map of idx depends on idx only: build it now on the side
             # stream, under the rest of the forward, instead of on the backward's critical path
             from . import ops
@@ -544,7 +555,7 @@ class EdgeConvFn(torch.autograd.Function):
              ptr(pz), ptr(arg), ptr(coef), slope, ptr(gout), ptr(dX), ldx, ptr(dW), ptr(dg), ptr(db), ptr(ws),
              ws.numel(), st)
         notify_grad_ready((W, gamma, beta))
-        return dX, None, None, None, None, None, None, None
+        return dX, None, None, None, None, None, None, None, None
 
 
 def edgeconv_fused_ok(conv, bn, cin: int) -> bool:
@@ -553,13 +564,15 @@ def edgeconv_fused_ok(conv, bn, cin: int) -> bool:
             and (cin % 4 == 0 or cin < 4))
 
 
-def edgeconv(x_rows: torch.Tensor, cin: int, idx: torch.Tensor, conv, bn, slope: float) -> torch.Tensor:
-    """x_rows (B*N, ld) point rows, idx (B, N, k) int32 -> pooled (B*N, Cout)."""
+def edgeconv(x_rows: torch.Tensor, cin: int, idx: torch.Tensor, conv, bn, slope: float,
+             inverse_side: bool = True) -> torch.Tensor:
+    """x_rows (B*N, ld) point rows, idx (B, N, k) int32 -> pooled (B*N, Cout).  inverse_side: build
+    the backward's inverse map of idx on the side stream during the forward (else in the backward)."""
     if not x_rows.is_cuda:
         raise RuntimeError('pcseg ops run only on the GPU (no CPU fallback); got a CPU tensor')
     if x_rows.shape[1] % 4 or not x_rows.is_contiguous():
         x_rows = pad_rows(x_rows[:, :cin])
-    return EdgeConvFn.apply(x_rows, idx.contiguous(), cin, slope, bn, conv.weight, bn.weight, bn.bias)
+    return EdgeConvFn.apply(x_rows, idx.contiguous(), cin, slope, bn, conv.weight, bn.weight, bn.bias, inverse_side)
 
 
 def storage_alias(base: torch.Tensor, col0: int, ncol: int) -> torch.Tensor:

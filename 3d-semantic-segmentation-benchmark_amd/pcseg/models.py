@@ -251,6 +251,7 @@ class EdgeConv(nn.Module):
             nn.Conv2d(in_channels * 2, out_channels, kernel_size=1, bias=False),
             nn.BatchNorm2d(out_channels),
             nn.LeakyReLU(negative_slope=0.2))
+        self.edge_inverse = 'side'      # where the backward's inverse kNN map is built (engine.set_edge_inverse)
 
     def forward_points(self, xp: torch.Tensor) -> torch.Tensor:
         """xp point-major (B, N, C) -> (B, N, Cout)."""
@@ -270,7 +271,8 @@ class EdgeConv(nn.Module):
             rp.rec_knn_idx.append(idx.detach().cpu())
         C = xp.shape[2]
         if edgeconv_fused_ok(self.conv[0], self.conv[1], C):
-            pooled = edgeconv(xp.reshape(B * N, C), C, idx, self.conv[0], self.conv[1], self.conv[2].negative_slope)
+            pooled = edgeconv(xp.reshape(B * N, C), C, idx, self.conv[0], self.conv[1], self.conv[2].negative_slope,
+                              inverse_side=self.edge_inverse == 'side')
             return pooled.view(B, N, -1), idx
         rows = ops.edge_rows(xp, idx)
         pooled = shared_mlp(rows, 2 * C, [self.conv[0]], [self.conv[1]], 'lrelu',

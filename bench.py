@@ -281,6 +281,7 @@ def run_workload(key, batch, npoints, args, world, rank, dev):
     torch.manual_seed(0)
     model = ctor(pcseg).to(dev).train()     # PyTorch default init (random weights)
     pcseg.engine.set_bwd_fuse(model, args.bwd_fuse)
+    pcseg.engine.set_edge_inverse(model, args.edge_inverse)
     broadcast_model(model)
     grads = FlatGradAllReduce(model)
     use_graph = args.graph and world == 1
@@ -404,6 +405,9 @@ def main():
                     help='do not enqueue the next step\'s FPS/ball-query/3-NN before this step\'s backward')
     ap.add_argument('--graph-geometry', choices=['graph', 'eager'], default='graph',
                     help="--graph: capture the next step's neighbour search too, or enqueue it eagerly per step")
+    ap.add_argument('--edge-inverse', choices=['side', 'backward'], default='side',
+                    help='DGCNN: build the EdgeConv backward\'s inverse kNN maps on the side stream during the '
+                         'forward (default) or in the backward')
     ap.add_argument('--bwd-fuse', choices=['default', 'off', 'all'], default='default',
                     help='backward kernel choice of the shared-MLP stacks (pcs_mlp_layer.bwd_fuse; A/B runs)')
     ap.add_argument('--check-launch', action='store_true',
