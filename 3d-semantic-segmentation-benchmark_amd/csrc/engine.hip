@@ -507,18 +507,24 @@ static int mlp_backward(const float* X, int ldx, int kin, int M, const pcs_mlp_l
             xop = bnbwd_op(dA, Cin, Q, S.alpha[pp], S.kb[pp]);
             da = (da + 1) % 3;
         } else {
-            zero_cols(dX, M, lddx, kin, st);     // the GEMM writes columns [0, kin)
-            if (xop.mode == PCS_OP_PLAIN && gemm_nt_ok(xop.data, xop.ld, S.wt, C, M, kin, C)) {
-                // a wide layer's materialised dZ: W^T once (kin x C, a few MB) and the wide GEMM,
-                // dX = dZ . (W^T)^T with both operands contiguous along C
+            // dX columns [c0, kin): a caller that reads no gradient of the first c0 input columns
+            // (the relative coordinates of grouped rows, pcs_mlp_layer.dx_col0) gets a GEMM of
+            // kin - c0 outputs on the rows c0.. of W^T -- e.g. 64 instead of 67 (SA2), 128 instead
+            // of 131 (SA3): whole column tiles instead of a nearly empty last one
+            int c0 = (int)P.dx_col0;
+            if (c0 < 0 || c0 >= kin || (c0 * C) % 4) c0 = 0;
+            zero_cols(dX, M, lddx, kin, st);     // the pad columns [kin, lddx)
+            const bool wide = xop.mode == PCS_OP_PLAIN &&
+                              gemm_nt_ok(xop.data, xop.ld, S.wt + (size_t)c0 * C, C, M, kin - c0, C);
+            if (wide || c0 > 0) {
+                // W^T (kin x C, a few MB) read row-major from column c0 on: the wide GEMM
+                // (dX = dZ . (W^T)^T, both operands contiguous along C) or the row GEMM
                 if (bt) {
                     const dim3 g((Cin + 31) / 32, (C + 31) / 32);
                     hipLaunchKernelGGL(transpose_kernel, g, dim3(256), 0, st, P.W, C, Cin, (int)P.ldw, S.wt);
                 }
-                Bw = S.wt;
-                ldb = C;
-                if (int e = gemm_rows_ex(&xop, M, C, Bw, ldb, 0, nullptr, dX, lddx, kin, nullptr, nullptr, nullptr,
-                                         stream))
+                if (int e = gemm_rows_ex(&xop, M, C, S.wt + (size_t)c0 * C, C, 0, nullptr, dX + c0, lddx, kin - c0,
+                                         nullptr, nullptr, nullptr, stream))
                     return fail(e);
             } else if (int e = gemm_rows_ex(&xop, M, C, Bw, ldb, bt, nullptr, dX, lddx, kin, nullptr, nullptr, nullptr,
                                             stream)) {

@@ -396,10 +396,12 @@ class MiniPointNet(nn.Module):
             prev = m
         self.bwd_fuse = 0           # backward kernel choice (pcseg.engine.set_bwd_fuse)
 
-    def forward_rows(self, x: torch.Tensor, kin: int | None = None, pool_k: int = 0) -> torch.Tensor:
-        """rows (M, ld) -> (M, C_L), or (M/pool_k, C_L) max-pooled over consecutive groups of pool_k rows."""
+    def forward_rows(self, x: torch.Tensor, kin: int | None = None, pool_k: int = 0, dx_from: int = 0) -> torch.Tensor:
+        """rows (M, ld) -> (M, C_L), or (M/pool_k, C_L) max-pooled over consecutive groups of pool_k rows.
+        dx_from: the first input column whose gradient is wanted (3 for grouped rows: their relative
+        coordinates need none)."""
         return shared_mlp(x, kin or x.shape[1], self.conv, self.batch, 'relu', 0.0, pool_k, bwd_fuse=self.bwd_fuse,
-                          cache=module_cache(self))
+                          cache=module_cache(self), dx_from=dx_from)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         B, Cin, H, W = x.shape
@@ -459,9 +461,9 @@ class SetAbstraction(nn.Module):
         rows = ops.group_rows(coords, features, cent, idx, self.radius, self.grouping_norm, inv)
         kin = 3 + features.shape[2]
         if self.pooling_type == 'max':
-            out = self.point_net.forward_rows(rows, kin, pool_k=self.K).view(B, self.C, -1)
+            out = self.point_net.forward_rows(rows, kin, pool_k=self.K, dx_from=3).view(B, self.C, -1)
         else:
-            act = self.point_net.forward_rows(rows, kin)
+            act = self.point_net.forward_rows(rows, kin, dx_from=3)
             out = reduce(act.view(B, self.C, self.K, -1), self.pooling_type)
         return cent, out
 
@@ -516,9 +518,9 @@ class InvResMLP(nn.Module):
         rows = ops.group_rows(coords, features, centroid_coords, idx, self.radius, True, inv)
         kin = 3 + features.shape[2]
         if self.pooling_type == 'max':
-            pooled = self.neighbour_features_mlp.forward_rows(rows, kin, pool_k=self.K)
+            pooled = self.neighbour_features_mlp.forward_rows(rows, kin, pool_k=self.K, dx_from=3)
         else:
-            act = self.neighbour_features_mlp.forward_rows(rows, kin)
+            act = self.neighbour_features_mlp.forward_rows(rows, kin, dx_from=3)
             pooled = reduce(act.view(B, C, self.K, -1), self.pooling_type).reshape(B * C, -1)
         out = self.point_features_mlp.forward_rows(pooled).view(B, C, -1)
         return centroid_coords, out + features

@@ -168,7 +168,7 @@ def _f32(shape, dev):
 
 
 # pcs_mlp_layer (include/pcseg.h): 24 little-endian 8-byte slots
-_REC = struct.Struct('<QqqqQQQQQQddqqdQQQQQQdqq')   # ... dW db dgamma dbeta drop_p drop_seed reserved
+_REC = struct.Struct('<QqqqQQQQQQddqqdQQQQQQdqqq')  # ... dW db dgamma dbeta drop_p drop_seed bwd_fuse dx_col0
 _ws_cache: dict = {}
 
 
@@ -238,11 +238,12 @@ def set_bwd_fuse(module: torch.nn.Module, policy: str = 'default') -> None:
 
 
 def set_edge_inverse(module: torch.nn.Module, where: str = 'side') -> None:
-    """Where every fused EdgeConv under `module` builds its backward's inverse kNN map: 'side'
-    (default: on the side stream during the forward) or 'backward' (on the caller's stream when
-    the backward needs it)."""
-    if where not in ('side', 'backward'):
-        raise ValueError(f"edge inverse must be 'side' or 'backward', got {where!r}")
+    """Where every fused EdgeConv under `module` builds its backward's inverse kNN map: 'side' (on
+    the side stream as soon as its forward is enqueued: it then competes with the next layer's kNN),
+    'backward' (on the caller's stream when the backward needs it), or 'deferred' (the model
+    enqueues all of them on the side stream once its EdgeConvs are done: EdgeInverseBatch)."""
+    if where not in ('side', 'backward', 'deferred'):
+        raise ValueError(f"edge inverse must be 'side', 'backward' or 'deferred', got {where!r}")
     for m in module.modules():
         if hasattr(m, 'edge_inverse'):
             m.edge_inverse = where
@@ -265,7 +266,7 @@ def _nz(p) -> int:
 
 
 _STATIC = struct.Struct('<QqqqQQQQQQddqqd')     # pcs_mlp_layer fields W .. slope
-_DYN = struct.Struct('<QQQQQQdqq')               # Z coef dW db dgamma dbeta drop_p drop_seed bwd_fuse
+_DYN = struct.Struct('<QQQQQQdqqq')              # Z coef dW db dgamma dbeta drop_p drop_seed bwd_fuse dx_col0
 assert _STATIC.size + _DYN.size == _REC.size
 
 
@@ -323,7 +324,7 @@ def _workspace_probe(lib, key, M, Kin, ldx, params, bns, nl, pool_K, couts, acts
         bn = bns[li]
         use_batch = bn.training or bn.running_mean is None
         recs.append(_REC.pack(16, ldw, cin, C, 0, 0, 0, 16, 16, 0, 0.0, 1e-5, int(use_batch), acts[li][0],
-                              acts[li][1], 16, 16, 0, 0, 0, 0, 0.0, 0, 0))
+                              acts[li][1], 16, 16, 0, 0, 0, 0, 0.0, 0, 0, 0))
         cin = C
     return _workspace(lib, key, M, Kin, ldx, b''.join(recs), nl, pool_K, 0)
 
@@ -336,7 +337,7 @@ class SharedMLPFn(torch.autograd.Function):
     record per layer."""
 
     @staticmethod
-    def forward(ctx, X, Kin, pool_K, acts, bns, dest, drop, bwd_fuse, cache, *params):
+    def forward(ctx, X, Kin, pool_K, acts, bns, dest, drop, bwd_fuse, cache, dx_from, *params):
         dev = X.device
         st = stream_ptr(dev)
         lib = load()
@@ -378,7 +379,7 @@ class SharedMLPFn(torch.autograd.Function):
         # drop = (p, seed): the training-mode Dropout after the stack, fused into its output
         dp, dseed = drop if drop is not None else (0.0, 0)
         recs = b''.join(statics[li] + _DYN.pack(zp, cp, 0, 0, 0, 0, dp if li == nl - 1 else 0.0,
-                                                  dseed if li == nl - 1 else 0, bwd_fuse)
+                                                  dseed if li == nl - 1 else 0, bwd_fuse, 0)
                         for li, (zp, cp) in enumerate(zptrs))
         CL = couts[-1]
         ldo = 0
@@ -412,6 +413,7 @@ class SharedMLPFn(torch.autograd.Function):
         ctx.meta = (Kin, pool_K, nl, statics, zptrs, couts, arg is not None)
         ctx.drop = drop
         ctx.bwd_fuse = bwd_fuse
+        ctx.dx_from = dx_from
         ctx.params = params
         return out
 
@@ -440,7 +442,8 @@ class SharedMLPFn(torch.autograd.Function):
         recs = b''.join(statics[li] + _DYN.pack(zp, cp, _nz(grad_target(params[4 * li])),
                                                   _nz(grad_target(params[4 * li + 1])),
                                                   _nz(grad_target(params[4 * li + 2])),
-                                                  _nz(grad_target(params[4 * li + 3])), 0.0, 0, ctx.bwd_fuse)
+                                                  _nz(grad_target(params[4 * li + 3])), 0.0, 0, ctx.bwd_fuse,
+                                                  ctx.dx_from if li == 0 else 0)
                         for li, (zp, cp) in enumerate(zptrs))
         dX = None
         if ctx.needs_input_grad[0]:
@@ -460,7 +463,7 @@ class SharedMLPFn(torch.autograd.Function):
                 t.record_stream(lane)
             _queue_lane_join(dev)
         notify_grad_ready(params)
-        return (dX, None, None, None, None, None, None, None, None, *([None] * len(params)))
+        return (dX, None, None, None, None, None, None, None, None, None, *([None] * len(params)))
 
 
 def _edge_ws(B, N, C, Cout, backward, dev):
@@ -481,7 +484,7 @@ class EdgeConvFn(torch.autograd.Function):
     (csrc/edgeconv.hip); the backward gathers over the CSR inverse of idx."""
 
     @staticmethod
-    def forward(ctx, X, idx, C, slope, bn, W, gamma, beta, inverse_side=True):
+    def forward(ctx, X, idx, C, slope, bn, W, gamma, beta, inverse_side=True, holder=None):
         dev = X.device
         st = stream_ptr(dev)
         B, N, k = idx.shape
@@ -508,7 +511,10 @@ class EdgeConvFn(torch.autograd.Function):
         if recording():
             record_act_mask(out > 0)          # LeakyReLU keeps the sign: out > 0 <=> y > 0 at the argmax
         ctx.inv = None
-        if inverse_side and any(ctx.needs_input_grad):
+        ctx.holder = holder if any(ctx.needs_input_grad) else None
+        if ctx.holder is not None:
+            ctx.holder.append((idx, N))          # built later on the side stream (EdgeInverseBatch)
+        elif inverse_side and any(ctx.needs_input_grad):
             # the backward's inverse map of idx depends on idx only: build it now on the side
             # stream, under the rest of the forward, instead of on the backward's critical path
             from . import ops
@@ -538,6 +544,9 @@ class EdgeConvFn(torch.autograd.Function):
         M, ldx = X.shape
         Cout = Wm.shape[0]
         gout = gout.contiguous()
+        if ctx.inv is None and ctx.holder is not None and len(ctx.holder) == 3:
+            ctx.inv = tuple(ctx.holder)
+        ctx.holder = None
         if ctx.inv is not None:
             off, ent, ev = ctx.inv
             torch.cuda.current_stream(dev).wait_event(ev)
@@ -555,7 +564,7 @@ class EdgeConvFn(torch.autograd.Function):
              ptr(pz), ptr(arg), ptr(coef), slope, ptr(gout), ptr(dX), ldx, ptr(dW), ptr(dg), ptr(db), ptr(ws),
              ws.numel(), st)
         notify_grad_ready((W, gamma, beta))
-        return dX, None, None, None, None, None, None, None, None
+        return dX, None, None, None, None, None, None, None, None, None
 
 
 def edgeconv_fused_ok(conv, bn, cin: int) -> bool:
@@ -565,14 +574,50 @@ def edgeconv_fused_ok(conv, bn, cin: int) -> bool:
 
 
 def edgeconv(x_rows: torch.Tensor, cin: int, idx: torch.Tensor, conv, bn, slope: float,
-             inverse_side: bool = True) -> torch.Tensor:
+             inverse_side: bool = True, holder: list | None = None) -> torch.Tensor:
     """x_rows (B*N, ld) point rows, idx (B, N, k) int32 -> pooled (B*N, Cout).  inverse_side: build
     the backward's inverse map of idx on the side stream during the forward (else in the backward)."""
     if not x_rows.is_cuda:
         raise RuntimeError('pcseg ops run only on the GPU (no CPU fallback); got a CPU tensor')
     if x_rows.shape[1] % 4 or not x_rows.is_contiguous():
         x_rows = pad_rows(x_rows[:, :cin])
-    return EdgeConvFn.apply(x_rows, idx.contiguous(), cin, slope, bn, conv.weight, bn.weight, bn.bias, inverse_side)
+    return EdgeConvFn.apply(x_rows, idx.contiguous(), cin, slope, bn, conv.weight, bn.weight, bn.bias, inverse_side,
+                            holder)
+
+
+class EdgeInverseBatch:
+    """Deferred inverse kNN maps of a forward's EdgeConvs: each fused EdgeConv that needs a
+    backward registers (idx, N) in its holder; `flush()` -- called by the model once its last
+    EdgeConv is enqueued, so the maps do not compete with the later kNN searches -- builds them
+    all on the side stream (after everything enqueued so far on the caller's stream), where
+    they run under the head's GEMMs."""
+
+    def __init__(self):
+        self.holders = []
+
+    def holder(self) -> list:
+        h = []
+        self.holders.append(h)
+        return h
+
+    def flush(self) -> None:
+        from . import ops
+        from .common import side_stream
+        pend = [h for h in self.holders if len(h) == 1]
+        self.holders = []
+        if not pend:
+            return
+        dev = pend[0][0][0].device
+        side = side_stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for h in pend:
+                idx, N = h.pop()
+                off, ent = ops.inverse_index(idx, N)
+                ev = torch.cuda.Event()
+                ev.record(side)
+                idx.record_stream(side)
+                h.extend((off, ent, ev))
 
 
 def storage_alias(base: torch.Tensor, col0: int, ncol: int) -> torch.Tensor:
@@ -593,7 +638,7 @@ def _rows_ok(x: torch.Tensor) -> bool:
 
 def shared_mlp(x_rows: torch.Tensor, kin: int, convs, bns, act='relu', slope=0.0,
                pool_k: int = 0, out: torch.Tensor | None = None, dropout: tuple | None = None,
-               bwd_fuse: int = 0, cache: dict | None = None) -> torch.Tensor:
+               bwd_fuse: int = 0, cache: dict | None = None, dx_from: int = 0) -> torch.Tensor:
     """Run a conv/BN/act stack on rows.  x_rows (M, W) with `kin` logical channels, W % 4 == 0,
     dense or a column block of a wider buffer (row stride >= W).  `act` / `slope` are one value
     for every layer or a sequence with one per layer ('relu', 'lrelu', 'none').  `out`: an
@@ -602,7 +647,9 @@ def shared_mlp(x_rows: torch.Tensor, kin: int, convs, bns, act='relu', slope=0.0
     (pcs_mlp_layer.drop_p; backward pcs_dropout_bwd recomputes the mask from the seed).
     `bwd_fuse`: the stack's backward kernel choice (BWD_FUSE values, pcs_mlp_layer.bwd_fuse).
     `cache`: a dict owned by the calling module, where the stack's static layer records are
-    kept between calls (host enqueue cost)."""
+    kept between calls (host enqueue cost).  `dx_from`: the first input column whose gradient
+    is wanted (pcs_mlp_layer.dx_col0): grouped rows start with 3 relative-coordinate columns
+    whose gradient no caller reads; the returned gradient's columns before it are undefined."""
     if not x_rows.is_cuda:
         raise RuntimeError('pcseg ops run only on the GPU (no CPU fallback); got a CPU tensor')
     if not _rows_ok(x_rows):
@@ -621,7 +668,7 @@ def shared_mlp(x_rows: torch.Tensor, kin: int, convs, bns, act='relu', slope=0.0
     if dropout is not None and (pool_k or not 0.0 < float(dropout[0]) < 1.0):
         raise ValueError('shared_mlp: dropout needs an un-pooled output and 0 < p < 1')
     return SharedMLPFn.apply(x_rows, kin, pool_k, acts, list(bns), None if out is None else (out,), dropout,
-                             int(bwd_fuse), cache, *params)
+                             int(bwd_fuse), cache, int(dx_from), *params)
 
 
 class RowLinearFn(torch.autograd.Function):

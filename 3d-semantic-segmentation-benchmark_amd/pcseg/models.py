@@ -17,7 +17,8 @@ import torch.nn.functional as F
 
 from . import ops
 from .common import SetAbstraction, FeaturePropagation, InvResMLP, UnitPointNet, GeometryPlan, GeometryPrefetch
-from .engine import shared_mlp, pad_rows, linear_rows, edgeconv, edgeconv_fused_ok, storage_alias, module_cache
+from .engine import (shared_mlp, pad_rows, linear_rows, edgeconv, edgeconv_fused_ok, storage_alias, module_cache,
+                     EdgeInverseBatch)
 from .replay import active as _replay
 from ._lib import call, ptr, stream_ptr
 
@@ -119,7 +120,7 @@ class PointNetppMSG(GeometryPrefetch, nn.Module):
         for q, sa in enumerate(branches):
             cent, idx, inv = geo.sa(level, q)
             rows = ops.group_rows(coords, feats, cent, idx, sa.radius, sa.grouping_norm, inv)
-            outs.append(sa.point_net.forward_rows(rows, 3 + feats.shape[2], pool_k=sa.K).view(B, C, -1))
+            outs.append(sa.point_net.forward_rows(rows, 3 + feats.shape[2], pool_k=sa.K, dx_from=3).view(B, C, -1))
         return cent, torch.cat(outs, dim=-1)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
@@ -251,13 +252,13 @@ class EdgeConv(nn.Module):
             nn.Conv2d(in_channels * 2, out_channels, kernel_size=1, bias=False),
             nn.BatchNorm2d(out_channels),
             nn.LeakyReLU(negative_slope=0.2))
-        self.edge_inverse = 'side'      # where the backward's inverse kNN map is built (engine.set_edge_inverse)
+        self.edge_inverse = 'deferred'  # where the backward's inverse kNN map is built (engine.set_edge_inverse)
 
     def forward_points(self, xp: torch.Tensor) -> torch.Tensor:
         """xp point-major (B, N, C) -> (B, N, Cout)."""
         return self.forward_graph(xp)[0]
 
-    def forward_graph(self, xp: torch.Tensor, seeds: torch.Tensor | None = None):
+    def forward_graph(self, xp: torch.Tensor, seeds: torch.Tensor | None = None, inv_batch=None):
         """(output (B, N, Cout), this layer's kNN graph (B, N, k) int32).  seeds: the previous
         EdgeConv's graph -- its neighbours' distances in this layer's feature space bound the
         search threshold from the start (same graph, less merge work)."""
@@ -271,8 +272,9 @@ class EdgeConv(nn.Module):
             rp.rec_knn_idx.append(idx.detach().cpu())
         C = xp.shape[2]
         if edgeconv_fused_ok(self.conv[0], self.conv[1], C):
+            holder = inv_batch.holder() if (inv_batch is not None and self.edge_inverse == 'deferred') else None
             pooled = edgeconv(xp.reshape(B * N, C), C, idx, self.conv[0], self.conv[1], self.conv[2].negative_slope,
-                              inverse_side=self.edge_inverse == 'side')
+                              inverse_side=self.edge_inverse == 'side', holder=holder)
             return pooled.view(B, N, -1), idx
         rows = ops.edge_rows(xp, idx)
         pooled = shared_mlp(rows, 2 * C, [self.conv[0]], [self.conv[1]], 'lrelu',
@@ -386,10 +388,12 @@ class DGCNN(nn.Module):
         B, _, N = x.shape
         xyz = x[:, :3, :] if x.size(1) == 6 else x
         xp = xyz.transpose(1, 2).contiguous()
-        x1, g = self.conv1.forward_graph(xp)
-        x2, g = self.conv2.forward_graph(x1, g)
-        x3, g = self.conv3.forward_graph(x2, g)
-        x4, _ = self.conv4.forward_graph(x3, g)
+        ib = EdgeInverseBatch()
+        x1, g = self.conv1.forward_graph(xp, inv_batch=ib)
+        x2, g = self.conv2.forward_graph(x1, g, inv_batch=ib)
+        x3, g = self.conv3.forward_graph(x2, g, inv_batch=ib)
+        x4, _ = self.conv4.forward_graph(x3, g, inv_batch=ib)
+        ib.flush()
         return _dgcnn_head(self, [x1, x2, x3, x4], B, N)
 
 
@@ -419,10 +423,12 @@ class DGCNNWithColor(nn.Module):
         xp = x.transpose(1, 2)                           # (B, N, 6) view of the (B,6,N) input
         xyz = xp[:, :, :3].contiguous()
         rgb = xp[:, :, 3:6].contiguous()
-        x1, g = self.conv1.forward_graph(xyz)
-        x2, g = self.conv2.forward_graph(x1, g)
-        x3, g = self.conv3.forward_graph(x2, g)
-        x4, _ = self.conv4.forward_graph(x3, g)
+        ib = EdgeInverseBatch()
+        x1, g = self.conv1.forward_graph(xyz, inv_batch=ib)
+        x2, g = self.conv2.forward_graph(x1, g, inv_batch=ib)
+        x3, g = self.conv3.forward_graph(x2, g, inv_batch=ib)
+        x4, _ = self.conv4.forward_graph(x3, g, inv_batch=ib)
+        ib.flush()
         color = _seq_rows(pad_rows(rgb.view(B * N, 3)), self.color_conv, 3).view(B, N, -1)
         return _dgcnn_head(self, [x1, x2, x3, x4, color], B, N)
 

@@ -405,9 +405,10 @@ def main():
                     help='do not enqueue the next step\'s FPS/ball-query/3-NN before this step\'s backward')
     ap.add_argument('--graph-geometry', choices=['graph', 'eager'], default='graph',
                     help="--graph: capture the next step's neighbour search too, or enqueue it eagerly per step")
-    ap.add_argument('--edge-inverse', choices=['side', 'backward'], default='side',
-                    help='DGCNN: build the EdgeConv backward\'s inverse kNN maps on the side stream during the '
-                         'forward (default) or in the backward')
+    ap.add_argument('--edge-inverse', choices=['side', 'backward', 'deferred'], default='deferred',
+                    help='DGCNN: where the EdgeConv backward\'s inverse kNN maps are built: on the side stream '
+                         'after the last EdgeConv (deferred, default), right after each EdgeConv (side), or in '
+                         'the backward')
     ap.add_argument('--bwd-fuse', choices=['default', 'off', 'all'], default='default',
                     help='backward kernel choice of the shared-MLP stacks (pcs_mlp_layer.bwd_fuse; A/B runs)')
     ap.add_argument('--check-launch', action='store_true',

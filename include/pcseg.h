@@ -280,6 +280,12 @@ typedef struct pcs_mlp_layer {
                            * weight gradient of a thin layer into one launch only over >= 2^19
                            * rows, _OFF never, _ALL for every eligible layer (same results to
                            * fp32 rounding; tests / A-B runs) */
+    int64_t dx_col0;      /* first layer, backward: the first input column whose data gradient
+                           * the caller needs -- the grouped rows of a SetAbstraction start with
+                           * 3 relative-coordinate columns whose gradient nobody reads
+                           * (common.py:64-65 gathers only features back); dX columns
+                           * [0, dx_col0) are then left unwritten and the data-gradient GEMM
+                           * covers kin - dx_col0 columns (0 = all) */
 } pcs_mlp_layer;
 
 #define PCS_BWD_FUSE_DEFAULT 0

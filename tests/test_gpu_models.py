@@ -461,3 +461,33 @@ def test_two_identical_steps_give_bitwise_equal_gradients(name):
     assert not diff, diff
     diff = [k for k in b0 if not torch.equal(b0[k], b1[k])]
     assert not diff, diff
+
+
+@pytest.mark.parametrize('name', ['dgcnn_color', 'dgcnn_xyz'])
+def test_edge_inverse_placement_gives_identical_gradients(name):
+    """Where the EdgeConv backward's inverse kNN maps are built (right after each EdgeConv on the
+    side stream, batched after the last EdgeConv, or in the backward) changes only the schedule:
+    the lists are sorted, so every gradient and running statistic is bit-identical."""
+    ctor, inp = DET_MODELS[name]
+    torch.manual_seed(321)
+    sd = ctor().state_dict()
+    pts, labels, lengths = make_batch(2, 4096, seed=909)
+    x = inp(pts.to(DEV))
+    runs = []
+    for where in ('side', 'deferred', 'backward'):
+        m = ctor()
+        m.load_state_dict(sd)
+        m = m.to(DEV).train()
+        pcseg.engine.set_edge_inverse(m, where)
+        torch.manual_seed(78)
+        logits = m(x)
+        logits = logits[0] if isinstance(logits, tuple) else logits
+        loss = pcseg.masked_onehot_cross_entropy(logits, labels[..., :logits.shape[-1]].to(DEV), lengths.to(DEV))
+        loss.backward()
+        torch.cuda.synchronize()
+        runs.append(({k: p.grad.clone() for k, p in m.named_parameters() if p.grad is not None},
+                     {k: b.clone() for k, b in m.named_buffers()}))
+    for g, b in runs[1:]:
+        assert g.keys() == runs[0][0].keys() and len(g) > 0
+        assert not [k for k in g if not torch.equal(g[k], runs[0][0][k])]
+        assert not [k for k in b if not torch.equal(b[k], runs[0][1][k])]
