@@ -279,8 +279,8 @@ def test_dgcnn_model_seeded_graphs_equal_unseeded():
     feats, graphs = [], []
     orig = pcseg.models.EdgeConv.forward_graph
 
-    def rec(self, xp, seeds=None):
-        out, idx = orig(self, xp, seeds)
+    def rec(self, xp, seeds=None, **kw):
+        out, idx = orig(self, xp, seeds, **kw)
         feats.append(xp.detach().clone())
         graphs.append(idx)
         return out, idx
