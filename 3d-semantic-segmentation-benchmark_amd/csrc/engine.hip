@@ -477,7 +477,8 @@ static int mlp_backward(const float* X, int ldx, int kin, int M, const pcs_mlp_l
         const bool bt = P.ldw % 4 == 0;
         const float* Bw = P.W;
         int ldb = (int)P.ldw;
-        if (!bt) {
+        const bool col0 = l == 0 && P.dx_col0 > 0 && P.dx_col0 < kin;   // k-major from column dx_col0
+        if (!bt && !col0) {
             const dim3 g((Cin + 31) / 32, (C + 31) / 32);
             hipLaunchKernelGGL(transpose_kernel, g, dim3(256), 0, st, P.W, C, Cin, (int)P.ldw, S.wt);
             Bw = S.wt;
@@ -512,18 +513,25 @@ static int mlp_backward(const float* X, int ldx, int kin, int M, const pcs_mlp_l
             // kin - c0 outputs on the rows c0.. of W^T -- e.g. 64 instead of 67 (SA2), 128 instead
             // of 131 (SA3): whole column tiles instead of a nearly empty last one
             int c0 = (int)P.dx_col0;
-            if (c0 < 0 || c0 >= kin || (c0 * C) % 4) c0 = 0;
-            zero_cols(dX, M, lddx, kin, st);     // the pad columns [kin, lddx)
-            const bool wide = xop.mode == PCS_OP_PLAIN &&
+            if (c0 < 0 || c0 >= kin) c0 = 0;
+            const bool wide = xop.mode == PCS_OP_PLAIN && (c0 * C) % 4 == 0 &&
                               gemm_nt_ok(xop.data, xop.ld, S.wt + (size_t)c0 * C, C, M, kin - c0, C);
-            if (wide || c0 > 0) {
-                // W^T (kin x C, a few MB) read row-major from column c0 on: the wide GEMM
-                // (dX = dZ . (W^T)^T, both operands contiguous along C) or the row GEMM
-                if (bt) {
+            if (c0 == 0) zero_cols(dX, M, lddx, kin, st);   // the pad columns [kin, lddx); with c0 > 0 the
+                                                           // caller reads only [c0, kin): none written
+            if (wide) {
+                // W^T (kin x C, a few MB) from column c0 on and the wide GEMM, dX = dZ . (W^T)^T with both
+                // operands contiguous along C (W^T is already there when the first layer took the
+                // transpose above: unaligned rows and c0 == 0)
+                if (bt || c0 > 0) {
                     const dim3 g((Cin + 31) / 32, (C + 31) / 32);
                     hipLaunchKernelGGL(transpose_kernel, g, dim3(256), 0, st, P.W, C, Cin, (int)P.ldw, S.wt);
                 }
                 if (int e = gemm_rows_ex(&xop, M, C, S.wt + (size_t)c0 * C, C, 0, nullptr, dX + c0, lddx, kin - c0,
+                                         nullptr, nullptr, nullptr, stream))
+                    return fail(e);
+            } else if (c0 > 0) {
+                // W read k-major in place from column c0 (scalar loads where its rows are unaligned)
+                if (int e = gemm_rows_ex(&xop, M, C, P.W + c0, (int)P.ldw, 1, nullptr, dX + c0, lddx, kin - c0,
                                          nullptr, nullptr, nullptr, stream))
                     return fail(e);
             } else if (int e = gemm_rows_ex(&xop, M, C, Bw, ldb, bt, nullptr, dX, lddx, kin, nullptr, nullptr, nullptr,

@@ -87,6 +87,7 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void gemm_rows_kernel(GemmArgs g) 
     // coefficient quad per slab serves all of them
     Quad q;
     const int lda_last = g.a.ld - 4, ldw_last = g.ldw - 4;
+    const bool bt_scalar = BT && ((g.ldw & 3) || (reinterpret_cast<uintptr_t>(g.W) & 15));
     auto gload = [&](int m0, int k0) {
         const int gk = k0 + 4 * (tid & 7);
         const int gkc = min(gk, lda_last);
@@ -101,9 +102,18 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void gemm_rows_kernel(GemmArgs g) 
             const int e = it * NT + tid;
             if constexpr (BT) {
                 const int gk = min(k0 + e / (BN / 4), g.K - 1);
-                const int gn = min(n0 + 4 * (e % (BN / 4)), ldw_last);
-                if (kBFull || e < BN * GBK / 4)
-                    rb[it] = *reinterpret_cast<const float4*>(g.W + (size_t)gk * g.ldw + gn);
+                if (bt_scalar) {      // k-major rows that are not 16-B aligned (a first layer's W from
+                                      // column dx_col0 on, rows of 3 + D): scalar loads
+                    const float* wr = g.W + (size_t)gk * g.ldw;
+                    const int gn = n0 + 4 * (e % (BN / 4)), nl = g.N - 1;
+                    if (kBFull || e < BN * GBK / 4)
+                        rb[it] = make_float4(wr[min(gn, nl)], wr[min(gn + 1, nl)], wr[min(gn + 2, nl)],
+                                             wr[min(gn + 3, nl)]);
+                } else {
+                    const int gn = min(n0 + 4 * (e % (BN / 4)), ldw_last);
+                    if (kBFull || e < BN * GBK / 4)
+                        rb[it] = *reinterpret_cast<const float4*>(g.W + (size_t)gk * g.ldw + gn);
+                }
             } else {
                 const int gn = min(n0 + (e >> 3), g.N - 1);
                 if (g.ldw & 3) {      // unpadded weight rows (a stack's first layer, K = 3 + D): scalar loads
@@ -1172,8 +1182,7 @@ int pcs::gemm_rows_ex(const pcs_operand* a, int M, int K, const float* W, int ld
     PCS_CHECK_ARG(!(stats && bstats), "pcs_gemm_rows: stats and bstats are exclusive");
     PCS_CHECK_ARG(!bstats || (epi && epi->z && epi->s && epi->t && epi->mean && epi->inv),
                   "pcs_gemm_rows: bstats needs epi z/s/t/mean/inv");
-    PCS_CHECK_ARG((ldw % 4 == 0 || !bt) && ldw >= (bt ? N : K),
-                  "pcs_gemm_rows: ldw=%d must be >= %d (and a multiple of 4 for k-major W)", ldw, bt ? N : K);
+    PCS_CHECK_ARG(ldw >= (bt ? N : K), "pcs_gemm_rows: ldw=%d must be >= %d", ldw, bt ? N : K);
     PCS_CHECK_ARG(!bt || a->mode != PCS_OP_BNACT, "pcs_gemm_rows: k-major W needs a PLAIN/BNBWD/POOLBWD A");
     // the epilogue addresses a 32-row block of C / epi Z with 32-bit offsets
     PCS_CHECK_ARG((long long)ldc * 32 + N < (1ll << 31) && (!epi || (long long)epi->ldz * 32 + N < (1ll << 31)),

@@ -159,3 +159,32 @@ def check_bitwise_reproducible():
         for ta, tb in zip(ga, gb):
             assert torch.equal(ta, tb)
     assert torch.equal(a[4], b[4])
+
+
+@pytest.mark.parametrize('cin,widths,rows,pool_k', [(67, [64, 64, 128], 32768, 32), (131, [128, 128, 256], 16384, 32),
+                                                     (259, [256, 256, 512], 8192, 32), (35, [32, 64], 5000, 0)])
+def test_first_layer_dx_from_column3(cin, widths, rows, pool_k):
+    """MiniPointNet.forward_rows(dx_from=3) (pcs_mlp_layer.dx_col0; SetAbstraction's grouped rows:
+    no caller reads the gradient of their 3 relative-coordinate columns): the data gradient of
+    columns [3, cin) -- a GEMM of cin - 3 outputs on W read k-major from column 3 with scalar loads
+    (rows of 3 + D floats are unaligned) -- equals the full-width gradient's columns, and every
+    weight gradient is unchanged."""
+    torch.manual_seed(11)
+    mod = pcseg.MiniPointNet(cin, widths).cuda().train()
+    x = torch.randn(rows, cin, device='cuda')
+    out_g = None
+    res = []
+    for dx_from in (0, 3):
+        for p in mod.parameters():
+            p.grad = None
+        xg = pcseg.engine.pad_rows(x).requires_grad_()
+        out = mod.forward_rows(xg, cin, pool_k=pool_k, dx_from=dx_from)
+        if out_g is None:
+            out_g = torch.randn(out.shape, device='cuda', generator=torch.Generator(device='cuda').manual_seed(5))
+        out.backward(out_g)
+        torch.cuda.synchronize()
+        res.append((xg.grad[:, 3:cin].clone(), [p.grad.clone() for p in mod.parameters()]))
+    (d0, g0), (d3, g3) = res
+    assert float((d3 - d0).norm() / d0.norm()) <= 1e-6
+    for a, b in zip(g0, g3):
+        assert torch.equal(a, b)
