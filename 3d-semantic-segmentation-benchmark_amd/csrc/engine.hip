@@ -477,7 +477,11 @@ static int mlp_backward(const float* X, int ldx, int kin, int M, const pcs_mlp_l
         const bool bt = P.ldw % 4 == 0;
         const float* Bw = P.W;
         int ldb = (int)P.ldw;
+#ifdef PCS_DX_TRANSPOSE
+        const bool col0 = false;        // A/B builds: W^T rows from dx_col0 (transpose launch)
+#else
         const bool col0 = l == 0 && P.dx_col0 > 0 && P.dx_col0 < kin;   // k-major from column dx_col0
+#endif
         if (!bt && !col0) {
             const dim3 g((Cin + 31) / 32, (C + 31) / 32);
             hipLaunchKernelGGL(transpose_kernel, g, dim3(256), 0, st, P.W, C, Cin, (int)P.ldw, S.wt);
@@ -529,6 +533,16 @@ static int mlp_backward(const float* X, int ldx, int kin, int M, const pcs_mlp_l
                 if (int e = gemm_rows_ex(&xop, M, C, S.wt + (size_t)c0 * C, C, 0, nullptr, dX + c0, lddx, kin - c0,
                                          nullptr, nullptr, nullptr, stream))
                     return fail(e);
+#ifdef PCS_DX_TRANSPOSE
+            } else if (c0 > 0 && (c0 * C) % 4 == 0) {
+                if (bt) {
+                    const dim3 g((Cin + 31) / 32, (C + 31) / 32);
+                    hipLaunchKernelGGL(transpose_kernel, g, dim3(256), 0, st, P.W, C, Cin, (int)P.ldw, S.wt);
+                }
+                if (int e = gemm_rows_ex(&xop, M, C, S.wt + (size_t)c0 * C, C, 0, nullptr, dX + c0, lddx, kin - c0,
+                                         nullptr, nullptr, nullptr, stream))
+                    return fail(e);
+#endif
             } else if (c0 > 0) {
                 // W read k-major in place from column c0 (scalar loads where its rows are unaligned)
                 if (int e = gemm_rows_ex(&xop, M, C, P.W + c0, (int)P.ldw, 1, nullptr, dX + c0, lddx, kin - c0,
