@@ -477,8 +477,9 @@ static int mlp_backward(const float* X, int ldx, int kin, int M, const pcs_mlp_l
         const bool bt = P.ldw % 4 == 0;
         const float* Bw = P.W;
         int ldb = (int)P.ldw;
-#ifdef PCS_DX_TRANSPOSE
-        const bool col0 = false;        // A/B builds: W^T rows from dx_col0 (transpose launch)
+#ifndef PCS_DX_KMAJOR
+        const bool col0 = false;        // W^T rows from dx_col0 (one transpose launch; measured 2 %
+                                        // faster than the k-major scalar-load form, PCS_DX_KMAJOR)
 #else
         const bool col0 = l == 0 && P.dx_col0 > 0 && P.dx_col0 < kin;   // k-major from column dx_col0
 #endif
@@ -533,7 +534,7 @@ static int mlp_backward(const float* X, int ldx, int kin, int M, const pcs_mlp_l
                 if (int e = gemm_rows_ex(&xop, M, C, S.wt + (size_t)c0 * C, C, 0, nullptr, dX + c0, lddx, kin - c0,
                                          nullptr, nullptr, nullptr, stream))
                     return fail(e);
-#ifdef PCS_DX_TRANSPOSE
+#ifndef PCS_DX_KMAJOR
             } else if (c0 > 0 && (c0 * C) % 4 == 0) {
                 if (bt) {
                     const dim3 g((Cin + 31) / 32, (C + 31) / 32);
