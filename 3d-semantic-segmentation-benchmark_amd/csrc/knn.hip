@@ -332,7 +332,7 @@ __global__ __launch_bounds__(64 * WPB, 2) void knn_wave_kernel(const float* __re
     if constexpr (PRE) xxq = xx_pre[(size_t)b * N + qr];
     float tau = -INFINITY;
     if constexpr (SEEDED) {
-        static_assert(MF && PRE, "seeded threshold: F % 4 == 0 with precomputed norms");
+        static_assert(PRE, "seeded threshold: precomputed norms");
         // the k-th best pd among the row's seeds (here: the minimum over k of them).  The scan's
         // pd comes from an MFMA dot in another summation order: the margin 2^-14 (|x_q|^2 + |x_s|^2)
         // covers that (|dot error| <= ~F u sum|x_q x_s| <= 64 u (|x_q|^2 + |x_s|^2) / 2)
@@ -349,15 +349,20 @@ __global__ __launch_bounds__(64 * WPB, 2) void knn_wave_kernel(const float* __re
             for (int u = 0; u < K; ++u) ok = ok && !(u < j && prev[u] == sc);
 #pragma unroll
             for (int u = 0; u < K; ++u) prev[u] = u == j ? sc : prev[u];
-            const float4* src = reinterpret_cast<const float4*>(X + (size_t)sc * F + h * FH);
             float part = 0.f;
+            if constexpr (MF) {
+                const float4* src = reinterpret_cast<const float4*>(X + (size_t)sc * F + h * FH);
 #pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-                const float4 v = src[q];
-                part = __fmaf_rn(a[4 * q], v.x, part);
-                part = __fmaf_rn(a[4 * q + 1], v.y, part);
-                part = __fmaf_rn(a[4 * q + 2], v.z, part);
-                part = __fmaf_rn(a[4 * q + 3], v.w, part);
+                for (int q = 0; q < NQ; ++q) {
+                    const float4 v = src[q];
+                    part = __fmaf_rn(a[4 * q], v.x, part);
+                    part = __fmaf_rn(a[4 * q + 1], v.y, part);
+                    part = __fmaf_rn(a[4 * q + 2], v.z, part);
+                    part = __fmaf_rn(a[4 * q + 3], v.w, part);
+                }
+            } else {            // F = 3: lane half 0 holds (x, y), half 1 (z, 0), as the query's a[]
+                const float* sp = X + (size_t)sc * 3;
+                part = __fmaf_rn(a[1], h ? 0.f : sp[1], __fmul_rn(a[0], h ? sp[2] : sp[0]));
             }
             const float dot = __fadd_rn(part, __shfl_xor(part, 32));
             const float cx = xx_pre[(size_t)b * N + sc];
@@ -533,7 +538,7 @@ static void launch_knn(const float* x, int B, int N, int* out, float* xx, const 
             hipLaunchKernelGGL((knn_sqnorm_kernel<F>), dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, x, P, xx);
             // algorithmic: the N x N inner-product tile per cloud (2F flops per pair, the
             // reference's bmm), x read + the k-lists written
-            if constexpr (F % 4 == 0) {
+            {
                 if (seeds) {
                     ProbeScope pr(s, 2.0 * F * (double)N * N * B, 4.0 * (double)B * N * (F + K),
                                   "pcs::knn_wave_kernel<%d, %d, %d, true, seeded>", F, K, KNN_WAVES);
@@ -580,7 +585,7 @@ static int knn_run(const float* x, int B, int N, int F, int k, int32_t* out_idx,
     hipStream_t s = as_stream(stream);
     int rc;
     switch (F) {
-        case 3: rc = dispatch_k<3>(x, B, N, k, out_idx, xx, nullptr, 0, s); break;
+        case 3: rc = dispatch_k<3>(x, B, N, k, out_idx, xx, xx ? seeds : nullptr, ks, s); break;
         case 64: rc = dispatch_k<64>(x, B, N, k, out_idx, xx, seeds, ks, s); break;
         default:
             set_error("pcs_knn: F=%d not instantiated (3, 64)", F);
@@ -614,11 +619,115 @@ PCS_API int pcs_knn_ws(const float* x, int B, int N, int F, int k, int32_t* out_
 // pcs_knn_ws whose rows start from the threshold of a previous neighbour list (seeds (B, N, ks)
 // int32, e.g. the previous EdgeConv's graph): the same lists, fewer survivors to merge.  Any
 // seeds are safe -- a row whose seeds are out of range, repeated or fewer than k is searched
-// unseeded.  Seeding applies to F = 64 (F = 3 ignores the seeds).
+// unseeded.  F = 3 rows can be seeded by pcs_knn_morton_seeds (there is no previous graph).
 PCS_API int pcs_knn_seeded(const float* x, int B, int N, int F, int k, const int32_t* seeds, int ks, int32_t* out_idx,
                            void* ws, size_t ws_bytes, void* stream) {
     PCS_CHECK_ARG(ws && ws_bytes >= (size_t)B * N * sizeof(float) + 256, "pcs_knn_seeded: workspace too small");
     PCS_CHECK_ARG(seeds && ks >= 1, "pcs_knn_seeded: null seeds or ks < 1");
     float* xx = reinterpret_cast<float*>((reinterpret_cast<uintptr_t>(ws) + 255) & ~uintptr_t(255));
     return knn_run(x, B, N, F, k, out_idx, xx, seeds, ks, stream);
+}
+
+// ---------------------------------------------------------------- Morton-order seeds (F = 3)
+// The first DGCNN graph is built on coordinates and has no previous graph to seed it.  Points
+// adjacent on a Z-order curve are mostly near in space, so each point's seeds are the ks points
+// around it in its cloud's Morton order: their k-th best distance bounds the row's threshold from
+// the start (pcs_knn_seeded; the lists do not change -- any seeds are safe).  One 1024-thread
+// workgroup per cloud: bounding box, 10-bit-per-axis Morton keys, an LDS bitonic sort of
+// (key, index), then a window of ks consecutive sorted points per point.
+namespace pcs {
+
+constexpr int kMortonMax = 8192;
+
+__device__ __forceinline__ unsigned spread3(unsigned v) {      // 10 bits -> every third bit
+    v &= 0x3FFu;
+    v = (v | (v << 16)) & 0x030000FFu;
+    v = (v | (v << 8)) & 0x0300F00Fu;
+    v = (v | (v << 4)) & 0x030C30C3u;
+    v = (v | (v << 2)) & 0x09249249u;
+    return v;
+}
+
+__global__ __launch_bounds__(1024) void morton_seeds_kernel(const float* __restrict__ x, int N, int ks,
+                                                            int* __restrict__ seeds) {
+    __shared__ unsigned s_key[kMortonMax];
+    __shared__ unsigned short s_idx[kMortonMax];
+    __shared__ float s_red[2][3][16];
+    const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const float* X = x + (size_t)b * N * 3;
+    float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int i = t; i < N; i += 1024)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const float v = X[3 * i + c];
+            mn[c] = fminf(mn[c], v);
+            mx[c] = fmaxf(mx[c], v);
+        }
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        for (int d = 32; d >= 1; d >>= 1) {
+            mn[c] = fminf(mn[c], __shfl_xor(mn[c], d));
+            mx[c] = fmaxf(mx[c], __shfl_xor(mx[c], d));
+        }
+        if (lane == 0) { s_red[0][c][w] = mn[c]; s_red[1][c][w] = mx[c]; }
+    }
+    __syncthreads();
+    float lo[3], sc[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        float a = INFINITY, z = -INFINITY;
+        for (int k = 0; k < 16; ++k) { a = fminf(a, s_red[0][c][k]); z = fmaxf(z, s_red[1][c][k]); }
+        lo[c] = a;
+        sc[c] = z > a ? 1023.f / (z - a) : 0.f;       // non-finite coordinates: keys still in range
+    }
+    int P = 1;
+    while (P < N) P <<= 1;
+    for (int i = t; i < P; i += 1024) {
+        unsigned key = 0xFFFFFFFFu;                    // padding sorts last
+        if (i < N) {
+            unsigned q[3];
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                const float f = (X[3 * i + c] - lo[c]) * sc[c];
+                q[c] = f >= 1023.f ? 1023u : (f > 0.f ? (unsigned)f : 0u);      // NaN -> 0
+            }
+            key = spread3(q[0]) | (spread3(q[1]) << 1) | (spread3(q[2]) << 2);
+        }
+        s_key[i] = key;
+        s_idx[i] = (unsigned short)(i < N ? i : 0);
+    }
+    __syncthreads();
+    for (int k = 2; k <= P; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = t; i < P / 2; i += 1024) {
+                const int a = 2 * i - (i & (j - 1)), c = a + j;
+                const unsigned ka = s_key[a], kc = s_key[c];
+                if ((ka > kc) == ((a & k) == 0)) {
+                    s_key[a] = kc; s_key[c] = ka;
+                    const unsigned short ia = s_idx[a];
+                    s_idx[a] = s_idx[c]; s_idx[c] = ia;
+                }
+            }
+            __syncthreads();
+        }
+    for (int p = t; p < N; p += 1024) {
+        const int st = min(max(p - ks / 2, 0), N - ks);
+        int* o = seeds + ((size_t)b * N + s_idx[p]) * ks;
+        for (int j = 0; j < ks; ++j) o[j] = s_idx[st + j];
+    }
+}
+
+}  // namespace pcs
+
+// seeds (B, N, ks) int32: for each point, the ks points around it in its cloud's Morton order
+// (distinct, in range; the point itself included).  N <= 8192, ks <= N.  Feeds pcs_knn_seeded
+// for DGCNN's coordinate graph (dgcnn.py:7-21 on xyz): same lists, fewer survivors.
+PCS_API int pcs_knn_morton_seeds(const float* xyz, int B, int N, int ks, int32_t* seeds, void* stream) {
+    using namespace pcs;
+    PCS_CHECK_ARG(B >= 0 && N >= 1 && N <= kMortonMax && ks >= 1 && ks <= N,
+                  "pcs_knn_morton_seeds: bad sizes B=%d N=%d ks=%d (N <= %d)", B, N, ks, kMortonMax);
+    PCS_CHECK_ARG(xyz && seeds, "pcs_knn_morton_seeds: null pointer");
+    if (B == 0) return 0;
+    hipLaunchKernelGGL(morton_seeds_kernel, dim3(B), dim3(1024), 0, as_stream(stream), xyz, N, ks, seeds);
+    return launch_status("pcs_knn_morton_seeds");
 }

@@ -62,6 +62,12 @@ int pcs_knn(const float* x, int B, int N, int F, int k, int32_t* out_idx,
 int pcs_knn_workspace(int B, int N, size_t* bytes);
 int pcs_knn_ws(const float* x, int B, int N, int F, int k, int32_t* out_idx,
                void* ws, size_t ws_bytes, void* stream);
+/* Seeds for pcs_knn_seeded on coordinates (F = 3, DGCNN's first graph, which has no previous
+ * graph): for each point the ks points around it in its cloud's Morton (Z-order) order,
+ * distinct and in range.  xyz (B, N, 3) fp32, seeds (B, N, ks) int32; N <= 8192, ks <= N.
+ * Reference: dgcnn.py:7-21 (knn on xyz) -- the lists do not depend on the seeds. */
+int pcs_knn_morton_seeds(const float* xyz, int B, int N, int ks, int32_t* seeds, void* stream);
+
 /* pcs_knn_ws whose rows start from the threshold of a previous neighbour list
  * (seeds (B,N,ks) int32: DGCNN's previous EdgeConv graph, dgcnn.py:183-189 feeding
  * get_graph_feature at :29-56): the same lists as pcs_knn, fewer survivors to merge.

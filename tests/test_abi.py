@@ -122,10 +122,11 @@ def test_engine_abi_argument_checks_without_gpu():
     lib = _lib.load()
     fake = 0x1000                       # never dereferenced: every call below fails its checks first
     op = _lib.Operand(fake, 12, _lib.OP_PLAIN, None, None, 0, 0.0, None, 0, None, None, None, None, None, 0)
-    # weight rows must hold K values (unpadded rows are fine on the LDS engine; k-major W must be 16-B aligned)
+    # weight rows must hold K values, k-major rows N values (unpadded / unaligned rows are fine:
+    # the loaders switch to scalar loads)
     assert lib.pcs_gemm_rows(op, 8, 9, fake, 8, None, fake, 32, 32, None, None, None, None) != 0
     assert b'ldw' in lib.pcs_last_error()
-    assert lib.pcs_gemm_rows_kmajor(op, 8, 9, fake, 33, fake, 32, 32, None, None, None) != 0
+    assert lib.pcs_gemm_rows_kmajor(op, 8, 9, fake, 31, fake, 32, 32, None, None, None) != 0
     assert b'ldw' in lib.pcs_last_error()
     # transform modes need K % 4 == 0 and their coefficient vectors
     bad = _lib.Operand(fake, 12, _lib.OP_BNACT, None, None, 0, 0.0, None, 0, None, None, None, None, None, 0)
