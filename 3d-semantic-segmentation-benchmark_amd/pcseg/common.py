@@ -423,10 +423,12 @@ class UnitPointNet(nn.Module):
             prev = m
         self.bwd_fuse = 0           # backward kernel choice (pcseg.engine.set_bwd_fuse)
 
-    def forward_rows(self, x: torch.Tensor, kin: int | None = None, dropout: tuple | None = None) -> torch.Tensor:
-        """dropout = (p, seed): a training-mode Dropout after the stack, fused into its output."""
+    def forward_rows(self, x: torch.Tensor, kin: int | None = None, dropout: tuple | None = None,
+                     dx_from: int = 0) -> torch.Tensor:
+        """dropout = (p, seed): a training-mode Dropout after the stack, fused into its output.
+        dx_from: the first input column whose gradient is wanted (pcs_mlp_layer.dx_col0)."""
         return shared_mlp(x, kin or x.shape[1], self.conv, self.batch, 'relu', 0.0, 0, dropout=dropout,
-                          bwd_fuse=self.bwd_fuse, cache=module_cache(self))
+                          bwd_fuse=self.bwd_fuse, cache=module_cache(self), dx_from=dx_from)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         B, Cin, N = x.shape
@@ -490,7 +492,10 @@ class FeaturePropagation(nn.Module):
             idx, dist = geo[0], geo[1]
             inv = geo[2] if len(geo) > 2 else None
         rows = ops.interp_cat_rows(features_1, features_2, idx, dist, inv)
-        return self.point_net.forward_rows(rows, dropout=dropout).view(B, N, -1)
+        # rows = [skip features_1 | interpolated]: a skip that takes no gradient (FP1's raw input
+        # features) needs no data-gradient columns
+        dx_from = features_1.shape[2] if features_1 is not None and not features_1.requires_grad else 0
+        return self.point_net.forward_rows(rows, dropout=dropout, dx_from=dx_from).view(B, N, -1)
 
 
 class InvResMLP(nn.Module):
