@@ -136,7 +136,6 @@ __global__ __launch_bounds__(BLOCK) void fps_kernel(const float* __restrict__ xy
     constexpr int NW = BLOCK / kWave;
     static_assert(NW == 1 || NW == 4 || NW == 8 || NW == 16, "slot reduction width");
     __shared__ __attribute__((aligned(16))) uint2 s_slot[2][NW];   // (mw + 1, idx<<1 | flag); 0 = empty wave
-    __shared__ __attribute__((aligned(16))) float4 s_sc[2][LDSC ? NW : 1];   // the slot's candidate's coordinates
     __shared__ __attribute__((aligned(16))) uint2 s_key[NW];       // slow path: (sqrt bits + 1, index)
     // Per-step global stores would make every __syncthreads wait for them (the
     // barrier's fence drains vmcnt): keep the picked centroids in LDS instead.
@@ -241,51 +240,21 @@ __global__ __launch_bounds__(BLOCK) void fps_kernel(const float* __restrict__ xy
         }
         // no candidate: 0xFFFFFFFE / 0xFFFFFFFF, above every real key
         const unsigned key = (ci << 1) | (cv != mw ? 1u : 0u);
-        // each lane fetches its own candidate's coordinates now: the LDS reads overlap the wave-min
-        // chain, and the winner's ride along in the slot -- no dependent LDS read after the barrier
-        float qx = 0.f, qy = 0.f, qz = 0.f;
-        if constexpr (LDSC) {
-            const unsigned cq = min(ci, (unsigned)(N - 1));
-            qx = s_px[cq];
-            qy = s_py[cq];
-            qz = s_pz[cq];
-        }
         FPS_STAMP(3);
         const unsigned wkey = wave_umin(key);
         FPS_STAMP(4);
         const int buf = i & 1;
-        if constexpr (LDSC) {
-            const unsigned long long mk = ballot(key == wkey);      // one lane (indices are unique)
-            const int wl = mk ? ffs64(mk) : 0;
-            const float wx = readlane_f(qx, wl), wy = readlane_f(qy, wl), wz = readlane_f(qz, wl);
-            if (lane == 0) {
-                s_slot[buf][w] = make_uint2(wk, wkey);
-                s_sc[buf][w] = make_float4(wx, wy, wz, 0.f);
-            }
-        } else if (lane == 0) {
-            s_slot[buf][w] = make_uint2(wk, wkey);
-        }
+        if (lane == 0) s_slot[buf][w] = make_uint2(wk, wkey);
         FPS_STAMP(5);
         __syncthreads();
         FPS_STAMP(6);
         const uint2 sl = lane < NW ? s_slot[buf][lane] : make_uint2(0u, 0xFFFFFFFFu);
-        float4 sc = make_float4(0.f, 0.f, 0.f, 0.f);
-        if constexpr (LDSC) sc = s_sc[buf][lane < NW ? lane : 0];
-        bool have = false;
         const unsigned Ms = NW == 1 ? readlane_u(sl.x, 0) : slot_umax<NW>(sl.x);
         const unsigned slo = Ms > kFpsWin + 1u ? Ms - kFpsWin : 1u;
         const bool near = sl.x >= slo && (sl.x != Ms || (sl.y & 1u));
         const unsigned fk = NW == 1 ? readlane_u(sl.y, 0) : slot_umin<NW>(sl.x == Ms ? sl.y : 0xFFFFFFFFu);
         if (__builtin_expect(ballot(near) == 0ull, 1)) {
             far = (int)(fk >> 1);
-            if constexpr (LDSC) {
-                const unsigned long long mk = ballot(lane < NW && sl.x == Ms && sl.y == fk);
-                const int sl_l = mk ? ffs64(mk) : 0;
-                cx = readlane_f(sc.x, sl_l);
-                cy = readlane_f(sc.y, sl_l);
-                cz = readlane_f(sc.z, sl_l);
-                have = true;
-            }
         } else {
             // exact keys: the wave's max sqrt S and the lowest index whose value has that sqrt
             unsigned kx = 0u, ky = 0xFFFFFFFFu;
@@ -304,16 +273,14 @@ __global__ __launch_bounds__(BLOCK) void fps_kernel(const float* __restrict__ xy
             const unsigned bs = NW == 1 ? readlane_u(k2.x, 0) : slot_umax<NW>(k2.x);
             far = (int)(NW == 1 ? readlane_u(k2.y, 0) : slot_umin<NW>(k2.x == bs ? k2.y : 0xFFFFFFFFu));
         }
-        if (!have) {
-            if constexpr (LDSC) {
-                cx = s_px[far];
-                cy = s_py[far];
-                cz = s_pz[far];
-            } else {
-                cx = P[3 * far + 0];
-                cy = P[3 * far + 1];
-                cz = P[3 * far + 2];
-            }
+        if constexpr (LDSC) {
+            cx = s_px[far];
+            cy = s_py[far];
+            cz = s_pz[far];
+        } else {
+            cx = P[3 * far + 0];
+            cy = P[3 * far + 1];
+            cz = P[3 * far + 2];
         }
 #ifdef PCS_FPS_STAMPS
         asm volatile("" ::"v"(cx), "v"(cy), "v"(cz));

@@ -492,10 +492,7 @@ class FeaturePropagation(nn.Module):
             idx, dist = geo[0], geo[1]
             inv = geo[2] if len(geo) > 2 else None
         rows = ops.interp_cat_rows(features_1, features_2, idx, dist, inv)
-        # rows = [skip features_1 | interpolated]: a skip that takes no gradient (FP1's raw input
-        # features) needs no data-gradient columns
-        dx_from = features_1.shape[2] if features_1 is not None and not features_1.requires_grad else 0
-        return self.point_net.forward_rows(rows, dropout=dropout, dx_from=dx_from).view(B, N, -1)
+        return self.point_net.forward_rows(rows, dropout=dropout).view(B, N, -1)
 
 
 class InvResMLP(nn.Module):

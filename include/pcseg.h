@@ -289,10 +289,9 @@ typedef struct pcs_mlp_layer {
     int64_t dx_col0;      /* first layer, backward: the first input column whose data gradient
                            * the caller needs -- the grouped rows of a SetAbstraction start with
                            * 3 relative-coordinate columns whose gradient nobody reads
-                           * (common.py:64-65 gathers only features back), and FP1's rows start
-                           * with the raw input features (common.py:236-238, no gradient); dX
-                           * columns outside [dx_col0, kin) are then left unwritten and the
-                           * data-gradient GEMM covers kin - dx_col0 columns (0 = all) */
+                           * (common.py:64-65 gathers only features back); dX columns
+                           * [0, dx_col0) are then left unwritten and the data-gradient GEMM
+                           * covers kin - dx_col0 columns (0 = all) */
 } pcs_mlp_layer;
 
 #define PCS_BWD_FUSE_DEFAULT 0
