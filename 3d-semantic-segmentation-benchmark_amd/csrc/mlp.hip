@@ -1194,7 +1194,7 @@ int pcs::gemm_rows_ex(const pcs_operand* a, int M, int K, const float* W, int ld
         int probe = -1;
         if (probe_enabled()) {
             char nm[96];
-            const bool b256 = (((N + 127) / 128) * 128 - N) >= (((N + 255) / 256) * 256 - N);
+            const bool b256 = gemm_nt_bn(N) == 256;
             snprintf(nm, sizeof nm, "pcs::gemm_nt_kernel<%d, %d, %d, %s>", b256 ? 256 : 128, b256 ? 2 : 4,
                      b256 ? 4 : 2, stats ? "true" : "false");
             const pcs_operand ac = *a;

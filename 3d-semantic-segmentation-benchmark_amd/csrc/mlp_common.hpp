@@ -148,6 +148,7 @@ int gemm_rows_ex(const pcs_operand* a, int M, int K, const float* W, int ldw, in
 // wide-layer GEMM on plain operands (gemm_big.hip): C = A . B^T, A (M x R), B (N x R) row-major
 bool gemm_nt_regime(int M, int N);                 // (M, N) the wide path is built for
 int gemm_nt_row_tiles(int M);                      // its BN-partial row blocks
+int gemm_nt_bn(int N);                             // its column tile (128 or 256)
 bool gemm_nt_ok(const float* A, int lda, const float* B, int ldb, int M, int N, int R);
 int gemm_nt(const float* A, int lda, const float* B, int ldb, int M, int N, int R, const float* bias, float* C, int ldc,
             double* stats, hipStream_t st);
