@@ -27,6 +27,7 @@ Also reported on the same JSON line, per workload:
 from __future__ import annotations
 
 import argparse
+import contextlib
 import json
 import os
 import socket
@@ -320,6 +321,14 @@ def run_workload(key, batch, npoints, args, world, rank, dev):
 
         def step():
             return cs.step()
+    prio = contextlib.ExitStack()
+    if args.stream_priority == 'high':
+        # the step (its critical path) on a high-priority stream; the geometry side stream and the
+        # wgrad lane keep the default (lowest) priority, so the hardware queue scheduler hands
+        # free CUs to the critical path first
+        hs = torch.cuda.Stream(device=dev, priority=torch.cuda.Stream.priority_range()[1])
+        hs.wait_stream(torch.cuda.current_stream(dev))
+        prio.enter_context(torch.cuda.stream(hs))
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
@@ -342,13 +351,16 @@ def run_workload(key, batch, npoints, args, world, rank, dev):
     roof = None
     if not args.no_roofline:
         roof = kernel_roofline(eager_step, dev, key, batch, npoints, replay=args.roofline_replay)
+    prio.close()
+    torch.cuda.synchronize(dev)
     ms = dt / args.steps * 1e3
     res = {'value': round(world * batch * npoints * args.steps / dt, 1), 'unit': 'points/s',
            'ms_per_step': round(ms, 3),
            'config': {'workload': f'{name} seg, {npoints} pts, batch {batch}/GPU, fwd+CE+bwd'
                                   f'{"+allreduce" if world > 1 else ""}+Adam',
                       'baseline_config': cfg, 'model': name, 'global_batch': world * batch, 'npoints': npoints,
-                      'parallelism': f'dp{world}', 'geometry_prefetch': prefetch, 'hip_graph': use_graph},
+                      'parallelism': f'dp{world}', 'geometry_prefetch': prefetch, 'hip_graph': use_graph,
+                      'stream_priority': args.stream_priority},
            'host_enqueue_ms_per_step': round(t_host / args.steps * 1e3, 3),
            'roofline': roof, 'step_roofline': step_roofline(key, npoints, batch, ms, roof)}
     del model, grads, opt
@@ -405,6 +417,8 @@ def main():
                     help='do not enqueue the next step\'s FPS/ball-query/3-NN before this step\'s backward')
     ap.add_argument('--graph-geometry', choices=['graph', 'eager'], default='graph',
                     help="--graph: capture the next step's neighbour search too, or enqueue it eagerly per step")
+    ap.add_argument('--stream-priority', choices=['default', 'high'], default='default',
+                    help='run the step on a high-priority stream (side streams keep the lowest priority)')
     ap.add_argument('--edge-inverse', choices=['side', 'backward', 'deferred'], default='deferred',
                     help='DGCNN: where the EdgeConv backward\'s inverse kNN maps are built: on the side stream '
                          'after the last EdgeConv (deferred, default), right after each EdgeConv (side), or in '
