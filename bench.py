@@ -417,8 +417,9 @@ def main():
                     help='do not enqueue the next step\'s FPS/ball-query/3-NN before this step\'s backward')
     ap.add_argument('--graph-geometry', choices=['graph', 'eager'], default='graph',
                     help="--graph: capture the next step's neighbour search too, or enqueue it eagerly per step")
-    ap.add_argument('--stream-priority', choices=['default', 'high'], default='default',
-                    help='run the step on a high-priority stream (side streams keep the lowest priority)')
+    ap.add_argument('--stream-priority', choices=['default', 'high'], default='high',
+                    help='run the step on a high-priority stream (default; pcseg\'s side streams -- the next '
+                         'step\'s geometry, the wgrad lane -- keep the lowest priority) or on the default stream')
     ap.add_argument('--edge-inverse', choices=['side', 'backward', 'deferred'], default='deferred',
                     help='DGCNN: where the EdgeConv backward\'s inverse kNN maps are built: on the side stream '
                          'after the last EdgeConv (deferred, default), right after each EdgeConv (side), or in '
