@@ -223,7 +223,13 @@ static WgradLane* wgrad_lane() {
     std::lock_guard<std::mutex> g(mu);
     WgradLane& L = lanes[dev];
     if (!L.side) {
+#ifdef PCS_LANE_HIGH
+        int lo_p = 0, hi_p = 0;     // A/B builds: the lane at the greatest priority
+        (void)hipDeviceGetStreamPriorityRange(&lo_p, &hi_p);
+        if (hipStreamCreateWithPriority(&L.side, hipStreamNonBlocking, hi_p) != hipSuccess) { L.side = nullptr; return nullptr; }
+#else
         if (hipStreamCreateWithFlags(&L.side, hipStreamNonBlocking) != hipSuccess) { L.side = nullptr; return nullptr; }
+#endif
         for (auto& e : L.ev)
             if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
     }
