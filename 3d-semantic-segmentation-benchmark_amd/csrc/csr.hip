@@ -8,7 +8,10 @@
 // list of gather slots that read it (CSR: offsets + entries).  The backward then
 // gathers: one thread per (source point, channel) sums its slots' gradients.
 //
-// Build: one workgroup per cloud, one launch per map.  Every slot of cloud b
+// Build (clouds of <= 8192 targets): a chunked stable counting sort over many workgroups,
+// lists ascending by construction (inverse_count / inverse_scan / inverse_rank below).
+// Larger clouds (PointNeXt's first ball query, 24 576 targets): one workgroup per cloud,
+// one launch per map.  Every slot of cloud b
 // reads a point of cloud b, so cloud b's entries are exactly positions
 // [b*per_batch, (b+1)*per_batch) and the clouds are independent: LDS histogram of
 // the cloud's targets -> in-LDS exclusive scan -> LDS-atomic scatter of the slots
@@ -164,6 +167,137 @@ __global__ __launch_bounds__(256) void inverse_sort_kernel(const int32_t* __rest
             rank += lo - r0;
         }
         entries[a + rank] = x;
+    }
+}
+
+// ---------------------------------------------------------------- chunked stable counting sort
+// The map of clouds with <= 8192 targets (every PointNet++ / DGCNN map and all but PointNeXt's
+// first ball query) is a stable counting sort of the slots by target, spread over many
+// workgroups and free of atomics on the ordering path, so every list comes out ascending with
+// no sort pass:
+//   1. inverse_count_kernel  (chunk c, cloud b): LDS histogram of chunk c's targets -> hist[b][c][t]
+//   2. inverse_scan_kernel   (cloud b): offsets[b][t] = b*per + sum over earlier targets of their
+//      totals; hist[b][c][t] := offsets[b][t] + the count of t in chunks < c (the chunk's base)
+//   3. inverse_rank_kernel   (chunk c, cloud b): each wave owns a contiguous quarter (half) of the
+//      chunk; per-wave LDS counts -> per-wave bases (the chunk base + the counts of the earlier
+//      waves); then each wave walks its slots in order, 64 at a time: the lanes reading the same
+//      target are found by a ballot over the target's bits (a match), a slot's position is its
+//      wave base + the number of matching lanes below it, and the group's last lane advances the
+//      base.  Slot order = list order: ascending, deterministic.
+// Chunks hold >= max(4096, targets) slots, so the hist workspace (B * chunks * targets ints) fits
+// in the B*per + B*targets ints the workspace already provides.
+constexpr int kChunkMin = 4096, kRankMaxTargets = 8192;
+
+static int rank_chunk(int targets) { return std::max(kChunkMin, (targets + 255) / 256 * 256); }
+
+__global__ __launch_bounds__(256) void inverse_count_kernel(const int32_t* __restrict__ idx, int per, int targets,
+                                                            int chunk, int nch, int* __restrict__ hist) {
+    extern __shared__ int cnt[];
+    const int c = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+    for (int t = tid; t < targets; t += 256) cnt[t] = 0;
+    __syncthreads();
+    const int32_t* id = idx + (size_t)b * per;
+    const int s1 = min(per, (c + 1) * chunk);
+    for (int s = c * chunk + tid; s < s1; s += 256) {
+        const unsigned t = (unsigned)id[s];
+        if (t < (unsigned)targets) atomicAdd(&cnt[t], 1);     // counts: order-free
+    }
+    __syncthreads();
+    int* h = hist + ((size_t)b * nch + c) * targets;
+    for (int t = tid; t < targets; t += 256) h[t] = cnt[t];
+}
+
+__global__ __launch_bounds__(1024) void inverse_scan_kernel(int* __restrict__ hist, int per, int targets, int nch,
+                                                            int nbatch, int32_t* __restrict__ offsets) {
+    __shared__ int wsum[kInvThreads / 64 + 1];
+    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    int* h = hist + (size_t)b * nch * targets;
+    const int pt = (targets + kInvThreads - 1) / kInvThreads;    // consecutive targets per thread
+    const int a = min(tid * pt, targets), z = min(a + pt, targets);
+    int local = 0;
+    for (int c = 0; c < nch; ++c)
+        for (int t = a; t < z; ++t) local += h[(size_t)c * targets + t];
+    int incl = local;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int v = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += v;
+    }
+    if (lane == 63) wsum[wv] = incl;
+    __syncthreads();
+    if (tid < 64) {
+        const int w = tid < kInvThreads / 64 ? wsum[tid] : 0;
+        int wi = w;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int v = __shfl_up(wi, d, 64);
+            if (tid >= d) wi += v;
+        }
+        if (tid < kInvThreads / 64) wsum[tid] = wi - w;
+    }
+    __syncthreads();
+    const int base = b * per;
+    int run = base + wsum[wv] + incl - local;
+    for (int t = a; t < z; ++t) {
+        offsets[(size_t)b * targets + t] = run;
+        for (int c = 0; c < nch; ++c) {
+            int* p = h + (size_t)c * targets + t;
+            const int v = *p;
+            *p = run;
+            run += v;
+        }
+    }
+    if (b == nbatch - 1 && tid == 0) offsets[(size_t)nbatch * targets] = nbatch * per;
+}
+
+template <int W>
+__global__ __launch_bounds__(W * 64) void inverse_rank_kernel(const int32_t* __restrict__ idx, int per, int targets,
+                                                              int chunk, int nch, int nbits,
+                                                              const int* __restrict__ hist,
+                                                              int32_t* __restrict__ entries) {
+    extern __shared__ int wb[];                         // [W][targets]: per-wave counts, then bases
+    const int c = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    for (int t = tid; t < W * targets; t += W * 64) wb[t] = 0;
+    __syncthreads();
+    const int32_t* id = idx + (size_t)b * per;
+    const int sub = chunk / W;                          // chunk is a multiple of 256
+    const int ws = min(per, c * chunk + wave * sub), we = min(per, c * chunk + (wave + 1) * sub);
+    int* mb = wb + wave * targets;
+    for (int s = ws + lane; s < we; s += 64) {
+        const unsigned t = (unsigned)id[s];
+        if (t < (unsigned)targets) atomicAdd(&mb[t], 1);
+    }
+    __syncthreads();
+    const int* h = hist + ((size_t)b * nch + c) * targets;
+    for (int t = tid; t < targets; t += W * 64) {
+        int run = h[t];
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+            const int v = wb[w * targets + t];
+            wb[w * targets + t] = run;
+            run += v;
+        }
+    }
+    __syncthreads();
+    const int gbase = b * per;
+    const unsigned long long lt = lanemask_lt();
+    for (int g = ws; g < we; g += 64) {
+        const int s = g + lane;
+        const int t = s < we ? id[s] : -1;
+        const bool ok = (unsigned)t < (unsigned)targets;
+        unsigned long long peers = ballot(ok);
+        for (int bit = 0; bit < nbits; ++bit) {
+            const bool on = (t >> bit) & 1;
+            const unsigned long long m = ballot(on);
+            peers &= on ? m : ~m;
+        }
+        const int rank = popc64(peers & lt), cnt = popc64(peers);
+        if (ok) {
+            const int p = mb[t];
+            entries[p + rank] = gbase + s;
+            if (rank == cnt - 1) mb[t] = p + cnt;      // the group's last lane advances the base
+        }
     }
 }
 
@@ -387,6 +521,26 @@ PCS_API int pcs_inverse_index(const int32_t* idx, int B, int per_batch, int targ
                   ws_bytes, inv_ws_bytes(n, T));
     hipStream_t s = as_stream(stream);
     int32_t* scratch = static_cast<int32_t*>(workspace);
+    if (targets <= kRankMaxTargets) {
+        // chunked stable counting sort (above): idx read twice, entries + offsets written
+        ProbeScope pr(s, 0.0, 12.0 * (double)n + 4.0 * (double)(T + 1), "pcs::inverse_index<rank>");
+        const int chunk = rank_chunk(targets), nch = (per_batch + chunk - 1) / chunk;
+        int* hist = reinterpret_cast<int*>(workspace);   // B * nch * targets <= n + T ints (chunk >= targets)
+        PCS_CHECK_ARG((size_t)B * nch * targets * 4 <= ws_bytes, "pcs_inverse_index: chunk histogram overflows");
+        int nbits = 0;
+        while ((1 << nbits) < targets) ++nbits;
+        hipLaunchKernelGGL(inverse_count_kernel, dim3(nch, B), dim3(256), targets * sizeof(int), s, idx, per_batch,
+                           targets, chunk, nch, hist);
+        hipLaunchKernelGGL(inverse_scan_kernel, dim3(B), dim3(kInvThreads), 0, s, hist, per_batch, targets, nch, B,
+                           offsets);
+        if (targets <= 4096)
+            hipLaunchKernelGGL(inverse_rank_kernel<4>, dim3(nch, B), dim3(256), 4 * targets * sizeof(int), s, idx,
+                               per_batch, targets, chunk, nch, nbits, hist, entries);
+        else
+            hipLaunchKernelGGL(inverse_rank_kernel<2>, dim3(nch, B), dim3(128), 2 * targets * sizeof(int), s, idx,
+                               per_batch, targets, chunk, nch, nbits, hist, entries);
+        return launch_status("pcs_inverse_index");
+    }
     // algorithmic bytes of the map (both kernels): idx read, entries + offsets written
     ProbeScope pr(s, 0.0, 8.0 * (double)n + 4.0 * (double)(T + 1),
                   targets <= kInvLdsTargets ? "pcs::inverse_index+sort<true>" : "pcs::inverse_index+sort<false>");

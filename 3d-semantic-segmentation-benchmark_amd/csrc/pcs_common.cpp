@@ -32,3 +32,5 @@ PCS_API const char* pcs_last_error(void) { return g_err; }
 PCS_API int pcs_abi_version(void) { return 2; }
 
 PCS_API int pcs_operand_size(void) { return (int)sizeof(pcs_operand); }
+
+PCS_API int pcs_mlp_layer_size(void) { return (int)sizeof(pcs_mlp_layer); }

@@ -84,6 +84,7 @@ SIGNATURES = {
     'pcs_wgrad_lane': [P],
     'pcs_wgrad_lane_join': [P],
     'pcs_operand_size': [],
+    'pcs_mlp_layer_size': [],
     'pcs_gemm_rows': [OPP, I32, I32, P, I32, P, P, I32, I32, P, OPP, P, P],
     'pcs_gemm_rows_kmajor': [OPP, I32, I32, P, I32, P, I32, I32, OPP, P, P],
     'pcs_gemm_nt': [P, I32, P, I32, I32, I32, I32, P, P, I32, P, P],

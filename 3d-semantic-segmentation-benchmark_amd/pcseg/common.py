@@ -187,8 +187,8 @@ class GeometryPlan:
                 self.nn_event = torch.cuda.Event()
                 self.nn_event.record(side)
         if not torch.cuda.is_current_stream_capturing():
-            # eager: tell the caching allocator about the cross-stream uses (under graph
-            # capture the graph's private pool keeps every block alive instead)
+            # eager: tell the caching allocator about the cross-stream uses (under graph capture
+            # the tensors are the `into` plan's, which outlives the graphs)
             coords.record_stream(side)
             for t in made:
                 t.record_stream(main)
@@ -230,7 +230,15 @@ class GeometryPlan:
             offs.append(o)
             o += (n + 63) // 64 * 64
         wso = o
-        buf = torch.empty(wso + (nws + 3) // 4 if into is None else (nws + 3) // 4, dtype=torch.int32, device=dev)
+        if into is None:
+            buf = torch.empty(wso + (nws + 3) // 4, dtype=torch.int32, device=dev)
+        else:
+            # the plan's native scratch (inverse-map counters) lives as long as the plan it writes
+            # into: under HIP-graph capture a block freed at the end of this call would be handed
+            # to the step's later main-stream allocations while the side branch still writes it
+            buf = into.__dict__.get('_pcs_scratch')
+            if buf is None or buf.numel() < (nws + 3) // 4:
+                buf = into._pcs_scratch = torch.empty((nws + 3) // 4, dtype=torch.int32, device=dev)
         parts = iter(zip(offs, sizes))
         evs = _event_set(dev, side, L)
 

@@ -167,7 +167,7 @@ def _f32(shape, dev):
     return torch.empty(shape, dtype=torch.float32, device=dev)
 
 
-# pcs_mlp_layer (include/pcseg.h): 24 little-endian 8-byte slots
+# pcs_mlp_layer (include/pcseg.h): 25 little-endian 8-byte slots (200 bytes)
 _REC = struct.Struct('<QqqqQQQQQQddqqdQQQQQQdqqq')  # ... dW db dgamma dbeta drop_p drop_seed bwd_fuse dx_col0
 _ws_cache: dict = {}
 
@@ -361,7 +361,11 @@ class SharedMLPFn(torch.autograd.Function):
         # e.g. a MiniPointNet's dict) while the parameters' storage and the BN modes are unchanged
         ent = None
         if cache is not None:
-            key = (Kin, acts, tuple(bn.training for bn in bns), tuple(_nz(p) for p in params))
+            # everything _layer_statics bakes into the records: parameter storage, the BN modes and
+            # hyper-parameters, and the running-statistics buffers (pcseg.ddp.FlatBuffers rebinds them)
+            key = (Kin, acts, tuple(_nz(p) for p in params),
+                   tuple((bn.training, bn.track_running_stats, bn.momentum, bn.eps, _nz(bn.running_mean),
+                          _nz(bn.running_var), _nz(bn.num_batches_tracked)) for bn in bns))
             ent = cache.get('static')
             if ent is not None and ent[0] != key:
                 ent = None

@@ -67,6 +67,7 @@ class CapturedStep:
         torch.cuda.synchronize(dev)
         for p in self.plans:
             p.settle()                       # complete: no cross-graph event waits
+        self.captured_lr = opt.lr
         pool = torch.cuda.graph_pool_handle()
         self.graphs, self.losses = [], []
         for k in range(2 if self.prefetch else 1):
@@ -111,6 +112,11 @@ class CapturedStep:
         return loss
 
     def step(self) -> torch.Tensor:
+        # the captured pcs_adam_dev launch holds the learning rate of capture time: a scheduler
+        # that changed opt.lr since would be silently ignored by the replay
+        if self.opt.lr != self.captured_lr:
+            raise RuntimeError(f'CapturedStep: opt.lr changed from {self.captured_lr} to {self.opt.lr} after '
+                               'capture (the replayed Adam step bakes it in); capture a new CapturedStep')
         k = self.k
         if not self.geo_eager:
             self.graphs[k].replay()

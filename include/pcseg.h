@@ -30,6 +30,8 @@ const char* pcs_last_error(void);
 int pcs_abi_version(void);
 /* sizeof(pcs_operand), for bindings to check their struct layout */
 int pcs_operand_size(void);
+/* sizeof(pcs_mlp_layer) (25 eight-byte slots = 200), likewise */
+int pcs_mlp_layer_size(void);
 
 /* ---- neighbour search ------------------------------------------------- */
 
@@ -71,8 +73,8 @@ int pcs_knn_morton_seeds(const float* xyz, int B, int N, int ks, int32_t* seeds,
 /* pcs_knn_ws whose rows start from the threshold of a previous neighbour list
  * (seeds (B,N,ks) int32: DGCNN's previous EdgeConv graph, dgcnn.py:183-189 feeding
  * get_graph_feature at :29-56): the same lists as pcs_knn, fewer survivors to merge.
- * Rows whose seeds are out of range, repeated or fewer than k search unseeded; F = 3
- * ignores the seeds. */
+ * Rows whose seeds are out of range, repeated or fewer than k search unseeded.  F = 3
+ * rows are seeded too (e.g. by pcs_knn_morton_seeds' spatial neighbours). */
 int pcs_knn_seeded(const float* x, int B, int N, int F, int k, const int32_t* seeds,
                    int ks, int32_t* out_idx, void* ws, size_t ws_bytes, void* stream);
 
