@@ -175,17 +175,19 @@ __global__ __launch_bounds__(256) void inverse_sort_kernel(const int32_t* __rest
 // first ball query) is a stable counting sort of the slots by target, spread over many
 // workgroups and free of atomics on the ordering path, so every list comes out ascending with
 // no sort pass:
-//   1. inverse_count_kernel  (chunk c, cloud b): LDS histogram of chunk c's targets -> hist[b][c][t]
-//   2. inverse_scan_kernel   (cloud b): offsets[b][t] = b*per + sum over earlier targets of their
-//      totals; hist[b][c][t] := offsets[b][t] + the count of t in chunks < c (the chunk's base)
-//   3. inverse_rank_kernel   (chunk c, cloud b): each wave owns a contiguous quarter (half) of the
-//      chunk; per-wave LDS counts -> per-wave bases (the chunk base + the counts of the earlier
-//      waves); then each wave walks its slots in order, 64 at a time: the lanes reading the same
-//      target are found by a ballot over the target's bits (a match), a slot's position is its
-//      wave base + the number of matching lanes below it, and the group's last lane advances the
-//      base.  Slot order = list order: ascending, deterministic.
-// Chunks hold >= max(4096, targets) slots, so the hist workspace (B * chunks * targets ints) fits
-// in the B*per + B*targets ints the workspace already provides.
+//   1. inverse_count_kernel (chunk c, cloud b; clouds of more than one chunk only): LDS
+//      histogram of chunk c's targets -> hist[b][c][t];
+//   2. inverse_rank_kernel (chunk c, cloud b): each wave owns a contiguous quarter (half) of the
+//      chunk and counts it per target in LDS; each thread then takes a run of targets, adds up
+//      their totals over the chunks (the LDS counts when the cloud is one chunk) and the counts
+//      of the chunks before c, and one block scan turns them into the targets' list offsets
+//      (written by chunk 0) and this chunk's per-wave list bases; finally each wave walks its
+//      slots in order, 64 at a time: the lanes reading the same target are found by a ballot
+//      over the target's bits (a match), a slot's position is its wave base + the number of
+//      matching lanes below it, and the group's last lane advances the base.
+// Slot order = list order: ascending, deterministic.  Chunks hold >= max(4096, targets) slots, so
+// the hist workspace (B * chunks * targets ints) fits in the B*per + B*targets ints the
+// workspace already provides.  One launch for a one-chunk cloud, two otherwise.
 constexpr int kChunkMin = 4096, kRankMaxTargets = 8192;
 
 static int rank_chunk(int targets) { return std::max(kChunkMin, (targets + 255) / 256 * 256); }
@@ -207,58 +209,18 @@ __global__ __launch_bounds__(256) void inverse_count_kernel(const int32_t* __res
     for (int t = tid; t < targets; t += 256) h[t] = cnt[t];
 }
 
-__global__ __launch_bounds__(1024) void inverse_scan_kernel(int* __restrict__ hist, int per, int targets, int nch,
-                                                            int nbatch, int32_t* __restrict__ offsets) {
-    __shared__ int wsum[kInvThreads / 64 + 1];
-    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    int* h = hist + (size_t)b * nch * targets;
-    const int pt = (targets + kInvThreads - 1) / kInvThreads;    // consecutive targets per thread
-    const int a = min(tid * pt, targets), z = min(a + pt, targets);
-    int local = 0;
-    for (int c = 0; c < nch; ++c)
-        for (int t = a; t < z; ++t) local += h[(size_t)c * targets + t];
-    int incl = local;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const int v = __shfl_up(incl, d, 64);
-        if (lane >= d) incl += v;
-    }
-    if (lane == 63) wsum[wv] = incl;
-    __syncthreads();
-    if (tid < 64) {
-        const int w = tid < kInvThreads / 64 ? wsum[tid] : 0;
-        int wi = w;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const int v = __shfl_up(wi, d, 64);
-            if (tid >= d) wi += v;
-        }
-        if (tid < kInvThreads / 64) wsum[tid] = wi - w;
-    }
-    __syncthreads();
-    const int base = b * per;
-    int run = base + wsum[wv] + incl - local;
-    for (int t = a; t < z; ++t) {
-        offsets[(size_t)b * targets + t] = run;
-        for (int c = 0; c < nch; ++c) {
-            int* p = h + (size_t)c * targets + t;
-            const int v = *p;
-            *p = run;
-            run += v;
-        }
-    }
-    if (b == nbatch - 1 && tid == 0) offsets[(size_t)nbatch * targets] = nbatch * per;
-}
-
 template <int W>
 __global__ __launch_bounds__(W * 64) void inverse_rank_kernel(const int32_t* __restrict__ idx, int per, int targets,
-                                                              int chunk, int nch, int nbits,
+                                                              int chunk, int nch, int nbatch, int nbits,
                                                               const int* __restrict__ hist,
+                                                              int32_t* __restrict__ offsets,
                                                               int32_t* __restrict__ entries) {
-    extern __shared__ int wb[];                         // [W][targets]: per-wave counts, then bases
+    constexpr int NT = W * 64;
+    extern __shared__ int wb[];                         // [W][targets]: per-wave counts, then bases; + [W]
+    int* wsum = wb + W * targets;
     const int c = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    for (int t = tid; t < W * targets; t += W * 64) wb[t] = 0;
+    for (int t = tid; t < W * targets; t += NT) wb[t] = 0;
     __syncthreads();
     const int32_t* id = idx + (size_t)b * per;
     const int sub = chunk / W;                          // chunk is a multiple of 256
@@ -269,16 +231,54 @@ __global__ __launch_bounds__(W * 64) void inverse_rank_kernel(const int32_t* __r
         if (t < (unsigned)targets) atomicAdd(&mb[t], 1);
     }
     __syncthreads();
-    const int* h = hist + ((size_t)b * nch + c) * targets;
-    for (int t = tid; t < targets; t += W * 64) {
-        int run = h[t];
+    // this thread's run of targets: totals over the cloud's chunks and the counts before chunk c
+    const int pt = (targets + NT - 1) / NT;
+    const int a = min(tid * pt, targets), z = min(a + pt, targets);
+    const int* hb = hist + (size_t)b * nch * targets;
+    auto totals = [&](int t, int& pre) {
+        int tot = 0;
+        pre = 0;
+        if (nch == 1) {
+#pragma unroll
+            for (int w = 0; w < W; ++w) tot += wb[w * targets + t];
+        } else {
+            for (int cc = 0; cc < nch; ++cc) {
+                const int v = hb[(size_t)cc * targets + t];
+                pre += cc < c ? v : 0;
+                tot += v;
+            }
+        }
+        return tot;
+    };
+    int local = 0;
+    for (int t = a; t < z; ++t) {
+        int pre;
+        local += totals(t, pre);
+    }
+    int incl = local;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int v = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += v;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    int run = b * per + incl - local;
+    for (int w = 0; w < wave; ++w) run += wsum[w];
+    for (int t = a; t < z; ++t) {
+        int pre;
+        const int tot = totals(t, pre);
+        if (c == 0) offsets[(size_t)b * targets + t] = run;
+        int base = run + pre;
 #pragma unroll
         for (int w = 0; w < W; ++w) {
             const int v = wb[w * targets + t];
-            wb[w * targets + t] = run;
-            run += v;
+            wb[w * targets + t] = base;
+            base += v;
         }
+        run += tot;
     }
+    if (b == nbatch - 1 && c == 0 && tid == 0) offsets[(size_t)nbatch * targets] = nbatch * per;
     __syncthreads();
     const int gbase = b * per;
     const unsigned long long lt = lanemask_lt();
@@ -529,16 +529,20 @@ PCS_API int pcs_inverse_index(const int32_t* idx, int B, int per_batch, int targ
         PCS_CHECK_ARG((size_t)B * nch * targets * 4 <= ws_bytes, "pcs_inverse_index: chunk histogram overflows");
         int nbits = 0;
         while ((1 << nbits) < targets) ++nbits;
-        hipLaunchKernelGGL(inverse_count_kernel, dim3(nch, B), dim3(256), targets * sizeof(int), s, idx, per_batch,
-                           targets, chunk, nch, hist);
-        hipLaunchKernelGGL(inverse_scan_kernel, dim3(B), dim3(kInvThreads), 0, s, hist, per_batch, targets, nch, B,
-                           offsets);
+        if (nch > 1)
+            hipLaunchKernelGGL(inverse_count_kernel, dim3(nch, B), dim3(256), targets * sizeof(int), s, idx, per_batch,
+                               targets, chunk, nch, hist);
         if (targets <= 4096)
-            hipLaunchKernelGGL(inverse_rank_kernel<4>, dim3(nch, B), dim3(256), 4 * targets * sizeof(int), s, idx,
-                               per_batch, targets, chunk, nch, nbits, hist, entries);
-        else
-            hipLaunchKernelGGL(inverse_rank_kernel<2>, dim3(nch, B), dim3(128), 2 * targets * sizeof(int), s, idx,
-                               per_batch, targets, chunk, nch, nbits, hist, entries);
+            hipLaunchKernelGGL(inverse_rank_kernel<4>, dim3(nch, B), dim3(256), (4 * targets + 4) * sizeof(int), s,
+                               idx, per_batch, targets, chunk, nch, B, nbits, hist, offsets, entries);
+        else {
+            static const hipError_t attr = hipFuncSetAttribute(
+                reinterpret_cast<const void*>(&inverse_rank_kernel<2>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                (2 * kRankMaxTargets + 2) * (int)sizeof(int));
+            (void)attr;
+            hipLaunchKernelGGL(inverse_rank_kernel<2>, dim3(nch, B), dim3(128), (2 * targets + 2) * sizeof(int), s,
+                               idx, per_batch, targets, chunk, nch, B, nbits, hist, offsets, entries);
+        }
         return launch_status("pcs_inverse_index");
     }
     // algorithmic bytes of the map (both kernels): idx read, entries + offsets written

@@ -223,13 +223,9 @@ static WgradLane* wgrad_lane() {
     std::lock_guard<std::mutex> g(mu);
     WgradLane& L = lanes[dev];
     if (!L.side) {
-#ifdef PCS_LANE_HIGH
-        int lo_p = 0, hi_p = 0;     // A/B builds: the lane at the greatest priority
-        (void)hipDeviceGetStreamPriorityRange(&lo_p, &hi_p);
-        if (hipStreamCreateWithPriority(&L.side, hipStreamNonBlocking, hi_p) != hipSuccess) { L.side = nullptr; return nullptr; }
-#else
+        // lowest priority: a high-priority caller stream keeps the critical path first
+        // (the lane at the caller's priority measured slower, profiles/r03_ab_s14_lane_priority.txt)
         if (hipStreamCreateWithFlags(&L.side, hipStreamNonBlocking) != hipSuccess) { L.side = nullptr; return nullptr; }
-#endif
         for (auto& e : L.ev)
             if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
     }
@@ -483,13 +479,9 @@ static int mlp_backward(const float* X, int ldx, int kin, int M, const pcs_mlp_l
         const bool bt = P.ldw % 4 == 0;
         const float* Bw = P.W;
         int ldb = (int)P.ldw;
-#ifndef PCS_DX_KMAJOR
-        const bool col0 = false;        // W^T rows from dx_col0 (one transpose launch; measured 2 %
-                                        // faster than the k-major scalar-load form, PCS_DX_KMAJOR)
-#else
-        const bool col0 = l == 0 && P.dx_col0 > 0 && P.dx_col0 < kin;   // k-major from column dx_col0
-#endif
-        if (!bt && !col0) {
+        // (a first layer's dX from column dx_col0 reads W^T's rows c0..: one transpose launch, measured
+        // equal to reading W k-major in place with scalar loads, profiles/r03_ab_ev3.txt)
+        if (!bt) {
             const dim3 g((Cin + 31) / 32, (C + 31) / 32);
             hipLaunchKernelGGL(transpose_kernel, g, dim3(256), 0, st, P.W, C, Cin, (int)P.ldw, S.wt);
             Bw = S.wt;
@@ -540,7 +532,6 @@ static int mlp_backward(const float* X, int ldx, int kin, int M, const pcs_mlp_l
                 if (int e = gemm_rows_ex(&xop, M, C, S.wt + (size_t)c0 * C, C, 0, nullptr, dX + c0, lddx, kin - c0,
                                          nullptr, nullptr, nullptr, stream))
                     return fail(e);
-#ifndef PCS_DX_KMAJOR
             } else if (c0 > 0 && (c0 * C) % 4 == 0) {
                 if (bt) {
                     const dim3 g((Cin + 31) / 32, (C + 31) / 32);
@@ -549,7 +540,6 @@ static int mlp_backward(const float* X, int ldx, int kin, int M, const pcs_mlp_l
                 if (int e = gemm_rows_ex(&xop, M, C, S.wt + (size_t)c0 * C, C, 0, nullptr, dX + c0, lddx, kin - c0,
                                          nullptr, nullptr, nullptr, stream))
                     return fail(e);
-#endif
             } else if (c0 > 0) {
                 // W read k-major in place from column c0 (scalar loads where its rows are unaligned)
                 if (int e = gemm_rows_ex(&xop, M, C, P.W + c0, (int)P.ldw, 1, nullptr, dX + c0, lddx, kin - c0,

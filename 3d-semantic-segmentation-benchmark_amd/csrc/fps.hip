@@ -87,7 +87,9 @@ constexpr unsigned kFpsWin = 16u;
 //     takes its local max;
 //  2. wave max mw (DPP chain), then the lowest index whose value lies in the window
 //     [mw - kFpsWin, mw] together with a flag "its value is not mw" -- one key (idx<<1 | flag),
-//     one wave-min chain; lane 0 publishes (mw + 1, key) in one 8-B LDS slot;
+//     one wave-min chain; lane 0 publishes (mw + 1, key) in one 8-B LDS slot (per-slot ballots
+//     with scalar selects instead measured 21 % slower, round 4: the CU's one scalar unit is
+//     shared by the 8 waves);
 //  3. after the barrier, lanes 0..NW-1 hold the slots: the block max M*, and the FAST PATH holds
 //     when every slot in M*'s window has exactly M* and a clear flag.  Then no point other than
 //     those with value M* lies in the window, all points of the reference's tie class (same
@@ -198,7 +200,6 @@ __global__ __launch_bounds__(BLOCK) void fps_kernel(const float* __restrict__ xy
         if (i == C - 1) break;
 
         unsigned M = 0u;
-#ifndef PCS_FPS_SCALAR
         if constexpr (PPT % 2 == 0) {
             // two points per packed op (v_pk_add/mul/fma_f32: per-component IEEE fp32, the
             // same roundings as the scalar chain) -- half the VALU issues of the distances
@@ -213,9 +214,7 @@ __global__ __launch_bounds__(BLOCK) void fps_kernel(const float* __restrict__ xy
                 best[j + 1] = min(__float_as_uint(d.y), best[j + 1]);
                 M = max(M, max(best[j], best[j + 1]));
             }
-        } else
-#endif
-        {
+        } else {
 #pragma unroll
             for (int j = 0; j < PPT; ++j) {
                 const float dx = px[j] - cx, dy = py[j] - cy, dz = pz[j] - cz;
@@ -326,14 +325,8 @@ PCS_API int pcs_fps(const float* xyz, int B, int N, int C, const int32_t* start,
     PCS_CHECK_ARG(xyz && start && out_idx && out_xyz, "pcs_fps: null pointer");
     if (B == 0) return 0;
     hipStream_t s = as_stream(stream);
-    // threads per cloud by size (round-1 sweep)
-#ifndef PCS_FPS_BLK2K
-#define PCS_FPS_BLK2K 256
-#endif
-#ifndef PCS_FPS_BLK8K
-#define PCS_FPS_BLK8K 512
-#endif
-    const int blk = N <= 256 ? 64 : (N <= 2048 ? PCS_FPS_BLK2K : (N <= 8192 ? PCS_FPS_BLK8K : 1024));
+    // threads per cloud by size (round-1 sweep; round 3: 256 threads at 4096 points measured equal)
+    const int blk = N <= 256 ? 64 : (N <= 2048 ? 256 : (N <= 8192 ? 512 : 1024));
     const int ppt = (N + blk - 1) / blk;
     // algorithmic: C serial steps over N points per cloud (8 fp32 flops per distance + update);
     // the cloud read once, C (index, xyz) written.  A latency-bound chain: see DESIGN.md 3.1

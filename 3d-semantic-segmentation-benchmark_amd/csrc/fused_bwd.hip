@@ -29,7 +29,6 @@
 namespace pcs {
 
 constexpr int FB_BM = 64;        // rows per tile
-constexpr int FB_BLOCKS_PER_CU = 2;
 
 struct FusedBwdArgs {
     Operand x;            // layer l's dZ operand: BNBWD / POOLBWD (rebuilt on load) or PLAIN, C wide
@@ -55,8 +54,11 @@ __device__ __forceinline__ int acc_row_of(int r, int h) { return (r & 3) + 8 * (
 // MFMA pipe fed through its LDS fragment reads.)
 // DA = false: weight gradient only (a stack's first layer, whose input needs no gradient):
 // the input is the plain raw rows (q.s == null: identity, no BN), kx <= CI columns.
-template <int C, int CI, int XM, bool DA>
-__global__ __launch_bounds__(256, 2) void fused_bwd_kernel(FusedBwdArgs f) {
+// WIDE: the wide layers (C + CI > 96) at ONE block per CU (one wave per SIMD, up to 512 VGPRs):
+// the next tile's raw loads are then held in registers under the current tile's MFMAs as on
+// the narrow layers, instead of being staged in chunks after the barrier.
+template <int C, int CI, int XM, bool DA, bool WIDE = false>
+__global__ __launch_bounds__(256, WIDE ? 1 : 2) void fused_bwd_kernel(FusedBwdArgs f) {
     constexpr int BM = FB_BM;
     constexpr int ZS = C + 2;                  // row stride = 2 (mod 64) banks: the dA fragment reads
                                                // (32 rows x 2 k) hit 64 distinct banks
@@ -67,7 +69,7 @@ __global__ __launch_bounds__(256, 2) void fused_bwd_kernel(FusedBwdArgs f) {
     constexpr int WR = TW >= 4 ? 1 : 4 / TW;   // waves splitting one dW tile's rows
     constexpr int NRT = NIT == 4 ? 2 : 1;      // dA row tiles per wave
     static_assert(C % 32 == 0 && CI % 32 == 0 && C <= 128 && CI <= 128, "fused backward widths");
-    __shared__ float Zs[BM * ZS];
+    __shared__ __attribute__((aligned(16))) float Zs[BM * ZS];
     __shared__ __attribute__((aligned(16))) float Xs[BM * XS];
     __shared__ double red[2][4][32];
     __shared__ float wred[WR > 1 ? (WR - 1) * TW * 1024 : 1];   // per (row subset, tile)
@@ -116,7 +118,7 @@ __global__ __launch_bounds__(256, 2) void fused_bwd_kernel(FusedBwdArgs f) {
     constexpr int IQ = CI / 4, RPI = 256 / IQ, NJX = BM / RPI;
     // PF: the narrow layers (SA1-sized, HBM-bound) hold the NEXT tile's raw loads in registers
     // while the current tile's MFMAs run; the wide ones stage in chunks after the barrier
-    constexpr bool PF = C + CI <= 96;
+    constexpr bool PF = C + CI <= 96 || WIDE;
     constexpr int CH = PF ? NJ : (NJ < 4 ? NJ : 4);      // rows in flight per chunk
     const int cq = tid % CQ, r0 = tid / CQ;
     const int iq = tid % IQ, s0 = tid / IQ;
@@ -130,6 +132,9 @@ __global__ __launch_bounds__(256, 2) void fused_bwd_kernel(FusedBwdArgs f) {
         for (int j = 0; j < CH; ++j)
             load_raw<XM>(f.x, min(m0 + r0 + (j0 + j) * RPP, M - 1), 4 * cq, pv[j], pz[j], pa[j]);
     };
+    // db: this thread's column-quad sums of dZ over the rows it stages (all tiles), added over the
+    // RPP threads of its quad at the end -- a fixed order, no per-tile LDS column walk
+    float4 dbv = make_float4(0.f, 0.f, 0.f, 0.f);
     auto commit_dz = [&](int m0, int j0) __attribute__((always_inline)) {
 #pragma unroll
         for (int j = 0; j < CH; ++j) {
@@ -138,6 +143,7 @@ __global__ __launch_bounds__(256, 2) void fused_bwd_kernel(FusedBwdArgs f) {
             if (m0 + r >= M) o = make_float4(0.f, 0.f, 0.f, 0.f);
             float* d = &Zs[r * ZS + 4 * cq];
             d[0] = o.x; d[1] = o.y; d[2] = o.z; d[3] = o.w;
+            dbv.x += o.x; dbv.y += o.y; dbv.z += o.z; dbv.w += o.w;
         }
     };
     auto issue_x = [&](int m0) __attribute__((always_inline)) {
@@ -184,47 +190,78 @@ __global__ __launch_bounds__(256, 2) void fused_bwd_kernel(FusedBwdArgs f) {
             for (int rt = 0; rt < NRT; ++rt)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) accA[rt][r] = 0.f;
+            // A fragments read PD k-steps ahead of their MFMAs (a static register ring: the loop
+            // is fully unrolled), so the LDS latency hides behind PD * NRT MFMAs
+            constexpr int PD = 4;
+            float ar[PD][NRT];
+            auto afrag = [&](int j, int sl) __attribute__((always_inline)) {
 #pragma unroll
-            for (int j = 0; j < C / 2; ++j)
+                for (int rt = 0; rt < NRT; ++rt) ar[sl][rt] = Zs[((a_rt0 + rt) * 32 + l32) * ZS + 2 * j + h];
+            };
 #pragma unroll
-                for (int rt = 0; rt < NRT; ++rt) {
-                    const float a = Zs[((a_rt0 + rt) * 32 + l32) * ZS + 2 * j + h];
-                    accA[rt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, wf[j], accA[rt], 0, 0, 0);
-                }
+            for (int j = 0; j < PD; ++j) afrag(j, j);
+#pragma unroll
+            for (int j = 0; j < C / 2; ++j) {
+                float a[NRT];
+#pragma unroll
+                for (int rt = 0; rt < NRT; ++rt) a[rt] = ar[j % PD][rt];
+                if (j + PD < C / 2) afrag(j + PD, j % PD);
+#pragma unroll
+                for (int rt = 0; rt < NRT; ++rt)
+                    accA[rt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[rt], wf[j], accA[rt], 0, 0, 0);
+            }
 #pragma unroll
             for (int rt = 0; rt < NRT; ++rt) {
                 const int rb = (a_rt0 + rt) * 32;
+                // the 16 z of this lane's rows read up front (one LDS round trip, not 16); rows
+                // past M (zero dZ, clamped z) are masked out of the store and the sums, no branch
+                float zz[16];
+#pragma unroll
+                for (int r = 0; r < 16; ++r) zz[r] = Xs[(rb + acc_row_of(r, h)) * XS + a_col];
+                const bool full = m0 + rb + 32 <= M;
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     const int row = rb + acc_row_of(r, h);
                     const float v = accA[rt][r];
-                    if (m0 + row < M) {
-                        f.dA[(size_t)(m0 + row) * f.ldd + a_col] = v;
-                        const float z = Xs[row * XS + a_col];
-                        const float dy = v * dact_f(z * es + et, 0, qslope);
-                        const float xh = (z - em) * ei;
-                        s1 += (double)dy;
-                        s2 += (double)dy * (double)xh;
-                    }
+                    const bool ok = full || m0 + row < M;
+                    if (ok) f.dA[(size_t)(m0 + row) * f.ldd + a_col] = v;
+                    const float dy = v * dact_f(zz[r] * es + et, 0, qslope);
+                    const float xh = (zz[r] - em) * ei;
+                    s1 += ok ? (double)dy : 0.0;
+                    s2 += ok ? (double)dy * (double)xh : 0.0;
                 }
             }
         }
-        // ---- dW += Zs^T . act(Xs*s + t)
-#pragma unroll 4
-        for (int pq = 0; pq < BM / 2 / WR; ++pq) {
-            const int r = 2 * (pq * WR + wsub) + h;
-            const float b = act_f(Xs[r * XS + b_col] * bs + bt, 0, qslope);
+        // ---- dW += Zs^T . act(Xs*s + t): the fragments of row pair pq + 1 are read while row pair
+        // pq's MFMAs run (two register slots), so no MFMA waits on its own LDS reads
+        {
+            constexpr int NP = BM / 2 / WR;
+            float xr[2], za[2][WPT];
+            auto frag = [&](int pq, int sl) __attribute__((always_inline)) {
+                const int r = 2 * (pq * WR + wsub) + h;
+                xr[sl] = Xs[r * XS + b_col];
 #pragma unroll
-            for (int u = 0; u < WPT; ++u) {
-                const int ct_c = (t_base + 4 * u) / NIT;
-                const float a = Zs[r * ZS + ct_c * 32 + l32];
-                accW[u] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, accW[u], 0, 0, 0);
+                for (int u = 0; u < WPT; ++u) za[sl][u] = Zs[r * ZS + ((t_base + 4 * u) / NIT) * 32 + l32];
+            };
+            frag(0, 0);
+#pragma unroll
+            for (int pq = 0; pq < NP; ++pq) {
+                const int sl = pq & 1;
+                if (pq + 1 < NP) frag(pq + 1, sl ^ 1);
+                const float b = act_f(xr[sl] * bs + bt, 0, qslope);
+#pragma unroll
+                for (int u = 0; u < WPT; ++u)
+                    accW[u] = __builtin_amdgcn_mfma_f32_32x32x2f32(za[sl][u], b, accW[u], 0, 0, 0);
             }
         }
-        // ---- db: column sums of dZ (row order)
-        if (f.pdb && tid < C) {
-#pragma unroll 8
-            for (int r = 0; r < BM; ++r) dbs += Zs[r * ZS + tid];
+    }
+    // db partials: the RPP threads of each column quad, added in thread order (Zs is free now)
+    __syncthreads();
+    if (f.pdb) {
+        *reinterpret_cast<float4*>(&Zs[r0 * C + 4 * cq]) = dbv;
+        __syncthreads();
+        if (tid < C) {
+            for (int j = 0; j < RPP; ++j) dbs += Zs[j * C + tid];
         }
     }
 
@@ -278,10 +315,11 @@ __global__ __launch_bounds__(256, 2) void fused_bwd_kernel(FusedBwdArgs f) {
 
 template <int C, int CI>
 static void launch_fused(dim3 grid, hipStream_t st, const FusedBwdArgs& a) {
+    constexpr bool W = C + CI > 96;
     switch (a.x.mode) {
-    case OP_PLAIN: hipLaunchKernelGGL((fused_bwd_kernel<C, CI, OP_PLAIN, true>), grid, dim3(256), 0, st, a); break;
-    case OP_BNBWD: hipLaunchKernelGGL((fused_bwd_kernel<C, CI, OP_BNBWD, true>), grid, dim3(256), 0, st, a); break;
-    default: hipLaunchKernelGGL((fused_bwd_kernel<C, CI, OP_POOLBWD, true>), grid, dim3(256), 0, st, a); break;
+    case OP_PLAIN: hipLaunchKernelGGL((fused_bwd_kernel<C, CI, OP_PLAIN, true, W>), grid, dim3(256), 0, st, a); break;
+    case OP_BNBWD: hipLaunchKernelGGL((fused_bwd_kernel<C, CI, OP_BNBWD, true, W>), grid, dim3(256), 0, st, a); break;
+    default: hipLaunchKernelGGL((fused_bwd_kernel<C, CI, OP_POOLBWD, true, W>), grid, dim3(256), 0, st, a); break;
     }
 }
 
@@ -325,7 +363,7 @@ bool fused_bwd_ok(int M, int C, int CI, int ldw, const pcs_operand* x, const pcs
 // for the weight-gradient-only form (<= 128 VGPRs): more tiles' loads in flight per CU
 int fused_bwd_grid(int M, int C, int CI, bool da) {
     const int tiles = (M + FB_BM - 1) / FB_BM;
-    const int per_cu = !da ? 4 : (C + CI <= 96 ? 3 : FB_BLOCKS_PER_CU);
+    const int per_cu = !da ? 4 : (C + CI <= 96 ? 3 : 1);
     return std::min(tiles, 256 * per_cu);
 }
 

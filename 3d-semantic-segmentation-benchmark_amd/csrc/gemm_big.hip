@@ -209,14 +209,10 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_kernel(const float* __restrict
     }
 }
 
-// the wide path's column tile for N outputs: 256 unless a 128-wide tile wastes less
-// column tile: 256 unless its padding is the larger one -- and, in PCS_NT_BN256 builds (A/B),
-// 256 wherever its padding stays under 1/8 of the columns (conv6's 1408 -> 6 x 256)
+// the wide path's column tile for N outputs: 256 unless a 128-wide tile wastes less (round 3:
+// 6 x 256 columns for conv6's 1408 measured slower than 11 x 128, profiles/r03_final_checks.txt)
 int gemm_nt_bn(int N) {
     const int w256 = ((N + 255) / 256) * 256 - N, w128 = ((N + 127) / 128) * 128 - N;
-#ifdef PCS_NT_BN256
-    if (8 * w256 < N + w256) return 256;
-#endif
     return w128 < w256 ? 128 : 256;
 }
 static int nt_bn(int N) { return gemm_nt_bn(N); }

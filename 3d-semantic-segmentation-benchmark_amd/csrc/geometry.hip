@@ -3,9 +3,11 @@
 // against the previous level for SetAbstraction, against the centroids themselves for
 // InvResMLP, common.py:288), the 3-NN of each FeaturePropagation (common.py:94-114) and the
 // inverse (CSR) map of every neighbour table for the atomic-free gather backward -- enqueued
-// by ONE host call on one stream, in the order pcseg.common.GeometryPlan issues them from
-// Python (same kernels, same arguments: bitwise the same plan), recording one caller event
-// per level (the forward's SA level l waits on it) and one after the 3-NN.
+// by ONE host call on one stream (same kernels, same arguments as pcseg.common.GeometryPlan's
+// Python path: bitwise the same plan), recording one caller event per level (the forward's SA
+// level l waits on it) and one after the 3-NN.  With interp, every level's FPS and ball queries
+// come first and the inverse maps (backward-only) after them, so a level's wait and the next
+// level's FPS never queue behind a map.
 //
 // One call replaces ~20 Python-level launches (each with its own allocation, ctypes
 // marshalling and caching-allocator stream bookkeeping): about 0.5 ms of host enqueue per
@@ -38,6 +40,13 @@ static int check_plan(int B, int N, const pcs_geo_level* lv, int L) {
         prev = (int)v.C;
     }
     return 0;
+}
+
+// the inverse map of level v's ball query q (np = the previous level's point count)
+static int ball_inverse(const pcs_geo_level& v, int q, int B, int np, void* ws, size_t ws_bytes, void* stream) {
+    const int C = (int)v.C, K = (int)v.K[q], ns = v.on_self[q] ? C : np;
+    PCS_CHECK_ARG(v.ball_off[q] && v.ball_ent[q], "pcs_geometry_plan: query %d: null map", q);
+    return pcs_inverse_index(v.ball[q], B, C * K, ns, v.ball_off[q], v.ball_ent[q], ws, ws_bytes, stream);
 }
 
 }  // namespace pcs
@@ -87,12 +96,8 @@ PCS_API int pcs_geometry_plan(const float* coords, int B, int N, const int32_t* 
             const int K = (int)v.K[q];
             PCS_CHECK_ARG(v.ball[q], "pcs_geometry_plan: level %d query %d: null ball output", l, q);
             if (int e = pcs_ball_query(v.cent, src, B, C, ns, (float)v.r2[q], K, v.ball[q], stream)) return e;
-            if (inverse) {
-                PCS_CHECK_ARG(v.ball_off[q] && v.ball_ent[q], "pcs_geometry_plan: level %d query %d: null map", l, q);
-                if (int e = pcs_inverse_index(v.ball[q], B, C * K, ns, v.ball_off[q], v.ball_ent[q], ws, ws_bytes,
-                                              stream))
-                    return e;
-            }
+            if (inverse && !interp)
+                if (int e = ball_inverse(v, q, B, np, ws, ws_bytes, stream)) return e;
         }
         if (v.event && hipEventRecord(static_cast<hipEvent_t>(v.event), st) != hipSuccess)
             return launch_status("pcs_geometry_plan: event record");
@@ -100,6 +105,15 @@ PCS_API int pcs_geometry_plan(const float* coords, int B, int N, const int32_t* 
         np = C;
     }
     if (interp) {
+        // the ball queries' inverse maps (read only by the backward) after every level's FPS and
+        // ball queries: the forward's level-l wait then does not include them, nor does the next
+        // level's FPS queue behind them; nn_event (after the 3-NN and their maps) covers them all
+        np = N;
+        for (int l = 0; l < L && inverse; ++l) {
+            for (int q = 0; q < lv[l].nq; ++q)
+                if (int e = ball_inverse(lv[l], q, B, np, ws, ws_bytes, stream)) return e;
+            np = (int)lv[l].C;
+        }
         // FP_L ... FP_1 (the reference's call order): 3-NN of level l's points among level l+1's
         for (int l = L - 1; l >= 0; --l) {
             const pcs_geo_level& v = lv[l];

@@ -125,10 +125,6 @@ constexpr int KNN_WAVES = 4;
 constexpr int KNN_QROWS = 32 * KNN_WAVES;
 constexpr int KNN_NMAX = 64;    // LDS items per row: top-k list + one survivor segment per lane half (<= 64: one per lane in a merge)
 constexpr int KNN_RS = KNN_NMAX;       // row stride in items
-#ifndef PCS_KNN_SLACK
-#define PCS_KNN_SLACK 0         // merge early when a segment has fewer free slots (0: only on overflow;
-                                // B=32 N=4096: 6 -> 0 is -6 % kNN time, fewer merges, rare re-appends)
-#endif
 
 // accumulator register i of lane half h holds candidate acc_row(i, h) of the tile
 // (v_mfma_f32_32x32x2_f32 C/D layout: row = (i & 3) + 8 (i >> 2) + 4 h, column = lane & 31)
@@ -199,13 +195,6 @@ __device__ __forceinline__ float knn_select_row(float2* L, int nl, int c0, int c
     if (n > K) {
         const unsigned key = have ? knn_key(it.x) : 0u;
         unsigned T;
-#ifdef PCS_KNN_BITSEARCH
-        T = 0;                         // diagnostic: 32-step bitwise search (key 0 never counts)
-        for (int bit = 31; bit >= 0; --bit) {
-            const unsigned c = T | (1u << bit);
-            if (knn_popc(ballot(key >= c)) >= K) T = c;
-        }
-#else
         // quickselect over the lanes: T is the rem-th largest key of `mask`; the pivot is
         // the mask's lowest lane (items sit in arrival order), each round drops the pivot
         unsigned long long mask = hm;
@@ -221,7 +210,6 @@ __device__ __forceinline__ float knn_select_row(float2* L, int nl, int c0, int c
             rem -= ce;
             mask &= ~ge;
         }
-#endif
         keep = ballot(key > T) & hm;
         unsigned long long eq = ballot(key == T) & hm;
         int need = K - knn_popc(keep);
@@ -461,7 +449,8 @@ __global__ __launch_bounds__(64 * WPB, 2) void knn_wave_kernel(const float* __re
                 cnt += (p && cnt < CAP) ? 1 : 0;
             }
         }
-        const unsigned long long nm = ballot(dropped != 0 || cnt > CAP - PCS_KNN_SLACK);
+        // merge only on overflow (merging at 6 free slots measured 6 % slower: more merges)
+        const unsigned long long nm = ballot(dropped != 0 || cnt > CAP);
         if (nm) {
             unsigned rows = (unsigned)nm | (unsigned)(nm >> 32);
             while (rows) {
@@ -619,115 +608,11 @@ PCS_API int pcs_knn_ws(const float* x, int B, int N, int F, int k, int32_t* out_
 // pcs_knn_ws whose rows start from the threshold of a previous neighbour list (seeds (B, N, ks)
 // int32, e.g. the previous EdgeConv's graph): the same lists, fewer survivors to merge.  Any
 // seeds are safe -- a row whose seeds are out of range, repeated or fewer than k is searched
-// unseeded.  F = 3 rows can be seeded by pcs_knn_morton_seeds (there is no previous graph).
+// unseeded.
 PCS_API int pcs_knn_seeded(const float* x, int B, int N, int F, int k, const int32_t* seeds, int ks, int32_t* out_idx,
                            void* ws, size_t ws_bytes, void* stream) {
     PCS_CHECK_ARG(ws && ws_bytes >= (size_t)B * N * sizeof(float) + 256, "pcs_knn_seeded: workspace too small");
     PCS_CHECK_ARG(seeds && ks >= 1, "pcs_knn_seeded: null seeds or ks < 1");
     float* xx = reinterpret_cast<float*>((reinterpret_cast<uintptr_t>(ws) + 255) & ~uintptr_t(255));
     return knn_run(x, B, N, F, k, out_idx, xx, seeds, ks, stream);
-}
-
-// ---------------------------------------------------------------- Morton-order seeds (F = 3)
-// The first DGCNN graph is built on coordinates and has no previous graph to seed it.  Points
-// adjacent on a Z-order curve are mostly near in space, so each point's seeds are the ks points
-// around it in its cloud's Morton order: their k-th best distance bounds the row's threshold from
-// the start (pcs_knn_seeded; the lists do not change -- any seeds are safe).  One 1024-thread
-// workgroup per cloud: bounding box, 10-bit-per-axis Morton keys, an LDS bitonic sort of
-// (key, index), then a window of ks consecutive sorted points per point.
-namespace pcs {
-
-constexpr int kMortonMax = 8192;
-
-__device__ __forceinline__ unsigned spread3(unsigned v) {      // 10 bits -> every third bit
-    v &= 0x3FFu;
-    v = (v | (v << 16)) & 0x030000FFu;
-    v = (v | (v << 8)) & 0x0300F00Fu;
-    v = (v | (v << 4)) & 0x030C30C3u;
-    v = (v | (v << 2)) & 0x09249249u;
-    return v;
-}
-
-__global__ __launch_bounds__(1024) void morton_seeds_kernel(const float* __restrict__ x, int N, int ks,
-                                                            int* __restrict__ seeds) {
-    __shared__ unsigned s_key[kMortonMax];
-    __shared__ unsigned short s_idx[kMortonMax];
-    __shared__ float s_red[2][3][16];
-    const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
-    const float* X = x + (size_t)b * N * 3;
-    float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
-    for (int i = t; i < N; i += 1024)
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            const float v = X[3 * i + c];
-            mn[c] = fminf(mn[c], v);
-            mx[c] = fmaxf(mx[c], v);
-        }
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-        for (int d = 32; d >= 1; d >>= 1) {
-            mn[c] = fminf(mn[c], __shfl_xor(mn[c], d));
-            mx[c] = fmaxf(mx[c], __shfl_xor(mx[c], d));
-        }
-        if (lane == 0) { s_red[0][c][w] = mn[c]; s_red[1][c][w] = mx[c]; }
-    }
-    __syncthreads();
-    float lo[3], sc[3];
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-        float a = INFINITY, z = -INFINITY;
-        for (int k = 0; k < 16; ++k) { a = fminf(a, s_red[0][c][k]); z = fmaxf(z, s_red[1][c][k]); }
-        lo[c] = a;
-        sc[c] = z > a ? 1023.f / (z - a) : 0.f;       // non-finite coordinates: keys still in range
-    }
-    int P = 1;
-    while (P < N) P <<= 1;
-    for (int i = t; i < P; i += 1024) {
-        unsigned key = 0xFFFFFFFFu;                    // padding sorts last
-        if (i < N) {
-            unsigned q[3];
-#pragma unroll
-            for (int c = 0; c < 3; ++c) {
-                const float f = (X[3 * i + c] - lo[c]) * sc[c];
-                q[c] = f >= 1023.f ? 1023u : (f > 0.f ? (unsigned)f : 0u);      // NaN -> 0
-            }
-            key = spread3(q[0]) | (spread3(q[1]) << 1) | (spread3(q[2]) << 2);
-        }
-        s_key[i] = key;
-        s_idx[i] = (unsigned short)(i < N ? i : 0);
-    }
-    __syncthreads();
-    for (int k = 2; k <= P; k <<= 1)
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = t; i < P / 2; i += 1024) {
-                const int a = 2 * i - (i & (j - 1)), c = a + j;
-                const unsigned ka = s_key[a], kc = s_key[c];
-                if ((ka > kc) == ((a & k) == 0)) {
-                    s_key[a] = kc; s_key[c] = ka;
-                    const unsigned short ia = s_idx[a];
-                    s_idx[a] = s_idx[c]; s_idx[c] = ia;
-                }
-            }
-            __syncthreads();
-        }
-    for (int p = t; p < N; p += 1024) {
-        const int st = min(max(p - ks / 2, 0), N - ks);
-        int* o = seeds + ((size_t)b * N + s_idx[p]) * ks;
-        for (int j = 0; j < ks; ++j) o[j] = s_idx[st + j];
-    }
-}
-
-}  // namespace pcs
-
-// seeds (B, N, ks) int32: for each point, the ks points around it in its cloud's Morton order
-// (distinct, in range; the point itself included).  N <= 8192, ks <= N.  Feeds pcs_knn_seeded
-// for DGCNN's coordinate graph (dgcnn.py:7-21 on xyz): same lists, fewer survivors.
-PCS_API int pcs_knn_morton_seeds(const float* xyz, int B, int N, int ks, int32_t* seeds, void* stream) {
-    using namespace pcs;
-    PCS_CHECK_ARG(B >= 0 && N >= 1 && N <= kMortonMax && ks >= 1 && ks <= N,
-                  "pcs_knn_morton_seeds: bad sizes B=%d N=%d ks=%d (N <= %d)", B, N, ks, kMortonMax);
-    PCS_CHECK_ARG(xyz && seeds, "pcs_knn_morton_seeds: null pointer");
-    if (B == 0) return 0;
-    hipLaunchKernelGGL(morton_seeds_kernel, dim3(B), dim3(1024), 0, as_stream(stream), xyz, N, ks, seeds);
-    return launch_status("pcs_knn_morton_seeds");
 }

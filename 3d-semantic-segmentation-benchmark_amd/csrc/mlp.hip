@@ -399,12 +399,8 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(Operand xo, int N, Operan
     // of remapped ids, tile-fastest -- the tiles of one row split (the same X / Y rows) run
     // together on one XCD and share its L2 instead of each fetching the rows from HBM
     const int lin = blockIdx.x + blockIdx.y * gridDim.x;
-#ifndef PCS_WGRAD_LINEAR
     const int nwg = gridDim.x * gridDim.y, q8 = nwg / 8, r8 = nwg % 8, xcd = lin % 8;
     const int rt = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + lin / 8;
-#else
-    const int rt = blockIdx.y + blockIdx.x * gridDim.y;     // A/B builds only: the round-2 order
-#endif
     const int sp = rt / gridDim.y, ti = rt - sp * gridDim.y;
     const int n0 = (ti / tiles_i) * BO;
     const int k0 = (ti % tiles_i) * BI;
@@ -607,7 +603,31 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
 }
 
 // ------------------------------------------------------------------ BN finalize (forward)
-// one block per channel: reduce nb partials -> mean/var -> s,t ; running-stat update
+// One WAVE per channel (4 channels per 256-thread block): each lane sums a strided share of the
+// channel's nb fp64 partials, then a fixed xor-butterfly over the 64 lanes -- no LDS tree and no
+// block barriers (round 3's block-per-channel LDS tree took 5-9 us per launch, ~44 launches per
+// PointNet++ step).  The summation order is fixed: bitwise reproducible.
+__device__ __forceinline__ double wave_sum_f64(double v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    return v;
+}
+
+__device__ __forceinline__ void channel_sums(const double* __restrict__ part, int nb, int N, int n, int lane,
+                                             double& S1, double& S2) {
+    const double* p1 = part + (size_t)n * nb;
+    const double* p2 = part + ((size_t)N + n) * nb;
+    double a0 = 0.0, a1 = 0.0, b0 = 0.0, b1 = 0.0;
+    int i = lane;
+    for (; i + 64 < nb; i += 128) {             // two loads in flight per array
+        a0 += p1[i]; a1 += p1[i + 64];
+        b0 += p2[i]; b1 += p2[i + 64];
+    }
+    if (i < nb) { a0 += p1[i]; b0 += p2[i]; }
+    S1 = wave_sum_f64(a0 + a1);
+    S2 = wave_sum_f64(b0 + b1);
+}
+
 __global__ __launch_bounds__(256) void bn_finalize_kernel(const double* __restrict__ part, int nb, int N, long long M,
                                                           const float* __restrict__ gamma,
                                                           const float* __restrict__ beta, float eps, float momentum,
@@ -615,27 +635,15 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const double* __restri
                                                           float* __restrict__ s, float* __restrict__ t,
                                                           float* __restrict__ mean_out, float* __restrict__ inv_out,
                                                           long long* __restrict__ nbt) {
-    __shared__ double r1[256], r2[256];
-    const int n = blockIdx.x;
-    double a = 0.0, b = 0.0;
-    for (int i = threadIdx.x; i < nb; i += 256) {
-        a += part[(size_t)n * nb + i];
-        b += part[((size_t)N + n) * nb + i];
-    }
-    r1[threadIdx.x] = a;
-    r2[threadIdx.x] = b;
-    __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-        if (threadIdx.x < o) {
-            r1[threadIdx.x] += r1[threadIdx.x + o];
-            r2[threadIdx.x] += r2[threadIdx.x + o];
-        }
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) {
+    const int lane = threadIdx.x & 63;
+    const int n = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (n >= N) return;
+    double S1, S2;
+    channel_sums(part, nb, N, n, lane, S1, S2);
+    if (lane == 0) {
         if (nbt && n == 0) nbt[0] += 1;         // BatchNorm.num_batches_tracked
-        const double mean = r1[0] / (double)M;
-        double var = r2[0] / (double)M - mean * mean;
+        const double mean = S1 / (double)M;
+        double var = S2 / (double)M - mean * mean;
         if (var < 0.0) var = 0.0;
         const float invstd = (float)(1.0 / sqrt(var + (double)eps));
         const float g = gamma ? gamma[n] : 1.f;
@@ -655,32 +663,19 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const double* __restri
 
 // ------------------------------------------------------------------ BN finalize (backward)
 // sums (sum dy, sum dy*xhat) -> dgamma, dbeta (added when `accum`) and the dZ coefficients
-// kB = s*sum_dy/M, kC = s*sum_dyx/M
+// kB = s*sum_dy/M, kC = s*sum_dyx/M; one wave per channel as above
 __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const double* __restrict__ part, int nb, int N,
                                                               long long M, const float* __restrict__ s,
                                                               const float* __restrict__ inv,
                                                               float* __restrict__ dgamma, float* __restrict__ dbeta,
                                                               float* __restrict__ kB, float* __restrict__ kC,
                                                               int accum) {
-    __shared__ double r1[256], r2[256];
-    const int n = blockIdx.x;
-    double a = 0.0, b = 0.0;
-    for (int i = threadIdx.x; i < nb; i += 256) {
-        a += part[(size_t)n * nb + i];
-        b += part[((size_t)N + n) * nb + i];
-    }
-    r1[threadIdx.x] = a;
-    r2[threadIdx.x] = b;
-    __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-        if (threadIdx.x < o) {
-            r1[threadIdx.x] += r1[threadIdx.x + o];
-            r2[threadIdx.x] += r2[threadIdx.x + o];
-        }
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-        const double S1 = r1[0], S2 = r2[0];
+    const int lane = threadIdx.x & 63;
+    const int n = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (n >= N) return;
+    double S1, S2;
+    channel_sums(part, nb, N, n, lane, S1, S2);
+    if (lane == 0) {
         if (dbeta) dbeta[n] = accum ? dbeta[n] + (float)S1 : (float)S1;
         if (dgamma) dgamma[n] = accum ? dgamma[n] + (float)S2 : (float)S2;
         kB[n] = (float)((double)s[n] * S1 / (double)M);
@@ -913,13 +908,13 @@ static unsigned dropout_thr(double p) {
 void bn_finalize_launch(const double* part, int nb, int N, long long M, const float* gamma, const float* beta,
                         float eps, float momentum, float* run_mean, float* run_var, float* s, float* t, float* mean,
                         float* invstd, long long* nbt, hipStream_t st) {
-    hipLaunchKernelGGL(bn_finalize_kernel, dim3(N), dim3(256), 0, st, part, nb, N, M, gamma, beta, eps, momentum,
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3((N + 3) / 4), dim3(256), 0, st, part, nb, N, M, gamma, beta, eps, momentum,
                        run_mean, run_var, s, t, mean, invstd, nbt);
 }
 
 void bn_bwd_finalize_launch(const double* part, int nb, int N, long long M, const float* s, const float* inv,
                             float* dgamma, float* dbeta, float* kB, float* kC, int accum, hipStream_t st) {
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(N), dim3(256), 0, st, part, nb, N, M, s, inv, dgamma, dbeta, kB,
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((N + 3) / 4), dim3(256), 0, st, part, nb, N, M, s, inv, dgamma, dbeta, kB,
                        kC, accum);
 }
 
@@ -1031,12 +1026,6 @@ static void gemm_tile(int M, int N, bool bwd, int* bm, int* bn, int* nt = nullpt
         c = wide ? big : mid;
     } else {
         wide = N > 64 && N >= 256 && M >= 65536;
-#ifdef PCS_DGRAD512
-        if (!wide && N > 64 && nt) {
-            *bm = 64; *bn = 128; *nt = 512;
-            return;
-        }
-#endif
         c = wide ? big : mid64;
     }
     const int nc = wide ? 4 : 2;
@@ -1056,8 +1045,8 @@ static int gemm_grid_x(int M, int N, int bm, int bn, int nt = 256) {
     const int mtiles = (M + bm - 1) / bm;
     const int lds = 4 * (bm + bn) * 2 * GLDK + 16 * bn;         // As + Bs + red (bytes)
     int per_cu = (160 * 1024) / lds;
-    // 512-thread tiles use > 128 VGPRs: 2 waves per SIMD, one block per CU
-    const int cap = nt == 512 ? 1 : 4;
+    const int cap = 4;
+    (void)nt;
     per_cu = per_cu < 1 ? 1 : (per_cu > cap ? cap : per_cu);
     const int ntiles = (N + bn - 1) / bn;
     const int slots = (256 * per_cu + ntiles - 1) / ntiles;
@@ -1068,8 +1057,8 @@ static int gemm_grid_x(int M, int N, int bm, int bn, int nt = 256) {
 
 // wave grid of a row-GEMM tile (mirrors the launch table in pcs_gemm_rows)
 static void gemm_waves(int bm, int bn, int nt, int* wm, int* wn) {
-    if (nt == 512) { *wm = 2; *wn = 4; }
-    else if (bn == 32 || (bm == 128 && bn == 64)) { *wm = 4; *wn = 1; }
+    (void)nt;
+    if (bn == 32 || (bm == 128 && bn == 64)) { *wm = 4; *wn = 1; }
     else if (bm == 32) { *wm = 1; *wn = 4; }
     else { *wm = 2; *wn = 2; }
 }
@@ -1228,10 +1217,6 @@ int pcs::gemm_rows_ex(const pcs_operand* a, int M, int K, const float* W, int ld
     // stats partials: one per row block as row_blocks() counts them (<= the row tiles: persistent)
     const int gx = (stats || bstats) ? row_blocks(M, N, bwd) : gemm_grid_x(M, N, bm, bn, nt);
     const bool b = bt != 0;
-#ifdef PCS_DGRAD512
-    if (nt == 512) launch_gemm<64, 128, 2, 4>(g, gx, b, s);
-    else
-#endif
     if (bn == 32) launch_gemm<128, 32, 4, 1>(g, gx, b, s);
     else if (bm == 128 && bn == 64) launch_gemm<128, 64, 4, 1>(g, gx, b, s);
     else if (bm == 128) launch_gemm<128, 128, 2, 2>(g, gx, b, s);
@@ -1260,10 +1245,8 @@ static void wgrad_plan(int N, int K, int M, int* BO, int* BI, int* splits, int* 
     *BO = N > 64 ? 128 : 64;
     *BI = K > 64 ? 128 : 64;
     const int tiles = ((N + *BO - 1) / *BO) * ((K + *BI - 1) / *BI);
-#ifndef PCS_WGRAD_BLOCKS
-#define PCS_WGRAD_BLOCKS 1024
-#endif
-    const int target = 2.0 * M * N * K >= 1.6e10 ? 2048 : PCS_WGRAD_BLOCKS;
+    // (512 / 256 blocks for the smaller ones measured +0.3 / +0.8 % on DGCNN, round 3)
+    const int target = 2.0 * M * N * K >= 1.6e10 ? 2048 : 1024;
     int sp = (target + tiles - 1) / tiles;
     // the partial tiles (sp x N x K floats, written once and read once by the reduce) stay
     // below half the operands' bytes M x (N + K), as long as >= 512 blocks remain
@@ -1379,7 +1362,7 @@ PCS_API int pcs_bn_finalize(const double* part, int nb, int N, long long M, cons
                             float eps, float momentum, float* run_mean, float* run_var, float* s, float* t,
                             float* mean, float* invstd, void* stream) {
     PCS_CHECK_ARG(nb >= 1 && N >= 1 && M >= 1, "pcs_bn_finalize: bad sizes");
-    hipLaunchKernelGGL(bn_finalize_kernel, dim3(N), dim3(256), 0, as_stream(stream), part, nb, N, M, gamma, beta, eps,
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3((N + 3) / 4), dim3(256), 0, as_stream(stream), part, nb, N, M, gamma, beta, eps,
                        momentum, run_mean, run_var, s, t, mean, invstd, (long long*)nullptr);
     return launch_status("pcs_bn_finalize");
 }
@@ -1388,7 +1371,7 @@ PCS_API int pcs_bn_finalize(const double* part, int nb, int N, long long M, cons
 PCS_API int pcs_bn_bwd_finalize(const double* part, int nb, int N, long long M, const float* s, const float* invstd,
                                 float* dgamma, float* dbeta, float* kB, float* kC, int accum, void* stream) {
     PCS_CHECK_ARG(nb >= 1 && N >= 1 && M >= 1, "pcs_bn_bwd_finalize: bad sizes");
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(N), dim3(256), 0, as_stream(stream), part, nb, N, M, s, invstd,
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((N + 3) / 4), dim3(256), 0, as_stream(stream), part, nb, N, M, s, invstd,
                        dgamma, dbeta, kB, kC, accum);
     return launch_status("pcs_bn_bwd_finalize");
 }

@@ -59,7 +59,6 @@ SIGNATURES = {
     'pcs_copy_cols': [P, I32, I32, I32, P, I32, P],
     'pcs_knn_ws': [P, I32, I32, I32, I32, P, P, ctypes.c_size_t, P],
     'pcs_knn_seeded': [P, I32, I32, I32, I32, P, I32, P, P, ctypes.c_size_t, P],
-    'pcs_knn_morton_seeds': [P, I32, I32, I32, P, P],
     'pcs_group_fwd': [P, P, P, P, I32, I32, I32, I32, I32, F32, I32, P, I32, P],
     'pcs_maxk_fwd': [P, I64, I32, I32, P, P, P],
     'pcs_maxk_bwd': [P, P, I64, I32, I32, P, P],

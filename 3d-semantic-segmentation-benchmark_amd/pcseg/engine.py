@@ -60,6 +60,22 @@ def grad_target(p: torch.Tensor | None) -> torch.Tensor | None:
     return g
 
 
+def grad_targets(params) -> list:
+    """grad_target of every parameter, the missing gradients created as views of ONE zeroed
+    buffer (one fill launch per stack call instead of one per parameter: an optimizer's
+    zero_grad(set_to_none=True), the harness default, leaves every .grad None each step)."""
+    need = [p for p in params if p is not None and p.requires_grad and p.grad is None]
+    if len(need) > 1:
+        flat = torch.zeros(sum(p.numel() for p in need), dtype=torch.float32, device=need[0].device)
+        off = 0
+        for p in need:
+            if p.dtype != torch.float32:
+                raise RuntimeError('pcseg engine: parameters must be fp32')
+            p.grad = flat[off:off + p.numel()].view_as(p)
+            off += p.numel()
+    return [grad_target(p) for p in params]
+
+
 def notify_grad_ready(params) -> None:
     for p in params:
         if p is not None:
@@ -282,7 +298,10 @@ def _layer_statics(Kin, bns, acts, params, couts, dev):
         C = couts[li]
         if C % 4:
             raise ValueError(f'engine: layer width {C} must be a multiple of 4')
-        Wm = W.reshape(C, -1)
+        # a DETACHED alias: a view of the parameter made here (autograd.Function.forward runs in
+        # no-grad mode) and saved for backward is rejected once an optimizer updates the parameter
+        # in place (torch.optim.Adam in the unchanged harness, Training/training.py:60)
+        Wm = W.detach().reshape(C, -1)
         if Wm.shape[1] % 4 and li > 0:    # 16-B weight rows (the pad columns are zero)
             Wp = torch.zeros((C, ld4(Wm.shape[1])), dtype=torch.float32, device=dev)
             Wp[:, :Wm.shape[1]] = Wm
@@ -443,10 +462,9 @@ class SharedMLPFn(torch.autograd.Function):
                  ptr(g2), couts[-1], st)
             gout = g2
         ldg = gout.stride(0)
-        recs = b''.join(statics[li] + _DYN.pack(zp, cp, _nz(grad_target(params[4 * li])),
-                                                  _nz(grad_target(params[4 * li + 1])),
-                                                  _nz(grad_target(params[4 * li + 2])),
-                                                  _nz(grad_target(params[4 * li + 3])), 0.0, 0, ctx.bwd_fuse,
+        gt = grad_targets(params)
+        recs = b''.join(statics[li] + _DYN.pack(zp, cp, _nz(gt[4 * li]), _nz(gt[4 * li + 1]), _nz(gt[4 * li + 2]),
+                                                  _nz(gt[4 * li + 3]), 0.0, 0, ctx.bwd_fuse,
                                                   ctx.dx_from if li == 0 else 0)
                         for li, (zp, cp) in enumerate(zptrs))
         dX = None
@@ -494,7 +512,7 @@ class EdgeConvFn(torch.autograd.Function):
         B, N, k = idx.shape
         M, ldx = X.shape
         Cout = W.shape[0]
-        Wm = W.reshape(Cout, 2 * C)
+        Wm = W.detach().reshape(Cout, 2 * C)      # detached alias (see _layer_statics)
         if not Wm.is_contiguous():
             Wm = Wm.contiguous()
         Y, PQ, S, out = (_f32((M, Cout), dev) for _ in range(4))
@@ -563,7 +581,7 @@ class EdgeConvFn(torch.autograd.Function):
         if dX is not None and ldx != C:
             dX.zero_()
         ws = _edge_ws(B, N, C, Cout, 1, dev)
-        dW, dg, db = grad_target(W), grad_target(gamma), grad_target(beta)
+        dW, dg, db = grad_targets((W, gamma, beta))
         call('pcs_edgeconv_bwd', ptr(X), ldx, C, ptr(off), ptr(ent), B, N, k, ptr(Wm), Cout, ptr(Y), ptr(Q), ptr(S),
              ptr(pz), ptr(arg), ptr(coef), slope, ptr(gout), ptr(dX), ldx, ptr(dW), ptr(dg), ptr(db), ptr(ws),
              ws.numel(), st)
@@ -685,7 +703,7 @@ class RowLinearFn(torch.autograd.Function):
         dev = x.device
         M, K = x.shape
         N = weight.shape[0]
-        Wm = weight.reshape(N, -1)
+        Wm = weight.detach().reshape(N, -1)       # detached alias (see _layer_statics)
         if Wm.shape[1] != K or K % 4:
             raise ValueError(f'row linear: x has {K} channels, weight expects {Wm.shape[1]} (need a multiple of 4)')
         Wm = Wm.contiguous()

@@ -362,15 +362,6 @@ def _dgcnn_head(self, parts: list[torch.Tensor], B: int, N: int):
     return logits, x5.view(B, N, -1).transpose(1, 2), None
 
 
-def _xyz_seeds(xyz: torch.Tensor, k: int):
-    """Morton-order seeds for the coordinate graph (ops.knn_morton_seeds): the search's
-    threshold starts from them; the kNN lists are the same (replayed graphs need none)."""
-    rp = _replay()
-    if rp is not None and rp.knn_idx:
-        return None
-    return ops.knn_morton_seeds(xyz, k)
-
-
 def _head_seq(cin, cout, dropout):
     return nn.Sequential(nn.Conv1d(cin, cout, kernel_size=1, bias=False), nn.BatchNorm1d(cout),
                          nn.LeakyReLU(negative_slope=0.2), nn.Dropout(dropout))
@@ -398,7 +389,7 @@ class DGCNN(nn.Module):
         xyz = x[:, :3, :] if x.size(1) == 6 else x
         xp = xyz.transpose(1, 2).contiguous()
         ib = EdgeInverseBatch()
-        x1, g = self.conv1.forward_graph(xp, _xyz_seeds(xp, self.k), inv_batch=ib)
+        x1, g = self.conv1.forward_graph(xp, None, inv_batch=ib)
         x2, g = self.conv2.forward_graph(x1, g, inv_batch=ib)
         x3, g = self.conv3.forward_graph(x2, g, inv_batch=ib)
         x4, _ = self.conv4.forward_graph(x3, g, inv_batch=ib)
@@ -433,7 +424,7 @@ class DGCNNWithColor(nn.Module):
         xyz = xp[:, :, :3].contiguous()
         rgb = xp[:, :, 3:6].contiguous()
         ib = EdgeInverseBatch()
-        x1, g = self.conv1.forward_graph(xyz, _xyz_seeds(xyz, self.k), inv_batch=ib)
+        x1, g = self.conv1.forward_graph(xyz, None, inv_batch=ib)
         x2, g = self.conv2.forward_graph(x1, g, inv_batch=ib)
         x3, g = self.conv3.forward_graph(x2, g, inv_batch=ib)
         x4, _ = self.conv4.forward_graph(x3, g, inv_batch=ib)

@@ -95,19 +95,6 @@ def knn(x: torch.Tensor, k: int, seeds: torch.Tensor | None = None) -> torch.Ten
     return out
 
 
-def knn_morton_seeds(xyz: torch.Tensor, ks: int) -> torch.Tensor | None:
-    """Seeds for knn(xyz, k, seeds=...) on coordinates: each point's ks neighbours in its cloud's
-    Morton order (B, N, ks) int32, or None where the kernel does not apply (N > 8192 or N < ks)."""
-    check_cuda(xyz)
-    xyz = _c(xyz.float())
-    B, N, F = xyz.shape
-    if F != 3 or N > 8192 or N < ks:
-        return None
-    seeds = torch.empty((B, N, ks), dtype=torch.int32, device=xyz.device)
-    call('pcs_knn_morton_seeds', ptr(xyz), B, N, ks, ptr(seeds), stream_ptr(xyz.device))
-    return seeds
-
-
 def inverse_index(idx: torch.Tensor, targets: int, out=None):
     """CSR inverse of a neighbour table idx (B, S, k) int32 with values in [0, targets):
     (offsets (B*targets+1,), entries (B*S*k,)) int32 -- the slots reading each source point,

@@ -62,8 +62,9 @@ HBM_PEAK_GBS = 8000.0           # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP32_PEAK_TFLOPS = 157.3        # fp32 MFMA dense (= fp32 vector) peak
 RIDGE = FP32_PEAK_TFLOPS * 1e12 / (HBM_PEAK_GBS * 1e9)     # flop / byte
 # reference-algorithm fwd+bwd GFLOP per sample (FlopCounterMode on the reference)
+# (MSG: the oracle composition, scripts/flops_msg.py -- same method, which reproduces SSG's 5.786)
 ALGO_GFLOP_PER_SAMPLE = {('pointnetpp', 4096): 5.786, ('pointnext', 4096): 10.791, ('pointnext', 24576): 19.592,
-                         ('dgcnn', 4096): 53.468, ('pointnet', 4096): 24.635}
+                         ('dgcnn', 4096): 53.468, ('pointnet', 4096): 24.635, ('pointnetpp_msg', 4096): 8.701}
 
 
 def model_input(pts, kind):
@@ -368,6 +369,59 @@ def run_workload(key, batch, npoints, args, world, rank, dev):
     return res
 
 
+def run_drop_in(key, batch, npoints, args, dev):
+    """The unchanged harness-A step (Training/training.py:56-60) on the pcseg model: torch.optim.Adam
+    over model.parameters(), optimizer.zero_grad() (grads set to None), outputs = model(points),
+    loss = criterion(...), loss.backward(), optimizer.step() -- on the default stream, with no
+    geometry prefetch and no flat gradient / optimizer buffers.  Also timed with the harness's
+    per-step `loss.item()` host sync (training.py:71).  Inputs resident in HBM as in `value`."""
+    import torch
+    import pcseg
+    from pcseg.synthetic import make_batch
+
+    name, ctor, kind, _, _, _ = WORKLOADS[key]
+    torch.manual_seed(0)
+    model = ctor(pcseg).to(dev).train()
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+    pts, labels, lengths = make_batch(batch, npoints, seed=2000)
+    x = model_input(pts.to(dev), kind)
+    lab = (labels.float() if kind == 'chfirst6' else labels).to(dev)
+    lengths = lengths.to(dev)
+
+    def step():
+        opt.zero_grad()
+        loss = pcseg.masked_onehot_cross_entropy(logits_of(model(x)), lab, lengths)
+        loss.backward()
+        opt.step()
+        return loss
+
+    def timed(sync_item):
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            loss = step()
+            if sync_item:
+                float(loss.item())
+        t_host = time.perf_counter() - t0
+        torch.cuda.synchronize(dev)
+        return (time.perf_counter() - t0) / args.steps * 1e3, t_host / args.steps * 1e3
+
+    ms, host = timed(False)
+    ms_sync, _ = timed(True)
+    roof = None if args.no_roofline else kernel_roofline(step, dev, key, batch, npoints)
+    out = {'ms_per_step': round(ms, 3), 'value': round(batch * npoints / (ms * 1e-3), 1), 'unit': 'points/s',
+           'host_enqueue_ms_per_step': round(host, 3),
+           'ms_per_step_with_loss_item_sync': round(ms_sync, 3),
+           'step': 'Training/training.py:56-60 unchanged: torch.optim.Adam, zero_grad(set_to_none), forward, '
+                   'criterion, backward, step; default stream, no geometry prefetch',
+           'roofline': roof, 'step_roofline': step_roofline(key, npoints, batch, ms, roof)}
+    del model, opt
+    torch.cuda.empty_cache()
+    return out
+
+
 # ----------------------------------------------------------------------------- launcher
 def _free_port():
     with socket.socket() as s:
@@ -405,6 +459,9 @@ def main():
     ap.add_argument('--cpu-threads', type=int, default=0)
     ap.add_argument('--cpu-baseline-worker', action='store_true')
     ap.add_argument('--no-roofline', action='store_true')
+    ap.add_argument('--no-drop-in', action='store_true',
+                    help='skip the unchanged harness-A step (torch.optim.Adam, default stream, no prefetch) '
+                         'reported as `drop_in` beside each workload (N=1 only)')
     ap.add_argument('--roofline-replay', action='store_true',
                     help='also time the dominant kernel\'s launches replayed back to back (rewrites outputs)')
     ap.add_argument('--graph', action='store_true',
@@ -477,6 +534,10 @@ def main():
     dev = torch.device('cuda', local)
 
     results = {k: run_workload(k, *sizes[k], args, world, rank, dev) for k in keys}
+    if world == 1 and not args.no_drop_in:
+        for k in keys:
+            print(f'[bench] {k}: drop-in harness-A step', file=sys.stderr, flush=True)
+            results[k]['drop_in'] = run_drop_in(k, *sizes[k], args, dev)
     if rank == 0:
         prim = results[args.model]
         res = {'metric': METRIC, 'value': prim['value'], 'unit': 'points/s', 'n_gpus': world,
@@ -486,6 +547,7 @@ def main():
                'config': dict(prim['config'], rccl_world=dist.get_world_size() if world > 1 else 1),
                'host_enqueue_ms_per_step': prim['host_enqueue_ms_per_step'],
                'roofline': prim['roofline'], 'step_roofline': prim['step_roofline'],
+               'drop_in': prim.get('drop_in'),
                'cpu_baseline': cpu_res.get(args.model)}
         for k in keys[1:]:
             r = results[k]

@@ -64,17 +64,10 @@ int pcs_knn(const float* x, int B, int N, int F, int k, int32_t* out_idx,
 int pcs_knn_workspace(int B, int N, size_t* bytes);
 int pcs_knn_ws(const float* x, int B, int N, int F, int k, int32_t* out_idx,
                void* ws, size_t ws_bytes, void* stream);
-/* Seeds for pcs_knn_seeded on coordinates (F = 3, DGCNN's first graph, which has no previous
- * graph): for each point the ks points around it in its cloud's Morton (Z-order) order,
- * distinct and in range.  xyz (B, N, 3) fp32, seeds (B, N, ks) int32; N <= 8192, ks <= N.
- * Reference: dgcnn.py:7-21 (knn on xyz) -- the lists do not depend on the seeds. */
-int pcs_knn_morton_seeds(const float* xyz, int B, int N, int ks, int32_t* seeds, void* stream);
-
 /* pcs_knn_ws whose rows start from the threshold of a previous neighbour list
  * (seeds (B,N,ks) int32: DGCNN's previous EdgeConv graph, dgcnn.py:183-189 feeding
  * get_graph_feature at :29-56): the same lists as pcs_knn, fewer survivors to merge.
- * Rows whose seeds are out of range, repeated or fewer than k search unseeded.  F = 3
- * rows are seeded too (e.g. by pcs_knn_morton_seeds' spatial neighbours). */
+ * Rows whose seeds are out of range, repeated or fewer than k search unseeded. */
 int pcs_knn_seeded(const float* x, int B, int N, int F, int k, const int32_t* seeds,
                    int ks, int32_t* out_idx, void* ws, size_t ws_bytes, void* stream);
 
@@ -83,11 +76,11 @@ int pcs_knn_seeded(const float* x, int B, int N, int F, int k, const int32_t* se
  * forward: per level l, FPS of the previous level's points (level 0: coords) down to C
  * centroids (pcs_fps, start = starts[l*B + b]), then its nq ball queries (pcs_ball_query
  * against the previous level's points, or the centroids themselves when on_self -- the
- * InvResMLP grouping, models/utils/common.py:288) with their inverse maps
- * (pcs_inverse_index, when inverse), then `event` is recorded (nullable); after all
- * levels, when interp, the 3-NN of each FeaturePropagation from level L-1 down to 0
- * (pcs_knn_select of level l-1's points (coords for l = 0) among level l's centroids, and
- * its inverse map), then nn_event.  Same kernels and arguments as the per-op calls:
+ * InvResMLP grouping, models/utils/common.py:288), then `event` is recorded (nullable);
+ * after all levels, when interp, the ball queries' inverse maps (pcs_inverse_index, when
+ * inverse) and the 3-NN of each FeaturePropagation from level L-1 down to 0 (pcs_knn_select
+ * of level l-1's points (coords for l = 0) among level l's centroids, and its inverse map),
+ * then nn_event (without interp each ball query's map follows it, before `event`).  Same kernels and arguments as the per-op calls:
  * bitwise the same plan.  Outputs caller-owned; the inverse maps share one workspace of
  * pcs_geometry_plan_workspace bytes.  Replaces pcseg.common.GeometryPlan's ~20 calls. */
 #define PCS_GEO_MAX_LEVELS 6

@@ -417,7 +417,8 @@ def test_interp_bwd_csr_with_and_without_forward_map(D2):
 @pytest.mark.parametrize('B,S,k,targets,kind', [(3, 500, 7, 1000, 'random'), (2, 1024, 32, 4096, 'same'),
                                                   (2, 3000, 3, 40000, 'random'), (1, 2048, 32, 50000, 'same'),
                                                   (2, 1, 1, 1, 'random'), (2, 1024, 32, 4096, 'skewed'),
-                                                  (2, 4096, 20, 4096, 'skewed')])
+                                                  (2, 4096, 20, 4096, 'skewed'), (2, 3000, 3, 6000, 'random'),
+                                                  (3, 2048, 20, 8192, 'skewed'), (4, 100, 5, 333, 'same')])
 def test_inverse_index_random_tables(B, S, k, targets, kind):
     """CSR of arbitrary tables: LDS-counter path (targets <= 32768) and global-counter path,
     including the degenerate table where every slot reads the same point, and skewed tables
@@ -471,25 +472,3 @@ def test_fps_sqrt_tie_is_correctly_rounded():
     ref = R.fps_indices(xyz, 1024, start)
     got, _ = ops.fps(xyz.to(DEV), 1024, start.to(DEV))
     assert torch.equal(got.cpu(), ref)
-
-
-@pytest.mark.parametrize('B,N,k,dup', [(2, 4096, 20, False), (3, 1000, 16, False), (2, 4096, 20, True),
-                                       (1, 37, 20, False)])
-def test_knn_xyz_morton_seeded_equals_unseeded(B, N, k, dup):
-    """DGCNN's coordinate graph seeded by Morton-order neighbours (pcs_knn_morton_seeds ->
-    pcs_knn_seeded, F = 3): the seeds are ks distinct in-range points per row including the
-    point itself, and the lists equal the unseeded search bit for bit (also with duplicated
-    points, where distance ties decide by index)."""
-    pts, _, _ = make_batch(B, N, seed=77)
-    xyz = pts[:, :, :3].contiguous()
-    if dup:
-        xyz[:, 1::2] = xyz[:, 0::2][:, :xyz[:, 1::2].shape[1]]
-    xyz = xyz.to(DEV)
-    seeds = ops.knn_morton_seeds(xyz, k)
-    assert seeds is not None and seeds.shape == (B, N, k)
-    s = seeds.cpu().long()
-    assert int(s.min()) >= 0 and int(s.max()) < N
-    srt = s.sort(-1).values
-    assert bool((srt[..., 1:] != srt[..., :-1]).all())                     # distinct
-    assert bool((s == torch.arange(N).view(1, N, 1)).any(-1).all())         # the point itself
-    assert torch.equal(ops.knn(xyz, k, seeds=seeds), ops.knn(xyz, k))
