@@ -359,11 +359,42 @@ bool fused_bwd_ok(int M, int C, int CI, int ldw, const pcs_operand* x, const pcs
     return q->data && q->ld % 4 == 0 && q->ld >= CI && q->s && q->t && q->mean && q->inv;
 }
 
-// persistent grid: 2 blocks per CU, 3 for the narrow prefetching layers (<= 194 VGPRs) and 4
-// for the weight-gradient-only form (<= 128 VGPRs): more tiles' loads in flight per CU
+// the kernel instance for (C, CI, operand mode, da), as the launchers pick it
+template <int C, int CI, bool DA>
+static const void* fb_kernel_ci(int xm) {
+    constexpr bool W = DA && C + CI > 96;
+    if (xm == OP_PLAIN) return reinterpret_cast<const void*>(&fused_bwd_kernel<C, CI, OP_PLAIN, DA, W>);
+    if (xm == OP_BNBWD) return reinterpret_cast<const void*>(&fused_bwd_kernel<C, CI, OP_BNBWD, DA, W>);
+    return reinterpret_cast<const void*>(&fused_bwd_kernel<C, CI, OP_POOLBWD, DA, W>);
+}
+template <int C>
+static const void* fb_kernel_c(int CI, int xm, bool da) {
+    if (!da) return fb_kernel_ci<C, 32, false>(xm);
+    if (CI == 32) return fb_kernel_ci<C, 32, true>(xm);
+    if (CI == 64) return fb_kernel_ci<C, 64, true>(xm);
+    return fb_kernel_ci<C, 128, true>(xm);
+}
+static const void* fb_kernel(int C, int CI, int xm, bool da) {
+    return C == 32 ? fb_kernel_c<32>(CI, xm, da) : (C == 64 ? fb_kernel_c<64>(CI, xm, da) : fb_kernel_c<128>(CI, xm, da));
+}
+
+// persistent grid: as many blocks per CU as are resident at once (the occupancy query: VGPRs and
+// LDS of the instance; the wide layers run one wave per SIMD), the smallest over the operand
+// modes, so the grid -- and the number of BN-backward partials -- depends on (C, CI, da) only
 int fused_bwd_grid(int M, int C, int CI, bool da) {
+    static int occ[3][3][2];                   // [C][CI][da], 0 = not queried
+    const int ci = C == 32 ? 0 : (C == 64 ? 1 : 2), ii = CI == 32 ? 0 : (CI == 64 ? 1 : 2);
+    int& per_cu = occ[ci][ii][da ? 1 : 0];
+    if (per_cu == 0) {
+        int m = 4;
+        for (int xm : {(int)OP_PLAIN, (int)OP_BNBWD, (int)OP_POOLBWD}) {
+            int n = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fb_kernel(C, CI, xm, da), 256, 0) != hipSuccess) n = 1;
+            m = std::min(m, std::max(n, 1));
+        }
+        per_cu = m;
+    }
     const int tiles = (M + FB_BM - 1) / FB_BM;
-    const int per_cu = !da ? 4 : (C + CI <= 96 ? 3 : 1);
     return std::min(tiles, 256 * per_cu);
 }
 

@@ -295,13 +295,13 @@ __global__ __launch_bounds__(512, 1) void wgrad_nt_kernel(const float* __restric
     for (int j = 0; j < XI; ++j) {
         const int e = (wave * XI + j) * 64 + lane;          // chunk index in the slab
         const int r = e / XCPR, c = e % XCPR;
-        xsrc[j] = X + (size_t)(rb + r) * ldx + min(n0 + 4 * (c ^ tn_swz(r)), ldx - 4);
+        xsrc[j] = X + (size_t)(rb + r) * ldx + min(n0 + 4 * (c ^ tn_swz(r)), ((N + 3) & ~3) - 4);
     }
 #pragma unroll
     for (int j = 0; j < YI; ++j) {
         const int e = (wave * YI + j) * 64 + lane;
         const int r = e / YCPR, c = e % YCPR;
-        ysrc[j] = Y + (size_t)(rb + r) * ldy + min(k0 + 4 * (c ^ tn_swz(r)), ldy - 4);
+        ysrc[j] = Y + (size_t)(rb + r) * ldy + min(k0 + 4 * (c ^ tn_swz(r)), ((K + 3) & ~3) - 4);
     }
     const unsigned lbase = lds_addr(lds);
     auto stage = [&](int buf, int slab) {

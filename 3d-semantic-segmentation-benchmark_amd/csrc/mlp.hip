@@ -86,7 +86,11 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void gemm_rows_kernel(GemmArgs g) 
     // every A float4 of this thread sits at the same k offset 4*(tid&7) of a slab, so one
     // coefficient quad per slab serves all of them
     Quad q;
-    const int lda_last = g.a.ld - 4, ldw_last = g.ldw - 4;
+    // clamps keep every load inside the operand's own K (N) channels, rounded up to a quad: a
+    // column-block alias (W + C of an EdgeConv, a row-stride view of a wider buffer) must not
+    // read past its last row's end
+    const int lda_last = ((g.K + 3) & ~3) - 4;
+    const int ldw_last = BT ? ((g.N + 3) & ~3) - 4 : ((g.K + 3) & ~3) - 4;
     const bool bt_scalar = BT && ((g.ldw & 3) || (reinterpret_cast<uintptr_t>(g.W) & 15));
     auto gload = [&](int m0, int k0) {
         const int gk = k0 + 4 * (tid & 7);
@@ -118,7 +122,7 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void gemm_rows_kernel(GemmArgs g) 
                 const int gn = min(n0 + (e >> 3), g.N - 1);
                 if (g.ldw & 3) {      // unpadded weight rows (a stack's first layer, K = 3 + D): scalar loads
                     const float* wr = g.W + (size_t)gn * g.ldw;
-                    const int gk = k0 + 4 * (e & 7), kl = g.ldw - 1;
+                    const int gk = k0 + 4 * (e & 7), kl = g.K - 1;
                     if (kBFull || e < BN * GBK / 4)
                         rb[it] = make_float4(wr[min(gk, kl)], wr[min(gk + 1, kl)], wr[min(gk + 2, kl)],
                                              wr[min(gk + 3, kl)]);
@@ -439,7 +443,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(Operand xo, int N, Operan
     static_assert(NS >= 1 && NS <= 4, "stages");
     float4 rx[NS][XV], rxz[NS][XV], ry[NS][YV], ryz[NS][YV];
     unsigned rxa[NS][XV], rya[NS][YV];
-    const int gnc = min(gn, xo.ld - 4), gkc = min(gk, yo.ld - 4);
+    const int gnc = min(gn, ((N + 3) & ~3) - 4), gkc = min(gk, ((K + 3) & ~3) - 4);   // inside the operands' channels
     auto gload = [&](int st, int r0) {
 #pragma unroll
         for (int it = 0; it < XV; ++it) {
@@ -1016,8 +1020,9 @@ static void gemm_tile(int M, int N, bool bwd, int* bm, int* bn, int* nt = nullpt
     // >= 64K rows) on the wide list despite its register pressure (DGCNN step -2 %).
     // Round 3 re-check: a 64 x 128 tile on EIGHT waves (512 threads, each wave the 32 x 32 block
     // of the 64 x 64 tile; the rebuilt dZ slab loaded and transformed once per 128 output columns
-    // instead of once per 64) made the PointNet++ step 1-2 % slower (same-box A/B, 2 rounds):
-    // kept as an option of the kernel (WM x WN = 8), off in the policy.
+    // instead of once per 64) made the PointNet++ step 1-2 % slower (same-box A/B, 2 rounds).
+    // Round 4: 32 x 128 tiles for the 128-wide data gradients (dZ read once, 4 waves across the
+    // columns): 5.24 vs 5.07 ms.
     if (nt) *nt = 256;
     bool wide;
     const T* c;

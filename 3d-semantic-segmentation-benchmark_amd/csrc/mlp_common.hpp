@@ -62,12 +62,24 @@ __device__ __forceinline__ void load_quad(const Operand& o, int c, int K, Quad& 
     }
 }
 
+// r / pool_k and r % pool_k of a POOLBWD operand: shifts when pool_k is a power of two (every
+// PointNet++-family pool: K = 16, 32, 64), a division otherwise -- the engine's group sizes made the
+// per-element 32-bit divisions a large share of the operand loaders' VALU work
+__device__ __forceinline__ int pool_group(const Operand& o, int r) {
+    const int k = o.pool_k;
+    return (k & (k - 1)) == 0 ? r >> (31 - __clz(k)) : r / k;
+}
+__device__ __forceinline__ unsigned pool_slot(const Operand& o, int r) {
+    const int k = o.pool_k;
+    return (unsigned)((k & (k - 1)) == 0 ? (r & (k - 1)) : r - (r / k) * k);
+}
+
 // raw global loads of one float4 at (row r, channels c..c+3); r and c must be in bounds
 // (callers clamp).  POOLBWD: v = dpool[g][c..], a = the 4 argmax bytes; z only for BNBWD/POOLBWD.
 template <int MODE>
 __device__ __forceinline__ void load_raw(const Operand& o, int r, int c, float4& v, float4& z, unsigned& a) {
     if (MODE == OP_POOLBWD) {
-        const int g = r / o.pool_k;
+        const int g = pool_group(o, r);
         v = *reinterpret_cast<const float4*>(o.data + (size_t)g * o.ld + c);
         a = *reinterpret_cast<const unsigned*>(o.arg + (size_t)g * o.ld + c);
     } else {
@@ -100,7 +112,7 @@ __device__ __forceinline__ float4 xform4(const Operand& o, float4 v, float4 z, u
         return v;
     }
     if (MODE == OP_POOLBWD) {
-        const unsigned k = (unsigned)(r - (r / o.pool_k) * o.pool_k);
+        const unsigned k = pool_slot(o, r);
         v.x = (a & 0xffu) == k ? v.x : 0.f;
         v.y = ((a >> 8) & 0xffu) == k ? v.y : 0.f;
         v.z = ((a >> 16) & 0xffu) == k ? v.z : 0.f;

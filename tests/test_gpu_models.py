@@ -313,10 +313,12 @@ def test_harness_a_loop_with_torch_adam_matches_oracle():
     forward, criterion, backward, step) over several steps: the product's weights are updated in
     place by torch's optimizer between steps (regression: a weight view saved by the forward was
     then rejected by autograd).  The loss trajectory is checked three-way like the gradients:
-    Adam's first steps move every weight by about lr * sign(g), so the reference's own fp32 run
-    drifts from the fp64 one by ~1e-3 after one step (rounding-level gradients of the pre-BN
-    biases flip sign); the GPU must stay within 1e-3 of the fp64 trajectory or within 3x the
-    reference fp32's own distance from it."""
+    Adam's first steps move every weight by about lr * sign(g), so free-running fp32 trajectories
+    drift chaotically from the fp64 one (rounding-level gradients of the pre-BN biases flip sign:
+    ~1e-3 after one step, with no stable ratio between two fp32 runs).  So after each optimizer
+    step the fp64 reference's new weights are written into both fp32 models IN PLACE (the same
+    kind of in-place update the regression is about) and each step's loss is compared from equal
+    weights: within 1e-5 of the fp64 loss (relative) or 3x the reference fp32's own distance from it."""
     pts, labels, lengths = make_batch(2, 2048, seed=108)
     prod, ref = prepare(lambda: pcseg.PointNetpp(14), lambda: R.PointNetpp(14), 5)
     ref64 = R.seeded_init_(R.PointNetpp(14), 5).double().train()
@@ -337,9 +339,14 @@ def test_harness_a_loop_with_torch_adam_matches_oracle():
             l.backward()
         for o in opts:
             o.step()
+        with torch.no_grad():
+            pp, pr = dict(prod.named_parameters()), dict(ref.named_parameters())
+            for k, p64 in ref64.named_parameters():
+                pp[k].copy_(p64.float().to(DEV))
+                pr[k].copy_(p64.float())
         t, e_gpu, e_ref = float(l64), abs(float(lp) - float(l64)), abs(float(l32) - float(l64))
         print(f'step {step}: fp64 {t:.7f}  gpu err {e_gpu:.2e}  ref fp32 err {e_ref:.2e}')
-        assert e_gpu <= max(RTOL * abs(t), 3.0 * e_ref), (step, float(lp), float(l32), t)
+        assert e_gpu <= max(1e-5 * abs(t), 3.0 * e_ref), (step, float(lp), float(l32), t)
 
 
 @pytest.mark.parametrize('name', ['DGCNNWithColor', 'PointNetSeg', 'PointNeXt', 'PointNetppMSG'])
