@@ -21,6 +21,8 @@
 // ceil(L/64) * L wave steps).  Every list ends up in ascending slot order whatever the
 // scatter's order, and the consumers walk a list in that order (fp64 accumulation),
 // so the backward is bitwise reproducible.
+#include <cstdlib>
+
 #include "pcs_common.hpp"
 
 namespace pcs {
@@ -174,55 +176,134 @@ __global__ __launch_bounds__(256) void inverse_sort_kernel(const int32_t* __rest
 // The map of clouds with <= 8192 targets (every PointNet++ / DGCNN map and all but PointNeXt's
 // first ball query) is a stable counting sort of the slots by target, spread over many
 // workgroups and free of atomics on the ordering path, so every list comes out ascending with
-// no sort pass:
-//   1. inverse_count_kernel (chunk c, cloud b; clouds of more than one chunk only): LDS
-//      histogram of chunk c's targets -> hist[b][c][t];
-//   2. inverse_rank_kernel (chunk c, cloud b): each wave owns a contiguous quarter (half) of the
-//      chunk and counts it per target in LDS; each thread then takes a run of targets, adds up
-//      their totals over the chunks (the LDS counts when the cloud is one chunk) and the counts
-//      of the chunks before c, and one block scan turns them into the targets' list offsets
-//      (written by chunk 0) and this chunk's per-wave list bases; finally each wave walks its
-//      slots in order, 64 at a time: the lanes reading the same target are found by a ballot
-//      over the target's bits (a match), a slot's position is its wave base + the number of
-//      matching lanes below it, and the group's last lane advances the base.
-// Slot order = list order: ascending, deterministic.  Chunks hold >= max(4096, targets) slots, so
-// the hist workspace (B * chunks * targets ints) fits in the B*per + B*targets ints the
-// workspace already provides.  One launch for a one-chunk cloud, two otherwise.
-constexpr int kChunkMin = 4096, kRankMaxTargets = 8192;
+// no sort pass.  Clouds of more than one chunk:
+//   1. inverse_count_kernel (chunk c, cloud b): LDS histogram of chunk c's targets -> hist[b][c][t];
+//   2. inverse_scan_kernel (cloud b, 1024 threads, one target per thread and slice of 1024):
+//      offsets[b][t] = b*per + the totals of the earlier targets (block scan), and in place
+//      hist[b][c][t] := offsets[b][t] + the counts of t in chunks < c (chunk c's list base).
+//      Every hist access is a coalesced row of targets; each column is walked once;
+//   3. inverse_rank_kernel (chunk c, cloud b): each wave owns a contiguous quarter (half) of the
+//      chunk and counts it per target in LDS; per-wave bases = the chunk's base + the counts of
+//      the earlier waves; then each wave walks its slots in order, 64 at a time: the lanes
+//      reading the same target are found by a ballot over the target's bits (a match), a
+//      slot's position is its wave base + the number of matching lanes below it, and the
+//      group's last lane advances the base.
+// A cloud of one chunk skips 1-2: the rank kernel scans its own LDS counts into the offsets.
+// Slot order = list order: ascending, deterministic.
+// BATCHED: the three kernels take up to kInvBatch maps (blockIdx.z = map), so a geometry plan's
+// 8 PointNet++ maps or a DGCNN forward's 4 kNN maps cost 3 launches, not 3 per map (the small
+// maps are launch-bound: 10-14 us each alone).  Each map has its own hist region.
+// (Round 4 first fused the scan into the rank kernel for every cloud: each of a cloud's chunks
+// then re-read all its chunks' counts -- quadratic in the chunk count, 0.98 ms per DGCNN map.)
+constexpr int kChunkMin = 4096, kRankMaxTargets = 8192, kInvBatch = 24;
 
 static int rank_chunk(int targets) { return std::max(kChunkMin, (targets + 255) / 256 * 256); }
 
-__global__ __launch_bounds__(256) void inverse_count_kernel(const int32_t* __restrict__ idx, int per, int targets,
-                                                            int chunk, int nch, int* __restrict__ hist) {
+struct InvMap {
+    const int32_t* idx;
+    int32_t* offsets;
+    int32_t* entries;
+    int* hist;                 // [B][nch][targets] (nch > 1)
+    int per, targets, chunk, nch, nbits;
+};
+struct InvBatch {
+    InvMap m[kInvBatch];
+};
+
+__global__ __launch_bounds__(256) void inverse_count_kernel(const InvBatch bat, int nbatch) {
     extern __shared__ int cnt[];
-    const int c = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+    const InvMap& m = bat.m[blockIdx.z];
+    const int c = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, targets = m.targets;
+    if (m.nch <= 1 || c >= m.nch) return;
     for (int t = tid; t < targets; t += 256) cnt[t] = 0;
     __syncthreads();
-    const int32_t* id = idx + (size_t)b * per;
-    const int s1 = min(per, (c + 1) * chunk);
-    for (int s = c * chunk + tid; s < s1; s += 256) {
+    const int32_t* id = m.idx + (size_t)b * m.per;
+    const int s1 = min(m.per, (c + 1) * m.chunk);
+    for (int s = c * m.chunk + tid; s < s1; s += 256) {
         const unsigned t = (unsigned)id[s];
         if (t < (unsigned)targets) atomicAdd(&cnt[t], 1);     // counts: order-free
     }
     __syncthreads();
-    int* h = hist + ((size_t)b * nch + c) * targets;
+    int* h = m.hist + ((size_t)b * m.nch + c) * targets;
     for (int t = tid; t < targets; t += 256) h[t] = cnt[t];
+    (void)nbatch;
+}
+
+// exclusive scan of one value per thread over a 1024-thread block; *all = the block's total
+__device__ __forceinline__ int block_scan_1024(int v, int* wsum, int* all) {
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    int incl = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int u = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += u;
+    }
+    if (lane == 63) wsum[wv] = incl;
+    __syncthreads();
+    int pre = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) {
+        const int x = wsum[w];
+        pre += w < wv ? x : 0;
+        tot += x;
+    }
+    __syncthreads();                                     // wsum is reused by the next call
+    *all = tot;
+    return pre + incl - v;
+}
+
+__global__ __launch_bounds__(1024) void inverse_scan_kernel(const InvBatch bat, int nbatch) {
+    __shared__ int wsum[16];
+    const InvMap& m = bat.m[blockIdx.y];
+    if (m.nch <= 1) return;
+    const int b = blockIdx.x, tid = threadIdx.x, targets = m.targets, nch = m.nch;
+    int* h = m.hist + (size_t)b * nch * targets;
+    int carry = b * m.per;
+    for (int t0 = 0; t0 < targets; t0 += 1024) {
+        const int t = t0 + tid;
+        const bool in = t < targets;
+        int tot = 0;
+        if (in) {
+            int c = 0;
+            for (; c + 4 <= nch; c += 4)
+                tot += h[(size_t)c * targets + t] + h[(size_t)(c + 1) * targets + t] +
+                       h[(size_t)(c + 2) * targets + t] + h[(size_t)(c + 3) * targets + t];
+            for (; c < nch; ++c) tot += h[(size_t)c * targets + t];
+        }
+        int all;
+        int run = carry + block_scan_1024(tot, wsum, &all);
+        if (in) {
+            m.offsets[(size_t)b * targets + t] = run;
+            for (int c = 0; c < nch; c += 8) {
+                int v[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) v[u] = c + u < nch ? h[(size_t)(c + u) * targets + t] : 0;
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    if (c + u < nch) {
+                        h[(size_t)(c + u) * targets + t] = run;
+                        run += v[u];
+                    }
+            }
+        }
+        carry += all;
+    }
+    if (b == nbatch - 1 && tid == 0) m.offsets[(size_t)nbatch * targets] = nbatch * m.per;
 }
 
 template <int W>
-__global__ __launch_bounds__(W * 64) void inverse_rank_kernel(const int32_t* __restrict__ idx, int per, int targets,
-                                                              int chunk, int nch, int nbatch, int nbits,
-                                                              const int* __restrict__ hist,
-                                                              int32_t* __restrict__ offsets,
-                                                              int32_t* __restrict__ entries) {
+__global__ __launch_bounds__(W * 64) void inverse_rank_kernel(const InvBatch bat, int nbatch) {
     constexpr int NT = W * 64;
     extern __shared__ int wb[];                         // [W][targets]: per-wave counts, then bases; + [W]
-    int* wsum = wb + W * targets;
+    const InvMap& m = bat.m[blockIdx.z];
     const int c = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
+    if (c >= m.nch) return;
+    const int targets = m.targets, per = m.per, chunk = m.chunk, nch = m.nch;
+    int* wsum = wb + W * targets;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     for (int t = tid; t < W * targets; t += NT) wb[t] = 0;
     __syncthreads();
-    const int32_t* id = idx + (size_t)b * per;
+    const int32_t* id = m.idx + (size_t)b * per;
     const int sub = chunk / W;                          // chunk is a multiple of 256
     const int ws = min(per, c * chunk + wave * sub), we = min(per, c * chunk + (wave + 1) * sub);
     int* mb = wb + wave * targets;
@@ -231,56 +312,50 @@ __global__ __launch_bounds__(W * 64) void inverse_rank_kernel(const int32_t* __r
         if (t < (unsigned)targets) atomicAdd(&mb[t], 1);
     }
     __syncthreads();
-    // this thread's run of targets: totals over the cloud's chunks and the counts before chunk c
-    const int pt = (targets + NT - 1) / NT;
-    const int a = min(tid * pt, targets), z = min(a + pt, targets);
-    const int* hb = hist + (size_t)b * nch * targets;
-    auto totals = [&](int t, int& pre) {
-        int tot = 0;
-        pre = 0;
-        if (nch == 1) {
+    if (nch > 1) {
+        // the chunk's list bases (inverse_scan_kernel) -> per-wave bases
+        const int* hc = m.hist + ((size_t)b * nch + c) * targets;
+        for (int t = tid; t < targets; t += NT) {
+            int run = hc[t];
 #pragma unroll
-            for (int w = 0; w < W; ++w) tot += wb[w * targets + t];
-        } else {
-            for (int cc = 0; cc < nch; ++cc) {
-                const int v = hb[(size_t)cc * targets + t];
-                pre += cc < c ? v : 0;
-                tot += v;
+            for (int w = 0; w < W; ++w) {
+                const int v = wb[w * targets + t];
+                wb[w * targets + t] = run;
+                run += v;
             }
         }
-        return tot;
-    };
-    int local = 0;
-    for (int t = a; t < z; ++t) {
-        int pre;
-        local += totals(t, pre);
-    }
-    int incl = local;
+    } else {
+        // one chunk: this block scans its own counts; each thread a run of consecutive targets
+        const int pt = (targets + NT - 1) / NT;
+        const int a = min(tid * pt, targets), z = min(a + pt, targets);
+        int local = 0;
+        for (int t = a; t < z; ++t)
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const int v = __shfl_up(incl, d, 64);
-        if (lane >= d) incl += v;
-    }
-    if (lane == 63) wsum[wave] = incl;
-    __syncthreads();
-    int run = b * per + incl - local;
-    for (int w = 0; w < wave; ++w) run += wsum[w];
-    for (int t = a; t < z; ++t) {
-        int pre;
-        const int tot = totals(t, pre);
-        if (c == 0) offsets[(size_t)b * targets + t] = run;
-        int base = run + pre;
+            for (int w = 0; w < W; ++w) local += wb[w * targets + t];
+        int incl = local;
 #pragma unroll
-        for (int w = 0; w < W; ++w) {
-            const int v = wb[w * targets + t];
-            wb[w * targets + t] = base;
-            base += v;
+        for (int d = 1; d < 64; d <<= 1) {
+            const int v = __shfl_up(incl, d, 64);
+            if (lane >= d) incl += v;
         }
-        run += tot;
+        if (lane == 63) wsum[wave] = incl;
+        __syncthreads();
+        int run = b * per + incl - local;
+        for (int w = 0; w < wave; ++w) run += wsum[w];
+        for (int t = a; t < z; ++t) {
+            m.offsets[(size_t)b * targets + t] = run;
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+                const int v = wb[w * targets + t];
+                wb[w * targets + t] = run;
+                run += v;
+            }
+        }
+        if (b == nbatch - 1 && tid == 0) m.offsets[(size_t)nbatch * targets] = nbatch * per;
     }
-    if (b == nbatch - 1 && c == 0 && tid == 0) offsets[(size_t)nbatch * targets] = nbatch * per;
     __syncthreads();
-    const int gbase = b * per;
+    const int gbase = b * per, nbits = m.nbits;
+    int32_t* entries = m.entries;
     const unsigned long long lt = lanemask_lt();
     for (int g = ws; g < we; g += 64) {
         const int s = g + lane;
@@ -289,8 +364,8 @@ __global__ __launch_bounds__(W * 64) void inverse_rank_kernel(const int32_t* __r
         unsigned long long peers = ballot(ok);
         for (int bit = 0; bit < nbits; ++bit) {
             const bool on = (t >> bit) & 1;
-            const unsigned long long m = ballot(on);
-            peers &= on ? m : ~m;
+            const unsigned long long mk = ballot(on);
+            peers &= on ? mk : ~mk;
         }
         const int rank = popc64(peers & lt), cnt = popc64(peers);
         if (ok) {
@@ -299,6 +374,68 @@ __global__ __launch_bounds__(W * 64) void inverse_rank_kernel(const int32_t* __r
             if (rank == cnt - 1) mb[t] = p + cnt;      // the group's last lane advances the base
         }
     }
+}
+
+// hist bytes of one map, 256-B aligned (0 for a one-chunk cloud).  B * nch * targets <= B * (per +
+// targets) ints (chunk >= targets): within the single-map workspace, inv_ws_bytes below
+static size_t hist_region(int B, int per, int targets) {
+    const int chunk = rank_chunk(targets), nch = (per + chunk - 1) / chunk;
+    return nch > 1 ? ((size_t)B * nch * targets * 4 + 255) / 256 * 256 : 0;
+}
+
+// enqueue the counting sort of maps[0, n) (every targets <= kRankMaxTargets, n <= kInvBatch);
+// hist regions carved from ws (hist_region each); returns the bytes carved
+static size_t rank_batch(const pcs_inverse_map* maps, int n, int B, char* ws, hipStream_t s) {
+    InvBatch bat{};
+    int maxnch = 1, maxT = 1, maxT4 = 0, maxT8 = 0;
+    bool any_multi = false;
+    size_t off = 0;
+    for (int i = 0; i < n; ++i) {
+        InvMap& m = bat.m[i];
+        m.idx = maps[i].idx;
+        m.offsets = maps[i].offsets;
+        m.entries = maps[i].entries;
+        m.per = maps[i].per_batch;
+        m.targets = maps[i].targets;
+        m.chunk = rank_chunk(m.targets);
+        m.nch = (m.per + m.chunk - 1) / m.chunk;
+        m.nbits = 0;
+        while ((1 << m.nbits) < m.targets) ++m.nbits;
+        m.hist = reinterpret_cast<int*>(ws + off);
+        off += hist_region(B, m.per, m.targets);
+        maxnch = std::max(maxnch, m.nch);
+        maxT = std::max(maxT, m.targets);
+        if (m.targets <= 4096) maxT4 = std::max(maxT4, m.targets);
+        else maxT8 = std::max(maxT8, m.targets);
+        any_multi |= m.nch > 1;
+    }
+    if (any_multi) {
+        hipLaunchKernelGGL(inverse_count_kernel, dim3(maxnch, B, n), dim3(256), maxT * sizeof(int), s, bat, B);
+        hipLaunchKernelGGL(inverse_scan_kernel, dim3(B, n), dim3(1024), 0, s, bat, B);
+    }
+    // rank: 4 waves for <= 4096 targets (64 KB of LDS counters), 2 above; one launch per width
+    // (the other width's maps get nch = 0 in its copy: their blocks exit at once)
+    for (int W : {4, 2}) {
+        const int mt = W == 4 ? maxT4 : maxT8;
+        if (!mt) continue;
+        InvBatch bw = bat;
+        int nchw = 1;
+        for (int i = 0; i < n; ++i) {
+            if ((bw.m[i].targets <= 4096) != (W == 4)) bw.m[i].nch = 0;
+            nchw = std::max(nchw, bw.m[i].nch);
+        }
+        const size_t lds = ((size_t)W * mt + W) * sizeof(int);
+        if (W == 4)
+            hipLaunchKernelGGL(inverse_rank_kernel<4>, dim3(nchw, B, n), dim3(256), lds, s, bw, B);
+        else {
+            static const hipError_t attr = hipFuncSetAttribute(
+                reinterpret_cast<const void*>(&inverse_rank_kernel<2>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                (2 * kRankMaxTargets + 2) * (int)sizeof(int));
+            (void)attr;
+            hipLaunchKernelGGL(inverse_rank_kernel<2>, dim3(nchw, B, n), dim3(128), lds, s, bw, B);
+        }
+    }
+    return off;
 }
 
 // Gather backward over the inverse maps: ONE WAVE PER SOURCE POINT, lanes over channels,
@@ -495,10 +632,55 @@ __global__ __launch_bounds__(256) void edge_bwd_csr_kernel(const float* __restri
 
 using namespace pcs;
 
-// workspace bytes of pcs_inverse_index: the scatter's scratch lists (one int per slot) and,
-// when one cloud's targets overflow the LDS counters, the global counters
+// workspace bytes of one map: the legacy path's scatter scratch (one int per slot) + global
+// counters, or the counting sort's chunk histogram, whichever is larger
 static size_t inv_ws_bytes(long long n_slots, long long n_targets) {
-    return ((size_t)n_slots * 4 + 255) / 256 * 256 + (size_t)n_targets * 4;
+    return ((size_t)n_slots * 4 + 255) / 256 * 256 + ((size_t)n_targets * 4 + 255) / 256 * 256;
+}
+
+static int check_map(const pcs_inverse_map& m, int B, const char* who) {
+    PCS_CHECK_ARG(m.per_batch >= 1 && m.targets >= 1, "%s: bad sizes per_batch=%d targets=%d", who, m.per_batch,
+                  m.targets);
+    PCS_CHECK_ARG((long long)B * m.per_batch < (1ll << 31) && (long long)B * m.targets < (1ll << 31),
+                  "%s: too many slots/targets", who);
+    PCS_CHECK_ARG(m.idx && m.offsets && m.entries, "%s: null pointer", who);
+    return 0;
+}
+
+// workspace of a batch: the counting-sort maps' hist regions side by side (they are live
+// together), or the largest legacy map's scratch (those run one after another, after them)
+static size_t batch_ws_bytes(const pcs_inverse_map* maps, int n, int B) {
+    size_t rank = 0, legacy = 256;
+    for (int i = 0; i < n; ++i) {
+        if (maps[i].targets <= kRankMaxTargets)
+            rank += hist_region(B, maps[i].per_batch, maps[i].targets);
+        else
+            legacy = std::max(legacy, inv_ws_bytes((long long)B * maps[i].per_batch, (long long)B * maps[i].targets));
+    }
+    return std::max(rank, legacy);
+}
+
+// one map of more than kRankMaxTargets targets: LDS (or global) counting scatter + list sort
+static void legacy_map(const pcs_inverse_map& m, int B, void* workspace, hipStream_t s) {
+    const long long n = (long long)B * m.per_batch, T = (long long)B * m.targets;
+    int32_t* scratch = static_cast<int32_t*>(workspace);
+    // algorithmic bytes of the map (both kernels): idx read, entries + offsets written
+    ProbeScope pr(s, 0.0, 8.0 * (double)n + 4.0 * (double)(T + 1),
+                  m.targets <= kInvLdsTargets ? "pcs::inverse_index+sort<true>" : "pcs::inverse_index+sort<false>");
+    int* gcnt = reinterpret_cast<int*>(static_cast<char*>(workspace) + ((size_t)n * 4 + 255) / 256 * 256);
+    if (m.targets <= kInvLdsTargets) {
+        static const hipError_t attr = hipFuncSetAttribute(
+            reinterpret_cast<const void*>(&inverse_index_kernel<true>), hipFuncAttributeMaxDynamicSharedMemorySize,
+            (32 + kInvLdsTargets) * (int)sizeof(int));
+        (void)attr;
+        hipLaunchKernelGGL(inverse_index_kernel<true>, dim3(B), dim3(kInvThreads), (32 + m.targets) * sizeof(int), s,
+                           m.idx, m.per_batch, m.targets, B, m.offsets, (int*)nullptr, scratch);
+    } else {
+        hipLaunchKernelGGL(inverse_index_kernel<false>, dim3(B), dim3(kInvThreads), 32 * sizeof(int), s, m.idx,
+                           m.per_batch, m.targets, B, m.offsets, gcnt, scratch);
+    }
+    hipLaunchKernelGGL(inverse_sort_kernel, dim3((unsigned)((T + 3) / 4)), dim3(256), 0, s, m.offsets, scratch, (int)T,
+                       m.entries);
 }
 
 PCS_API int pcs_inverse_index_workspace(long long n_slots, long long n_targets, size_t* bytes) {
@@ -506,6 +688,49 @@ PCS_API int pcs_inverse_index_workspace(long long n_slots, long long n_targets, 
                   "pcs_inverse_index_workspace: bad sizes");
     *bytes = inv_ws_bytes(n_slots, n_targets);
     return 0;
+}
+
+PCS_API int pcs_inverse_index_batch_workspace(const pcs_inverse_map* maps, int nmaps, int B, size_t* bytes) {
+    PCS_CHECK_ARG(maps && nmaps >= 1 && B >= 1 && bytes, "pcs_inverse_index_batch_workspace: bad arguments");
+    for (int i = 0; i < nmaps; ++i)
+        PCS_CHECK_ARG(maps[i].per_batch >= 1 && maps[i].targets >= 1, "pcs_inverse_index_batch_workspace: map %d", i);
+    *bytes = batch_ws_bytes(maps, nmaps, B);
+    return 0;
+}
+
+// the inverse maps of several neighbour tables of B clouds each (see pcs_inverse_index), in as
+// few launches as their shapes allow: 3 for any number of <= 8192-target maps
+PCS_API int pcs_inverse_index_batch(const pcs_inverse_map* maps, int nmaps, int B, void* workspace, size_t ws_bytes,
+                                    void* stream) {
+    PCS_CHECK_ARG(maps && nmaps >= 1 && B >= 1, "pcs_inverse_index_batch: bad arguments");
+    for (int i = 0; i < nmaps; ++i)
+        if (int e = check_map(maps[i], B, "pcs_inverse_index_batch")) return e;
+    const size_t need = batch_ws_bytes(maps, nmaps, B);
+    PCS_CHECK_ARG(workspace && ws_bytes >= need, "pcs_inverse_index_batch: workspace %zu < %zu bytes", ws_bytes, need);
+    hipStream_t s = as_stream(stream);
+    pcs_inverse_map rk[kInvBatch];
+    int nr = 0;
+    double bytes = 0.0;
+    for (int i = 0; i < nmaps; ++i)
+        if (maps[i].targets <= kRankMaxTargets)
+            bytes += 12.0 * B * (double)maps[i].per_batch + 4.0 * ((double)B * maps[i].targets + 1);
+    {
+        // chunked stable counting sort (above): idx read twice, entries + offsets written
+        ProbeScope pr(s, 0.0, bytes, "pcs::inverse_index<rank>");
+        char* ws = static_cast<char*>(workspace);
+        for (int i = 0; i < nmaps; ++i) {
+            if (maps[i].targets > kRankMaxTargets) continue;
+            rk[nr++] = maps[i];
+            if (nr == kInvBatch) {        // the next group's hist regions follow this group's
+                ws += rank_batch(rk, nr, B, ws, s);
+                nr = 0;
+            }
+        }
+        if (nr) rank_batch(rk, nr, B, ws, s);
+    }
+    for (int i = 0; i < nmaps; ++i)
+        if (maps[i].targets > kRankMaxTargets) legacy_map(maps[i], B, workspace, s);
+    return launch_status("pcs_inverse_index_batch");
 }
 
 // idx: (B * per_batch) int32 neighbour table, values in [0, targets); offsets (B*targets + 1),
@@ -519,50 +744,8 @@ PCS_API int pcs_inverse_index(const int32_t* idx, int B, int per_batch, int targ
     PCS_CHECK_ARG(idx && offsets && entries, "pcs_inverse_index: null pointer");
     PCS_CHECK_ARG(workspace && ws_bytes >= inv_ws_bytes(n, T), "pcs_inverse_index: workspace %zu < %zu bytes",
                   ws_bytes, inv_ws_bytes(n, T));
-    hipStream_t s = as_stream(stream);
-    int32_t* scratch = static_cast<int32_t*>(workspace);
-    if (targets <= kRankMaxTargets) {
-        // chunked stable counting sort (above): idx read twice, entries + offsets written
-        ProbeScope pr(s, 0.0, 12.0 * (double)n + 4.0 * (double)(T + 1), "pcs::inverse_index<rank>");
-        const int chunk = rank_chunk(targets), nch = (per_batch + chunk - 1) / chunk;
-        int* hist = reinterpret_cast<int*>(workspace);   // B * nch * targets <= n + T ints (chunk >= targets)
-        PCS_CHECK_ARG((size_t)B * nch * targets * 4 <= ws_bytes, "pcs_inverse_index: chunk histogram overflows");
-        int nbits = 0;
-        while ((1 << nbits) < targets) ++nbits;
-        if (nch > 1)
-            hipLaunchKernelGGL(inverse_count_kernel, dim3(nch, B), dim3(256), targets * sizeof(int), s, idx, per_batch,
-                               targets, chunk, nch, hist);
-        if (targets <= 4096)
-            hipLaunchKernelGGL(inverse_rank_kernel<4>, dim3(nch, B), dim3(256), (4 * targets + 4) * sizeof(int), s,
-                               idx, per_batch, targets, chunk, nch, B, nbits, hist, offsets, entries);
-        else {
-            static const hipError_t attr = hipFuncSetAttribute(
-                reinterpret_cast<const void*>(&inverse_rank_kernel<2>), hipFuncAttributeMaxDynamicSharedMemorySize,
-                (2 * kRankMaxTargets + 2) * (int)sizeof(int));
-            (void)attr;
-            hipLaunchKernelGGL(inverse_rank_kernel<2>, dim3(nch, B), dim3(128), (2 * targets + 2) * sizeof(int), s,
-                               idx, per_batch, targets, chunk, nch, B, nbits, hist, offsets, entries);
-        }
-        return launch_status("pcs_inverse_index");
-    }
-    // algorithmic bytes of the map (both kernels): idx read, entries + offsets written
-    ProbeScope pr(s, 0.0, 8.0 * (double)n + 4.0 * (double)(T + 1),
-                  targets <= kInvLdsTargets ? "pcs::inverse_index+sort<true>" : "pcs::inverse_index+sort<false>");
-    int* gcnt = reinterpret_cast<int*>(static_cast<char*>(workspace) + ((size_t)n * 4 + 255) / 256 * 256);
-    if (targets <= kInvLdsTargets) {
-        static const hipError_t attr = hipFuncSetAttribute(
-            reinterpret_cast<const void*>(&inverse_index_kernel<true>), hipFuncAttributeMaxDynamicSharedMemorySize,
-            (32 + kInvLdsTargets) * (int)sizeof(int));
-        (void)attr;
-        hipLaunchKernelGGL(inverse_index_kernel<true>, dim3(B), dim3(kInvThreads), (32 + targets) * sizeof(int), s,
-                           idx, per_batch, targets, B, offsets, (int*)nullptr, scratch);
-    } else {
-        hipLaunchKernelGGL(inverse_index_kernel<false>, dim3(B), dim3(kInvThreads), 32 * sizeof(int), s, idx,
-                           per_batch, targets, B, offsets, gcnt, scratch);
-    }
-    hipLaunchKernelGGL(inverse_sort_kernel, dim3((unsigned)((T + 3) / 4)), dim3(256), 0, s, offsets, scratch, (int)T,
-                       entries);
-    return launch_status("pcs_inverse_index");
+    const pcs_inverse_map m{idx, per_batch, targets, offsets, entries};
+    return pcs_inverse_index_batch(&m, 1, B, workspace, ws_bytes, stream);
 }
 
 // grad_feats (B, N, D) = backward of group's feature gather (overwrites; no zero fill needed).

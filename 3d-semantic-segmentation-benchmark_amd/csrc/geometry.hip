@@ -7,7 +7,7 @@
 // Python path: bitwise the same plan), recording one caller event per level (the forward's SA
 // level l waits on it) and one after the 3-NN.  With interp, every level's FPS and ball queries
 // come first and the inverse maps (backward-only) after them, so a level's wait and the next
-// level's FPS never queue behind a map.
+// level's FPS never queue behind a map: all maps are one batched call at the end.
 //
 // One call replaces ~20 Python-level launches (each with its own allocation, ctypes
 // marshalling and caching-allocator stream bookkeeping): about 0.5 ms of host enqueue per
@@ -18,10 +18,6 @@
 #include <algorithm>
 
 namespace pcs {
-
-static size_t inv_scratch_bytes(long long n_slots, long long n_targets) {
-    return ((size_t)n_slots * 4 + 255) / 256 * 256 + (size_t)n_targets * 4;
-}
 
 static int check_plan(int B, int N, const pcs_geo_level* lv, int L) {
     PCS_CHECK_ARG(B >= 1 && N >= 1 && lv && L >= 1 && L <= PCS_GEO_MAX_LEVELS, "pcs_geometry_plan: bad sizes B=%d N=%d L=%d",
@@ -42,12 +38,31 @@ static int check_plan(int B, int N, const pcs_geo_level* lv, int L) {
     return 0;
 }
 
-// the inverse map of level v's ball query q (np = the previous level's point count)
-static int ball_inverse(const pcs_geo_level& v, int q, int B, int np, void* ws, size_t ws_bytes, void* stream) {
-    const int C = (int)v.C, K = (int)v.K[q], ns = v.on_self[q] ? C : np;
-    PCS_CHECK_ARG(v.ball_off[q] && v.ball_ent[q], "pcs_geometry_plan: query %d: null map", q);
-    return pcs_inverse_index(v.ball[q], B, C * K, ns, v.ball_off[q], v.ball_ent[q], ws, ws_bytes, stream);
+// every inverse map of the plan (ball queries level by level, then with interp the 3-NN
+// tables FP_L .. FP_1), as one pcs_inverse_index_batch: 3 launches for all of them
+static int plan_maps(int B, int N, const pcs_geo_level* lv, int L, int interp, pcs_inverse_map* maps, int* n) {
+    int np = N, k = 0;
+    for (int l = 0; l < L; ++l) {
+        const pcs_geo_level& v = lv[l];
+        for (int q = 0; q < v.nq; ++q) {
+            PCS_CHECK_ARG(v.ball_off[q] && v.ball_ent[q], "pcs_geometry_plan: level %d query %d: null map", l, q);
+            maps[k++] = pcs_inverse_map{v.ball[q], (int)(v.C * v.K[q]), v.on_self[q] ? (int)v.C : np, v.ball_off[q],
+                                        v.ball_ent[q]};
+        }
+        np = (int)v.C;
+    }
+    if (interp)
+        for (int l = L - 1; l >= 0; --l) {
+            const pcs_geo_level& v = lv[l];
+            const int nf = l == 0 ? N : (int)lv[l - 1].C;
+            PCS_CHECK_ARG(v.nn_off && v.nn_ent, "pcs_geometry_plan: level %d: null 3-NN map", l);
+            maps[k++] = pcs_inverse_map{v.nn_idx, nf * 3, (int)v.C, v.nn_off, v.nn_ent};
+        }
+    *n = k;
+    return 0;
 }
+
+constexpr int kPlanMaps = PCS_GEO_MAX_LEVELS * (PCS_GEO_MAX_QUERIES + 1);
 
 }  // namespace pcs
 
@@ -59,15 +74,22 @@ PCS_API int pcs_geometry_plan_workspace(int B, int N, const pcs_geo_level* lv, i
     PCS_CHECK_ARG(bytes, "pcs_geometry_plan_workspace: null bytes");
     size_t m = 256;
     if (inverse) {
-        long long prev = N;
+        pcs_inverse_map maps[kPlanMaps];
+        int n = 0;
+        // sizes only: the output pointers may still be null here
+        int np = N;
         for (int l = 0; l < L; ++l) {
-            for (int q = 0; q < lv[l].nq; ++q) {
-                const long long src = lv[l].on_self[q] ? lv[l].C : prev;
-                m = std::max(m, inv_scratch_bytes((long long)B * lv[l].C * lv[l].K[q], (long long)B * src));
-            }
-            if (interp) m = std::max(m, inv_scratch_bytes((long long)B * prev * 3, (long long)B * lv[l].C));
-            prev = lv[l].C;
+            for (int q = 0; q < lv[l].nq; ++q)
+                maps[n++] = pcs_inverse_map{nullptr, (int)(lv[l].C * lv[l].K[q]), lv[l].on_self[q] ? (int)lv[l].C : np,
+                                            nullptr, nullptr};
+            np = (int)lv[l].C;
         }
+        if (interp)
+            for (int l = L - 1; l >= 0; --l)
+                maps[n++] = pcs_inverse_map{nullptr, (l == 0 ? N : (int)lv[l - 1].C) * 3, (int)lv[l].C, nullptr, nullptr};
+        if (n)
+            if (int e = pcs_inverse_index_batch_workspace(maps, n, B, &m)) return e;
+        m = std::max(m, (size_t)256);
     }
     *bytes = m;
     return 0;
@@ -96,8 +118,16 @@ PCS_API int pcs_geometry_plan(const float* coords, int B, int N, const int32_t* 
             const int K = (int)v.K[q];
             PCS_CHECK_ARG(v.ball[q], "pcs_geometry_plan: level %d query %d: null ball output", l, q);
             if (int e = pcs_ball_query(v.cent, src, B, C, ns, (float)v.r2[q], K, v.ball[q], stream)) return e;
-            if (inverse && !interp)
-                if (int e = ball_inverse(v, q, B, np, ws, ws_bytes, stream)) return e;
+        }
+        if (inverse && !interp && v.nq) {
+            // no 3-NN: the level's maps before its event (the backward's wait covers them)
+            pcs_inverse_map maps[PCS_GEO_MAX_QUERIES];
+            for (int q = 0; q < v.nq; ++q) {
+                PCS_CHECK_ARG(v.ball_off[q] && v.ball_ent[q], "pcs_geometry_plan: level %d query %d: null map", l, q);
+                maps[q] = pcs_inverse_map{v.ball[q], C * (int)v.K[q], v.on_self[q] ? C : np, v.ball_off[q],
+                                          v.ball_ent[q]};
+            }
+            if (int e = pcs_inverse_index_batch(maps, (int)v.nq, B, ws, ws_bytes, stream)) return e;
         }
         if (v.event && hipEventRecord(static_cast<hipEvent_t>(v.event), st) != hipSuccess)
             return launch_status("pcs_geometry_plan: event record");
@@ -105,15 +135,6 @@ PCS_API int pcs_geometry_plan(const float* coords, int B, int N, const int32_t* 
         np = C;
     }
     if (interp) {
-        // the ball queries' inverse maps (read only by the backward) after every level's FPS and
-        // ball queries: the forward's level-l wait then does not include them, nor does the next
-        // level's FPS queue behind them; nn_event (after the 3-NN and their maps) covers them all
-        np = N;
-        for (int l = 0; l < L && inverse; ++l) {
-            for (int q = 0; q < lv[l].nq; ++q)
-                if (int e = ball_inverse(lv[l], q, B, np, ws, ws_bytes, stream)) return e;
-            np = (int)lv[l].C;
-        }
         // FP_L ... FP_1 (the reference's call order): 3-NN of level l's points among level l+1's
         for (int l = L - 1; l >= 0; --l) {
             const pcs_geo_level& v = lv[l];
@@ -121,14 +142,18 @@ PCS_API int pcs_geometry_plan(const float* coords, int B, int N, const int32_t* 
             const int nf = l == 0 ? N : (int)lv[l - 1].C;
             PCS_CHECK_ARG(v.nn_idx && v.nn_dist, "pcs_geometry_plan: level %d: null 3-NN output", l);
             if (int e = pcs_knn_select(fine, v.cent, B, nf, (int)v.C, 3, v.nn_idx, v.nn_dist, stream)) return e;
-            if (inverse) {
-                PCS_CHECK_ARG(v.nn_off && v.nn_ent, "pcs_geometry_plan: level %d: null 3-NN map", l);
-                if (int e = pcs_inverse_index(v.nn_idx, B, nf * 3, (int)v.C, v.nn_off, v.nn_ent, ws, ws_bytes, stream))
-                    return e;
-            }
         }
-        if (nn_event && hipEventRecord(static_cast<hipEvent_t>(nn_event), st) != hipSuccess)
-            return launch_status("pcs_geometry_plan: event record");
     }
+    if (inverse && interp) {
+        // the inverse maps (read only by the backward) after every FPS, ball query and 3-NN: no
+        // level's wait and no FPS queues behind them; nn_event (after them) covers them all
+        pcs_inverse_map maps[kPlanMaps];
+        int n = 0;
+        if (int e = plan_maps(B, N, lv, L, interp, maps, &n)) return e;
+        if (n)
+            if (int e = pcs_inverse_index_batch(maps, n, B, ws, ws_bytes, stream)) return e;
+    }
+    if (interp && nn_event && hipEventRecord(static_cast<hipEvent_t>(nn_event), st) != hipSuccess)
+        return launch_status("pcs_geometry_plan: event record");
     return launch_status("pcs_geometry_plan");
 }

@@ -45,6 +45,12 @@ class Operand(ctypes.Structure):
                 ('arg', P), ('pool_k', ctypes.c_int)]
 
 
+class InverseMap(ctypes.Structure):
+    """pcs_inverse_map (include/pcseg.h): one neighbour table of a batched inverse-map call."""
+    _fields_ = [('idx', P), ('per_batch', ctypes.c_int), ('targets', ctypes.c_int), ('offsets', P),
+                ('entries', P)]
+
+
 OP_PLAIN, OP_BNACT, OP_BNBWD, OP_POOLBWD = 0, 1, 2, 3
 OPP = ctypes.POINTER(Operand)
 
@@ -111,6 +117,8 @@ SIGNATURES = {
     # inverse neighbour maps
     'pcs_inverse_index_workspace': [I64, I64, P],
     'pcs_inverse_index': [P, I32, I32, I32, P, P, P, ctypes.c_size_t, P],
+    'pcs_inverse_index_batch_workspace': [P, I32, I32, P],
+    'pcs_inverse_index_batch': [P, I32, I32, P, ctypes.c_size_t, P],
     'pcs_group_bwd_csr': [P, I32, P, P, I32, I32, I32, P, P],
     'pcs_interp_bwd_csr': [P, I32, I32, P, P, P, I32, I32, I32, P, P],
     # block batches

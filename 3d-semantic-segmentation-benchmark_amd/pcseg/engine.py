@@ -633,11 +633,11 @@ class EdgeInverseBatch:
         side = side_stream(dev)
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):
-            for h in pend:
-                idx, N = h.pop()
-                off, ent = ops.inverse_index(idx, N)
-                ev = torch.cuda.Event()
-                ev.record(side)
+            tabs = [h.pop() for h in pend]
+            maps = ops.inverse_index_batch(tabs)       # one native call, 3 launches for all
+            ev = torch.cuda.Event()
+            ev.record(side)
+            for h, (idx, _), (off, ent) in zip(pend, tabs, maps):
                 idx.record_stream(side)
                 h.extend((off, ent, ev))
 

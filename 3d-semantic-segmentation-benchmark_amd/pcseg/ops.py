@@ -106,8 +106,8 @@ def inverse_index(idx: torch.Tensor, targets: int, out=None):
     B = idx.shape[0]
     per = idx[0].numel()
     n, T = B * per, B * targets
-    # pcs_inverse_index_workspace: the scatter scratch (n ints, 256-B aligned) + T counters
-    nws = (n * 4 + 255) // 256 * 256 + T * 4
+    # pcs_inverse_index_workspace: the scatter scratch (n ints) + T counters, each 256-B aligned
+    nws = (n * 4 + 255) // 256 * 256 + (T * 4 + 255) // 256 * 256
     if out is None:
         # one int32 allocation: [offsets (T+1) | entries (n) | workspace], 256-B aligned parts
         o_ent = (T + 1 + 63) // 64 * 64
@@ -122,6 +122,43 @@ def inverse_index(idx: torch.Tensor, targets: int, out=None):
     call('pcs_inverse_index', ptr(idx), B, per, targets, ptr(offsets), ptr(entries), wsp, nws,
          stream_ptr(idx.device))
     return offsets, entries
+
+
+def inverse_index_batch(tables) -> list:
+    """Inverse maps of several neighbour tables in one native call (pcs_inverse_index_batch: 3
+    launches for all maps of <= 8192 targets).  tables = [(idx (B, S, k) int32, targets), ...],
+    one B for all; returns [(offsets, entries), ...] as inverse_index would, all views of one
+    int32 allocation on the current stream."""
+    import ctypes
+    from ._lib import InverseMap
+    B = tables[0][0].shape[0]
+    dev = tables[0][0].device
+    idxs = []
+    for idx, _ in tables:
+        check_cuda(idx)
+        if idx.shape[0] != B:
+            raise ValueError('inverse_index_batch: one batch size for all tables')
+        idxs.append(_c(idx if idx.dtype == torch.int32 else idx.to(torch.int32)))
+    maps = (InverseMap * len(tables))()
+    sizes, o = [], 0
+    for i, (idx, (_, T)) in enumerate(zip(idxs, tables)):
+        per = idx[0].numel()
+        maps[i].per_batch, maps[i].targets = per, T
+        sizes.append((o, B * T + 1))
+        o += (B * T + 1 + 63) // 64 * 64
+        sizes.append((o, B * per))
+        o += (B * per + 63) // 64 * 64
+    nws = ctypes.c_size_t(0)
+    call('pcs_inverse_index_batch_workspace', maps, len(tables), B, ctypes.byref(nws))
+    buf = torch.empty(o + (nws.value + 3) // 4, dtype=torch.int32, device=dev)
+    out = []
+    for i, idx in enumerate(idxs):
+        (oo, no), (oe, ne) = sizes[2 * i], sizes[2 * i + 1]
+        off, ent = buf[oo:oo + no], buf[oe:oe + ne]
+        maps[i].idx, maps[i].offsets, maps[i].entries = idx.data_ptr(), off.data_ptr(), ent.data_ptr()
+        out.append((off, ent))
+    call('pcs_inverse_index_batch', maps, len(tables), B, buf.data_ptr() + 4 * o, nws.value, stream_ptr(dev))
+    return out
 
 
 # ------------------------------------------------------------------ differentiable gathers

@@ -414,6 +414,22 @@ int pcs_inverse_index_workspace(long long n_slots, long long n_targets,
 int pcs_inverse_index(const int32_t* idx, int B, int per_batch, int targets,
                       int32_t* offsets, int32_t* entries, void* workspace,
                       size_t ws_bytes, void* stream);
+/* Several maps of B clouds each in one call: the maps of <= 8192 targets share three
+ * launches (chunk counts, scan, ranked scatter; blockIdx.z = map), larger ones follow one
+ * by one.  Same outputs as one pcs_inverse_index per map.  Replaces the per-table
+ * index/sort loop of the reference's scatter-add backward (common.py:64-65, :120-122;
+ * dgcnn.py:60-77 get_graph_feature's gather) -- there autograd's index_add. */
+typedef struct pcs_inverse_map {
+    const int32_t* idx;    /* (B * per_batch) neighbour table */
+    int per_batch;
+    int targets;
+    int32_t* offsets;      /* (B * targets + 1) */
+    int32_t* entries;      /* (B * per_batch) */
+} pcs_inverse_map;
+int pcs_inverse_index_batch_workspace(const pcs_inverse_map* maps, int nmaps, int B,
+                                      size_t* bytes);
+int pcs_inverse_index_batch(const pcs_inverse_map* maps, int nmaps, int B, void* workspace,
+                            size_t ws_bytes, void* stream);
 /* common.py:64-65 backward without atomics: grad_feats (B,N,D) = sum of
  * grad_out[slot][3 + c] over the slots reading each point (overwrites). */
 int pcs_group_bwd_csr(const float* grad_out, int ld_gout, const int32_t* offsets,

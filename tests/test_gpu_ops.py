@@ -440,6 +440,30 @@ def test_inverse_index_random_tables(B, S, k, targets, kind):
         assert counts.max() > 1024 and ((counts > 64) & (counts <= 1024)).any()
 
 
+def test_inverse_index_batch_matches_single_maps():
+    """pcs_inverse_index_batch (one call, shared launches; blockIdx.z = map) == one
+    pcs_inverse_index per table, bitwise: one-chunk and multi-chunk clouds, 4096- and
+    8192-target rank widths, a > 8192-target table (legacy path after the batch), a skewed
+    table 30 tables (two launch groups)."""
+    g = torch.Generator().manual_seed(11)
+    B = 3
+    shapes = [(1024, 32, 4096), (256, 32, 1024), (64, 32, 256), (16, 32, 64), (4096, 3, 1024),
+              (4096, 20, 4096), (3000, 3, 6000), (2048, 3, 20000), (100, 5, 333)]
+    tabs = []
+    for i in range(30):
+        S, k, T = shapes[i % len(shapes)]
+        if i % 4 == 1:
+            w = 1.0 / torch.arange(1, T + 1, dtype=torch.float64) ** 1.1
+            idx = torch.multinomial(w, B * S * k, replacement=True, generator=g).view(B, S, k).to(torch.int32)
+        else:
+            idx = torch.randint(0, T, (B, S, k), generator=g, dtype=torch.int32)
+        tabs.append((idx.to(DEV), T))
+    got = ops.inverse_index_batch(tabs)
+    for (idx, T), (off, ent) in zip(tabs, got):
+        o1, e1 = ops.inverse_index(idx, T)
+        assert torch.equal(off, o1) and torch.equal(ent, e1), (idx.shape, T)
+
+
 @pytest.mark.parametrize('D1,D2', [(0, 128), (64, 256), (12, 8)])
 def test_interp_cat_fused_bit_exact(D1, D2):
     """pcs_interp_cat_fwd (float4, skip copy fused) == the scalar pcs_interp_fwd + copy, bitwise."""
