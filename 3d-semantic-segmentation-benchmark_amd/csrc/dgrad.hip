@@ -1,0 +1,304 @@
+// Data-gradient GEMM of a shared-MLP layer with its BN-backward operand, LDS-DMA staged:
+//   dA[M x N] = dZ[M x K] . W[K x N],  dZ = the layer's BN+activation backward rebuilt from
+//   (dy, z) (xform4<OP_BNBWD>), W the layer's weights read k-major (N = its input width);
+//   optional epilogue: the previous layer's BN-backward partial sums (sum dy', sum dy'*xhat')
+//   over this block's rows -- exactly gemm_rows_kernel<64, 64, 2, 2, BNBWD, true, EPI> of mlp.hip
+//   (same k order inside a slab, same two-level fp32 accumulation, same epilogue), so the
+//   outputs are bitwise those of that kernel.
+// Reference: the backward of models/utils/common.py:125-178 (MiniPointNet / UnitPointNet:
+// conv -> BN -> ReLU) as autograd runs it.
+//
+// Why a second kernel (VERDICT r3 #1b): the register-staged row GEMM holds one slab of (dy, z, W)
+// in VGPRs while computing the previous one and needs 240 VGPRs with its epilogue -- 2 waves per
+// SIMD, one slab in flight per block: a latency-bound ~0.25 of HBM on the PointNet++ critical
+// path.  Here the raw slabs go global -> LDS by LDS-DMA (global_load_lds_dwordx4, no VGPR
+// destination) through a 3-stage ring, two slabs ahead; the BN-backward transform is applied
+// once per element in a pass over the landed slab (LDS -> VGPR -> LDS, in place), then the MFMAs
+// read the transformed slab.  Per 256-thread block and stage: dy 64x32, z 64x32, the W slab
+// 32x64 and the slab's 5 x 32 BN-backward coefficients (25 KB; 75 KB for 3 stages: 2 blocks per
+// CU).  Every wave issues the same 7 DMA instructions per stage, so a stage is retired by a
+// counted `s_waitcnt vmcnt(7)` (one stage left in flight) + a raw s_barrier -- never
+// __syncthreads(), whose fence would drain the ring (cdna_hip_programming.md, glds rules).
+// LDS images are lane-linear (an LDS-DMA writes base + 16 * lane); the dy / z rows (32 floats)
+// have their 16-B chunks XOR-swizzled by (row >> 1) & 7 on the SOURCE address and on every read,
+// so the fragment reads (ds_read_b128 of 16 rows) are bank-conflict free.  The W slab is stored
+// [k][n] as it lies in memory; a lane's B fragment is 4 ds_read_b32 down a column.
+// Grid: (row blocks) x (64-column tiles), persistent over row tiles like the row GEMM; the two
+// column tiles of a row block are adjacent in the XCD-remapped order, so the second read of its
+// (dy, z) rows is an L2 hit.
+#include "mlp_common.hpp"
+
+namespace pcs {
+
+constexpr int DG_BM = 64, DG_BN = 64, DG_BK = 32, DG_NS = 3;
+constexpr int DG_A = DG_BM * DG_BK;                  // floats of one dy (or z) slab: 8 KB
+constexpr int DG_B = DG_BK * DG_BN;                  // the W slab: 8 KB
+constexpr int DG_C = 256;                            // coefficients: s, t, mean, alpha, kb x 32 (+ pad)
+constexpr int DG_STAGE = 2 * DG_A + DG_B + DG_C;     // 6400 floats = 25 KB
+constexpr int DG_DMA = 7;                            // DMA instructions per wave and stage
+
+struct DgradArgs {
+    Operand a;                 // BNBWD: data = dy (ld), z (ldz), s, t, mean, alpha, kb, act/slope
+    int M, K;
+    const float* W;            // k-major: B[k][n] = W[k * ldw + n]
+    int ldw;
+    float* C;                  // M x N, row stride ldc
+    int ldc, N;
+    Operand e;                 // epilogue: the previous layer's z (ldz), s, t, mean, inv, act/slope
+    double* bstats;            // [2][N][gx] or null
+    int gx, ntn;               // row blocks, column tiles
+};
+
+__device__ __forceinline__ int dg_swz(int r) { return (r >> 1) & 7; }
+
+// one LDS-DMA: 16 B per active lane to LDS byte address dst + 16 * lane, from inline asm so the
+// compiler does not track it (it would drain the ring at every LDS read otherwise); M0 is saved
+// and restored inside the statement (compiler-reserved)
+__device__ __forceinline__ void dg_glds16(const float* gsrc, unsigned dst) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(gsrc), "s"(dst)
+                 : "memory");
+}
+
+__device__ __forceinline__ unsigned dg_lds_addr(const float* p) {
+    return (unsigned)(uintptr_t)((const __attribute__((address_space(3))) float*)p);
+}
+
+__device__ __forceinline__ void dg_barrier() { asm volatile("s_barrier" ::: "memory"); }
+
+template <bool BWD>
+__global__ __launch_bounds__(256, 2) void dgrad_kernel(const DgradArgs g) {
+    __shared__ __attribute__((aligned(16))) float lds[DG_NS * DG_STAGE];
+    __shared__ double red[2][2][DG_BN];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 1, wn = wave & 1;
+    const int h = lane >> 5, l32 = lane & 31;
+
+    // XCD-aware (row block, column tile): consecutive remapped ids share an XCD, and the column
+    // tiles of one row block are consecutive
+    const int nwg = gridDim.x, bid = blockIdx.x;
+    const int q8 = nwg / 8, r8 = nwg % 8, xcd = bid % 8;
+    const int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+    const int rb = t / g.ntn, ct = t - rb * g.ntn;
+    const int n0 = ct * DG_BN;
+
+    const int nk = g.K / DG_BK;
+    const int mtiles = (g.M + DG_BM - 1) / DG_BM;
+    const int my_tiles = rb < mtiles ? (mtiles - 1 - rb) / g.gx + 1 : 0;
+    const int total = my_tiles * nk;
+    const unsigned lbase = dg_lds_addr(lds);
+    const int nlast = ((g.N + 3) & ~3) - 4;                // last in-range column quad
+
+    // ---- DMA of flattened iteration it (row tile it / nk, slab it % nk) into stage it % 3
+    auto issue = [&](int it) {
+        const int ti = it / nk, ks = it - ti * nk;
+        const int m0 = (rb + ti * g.gx) * DG_BM, k0 = ks * DG_BK;
+        const unsigned sb = lbase + 4u * (unsigned)((it % DG_NS) * DG_STAGE);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int r = 8 * (2 * wave + j) + (lane >> 3);
+            const int row = min(m0 + r, g.M - 1);
+            const int ch = 4 * ((lane & 7) ^ dg_swz(r));
+            const unsigned d = __builtin_amdgcn_readfirstlane(sb + 4u * (unsigned)((2 * wave + j) * 256));
+            dg_glds16(g.a.data + (size_t)row * g.a.ld + k0 + ch, d);
+            dg_glds16(g.a.z + (size_t)row * g.a.ldz + k0 + ch, d + 4u * DG_A);
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int kr = 4 * (2 * wave + j) + (lane >> 4);
+            const int col = min(n0 + 4 * (lane & 15), nlast);
+            const unsigned d = __builtin_amdgcn_readfirstlane(sb + 4u * (unsigned)(2 * DG_A + (2 * wave + j) * 256));
+            dg_glds16(g.W + (size_t)(k0 + kr) * g.ldw + col, d);
+        }
+        // coefficients: wave 0 s | t, wave 1 mean | alpha, wave 2 kb | kb, wave 3 kb | kb (pad)
+        if (lane < 16) {
+            const float* src = wave == 0 ? (lane < 8 ? g.a.s : g.a.t)
+                             : wave == 1 ? (lane < 8 ? g.a.mean : g.a.alpha) : g.a.kb;
+            const unsigned d = __builtin_amdgcn_readfirstlane(sb + 4u * (unsigned)(2 * DG_A + DG_B + wave * 64));
+            dg_glds16(src + k0 + 4 * (lane & 7), d);
+        }
+    };
+
+    f32x16 acc = {};
+    double s1 = 0.0, s2 = 0.0;
+    // the epilogue's 16 Z values of this lane (previous layer's pre-BN output), loaded PF slabs
+    // before the tile's last one so their HBM latency hides under those slabs' work
+    const int PF = nk >= 3 ? 2 : nk - 1;
+    const int col = n0 + wn * 32 + l32;
+    const bool cok = col < g.N;
+    const int colc = cok ? col : g.N - 1;
+    float zt[16];
+    // the epilogue's per-column coefficients, before any DMA (a load issued later would make the
+    // compiler's wait for it drain the ring)
+    bool stores_full = false;                  // the last epilogue's 16 stores were unconditional
+    float sp = 0.f, tp = 0.f, mp = 0.f, ip = 0.f;
+    if (BWD) { sp = g.e.s[colc]; tp = g.e.t[colc]; mp = g.e.mean[colc]; ip = g.e.inv[colc]; }
+    for (int s = 0; s < DG_NS - 1; ++s)
+        if (s < total) issue(s);
+
+    for (int it = 0; it < total; ++it) {
+        const int ti = it / nk, ks = it - ti * nk;
+        const int m0 = (rb + ti * g.gx) * DG_BM;
+        float* st = lds + (it % DG_NS) * DG_STAGE;
+        // stage it landed (this wave's DMAs), then everyone's.  Issued after this wave's stage-it
+        // DMAs and allowed to stay in flight: the next stage's 7 DMAs, and the Z prefetch's 16 loads
+        // between its issue (slab nk-1-PF) and the epilogue
+        // (and a full tile's 16 stores issued right after the previous tile's last DMA)
+        {
+            const bool nxt = min(total - 1, it + DG_NS - 2) > it;
+            const bool zf = (BWD && ks > nk - 1 - PF) || (ks == 0 && it > 0 && stores_full);
+            if (nxt && zf) asm volatile("s_waitcnt vmcnt(23)" ::: "memory");
+            else if (zf) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+            else if (nxt) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        dg_barrier();
+        // ---- BN-backward transform of the dy slab, in place: thread = (k quad kq, rows r, r + 32)
+        {
+            const int kq = tid & 7;
+            const float* cf = st + 2 * DG_A + DG_B;
+            Quad q;
+            q.s = *reinterpret_cast<const float4*>(cf + 4 * kq);
+            q.t = *reinterpret_cast<const float4*>(cf + 32 + 4 * kq);
+            q.mean = *reinterpret_cast<const float4*>(cf + 64 + 4 * kq);
+            q.alpha = *reinterpret_cast<const float4*>(cf + 96 + 4 * kq);
+            q.kb = *reinterpret_cast<const float4*>(cf + 128 + 4 * kq);
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int r = (tid >> 3) + 32 * i;
+                float* p = st + r * DG_BK + 4 * (kq ^ dg_swz(r));
+                const float4 v = *reinterpret_cast<const float4*>(p);
+                const float4 z = *reinterpret_cast<const float4*>(p + DG_A);
+                *reinterpret_cast<float4*>(p) = xform4<OP_BNBWD>(g.a, v, z, 0u, m0 + r, q, ks * DG_BK + 4 * kq, g.K);
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        dg_barrier();
+        const bool last = ks == nk - 1;
+        // the next DMA (into the stage every wave finished reading one iteration ago); after the
+        // epilogue instead on a tile's last slab, whose global loads would drain it early
+        if (!last && it + DG_NS - 1 < total) issue(it + DG_NS - 1);
+        if (BWD && ks == nk - 1 - PF) {
+            const int rb0 = m0 + wm * 32;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = min(rb0 + (r & 3) + 8 * (r >> 2) + 4 * h, g.M - 1);
+                zt[r] = g.e.z[(size_t)row * g.e.ldz + colc];
+            }
+        }
+        // ---- MFMAs: slab into a fresh accumulator, then added (two-level, as the row GEMM)
+        {
+            const float* As = st;
+            const float* Bs = st + 2 * DG_A;
+            const int ar = wm * 32 + l32;
+            const int bc = wn * 32 + l32;
+            f32x16 sacc;
+#pragma unroll
+            for (int qq = 0; qq < 4; ++qq) {
+                const float4 a = *reinterpret_cast<const float4*>(As + ar * DG_BK + 4 * ((4 * h + qq) ^ dg_swz(ar)));
+                const int kb = 16 * h + 4 * qq;
+                const float b0 = Bs[(kb + 0) * DG_BN + bc], b1 = Bs[(kb + 1) * DG_BN + bc];
+                const float b2 = Bs[(kb + 2) * DG_BN + bc], b3 = Bs[(kb + 3) * DG_BN + bc];
+                const f32x16 c0 = {};
+                sacc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, b0, qq == 0 ? c0 : sacc, 0, 0, 0);
+                sacc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b1, sacc, 0, 0, 0);
+                sacc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, b2, sacc, 0, 0, 0);
+                sacc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b3, sacc, 0, 0, 0);
+            }
+            acc += sacc;
+        }
+        if (last) {
+            // ---- tile epilogue (gemm_rows_kernel's, one 32 x 32 block per wave): the BN-backward
+            // sums first (they wait for the prefetched Z), then the next DMA, then the stores --
+            // unconditional on a full tile, so the next wait can count them
+            const int rb0 = m0 + wm * 32;
+            const bool full = m0 + DG_BM <= g.M && n0 + DG_BN <= g.N;
+            float v[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                v[r] = acc[r] + 0.f;                     // (the row GEMM's "+ bias" with bias 0: -0 -> +0)
+                acc[r] = 0.f;
+            }
+            if (BWD) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int row = rb0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                    const bool ok = full || (row < g.M && cok);
+                    const float z = zt[r];
+                    const float dy = v[r] * dact_f(z * sp + tp, g.e.act, g.e.slope);
+                    const float xh = (z - mp) * ip;
+                    const double dd = ok ? (double)dy : 0.0;
+                    s1 += dd;
+                    s2 += dd * (double)xh;
+                }
+            }
+            if (it + DG_NS - 1 < total) issue(it + DG_NS - 1);
+            stores_full = full;
+            if (full) {
+                float* cb = g.C + (size_t)rb0 * g.ldc + col;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) cb[(size_t)((r & 3) + 8 * (r >> 2) + 4 * h) * g.ldc] = v[r];
+            } else {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int row = rb0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                    if (row < g.M && cok) g.C[(size_t)row * g.ldc + col] = v[r];
+                }
+            }
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+    if (BWD) {
+        const int lc = wn * 32 + l32;
+        const double a = s1 + __shfl_xor(s1, 32);
+        const double b = s2 + __shfl_xor(s2, 32);
+        if (lane < 32) {
+            red[0][wm][lc] = a;
+            red[1][wm][lc] = b;
+        }
+        __syncthreads();
+        for (int c = tid; c < DG_BN; c += 256) {
+            const int col = n0 + c;
+            if (col < g.N) {
+                g.bstats[(size_t)col * g.gx + rb] = red[0][0][c] + red[0][1][c];
+                g.bstats[((size_t)g.N + col) * g.gx + rb] = red[1][0][c] + red[1][1][c];
+            }
+        }
+    }
+}
+
+bool dgrad_dma_ok(const pcs_operand* a, int M, int K, const float* W, int ldw, int N) {
+    auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+    return a && a->mode == PCS_OP_BNBWD && M >= 1 && K >= DG_BK && K % DG_BK == 0 && N >= 4 && N % 4 == 0 &&
+           ldw % 4 == 0 && ldw >= N && al16(W) && a->ld % 4 == 0 && a->ldz % 4 == 0 && al16(a->data) &&
+           al16(a->z) && al16(a->s) && al16(a->t) && al16(a->mean) && al16(a->alpha) && al16(a->kb);
+}
+
+int dgrad_dma(const pcs_operand* a, int M, int K, const float* W, int ldw, float* C, int ldc, int N,
+              const pcs_operand* epi, double* bstats, int gx, hipStream_t st) {
+    DgradArgs g{};
+    g.a = to_dev_operand(a);
+    g.M = M;
+    g.K = K;
+    g.W = W;
+    g.ldw = ldw;
+    g.C = C;
+    g.ldc = ldc;
+    g.N = N;
+    if (epi) g.e = to_dev_operand(epi);
+    g.bstats = bstats;
+    g.gx = gx;
+    g.ntn = (N + DG_BN - 1) / DG_BN;
+    const long long blocks = (long long)gx * g.ntn;
+    PCS_CHECK_ARG(gx >= 1 && blocks < (1ll << 31), "dgrad_dma: bad grid");
+    if (bstats) hipLaunchKernelGGL(dgrad_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, st, g);
+    else hipLaunchKernelGGL(dgrad_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, st, g);
+    return 0;
+}
+
+}  // namespace pcs

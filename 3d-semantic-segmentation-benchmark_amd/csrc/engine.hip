@@ -144,6 +144,7 @@ struct BwdScratch {
     size_t wg0_bytes;
     char* fw;              // fused inner layers' dW partials (caller's stream only)
     size_t fw_bytes;
+    float* drop;           // the top layer's output gradient through its dropout (when not materialised)
 };
 
 static size_t carve_backward(Carve& cv, int M, int kin, int ldx, const pcs_mlp_layer* L, int nl, int pool_k,
@@ -174,6 +175,7 @@ static size_t carve_backward(Carve& cv, int M, int kin, int ldx, const pcs_mlp_l
     s.fw_bytes = fw;
     s.fw = cv.take<char>(fw);
     s.dz = materialize_dz_of(L[nl - 1], M, true) ? cv.take<float>((size_t)M * (size_t)L[nl - 1].cout) : nullptr;
+    s.drop = L[nl - 1].drop_p > 0.0 && !s.dz ? cv.take<float>((size_t)M * (size_t)L[nl - 1].cout) : nullptr;
     if (out) *out = s;
     return cv.used;
 }
@@ -390,9 +392,38 @@ static int mlp_backward(const float* X, int ldx, int kin, int M, const pcs_mlp_l
             return e;
     } else {
         nb = pcs_bn_bwd_reduce_blocks(M);
-        if (int e = pcs_bn_bwd_reduce(gout, ldg, T.Z, CL, M, CL, sT, sT + CL, sT + 2 * CL, sT + 3 * CL, (int)T.act,
-                                      (float)T.slope, S.part, stream))
+        // the stack's fused dropout (DGCNN conv6 / conv7, dgcnn.py:196-207; PointNet++ FP1's
+        // head): where the top layer's dZ is materialised (the wide layers), the mask is applied
+        // on load by this reduce and by the dZ pass -- no masked copy of the gradient; otherwise
+        // the masked gradient is written once and read by both consumers
+        bool drop_on_load = false;
+        if (T.drop_p > 0.0) {
+            const pcs_operand xt = bnbwd_op(gout, ldg, T, S.alpha[0], S.kb[0]);
+            bool fused_top = false;
+            if (nl > 1 && T.dW && fused_bwd_wanted((int)T.bwd_fuse, M)) {
+                pcs_operand q = bnbwd_op(nullptr, 0, layers[nl - 2], nullptr, nullptr);
+                q.data = layers[nl - 2].Z;
+                q.ld = (int)T.cin;
+                fused_top = fused_bwd_ok(M, CL, (int)T.cin, (int)T.ldw, &xt, &q);
+            }
+            drop_on_load = !fused_top && materialize_dz_of(T, M, nl > 1 || dX) && S.dz;
+            if (!drop_on_load) {
+                float* g2 = S.drop ? S.drop : S.dz;
+                PCS_CHECK_ARG(g2, "pcs_mlp_backward: no dropout scratch");
+                if (int e = pcs_dropout_bwd(gout, ldg, M, CL, T.drop_p, T.drop_seed, g2, CL, stream)) return e;
+                gout = g2;
+                ldg = CL;
+            }
+        }
+        if (drop_on_load) {
+            if (int e = bn_bwd_reduce_dropout(gout, ldg, T.Z, CL, M, CL, sT, sT + CL, sT + 2 * CL, sT + 3 * CL,
+                                              (int)T.act, (float)T.slope, S.part, T.drop_p, (long long)T.drop_seed,
+                                              st))
+                return e;
+        } else if (int e = pcs_bn_bwd_reduce(gout, ldg, T.Z, CL, M, CL, sT, sT + CL, sT + 2 * CL, sT + 3 * CL,
+                                             (int)T.act, (float)T.slope, S.part, stream)) {
             return e;
+        }
     }
     int pp = 0;
     if (int e = pcs_bn_bwd_finalize(S.part, nb, CL, M, sT, sT + 3 * CL, T.dgamma, T.dbeta, S.kb[pp], S.alpha[pp], 1,
@@ -440,7 +471,10 @@ static int mlp_backward(const float* X, int ldx, int kin, int M, const pcs_mlp_l
             // the top layer's into its own buffer (gout is the caller's), inner ones in place
             // over the dA buffer the rebuilt operand reads
             float* dst = l == nl - 1 ? S.dz : const_cast<float*>(xop.data);
-            if (int e = materialize_dz(&xop, M, C, dst, C, st)) return fail(e);
+            // the top layer's gradient still carries its dropout when the mask is applied on load
+            const bool dm = l == nl - 1 && P.drop_p > 0.0 && xop.data != S.drop && xop.data != S.dz;
+            if (int e = materialize_dz(&xop, M, C, dst, C, st, dm ? P.drop_p : 0.0, dm ? (long long)P.drop_seed : 0))
+                return fail(e);
             xop = plain_op(dst, C);
         }
         // the first layer's wgrad goes to the caller's stream when no dgrad follows it (the

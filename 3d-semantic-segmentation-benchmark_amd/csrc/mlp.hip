@@ -54,6 +54,7 @@ __device__ __forceinline__ int lds_swz(int c) { return ((c >> 3) & 7) << 2; }
 // the arguments at run time: the combinations the engine never issues).
 constexpr int EPI_STATS = 1, EPI_BWD = 2, EPI_POOL = 4, EPI_GENERIC = 8;
 
+
 template <int BM, int BN, int WM, int WN, int AM, bool BT, int EPI>
 __global__ __launch_bounds__(WM * WN * 64, 2) void gemm_rows_kernel(GemmArgs g) {
     constexpr int NT = WM * WN * 64;
@@ -709,7 +710,8 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restr
                                                             const float* __restrict__ s, const float* __restrict__ t,
                                                             const float* __restrict__ mean,
                                                             const float* __restrict__ inv, int act, float slope,
-                                                            int rows_per_block, double* __restrict__ part) {
+                                                            int rows_per_block, double* __restrict__ part,
+                                                            DropMask dm) {
     extern __shared__ double red_dyn[];   // [2][256][4]
     const int nq = N / 4;                 // channel quads; blockIdx.y walks 256-quad column tiles
     const int q0 = blockIdx.y * 256;
@@ -726,7 +728,11 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restr
         for (int j = 0; j < 4; ++j) { sc[j] = s[c + j]; tc[j] = t[c + j]; mc[j] = mean[c + j]; ic[j] = inv[c + j]; }
         for (int r = rb + rlane; r < re; r += rstep) {
             const F4 z = ld4(Z + (size_t)r * ldz + c);
-            const F4 g = ld4(dA + (size_t)r * ldd + c);
+            F4 g = ld4(dA + (size_t)r * ldd + c);
+            if (dm.on) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) g.v[j] = dm.apply(g.v[j], (unsigned long long)r * N + c + j);
+            }
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const float dy = g.v[j] * dact_f(z.v[j] * sc[j] + tc[j], act, slope);
@@ -859,14 +865,6 @@ __global__ __launch_bounds__(256) void bn_act_kernel(const float* __restrict__ Z
     }
 }
 
-// inverted-dropout keep test of element i (counter-based: splitmix64 finaliser of seed + i*phi)
-__device__ __forceinline__ bool dropout_keep(unsigned long long seed, unsigned long long i, unsigned thr) {
-    unsigned long long z = seed + i * 0x9E3779B97F4A7C15ull;
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    z ^= z >> 31;
-    return (unsigned)(z >> 32) >= thr;
-}
 
 // bn_act with the training-mode dropout that follows it fused in (no mask stored)
 __global__ __launch_bounds__(256) void bn_act_drop_kernel(const float* __restrict__ Z, int ldz, int total4, int nq,
@@ -907,6 +905,15 @@ __global__ __launch_bounds__(256) void dropout_bwd_kernel(const float* __restric
 static unsigned dropout_thr(double p) {
     const double v = p * 4294967296.0;
     return v >= 4294967295.0 ? 4294967295u : (unsigned)v;
+}
+
+DropMask drop_mask(double p, long long seed) {
+    DropMask d{};
+    d.seed = (unsigned long long)seed;
+    d.thr = dropout_thr(p);
+    d.scale = (float)(1.0 / (1.0 - p));
+    d.on = 1;
+    return d;
 }
 
 void bn_finalize_launch(const double* part, int nb, int N, long long M, const float* gamma, const float* beta,
@@ -1022,7 +1029,9 @@ static void gemm_tile(int M, int N, bool bwd, int* bm, int* bn, int* nt = nullpt
     // of the 64 x 64 tile; the rebuilt dZ slab loaded and transformed once per 128 output columns
     // instead of once per 64) made the PointNet++ step 1-2 % slower (same-box A/B, 2 rounds).
     // Round 4: 32 x 128 tiles for the 128-wide data gradients (dZ read once, 4 waves across the
-    // columns): 5.24 vs 5.07 ms.
+    // columns): 5.24 vs 5.07 ms.  Compiling the 64 x 64 tiles for 3 / 4 blocks per CU (168 / 128
+    // VGPRs) spills: 5.31 / 5.61 vs 5.05 ms.  The BN-backward 64 x 64 data gradient now runs on
+    // the LDS-DMA kernel of dgrad.hip (bitwise the same results).
     if (nt) *nt = 256;
     bool wide;
     const T* c;
@@ -1078,6 +1087,15 @@ static double operand_bytes(const pcs_operand& o, int M, int K) {
 // Forward GEMMs in the wide regime (gemm_nt_regime) write one BN partial per 256-row tile,
 // whichever kernel runs them (gemm_nt, or the row GEMM with that many persistent blocks when
 // the operand needs an on-load transform), so the partial count depends on (M, N) only.
+// PCS_DGRAD_DMA=0: the register-staged row GEMM for every data gradient (A/B only)
+static bool dgrad_dma_enabled() {
+    static const bool on = [] {
+        const char* v = getenv("PCS_DGRAD_DMA");
+        return !(v && v[0] == '0');
+    }();
+    return on;
+}
+
 static int row_blocks(int M, int N, bool bwd) {
     if (!bwd && gemm_nt_regime(M, N)) return gemm_nt_row_tiles(M);
     int bm, bn, nt;
@@ -1128,7 +1146,8 @@ void pcs::wgrad_reduce_launch(const float* part, int splits, long long nk, float
 // weight gradient; for ceil(Cin / 128) >= 3 one pass here is cheaper than rebuilding it in
 // every tile (DGCNN conv5-7: -2.1 ms of GEMM time for +0.5 ms here, scripts/dgcnn_head_ab.py).
 template <int MODE>
-__global__ __launch_bounds__(256) void dz_kernel(Operand o, int total4, int nq, float* __restrict__ out, int ldo) {
+__global__ __launch_bounds__(256) void dz_kernel(Operand o, int total4, int nq, float* __restrict__ out, int ldo,
+                                                 DropMask dm) {
     const int C = 4 * nq;
     for (int e = blockIdx.x * 256 + threadIdx.x; e < total4; e += gridDim.x * 256) {
         const int r = e / nq;
@@ -1138,11 +1157,19 @@ __global__ __launch_bounds__(256) void dz_kernel(Operand o, int total4, int nq, 
         float4 v, z;
         unsigned a = 0;
         load_raw<MODE>(o, r, c, v, z, a);
+        if (dm.on) {                 // the stack's fused dropout, on the top layer's output gradient
+            const unsigned long long i0 = (unsigned long long)r * C + c;
+            v.x = dm.apply(v.x, i0);
+            v.y = dm.apply(v.y, i0 + 1);
+            v.z = dm.apply(v.z, i0 + 2);
+            v.w = dm.apply(v.w, i0 + 3);
+        }
         *reinterpret_cast<float4*>(out + (size_t)r * ldo + c) = xform4<MODE>(o, v, z, a, r, q, c, C);
     }
 }
 
-int pcs::materialize_dz(const pcs_operand* x, int M, int C, float* out, int ldo, hipStream_t st) {
+int pcs::materialize_dz(const pcs_operand* x, int M, int C, float* out, int ldo, hipStream_t st, double drop_p,
+                        long long drop_seed) {
     PCS_CHECK_ARG(x && (x->mode == PCS_OP_BNBWD || x->mode == PCS_OP_POOLBWD) && C % 4 == 0 && ldo % 4 == 0 &&
                       ldo >= C && out,
                   "materialize_dz: needs a BNBWD/POOLBWD operand, C %% 4 == 0, ldo >= C");
@@ -1152,10 +1179,10 @@ int pcs::materialize_dz(const pcs_operand* x, int M, int C, float* out, int ldo,
     const Operand o = to_dev(x);
     if (x->mode == PCS_OP_BNBWD)
         hipLaunchKernelGGL(dz_kernel<OP_BNBWD>, dim3(ew_grid(total4)), dim3(256), 0, st, o, (int)total4, C / 4, out,
-                           ldo);
+                           ldo, drop_p > 0.0 ? drop_mask(drop_p, drop_seed) : DropMask{});
     else
         hipLaunchKernelGGL(dz_kernel<OP_POOLBWD>, dim3(ew_grid(total4)), dim3(256), 0, st, o, (int)total4, C / 4, out,
-                           ldo);
+                           ldo, DropMask{});
     return launch_status("materialize_dz");
 }
 
@@ -1199,6 +1226,30 @@ int pcs::gemm_rows_ex(const pcs_operand* a, int M, int K, const float* W, int ld
         const int e = gemm_nt(a->data, a->ld, W, ldw, M, N, K, bias, C, ldc, stats, s);
         probe_stop(probe, s);
         return e;
+    }
+    // the 64 x 64 BN-backward data gradient: LDS-DMA ring kernel (dgrad.hip), bitwise the same
+    if (bt && a->mode == PCS_OP_BNBWD && !stats && !pool_k && !bias && dgrad_dma_enabled() &&
+        dgrad_dma_ok(a, M, K, W, ldw, N)) {
+        int bm, bn;
+        gemm_tile(M, N, true, &bm, &bn);
+        if (bm == 64 && bn == 64) {
+            const int gx = bstats ? row_blocks(M, N, true) : gemm_grid_x(M, N, 64, 64);
+            int probe = -1;
+            if (probe_enabled()) {
+                const double bytes = operand_bytes(*a, M, K) + 4.0 * M * N * (bstats ? 2 : 1);
+                const pcs_operand ac = *a, ec = epi ? *epi : pcs_operand{};
+                const bool he = epi != nullptr;
+                probe = probe_start(bstats ? "pcs::dgrad_kernel<true>" : "pcs::dgrad_kernel<false>", 2.0 * M * K * N,
+                                    bytes, s, [=]() {
+                                        gemm_rows_ex(&ac, M, K, W, ldw, bt, bias, C, ldc, N, stats, he ? &ec : nullptr,
+                                                     bstats, stream);
+                                    });
+            }
+            const int e = dgrad_dma(a, M, K, W, ldw, C, ldc, N, epi, bstats, gx, s);
+            probe_stop(probe, s);
+            if (e) return e;
+            return launch_status("pcs_gemm_rows");
+        }
     }
     GemmArgs g{to_dev(a), M, K, W, ldw, bias, C, ldc, N, stats, to_dev(epi), bstats, pz, pa, pool_k};
     int probe = -1;
@@ -1393,8 +1444,20 @@ PCS_API int pcs_bn_bwd_reduce(const float* dA, int ldd, const float* Z, int ldz,
     const int nq = N / 4;
     const dim3 grid((M + kRedRows - 1) / kRedRows, (nq + 255) / 256);
     hipLaunchKernelGGL(bn_bwd_reduce_kernel, grid, dim3(256), 2 * 256 * 4 * sizeof(double), as_stream(stream), dA, ldd,
-                       Z, ldz, M, N, s, t, mean, inv, act, eff_slope(act, slope), kRedRows, part);
+                       Z, ldz, M, N, s, t, mean, inv, act, eff_slope(act, slope), kRedRows, part, DropMask{});
     return launch_status("pcs_bn_bwd_reduce");
+}
+
+// the same with the stack's fused dropout applied to dA on load (its mask recomputed from the seed)
+int pcs::bn_bwd_reduce_dropout(const float* dA, int ldd, const float* Z, int ldz, int M, int N, const float* s,
+                               const float* t, const float* mean, const float* inv, int act, float slope,
+                               double* part, double p, long long seed, hipStream_t st) {
+    PCS_CHECK_ARG(M >= 1 && N >= 4 && N % 4 == 0 && ldd % 4 == 0 && ldz % 4 == 0 && p > 0.0 && p < 1.0,
+                  "bn_bwd_reduce_dropout: bad sizes or p");
+    const dim3 grid((M + kRedRows - 1) / kRedRows, (N / 4 + 255) / 256);
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel, grid, dim3(256), 2 * 256 * 4 * sizeof(double), st, dA, ldd, Z, ldz, M, N,
+                       s, t, mean, inv, act, eff_slope(act, slope), kRedRows, part, drop_mask(p, seed));
+    return launch_status("bn_bwd_reduce_dropout");
 }
 
 PCS_API int pcs_pool_fwd(const float* Z, int N, long long G, int K, const float* s, const float* t, int act,

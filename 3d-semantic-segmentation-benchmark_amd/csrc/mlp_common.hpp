@@ -127,6 +127,32 @@ __device__ __forceinline__ float4 xform4(const Operand& o, float4 v, float4 z, u
     return in ? out : make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
+// inverted-dropout keep test of element i (counter-based: splitmix64 finaliser of seed + i*phi)
+__device__ __forceinline__ bool dropout_keep(unsigned long long seed, unsigned long long i, unsigned thr) {
+    unsigned long long z = seed + i * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    return (unsigned)(z >> 32) >= thr;
+}
+
+// a stack's fused inverted dropout, applied to its output gradient where that is read
+// (seed, keep threshold, 1 / (1 - p)); on = 0: off
+struct DropMask {
+    unsigned long long seed;
+    unsigned thr;
+    float scale;
+    int on;
+    __device__ __forceinline__ float apply(float g, unsigned long long i) const {
+        return dropout_keep(seed, i, thr) ? g * scale : 0.f;
+    }
+};
+DropMask drop_mask(double p, long long seed);
+// pcs_bn_bwd_reduce with the stack's dropout applied to dA on load (mlp.hip)
+int bn_bwd_reduce_dropout(const float* dA, int ldd, const float* Z, int ldz, int M, int N, const float* s,
+                          const float* t, const float* mean, const float* inv, int act, float slope, double* part,
+                          double p, long long seed, hipStream_t st);
+
 struct GemmArgs {
     Operand a; int M; int K;                   // A rows (M x K) through its transform
     const float* W; int ldw;                   // B[k][n] = W[n*ldw + k]
@@ -152,11 +178,19 @@ void bn_bwd_finalize_launch(const double* part, int nb, int N, long long M, cons
 // column passes of a layer's backward GEMMs over its dZ (M x C; cin = the layer's input width)
 int dz_passes(int M, int C, int cin, bool dgrad, bool wgrad);
 // out (M x C, stride ldo) = the BNBWD / POOLBWD operand x materialised (bitwise the on-load values)
-int materialize_dz(const pcs_operand* x, int M, int C, float* out, int ldo, hipStream_t st);
+// (drop_p > 0: the BNBWD operand's gradient through the stack's dropout mask, drop_seed)
+int materialize_dz(const pcs_operand* x, int M, int C, float* out, int ldo, hipStream_t st, double drop_p = 0.0,
+                   long long drop_seed = 0);
 // row GEMM with W row-major N x K (bt = 0, = pcs_gemm_rows) or K x N (bt = 1)
 int gemm_rows_ex(const pcs_operand* a, int M, int K, const float* W, int ldw, int bt, const float* bias, float* C,
                  int ldc, int N, double* stats, const pcs_operand* epi, double* bstats, void* stream,
                  float* pz = nullptr, unsigned char* pa = nullptr, int pool_k = 0);
+// the 64 x 64 BN-backward data gradient through an LDS-DMA ring (dgrad.hip): bitwise
+// gemm_rows_kernel<64, 64, 2, 2, BNBWD, true, 0 | EPI_BWD> for the shapes dgrad_dma_ok accepts;
+// gx = the row blocks (= BN-backward partials per column)
+bool dgrad_dma_ok(const pcs_operand* a, int M, int K, const float* W, int ldw, int N);
+int dgrad_dma(const pcs_operand* a, int M, int K, const float* W, int ldw, float* C, int ldc, int N,
+              const pcs_operand* epi, double* bstats, int gx, hipStream_t st);
 // wide-layer GEMM on plain operands (gemm_big.hip): C = A . B^T, A (M x R), B (N x R) row-major
 bool gemm_nt_regime(int M, int N);                 // (M, N) the wide path is built for
 int gemm_nt_row_tiles(int M);                      // its BN-partial row blocks

@@ -456,21 +456,20 @@ class SharedMLPFn(torch.autograd.Function):
         if not (gout.dim() == 2 and gout.stride(1) == 1 and gout.stride(0) % 4 == 0 and gout.data_ptr() % 16 == 0
                 and (pool_K == 0 or gout.is_contiguous())):
             gout = gout.contiguous()
-        if ctx.drop is not None:       # the fused dropout's backward: the mask is recomputed from its seed
-            g2 = _f32((M, couts[-1]), dev)
-            call('pcs_dropout_bwd', ptr(gout), gout.stride(0), M, couts[-1], float(ctx.drop[0]), int(ctx.drop[1]),
-                 ptr(g2), couts[-1], st)
-            gout = g2
         ldg = gout.stride(0)
         gt = grad_targets(params)
+        # the fused dropout's backward runs inside the engine (its mask recomputed from the seed,
+        # applied where the top layer's gradient is read): the top record carries (p, seed)
+        dp, ds = (float(ctx.drop[0]), int(ctx.drop[1])) if ctx.drop is not None else (0.0, 0)
         recs = b''.join(statics[li] + _DYN.pack(zp, cp, _nz(gt[4 * li]), _nz(gt[4 * li + 1]), _nz(gt[4 * li + 2]),
-                                                  _nz(gt[4 * li + 3]), 0.0, 0, ctx.bwd_fuse,
+                                                  _nz(gt[4 * li + 3]), dp if li == nl - 1 else 0.0,
+                                                  ds if li == nl - 1 else 0, ctx.bwd_fuse,
                                                   ctx.dx_from if li == 0 else 0)
                         for li, (zp, cp) in enumerate(zptrs))
         dX = None
         if ctx.needs_input_grad[0]:
             dX = _f32((M, X.shape[1]), dev)       # dense, X's width (its pad columns zeroed)
-        key = (M, Kin, ldx, tuple(couts), pool_K, 1)
+        key = (M, Kin, ldx, tuple(couts), pool_K, 1, dp > 0.0)
         nws = _workspace(lib, key, M, Kin, ldx, recs, nl, pool_K, 1)
         ws = torch.empty((nws,), dtype=torch.uint8, device=dev)
         lane = wgrad_lane(dev)

@@ -1,0 +1,75 @@
+"""The LDS-DMA data-gradient kernel (csrc/dgrad.hip) against the register-staged row GEMM it
+replaces (gemm_rows_kernel<64, 64, 2, 2, BNBWD, true, EPI>): BITWISE equal outputs and
+BN-backward partials, with and without the fused epilogue, on the PointNet++ dgrad shapes and
+ragged ones (M not a multiple of 64, N not a multiple of 64, several column tiles).  The row
+GEMM is selected by PCS_DGRAD_DMA=0, read once per process, so each side runs in a child
+process; the launch probe in each child names the kernel that ran.  Values against fp64 are
+covered by tests/test_gpu_engine.py::test_gemm_rows_kmajor_vs_fp64 (now on this kernel)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), '..')
+
+# M, K (the layer's cout: contraction), N (its cin: outputs)
+SHAPES = [(131072, 128, 128), (262144, 64, 64), (65536, 256, 128), (4099, 64, 64), (515, 256, 260),
+          (1000, 32, 36), (70001, 128, 128)]
+
+CHILD = r'''
+import json, math, sys, torch
+sys.path.insert(0, sys.argv[1]); sys.path.insert(0, sys.argv[1] + '/3d-semantic-segmentation-benchmark_amd')
+from pcseg._lib import load, stream_ptr, OP_BNBWD
+from pcseg.engine import operand, gemm_rows_kmajor, ld4, KernelProbe
+out, names = {}, []
+dev = torch.device('cuda'); st = stream_ptr(dev)
+for (M, K, N) in json.loads(sys.argv[3]):
+    g = torch.Generator(device='cuda').manual_seed(M + 3 * K + 7 * N)
+    r = lambda *s: torch.randn(*s, device='cuda', generator=g)
+    lda, ldw = ld4(K), ld4(N)
+    dy, z = r(M, lda), r(M, lda)
+    s, t = torch.rand(K, device='cuda', generator=g) + 0.5, r(K) * 0.3
+    mean, alpha, kb = r(K) * 0.1, r(K) * 0.05, r(K) * 0.05
+    x = operand(dy, lda, OP_BNBWD, s, t, 1, 0.0, z, lda, mean, None, alpha, kb)
+    W = r(K, ldw) / math.sqrt(K)
+    ze = r(M, N)
+    se, te = torch.rand(N, device='cuda', generator=g) + 0.5, r(N) * 0.3
+    me, ie = r(N) * 0.1, torch.rand(N, device='cuda', generator=g) + 0.5
+    epi = operand(None, 0, OP_BNBWD, se, te, 1, 0.0, ze, N, me, ie)
+    nb = load().pcs_gemm_row_blocks_dgrad(M, N)
+    C1 = torch.full((M, N), float('nan'), device='cuda'); C2 = torch.full((M, N), float('nan'), device='cuda')
+    bp = torch.full((2, N, nb), float('nan'), dtype=torch.float64, device='cuda')
+    with KernelProbe() as kp:
+        gemm_rows_kmajor(x, M, K, W, ldw, C1, N, N, epi, bp, st=st)
+        gemm_rows_kmajor(x, M, K, W, ldw, C2, N, N, st=st)
+    names.append([rr[0] for rr in kp.records()])
+    key = f'{M}_{K}_{N}'
+    out[key + '_c1'], out[key + '_c2'], out[key + '_bp'] = C1.cpu(), C2.cpu(), bp.cpu()
+torch.save(out, sys.argv[2])
+print(json.dumps(names))
+'''
+
+
+def _run(tmp_path, dma: str):
+    path = str(tmp_path / f'dgrad_{dma}.pt')
+    env = dict(os.environ, PCS_DGRAD_DMA=dma)
+    p = subprocess.run([sys.executable, '-c', CHILD, ROOT, path, json.dumps(SHAPES)], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    return torch.load(path, weights_only=True), json.loads(p.stdout.strip().splitlines()[-1])
+
+
+def test_dgrad_dma_bitwise_equal_to_row_gemm(tmp_path):
+    new, names_new = _run(tmp_path, '1')
+    old, names_old = _run(tmp_path, '0')
+    for (M, K, N), nn, no in zip(SHAPES, names_new, names_old):
+        assert nn == ['pcs::dgrad_kernel<true>', 'pcs::dgrad_kernel<false>'], (M, K, N, nn)
+        assert all(n.startswith('pcs::gemm_rows_kernel<64, 64, 2, 2, 2, true') for n in no), (M, K, N, no)
+    for k in new:
+        assert torch.equal(new[k], old[k]), k
+        assert not torch.isnan(new[k]).any(), k

@@ -44,19 +44,27 @@ def test_fused_dropout_forward_properties(p):
     assert not torch.equal(y != 0, other != 0)
 
 
-def test_fused_dropout_backward_matches_masked_gradient():
+@pytest.mark.parametrize('M,cin,cout,xgrad', [(32768, 64, 128, False),
+                                              # a wide layer whose dZ is materialised (DGCNN conv7's
+                                              # shape): the mask is applied on load by the BN-backward
+                                              # reduce and the dZ pass, no masked copy
+                                              (65536, 512, 256, True)])
+def test_fused_dropout_backward_matches_masked_gradient(M, cin, cout, xgrad):
     p, seed = 0.5, 777
-    seq_a, seq_b = _stack(seed=3), _stack(seed=3)
-    x = torch.randn(32768, 64, device=DEV)
-    g = torch.randn(32768, 128, device=DEV)
-    y0 = _run(seq_b, x, None)
-    y = _run(seq_a, x, (p, seed))
+    seq_a, seq_b = _stack(cin, cout, seed=3), _stack(cin, cout, seed=3)
+    xa = torch.randn(M, cin, device=DEV, requires_grad=xgrad)
+    xb = xa.detach().clone().requires_grad_(xgrad)
+    g = torch.randn(M, cout, device=DEV)
+    y0 = _run(seq_b, xb, None)
+    y = _run(seq_a, xa, (p, seed))
     kept = ((y != 0) | (y0 == 0)).float()
     y.backward(g)
     y0.backward(g * kept * 2.0)
     torch.cuda.synchronize()
     for a, b in zip(seq_a.parameters(), seq_b.parameters()):
         assert torch.equal(a.grad, b.grad)
+    if xgrad:
+        assert torch.equal(xa.grad, xb.grad)
 
 
 def test_dgcnn_head_uses_fused_dropout():
