@@ -140,10 +140,16 @@ __global__ __launch_bounds__(BLOCK) void fps_kernel(const float* __restrict__ xy
     __shared__ __attribute__((aligned(16))) uint2 s_slot[2][NW];   // (mw + 1, idx<<1 | flag); 0 = empty wave
     __shared__ __attribute__((aligned(16))) uint2 s_key[NW];       // slow path: (sqrt bits + 1, index)
     // Per-step global stores would make every __syncthreads wait for them (the
-    // barrier's fence drains vmcnt): keep the picked centroids in LDS instead.
-    __shared__ float4 s_out[kFpsLdsOut];
-    __shared__ float s_px[LDSC ? kFpsLdsCloud : 1], s_py[LDSC ? kFpsLdsCloud : 1], s_pz[LDSC ? kFpsLdsCloud : 1];
+    // barrier's fence drains vmcnt): keep the picked centroids in LDS instead.  Dynamic LDS,
+    // sized to THIS call (fps_lds_bytes): [C centroids | x | y | z of the N points] -- the
+    // prefetched SA1 FPS holds its CU's LDS for the whole backward it runs under, so a
+    // worst-case static size (128 KB) starved the main stream's GEMMs on those 32 CUs
+    extern __shared__ float4 fps_lds[];
     const bool lds_out = C <= kFpsLdsOut;
+    float4* s_out = fps_lds;
+    float* s_px = reinterpret_cast<float*>(fps_lds + (lds_out ? C : 0));
+    float* s_py = s_px + N;
+    float* s_pz = s_py + N;
 
     const int b = blockIdx.x;
     const int t = threadIdx.x;
@@ -303,15 +309,27 @@ __global__ __launch_bounds__(BLOCK) void fps_kernel(const float* __restrict__ xy
     }
 }
 
+// dynamic LDS of one FPS launch (fps_kernel's layout)
+static size_t fps_lds_bytes(int N, int C) {
+    return (C <= kFpsLdsOut ? (size_t)C * 16 : 0) + (N <= kFpsLdsCloud ? (size_t)N * 12 : 0);
+}
+
+template <int BLOCK, int PPT, bool LDSC>
+static void launch_fps_lds(const float* xyz, int B, int N, int C, const int* start, int* out_idx, float* out_xyz,
+                           hipStream_t s) {
+    static const hipError_t attr = hipFuncSetAttribute(
+        reinterpret_cast<const void*>(&fps_kernel<BLOCK, PPT, LDSC>), hipFuncAttributeMaxDynamicSharedMemorySize,
+        (int)(kFpsLdsOut * 16 + (LDSC ? kFpsLdsCloud * 12 : 0)));
+    (void)attr;
+    hipLaunchKernelGGL((fps_kernel<BLOCK, PPT, LDSC>), dim3(B), dim3(BLOCK), fps_lds_bytes(N, C), s, xyz, N, C, start,
+                       out_idx, out_xyz);
+}
+
 template <int BLOCK, int PPT>
 static void launch_fps(const float* xyz, int B, int N, int C, const int* start, int* out_idx, float* out_xyz,
                        hipStream_t s) {
-    if (N <= kFpsLdsCloud)
-        hipLaunchKernelGGL((fps_kernel<BLOCK, PPT, true>), dim3(B), dim3(BLOCK), 0, s, xyz, N, C, start, out_idx,
-                           out_xyz);
-    else
-        hipLaunchKernelGGL((fps_kernel<BLOCK, PPT, false>), dim3(B), dim3(BLOCK), 0, s, xyz, N, C, start, out_idx,
-                           out_xyz);
+    if (N <= kFpsLdsCloud) launch_fps_lds<BLOCK, PPT, true>(xyz, B, N, C, start, out_idx, out_xyz, s);
+    else launch_fps_lds<BLOCK, PPT, false>(xyz, B, N, C, start, out_idx, out_xyz, s);
 }
 
 }  // namespace pcs

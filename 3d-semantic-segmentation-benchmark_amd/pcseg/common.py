@@ -364,6 +364,11 @@ class GeometryPrefetch:
         geometry launches leave the GPU idle: the forward has drained its queue by then."""
         self._pcs_prefetch_armed = x
 
+    def prefetch_geometry_at_start(self, x: torch.Tensor) -> None:
+        """Arm a prefetch for the NEXT forward that is enqueued as soon as THIS forward has taken
+        its own (prefetched) plan: the next batch's FPS then runs under this forward and backward."""
+        self._pcs_prefetch_next = x
+
     def _prefetch_point(self, t: torch.Tensor) -> torch.Tensor:
         x = getattr(self, '_pcs_prefetch_armed', None)
         if x is not None and torch.is_grad_enabled() and t.requires_grad:
@@ -380,9 +385,15 @@ class GeometryPrefetch:
         pf = getattr(self, '_pcs_prefetched', None)
         self._pcs_prefetched = None
         if pf is not None and pf[0] is x and pf[1] == x._version:
-            return pf[2]
-        # the inverse maps serve only the backward of the gathers: none under no_grad (eval)
-        return self._plan_for(coords, inverse=torch.is_grad_enabled())
+            plan = pf[2]
+        else:
+            # the inverse maps serve only the backward of the gathers: none under no_grad (eval)
+            plan = self._plan_for(coords, inverse=torch.is_grad_enabled())
+        nxt = getattr(self, '_pcs_prefetch_next', None)
+        if nxt is not None:
+            self._pcs_prefetch_next = None
+            self.prefetch_geometry(nxt)
+        return plan
 
     @staticmethod
     def _coords_of(x: torch.Tensor) -> torch.Tensor:

@@ -295,6 +295,7 @@ def run_workload(key, batch, npoints, args, world, rank, dev):
     prefetch = hasattr(model, 'prefetch_geometry') and not args.no_prefetch
 
     in_bwd = args.prefetch_point == 'backward'
+    at_start = args.prefetch_point == 'start'
 
     def step():
         grads.zero_grad()
@@ -303,8 +304,10 @@ def run_workload(key, batch, npoints, args, world, rank, dev):
             # blocks, fresh FPS starts) runs on the side stream under this backward,
             # enqueued from a gradient hook once the first backward stages are queued
             model.prefetch_geometry_in_backward(x)
+        if prefetch and at_start:
+            model.prefetch_geometry_at_start(x)      # enqueued right after this forward takes its plan
         loss = pcseg.masked_onehot_cross_entropy(logits_of(model(x)), lab, lengths)
-        if prefetch and not in_bwd:
+        if prefetch and not in_bwd and not at_start:
             model.prefetch_geometry(x)
         loss.backward()
         grads.synchronize()
@@ -467,7 +470,7 @@ def main():
     ap.add_argument('--graph', action='store_true',
                     help='capture the training step in HIP graphs (pcseg.graphs.CapturedStep) and time its replays '
                          '(N=1 only; multi-GPU steps run eagerly)')
-    ap.add_argument('--prefetch-point', choices=['backward', 'loss'], default='loss',
+    ap.add_argument('--prefetch-point', choices=['backward', 'loss', 'start'], default='loss',
                     help="where the next step's geometry is enqueued: between the loss and backward() (default) "
                          "or from a gradient hook inside the backward (round 2 A/B: within noise, 5.50 vs 5.52 ms)")
     ap.add_argument('--no-prefetch', action='store_true',
