@@ -28,14 +28,18 @@
 // (dy, z) rows is an L2 hit.
 #include "mlp_common.hpp"
 
+#include <cstdlib>
+#include <cstring>
+
 namespace pcs {
 
-constexpr int DG_BM = 64, DG_BN = 64, DG_BK = 32, DG_NS = 3;
+constexpr int DG_BM = 64, DG_BK = 32;
 constexpr int DG_A = DG_BM * DG_BK;                  // floats of one dy (or z) slab: 8 KB
-constexpr int DG_B = DG_BK * DG_BN;                  // the W slab: 8 KB
 constexpr int DG_C = 256;                            // coefficients: s, t, mean, alpha, kb x 32 (+ pad)
-constexpr int DG_STAGE = 2 * DG_A + DG_B + DG_C;     // 6400 floats = 25 KB
-constexpr int DG_DMA = 7;                            // DMA instructions per wave and stage
+
+// waitcnt immediate for "vmcnt(n)" alone (gfx9 encoding: vmcnt[3:0] at bits 3:0, vmcnt[5:4] at
+// 15:14; expcnt and lgkmcnt left at their maxima)
+constexpr int dg_vmcnt(int n) { return (n & 15) | ((n >> 4) << 14) | (7 << 4) | (15 << 8); }
 
 struct DgradArgs {
     Operand a;                 // BNBWD: data = dy (ld), z (ldz), s, t, mean, alpha, kb, act/slope
@@ -68,10 +72,18 @@ __device__ __forceinline__ unsigned dg_lds_addr(const float* p) {
 
 __device__ __forceinline__ void dg_barrier() { asm volatile("s_barrier" ::: "memory"); }
 
-template <bool BWD>
-__global__ __launch_bounds__(256, 2) void dgrad_kernel(const DgradArgs g) {
-    __shared__ __attribute__((aligned(16))) float lds[DG_NS * DG_STAGE];
-    __shared__ double red[2][2][DG_BN];
+// BN = 64 or 128 output columns per block (4 waves as 2 x 2: a wave owns 32 rows x BN/2
+// columns, TN = BN / 64 MFMA blocks), NS ring stages
+template <bool BWD, int BN, int NS>
+__global__ __launch_bounds__(256, BN == 64 || NS == 2 ? 2 : 1) void dgrad_kernel(const DgradArgs g) {
+    constexpr int TN = BN / 64;
+    constexpr int DB = DG_BK * BN;                      // the W slab
+    constexpr int STAGE = 2 * DG_A + DB + DG_C;         // floats per stage
+    constexpr int BI = BN / 32;                         // W-slab DMA instructions per wave (BN/16 per block)
+    constexpr int D = 5 + BI;                           // DMA instructions per wave and stage
+    constexpr int E = 16 * TN;                          // prefetched Z loads / full-tile stores per lane
+    __shared__ __attribute__((aligned(16))) float lds[NS * STAGE];
+    __shared__ double red[2][2][BN];
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -84,7 +96,7 @@ __global__ __launch_bounds__(256, 2) void dgrad_kernel(const DgradArgs g) {
     const int q8 = nwg / 8, r8 = nwg % 8, xcd = bid % 8;
     const int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
     const int rb = t / g.ntn, ct = t - rb * g.ntn;
-    const int n0 = ct * DG_BN;
+    const int n0 = ct * BN;
 
     const int nk = g.K / DG_BK;
     const int mtiles = (g.M + DG_BM - 1) / DG_BM;
@@ -93,11 +105,11 @@ __global__ __launch_bounds__(256, 2) void dgrad_kernel(const DgradArgs g) {
     const unsigned lbase = dg_lds_addr(lds);
     const int nlast = ((g.N + 3) & ~3) - 4;                // last in-range column quad
 
-    // ---- DMA of flattened iteration it (row tile it / nk, slab it % nk) into stage it % 3
+    // ---- DMA of flattened iteration it (row tile it / nk, slab it % nk) into stage it % NS
     auto issue = [&](int it) {
         const int ti = it / nk, ks = it - ti * nk;
         const int m0 = (rb + ti * g.gx) * DG_BM, k0 = ks * DG_BK;
-        const unsigned sb = lbase + 4u * (unsigned)((it % DG_NS) * DG_STAGE);
+        const unsigned sb = lbase + 4u * (unsigned)((it % NS) * STAGE);
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             const int r = 8 * (2 * wave + j) + (lane >> 3);
@@ -107,60 +119,77 @@ __global__ __launch_bounds__(256, 2) void dgrad_kernel(const DgradArgs g) {
             dg_glds16(g.a.data + (size_t)row * g.a.ld + k0 + ch, d);
             dg_glds16(g.a.z + (size_t)row * g.a.ldz + k0 + ch, d + 4u * DG_A);
         }
+        // W slab rows k0 .. k0+31, columns n0 .. n0+BN-1: 64 lanes x 16 B = 256 / BN * 4 rows per
+        // instruction, BI instructions per wave
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int kr = 4 * (2 * wave + j) + (lane >> 4);
-            const int col = min(n0 + 4 * (lane & 15), nlast);
-            const unsigned d = __builtin_amdgcn_readfirstlane(sb + 4u * (unsigned)(2 * DG_A + (2 * wave + j) * 256));
+        for (int j = 0; j < BI; ++j) {
+            const int e = (wave * BI + j) * 64 + lane;        // 16-B chunk of the slab
+            const int kr = e / (BN / 4), cq = e - kr * (BN / 4);
+            const int col = min(n0 + 4 * cq, nlast);
+            const unsigned d = __builtin_amdgcn_readfirstlane(sb + 4u * (unsigned)(2 * DG_A + (wave * BI + j) * 256));
             dg_glds16(g.W + (size_t)(k0 + kr) * g.ldw + col, d);
         }
         // coefficients: wave 0 s | t, wave 1 mean | alpha, wave 2 kb | kb, wave 3 kb | kb (pad)
         if (lane < 16) {
             const float* src = wave == 0 ? (lane < 8 ? g.a.s : g.a.t)
                              : wave == 1 ? (lane < 8 ? g.a.mean : g.a.alpha) : g.a.kb;
-            const unsigned d = __builtin_amdgcn_readfirstlane(sb + 4u * (unsigned)(2 * DG_A + DG_B + wave * 64));
+            const unsigned d = __builtin_amdgcn_readfirstlane(sb + 4u * (unsigned)(2 * DG_A + DB + wave * 64));
             dg_glds16(src + k0 + 4 * (lane & 7), d);
         }
     };
 
-    f32x16 acc = {};
-    double s1 = 0.0, s2 = 0.0;
-    // the epilogue's 16 Z values of this lane (previous layer's pre-BN output), loaded PF slabs
+    f32x16 acc[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[j] = f32x16{};
+    double s1[TN], s2[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) { s1[j] = 0.0; s2[j] = 0.0; }
+    // the epilogue's Z values of this lane (previous layer's pre-BN output), loaded PF slabs
     // before the tile's last one so their HBM latency hides under those slabs' work
     const int PF = nk >= 3 ? 2 : nk - 1;
-    const int col = n0 + wn * 32 + l32;
-    const bool cok = col < g.N;
-    const int colc = cok ? col : g.N - 1;
-    float zt[16];
+    int col[TN], colc[TN];
+    bool cok[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        col[j] = n0 + wn * (BN / 2) + 32 * j + l32;
+        cok[j] = col[j] < g.N;
+        colc[j] = cok[j] ? col[j] : g.N - 1;
+    }
+    float zt[TN][16];
+    bool stores_full = false;                  // the last epilogue's stores were unconditional
     // the epilogue's per-column coefficients, before any DMA (a load issued later would make the
     // compiler's wait for it drain the ring)
-    bool stores_full = false;                  // the last epilogue's 16 stores were unconditional
-    float sp = 0.f, tp = 0.f, mp = 0.f, ip = 0.f;
-    if (BWD) { sp = g.e.s[colc]; tp = g.e.t[colc]; mp = g.e.mean[colc]; ip = g.e.inv[colc]; }
-    for (int s = 0; s < DG_NS - 1; ++s)
+    float sp[TN], tp[TN], mp[TN], ip[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        sp[j] = tp[j] = mp[j] = ip[j] = 0.f;
+        if (BWD) { sp[j] = g.e.s[colc[j]]; tp[j] = g.e.t[colc[j]]; mp[j] = g.e.mean[colc[j]]; ip[j] = g.e.inv[colc[j]]; }
+    }
+    for (int s = 0; s < NS - 1; ++s)
         if (s < total) issue(s);
 
     for (int it = 0; it < total; ++it) {
         const int ti = it / nk, ks = it - ti * nk;
         const int m0 = (rb + ti * g.gx) * DG_BM;
-        float* st = lds + (it % DG_NS) * DG_STAGE;
+        float* st = lds + (it % NS) * STAGE;
         // stage it landed (this wave's DMAs), then everyone's.  Issued after this wave's stage-it
-        // DMAs and allowed to stay in flight: the next stage's 7 DMAs, and the Z prefetch's 16 loads
-        // between its issue (slab nk-1-PF) and the epilogue
-        // (and a full tile's 16 stores issued right after the previous tile's last DMA)
+        // DMAs and allowed to stay in flight: the next stage's D DMAs (NS = 3), the Z prefetch's
+        // loads between its issue and the epilogue, a full tile's stores right before the last DMA
         {
-            const bool nxt = min(total - 1, it + DG_NS - 2) > it;
-            const bool zf = (BWD && ks > nk - 1 - PF) || (ks == 0 && it > 0 && stores_full);
-            if (nxt && zf) asm volatile("s_waitcnt vmcnt(23)" ::: "memory");
-            else if (zf) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-            else if (nxt) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const bool nxt = min(total - 1, it + NS - 2) > it;
+            // (the Z loads count when issued after stage it's DMAs: at most NS - 1 slabs ago)
+            const bool ex = (BWD && ks > nk - 1 - PF && ks <= nk - 2 - PF + NS) || (ks == 0 && it > 0 && stores_full);
+            if (nxt && ex) __builtin_amdgcn_s_waitcnt(dg_vmcnt(D + E));
+            else if (ex) __builtin_amdgcn_s_waitcnt(dg_vmcnt(E));
+            else if (nxt) __builtin_amdgcn_s_waitcnt(dg_vmcnt(D));
+            else __builtin_amdgcn_s_waitcnt(dg_vmcnt(0));
+            asm volatile("" ::: "memory");
         }
         dg_barrier();
         // ---- BN-backward transform of the dy slab, in place: thread = (k quad kq, rows r, r + 32)
         {
             const int kq = tid & 7;
-            const float* cf = st + 2 * DG_A + DG_B;
+            const float* cf = st + 2 * DG_A + DB;
             Quad q;
             q.s = *reinterpret_cast<const float4*>(cf + 4 * kq);
             q.t = *reinterpret_cast<const float4*>(cf + 32 + 4 * kq);
@@ -180,93 +209,111 @@ __global__ __launch_bounds__(256, 2) void dgrad_kernel(const DgradArgs g) {
         dg_barrier();
         const bool last = ks == nk - 1;
         // the next DMA (into the stage every wave finished reading one iteration ago); after the
-        // epilogue instead on a tile's last slab, whose global loads would drain it early
-        if (!last && it + DG_NS - 1 < total) issue(it + DG_NS - 1);
+        // epilogue's sums instead on a tile's last slab
+        if (!last && it + NS - 1 < total) issue(it + NS - 1);
         if (BWD && ks == nk - 1 - PF) {
             const int rb0 = m0 + wm * 32;
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int row = min(rb0 + (r & 3) + 8 * (r >> 2) + 4 * h, g.M - 1);
-                zt[r] = g.e.z[(size_t)row * g.e.ldz + colc];
-            }
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int row = min(rb0 + (r & 3) + 8 * (r >> 2) + 4 * h, g.M - 1);
+                    zt[j][r] = g.e.z[(size_t)row * g.e.ldz + colc[j]];
+                }
         }
         // ---- MFMAs: slab into a fresh accumulator, then added (two-level, as the row GEMM)
         {
             const float* As = st;
             const float* Bs = st + 2 * DG_A;
             const int ar = wm * 32 + l32;
-            const int bc = wn * 32 + l32;
-            f32x16 sacc;
+            f32x16 sacc[TN];
 #pragma unroll
             for (int qq = 0; qq < 4; ++qq) {
                 const float4 a = *reinterpret_cast<const float4*>(As + ar * DG_BK + 4 * ((4 * h + qq) ^ dg_swz(ar)));
                 const int kb = 16 * h + 4 * qq;
-                const float b0 = Bs[(kb + 0) * DG_BN + bc], b1 = Bs[(kb + 1) * DG_BN + bc];
-                const float b2 = Bs[(kb + 2) * DG_BN + bc], b3 = Bs[(kb + 3) * DG_BN + bc];
-                const f32x16 c0 = {};
-                sacc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, b0, qq == 0 ? c0 : sacc, 0, 0, 0);
-                sacc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b1, sacc, 0, 0, 0);
-                sacc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, b2, sacc, 0, 0, 0);
-                sacc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b3, sacc, 0, 0, 0);
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    const int bc = wn * (BN / 2) + 32 * j + l32;
+                    const float b0 = Bs[(kb + 0) * BN + bc], b1 = Bs[(kb + 1) * BN + bc];
+                    const float b2 = Bs[(kb + 2) * BN + bc], b3 = Bs[(kb + 3) * BN + bc];
+                    const f32x16 c0 = {};
+                    sacc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, b0, qq == 0 ? c0 : sacc[j], 0, 0, 0);
+                    sacc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b1, sacc[j], 0, 0, 0);
+                    sacc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, b2, sacc[j], 0, 0, 0);
+                    sacc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b3, sacc[j], 0, 0, 0);
+                }
             }
-            acc += sacc;
+#pragma unroll
+            for (int j = 0; j < TN; ++j) acc[j] += sacc[j];
         }
         if (last) {
-            // ---- tile epilogue (gemm_rows_kernel's, one 32 x 32 block per wave): the BN-backward
-            // sums first (they wait for the prefetched Z), then the next DMA, then the stores --
-            // unconditional on a full tile, so the next wait can count them
+            // ---- tile epilogue (gemm_rows_kernel's): the BN-backward sums first (they wait for the
+            // prefetched Z), then the next DMA, then the stores -- unconditional on a full tile, so
+            // the next wait can count them
             const int rb0 = m0 + wm * 32;
-            const bool full = m0 + DG_BM <= g.M && n0 + DG_BN <= g.N;
-            float v[16];
+            const bool full = m0 + DG_BM <= g.M && n0 + BN <= g.N;
+            float v[TN][16];
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                v[r] = acc[r] + 0.f;                     // (the row GEMM's "+ bias" with bias 0: -0 -> +0)
-                acc[r] = 0.f;
-            }
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    v[j][r] = acc[j][r] + 0.f;           // (the row GEMM's "+ bias" with bias 0: -0 -> +0)
+                    acc[j][r] = 0.f;
+                }
             if (BWD) {
 #pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int row = rb0 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                    const bool ok = full || (row < g.M && cok);
-                    const float z = zt[r];
-                    const float dy = v[r] * dact_f(z * sp + tp, g.e.act, g.e.slope);
-                    const float xh = (z - mp) * ip;
-                    const double dd = ok ? (double)dy : 0.0;
-                    s1 += dd;
-                    s2 += dd * (double)xh;
-                }
+                for (int j = 0; j < TN; ++j)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int row = rb0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                        const bool ok = full || (row < g.M && cok[j]);
+                        const float z = zt[j][r];
+                        const float dy = v[j][r] * dact_f(z * sp[j] + tp[j], g.e.act, g.e.slope);
+                        const float xh = (z - mp[j]) * ip[j];
+                        const double dd = ok ? (double)dy : 0.0;
+                        s1[j] += dd;
+                        s2[j] += dd * (double)xh;
+                    }
             }
-            if (it + DG_NS - 1 < total) issue(it + DG_NS - 1);
+            if (it + NS - 1 < total) issue(it + NS - 1);
             stores_full = full;
             if (full) {
-                float* cb = g.C + (size_t)rb0 * g.ldc + col;
 #pragma unroll
-                for (int r = 0; r < 16; ++r) cb[(size_t)((r & 3) + 8 * (r >> 2) + 4 * h) * g.ldc] = v[r];
+                for (int j = 0; j < TN; ++j) {
+                    float* cb = g.C + (size_t)rb0 * g.ldc + col[j];
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) cb[(size_t)((r & 3) + 8 * (r >> 2) + 4 * h) * g.ldc] = v[j][r];
+                }
             } else {
 #pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int row = rb0 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                    if (row < g.M && cok) g.C[(size_t)row * g.ldc + col] = v[r];
-                }
+                for (int j = 0; j < TN; ++j)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int row = rb0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                        if (row < g.M && cok[j]) g.C[(size_t)row * g.ldc + col[j]] = v[j][r];
+                    }
             }
         }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_waitcnt(dg_vmcnt(0));
 
     if (BWD) {
-        const int lc = wn * 32 + l32;
-        const double a = s1 + __shfl_xor(s1, 32);
-        const double b = s2 + __shfl_xor(s2, 32);
-        if (lane < 32) {
-            red[0][wm][lc] = a;
-            red[1][wm][lc] = b;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int lc = wn * (BN / 2) + 32 * j + l32;
+            const double a = s1[j] + __shfl_xor(s1[j], 32);
+            const double b = s2[j] + __shfl_xor(s2[j], 32);
+            if (lane < 32) {
+                red[0][wm][lc] = a;
+                red[1][wm][lc] = b;
+            }
         }
         __syncthreads();
-        for (int c = tid; c < DG_BN; c += 256) {
-            const int col = n0 + c;
-            if (col < g.N) {
-                g.bstats[(size_t)col * g.gx + rb] = red[0][0][c] + red[0][1][c];
-                g.bstats[((size_t)g.N + col) * g.gx + rb] = red[1][0][c] + red[1][1][c];
+        for (int c = tid; c < BN; c += 256) {
+            const int cl = n0 + c;
+            if (cl < g.N) {
+                g.bstats[(size_t)cl * g.gx + rb] = red[0][0][c] + red[0][1][c];
+                g.bstats[((size_t)g.N + cl) * g.gx + rb] = red[1][0][c] + red[1][1][c];
             }
         }
     }
@@ -277,6 +324,36 @@ bool dgrad_dma_ok(const pcs_operand* a, int M, int K, const float* W, int ldw, i
     return a && a->mode == PCS_OP_BNBWD && M >= 1 && K >= DG_BK && K % DG_BK == 0 && N >= 4 && N % 4 == 0 &&
            ldw % 4 == 0 && ldw >= N && al16(W) && a->ld % 4 == 0 && a->ldz % 4 == 0 && al16(a->data) &&
            al16(a->z) && al16(a->s) && al16(a->t) && al16(a->mean) && al16(a->alpha) && al16(a->kb);
+}
+
+// variant: column tile x ring stages.  Default 128 x 2 (N > 64: one column tile reads the row
+// block's dy and Z once; two stages fit two blocks per CU): the PointNet++ 131072 x 128 x 128
+// dgrad 95.5 -> 80.2 us isolated, step 5.05 -> 5.01 ms; 128 x 3 (one block per CU) 105.8 us
+// (profiles/r04_ab_dgrad_variants.txt).  PCS_DGRAD_VAR = "64x3" | "128x2" | "128x3" (A/B)
+static int dgrad_variant() {
+    static const int v = [] {
+        const char* e = getenv("PCS_DGRAD_VAR");
+        if (e && !strcmp(e, "64x3")) return 0;
+        if (e && !strcmp(e, "128x3")) return 2;
+        return 1;
+    }();
+    return v;
+}
+
+int dgrad_dma_bn(int N) { return dgrad_variant() && N > 64 ? 128 : 64; }
+
+const char* dgrad_dma_name(bool bwd, int N) {
+    static const char* const names[2][3] = {
+        {"pcs::dgrad_kernel<false, 64, 3>", "pcs::dgrad_kernel<false, 128, 2>", "pcs::dgrad_kernel<false, 128, 3>"},
+        {"pcs::dgrad_kernel<true, 64, 3>", "pcs::dgrad_kernel<true, 128, 2>", "pcs::dgrad_kernel<true, 128, 3>"}};
+    return names[bwd][dgrad_dma_bn(N) == 64 ? 0 : dgrad_variant()];
+}
+
+template <int BN, int NS>
+static void launch_dgrad(const DgradArgs& g, bool bwd, hipStream_t st) {
+    const unsigned blocks = (unsigned)((long long)g.gx * g.ntn);
+    if (bwd) hipLaunchKernelGGL((dgrad_kernel<true, BN, NS>), dim3(blocks), dim3(256), 0, st, g);
+    else hipLaunchKernelGGL((dgrad_kernel<false, BN, NS>), dim3(blocks), dim3(256), 0, st, g);
 }
 
 int dgrad_dma(const pcs_operand* a, int M, int K, const float* W, int ldw, float* C, int ldc, int N,
@@ -293,11 +370,14 @@ int dgrad_dma(const pcs_operand* a, int M, int K, const float* W, int ldw, float
     if (epi) g.e = to_dev_operand(epi);
     g.bstats = bstats;
     g.gx = gx;
-    g.ntn = (N + DG_BN - 1) / DG_BN;
+    const int bn = dgrad_dma_bn(N);
+    g.ntn = (N + bn - 1) / bn;
     const long long blocks = (long long)gx * g.ntn;
     PCS_CHECK_ARG(gx >= 1 && blocks < (1ll << 31), "dgrad_dma: bad grid");
-    if (bstats) hipLaunchKernelGGL(dgrad_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, st, g);
-    else hipLaunchKernelGGL(dgrad_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, st, g);
+    const int v = dgrad_variant();
+    if (bn == 64) launch_dgrad<64, 3>(g, bstats != nullptr, st);
+    else if (v == 1) launch_dgrad<128, 2>(g, bstats != nullptr, st);
+    else launch_dgrad<128, 3>(g, bstats != nullptr, st);
     return 0;
 }
 

@@ -1239,7 +1239,7 @@ int pcs::gemm_rows_ex(const pcs_operand* a, int M, int K, const float* W, int ld
                 const double bytes = operand_bytes(*a, M, K) + 4.0 * M * N * (bstats ? 2 : 1);
                 const pcs_operand ac = *a, ec = epi ? *epi : pcs_operand{};
                 const bool he = epi != nullptr;
-                probe = probe_start(bstats ? "pcs::dgrad_kernel<true>" : "pcs::dgrad_kernel<false>", 2.0 * M * K * N,
+                probe = probe_start(dgrad_dma_name(bstats != nullptr, N), 2.0 * M * K * N,
                                     bytes, s, [=]() {
                                         gemm_rows_ex(&ac, M, K, W, ldw, bt, bias, C, ldc, N, stats, he ? &ec : nullptr,
                                                      bstats, stream);

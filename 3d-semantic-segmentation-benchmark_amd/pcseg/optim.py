@@ -12,6 +12,8 @@ graph (pcseg.graphs) replays with the right corrections.
 """
 from __future__ import annotations
 
+import collections
+
 import torch
 
 from ._lib import call, ptr, stream_ptr
@@ -20,9 +22,19 @@ from .engine import lane_join
 
 class FlatAdam:
     def __init__(self, grads, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
-                 weight_decay: float = 0.0):
-        """grads: a pcseg.ddp.FlatGradAllReduce over the model's trainable parameters."""
+                 weight_decay: float = 0.0, max_inflight: int = 3):
+        """grads: a pcseg.ddp.FlatGradAllReduce over the model's trainable parameters.
+
+        max_inflight: training steps the host may enqueue ahead of the GPU (0: unbounded).  A
+        step's buffers read by the side streams (the wgrad lane, the geometry stream) are held
+        by the caching allocator until those streams pass the point where they were freed, so
+        a host running N steps ahead holds N steps of them: DGCNN 5 GiB per step, until an
+        allocation fails and the allocator frees its whole cache (a multi-second stall,
+        profiles/r04_host_runahead.txt).  Each step() waits for the step max_inflight back,
+        which leaves the GPU that many steps of queued work."""
         self.grads = grads
+        self.max_inflight = int(max_inflight)
+        self._inflight: collections.deque = collections.deque()
         self.lr, self.betas, self.eps, self.weight_decay = float(lr), tuple(betas), float(eps), float(weight_decay)
         flat_g = grads.flat
         self.flat = torch.zeros_like(flat_g)       # (alignment pads between parameters stay 0)
@@ -56,3 +68,9 @@ class FlatAdam:
         call('pcs_adam_dev', ptr(self.flat), ptr(self.grads.flat), ptr(self.exp_avg), ptr(self.exp_avg_sq),
              self.flat.numel(), 1 - b1, b2, 1 - b2, self.lr, b1, b2, self.eps, self.weight_decay, ptr(self.state),
              stream_ptr(self.flat.device))
+        if self.max_inflight > 0 and not torch.cuda.is_current_stream_capturing():
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.flat.device))
+            self._inflight.append(ev)
+            while len(self._inflight) > self.max_inflight:
+                self._inflight.popleft().synchronize()

@@ -338,10 +338,42 @@ def run_workload(key, batch, npoints, args, world, rank, dev):
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
+    # PCS_BENCH_STEPLOG=1: per-step host enqueue times, and the main thread's stack whenever one
+    # step's enqueue has taken over 200 ms (a host stall: where it blocks)
+    steplog = os.environ.get('PCS_BENCH_STEPLOG') == '1'
+    th, stalls, cur, mem = [], [], [None], []
+    if steplog:
+        import threading
+        import traceback
+        main_id, done = threading.get_ident(), threading.Event()
+
+        def watch():
+            while not done.wait(0.1):
+                ts = cur[0]
+                if ts is not None and time.perf_counter() - ts > 0.2:
+                    fr = sys._current_frames().get(main_id)
+                    stalls.append(f'+{(time.perf_counter() - ts) * 1e3:.0f} ms: ' +
+                                  ' <- '.join(f'{os.path.basename(f.filename)}:{f.lineno}:{f.name}'
+                                              for f in reversed(traceback.extract_stack(fr)[-8:])))
+        wt = threading.Thread(target=watch, daemon=True)
+        wt.start()
     t0 = time.perf_counter()
     for _ in range(args.steps):
+        cur[0] = time.perf_counter()
         loss = step()
+        if steplog:
+            th.append(time.perf_counter())
+            mem.append(torch.cuda.memory_reserved(dev) / 2**30)
+    cur[0] = None
     t_host = time.perf_counter() - t0          # host enqueue time (the step has no host sync)
+    if steplog:
+        done.set()
+        wt.join()
+        print(f'[bench] {name} host ms per step: ' + ' '.join(f'{(b - a) * 1e3:.1f}' for a, b in zip([t0] + th, th)),
+              file=sys.stderr, flush=True)
+        print(f'[bench] {name} reserved GiB per step: ' + ' '.join(f'{m:.0f}' for m in mem), file=sys.stderr, flush=True)
+        for x in stalls:
+            print(f'[bench] {name} stall {x}', file=sys.stderr, flush=True)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()

@@ -1,13 +1,13 @@
 """Isolated timing of the BN-backward data gradient (pcs_gemm_rows_kmajor, BNBWD operand, fused
 BN-backward epilogue) on the PointNet++ dgrad shapes; PCS_DGRAD_DMA=0 selects the register-staged
-row GEMM (run the script once per setting).  Prints us per launch and algorithmic GB/s."""
+row GEMM, PCS_DGRAD_VAR the DMA kernel's column tile x ring depth (run the script once per setting).  Prints us per launch and algorithmic GB/s."""
 import math, os, sys
 import torch
 sys.path[:0] = [os.path.join(os.path.dirname(os.path.abspath(__file__)), '..', '3d-semantic-segmentation-benchmark_amd')]
 from pcseg._lib import load, stream_ptr, OP_BNBWD
 from pcseg.engine import operand, gemm_rows_kmajor, ld4
 
-tag = os.environ.get('PCS_DGRAD_DMA', '1')
+tag = os.environ.get('PCS_DGRAD_DMA', '1') + ' var=' + os.environ.get('PCS_DGRAD_VAR', '64x3')
 st = stream_ptr(torch.device('cuda'))
 for (M, K, N) in [(131072, 128, 128), (262144, 64, 64), (65536, 256, 128), (65536, 128, 128), (32768, 256, 256)]:
     g = torch.Generator(device='cuda').manual_seed(1)

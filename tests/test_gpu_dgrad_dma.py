@@ -55,20 +55,22 @@ print(json.dumps(names))
 '''
 
 
-def _run(tmp_path, dma: str):
-    path = str(tmp_path / f'dgrad_{dma}.pt')
-    env = dict(os.environ, PCS_DGRAD_DMA=dma)
+def _run(tmp_path, dma: str, var: str = '64x3'):
+    path = str(tmp_path / f'dgrad_{dma}_{var}.pt')
+    env = dict(os.environ, PCS_DGRAD_DMA=dma, PCS_DGRAD_VAR=var)
     p = subprocess.run([sys.executable, '-c', CHILD, ROOT, path, json.dumps(SHAPES)], env=env,
                        capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stderr[-3000:]
     return torch.load(path, weights_only=True), json.loads(p.stdout.strip().splitlines()[-1])
 
 
-def test_dgrad_dma_bitwise_equal_to_row_gemm(tmp_path):
-    new, names_new = _run(tmp_path, '1')
+@pytest.mark.parametrize('var', ['64x3', '128x2', '128x3'])
+def test_dgrad_dma_bitwise_equal_to_row_gemm(tmp_path, var):
+    new, names_new = _run(tmp_path, '1', var)
     old, names_old = _run(tmp_path, '0')
     for (M, K, N), nn, no in zip(SHAPES, names_new, names_old):
-        assert nn == ['pcs::dgrad_kernel<true>', 'pcs::dgrad_kernel<false>'], (M, K, N, nn)
+        tile = '64, 3' if var == '64x3' or N <= 64 else var.replace('x', ', ')
+        assert nn == [f'pcs::dgrad_kernel<true, {tile}>', f'pcs::dgrad_kernel<false, {tile}>'], (M, K, N, nn)
         assert all(n.startswith('pcs::gemm_rows_kernel<64, 64, 2, 2, 2, true') for n in no), (M, K, N, no)
     for k in new:
         assert torch.equal(new[k], old[k]), k
