@@ -15,6 +15,7 @@ gradient GEMMs) from the output gradient and Z, so it is never stored either.
 """
 from __future__ import annotations
 
+import collections
 import ctypes
 import math
 import struct
@@ -196,6 +197,13 @@ _ws_cache: dict = {}
 # FlatGradAllReduce.synchronize join again, unconditionally).
 _lanes: dict = {}
 _join_queued: dict = {}      # device index -> autograd graph task whose backward has a join queued
+# Backward passes the host may run ahead of the GPU (0: unbounded).  The lane's inputs are
+# record_stream'ed, so the caching allocator holds them until the lane passes their free point:
+# a host N backward passes ahead holds N passes of them (DGCNN ~5 GiB each) until an allocation
+# fails and the allocator drops its whole cache, a multi-second stall
+# (profiles/r04_host_runahead.txt).  The join waits for the pass MAX_INFLIGHT_BACKWARDS back.
+MAX_INFLIGHT_BACKWARDS = 3
+_inflight: dict = {}         # device index -> deque of join events
 
 BWD_FUSE = {'default': 0, 'off': 1, 'all': 2}   # pcs_mlp_layer.bwd_fuse (include/pcseg.h)
 
@@ -226,6 +234,13 @@ def _queue_lane_join(dev: torch.device) -> None:
             del _join_queued[idx]
         with torch.cuda.device(idx):
             call('pcs_wgrad_lane_join', stream_ptr(torch.device('cuda', idx)))
+            if MAX_INFLIGHT_BACKWARDS > 0 and not torch.cuda.is_current_stream_capturing():
+                ev = torch.cuda.Event()
+                ev.record()
+                q = _inflight.setdefault(idx, collections.deque())
+                q.append(ev)
+                while len(q) > MAX_INFLIGHT_BACKWARDS:
+                    q.popleft().synchronize()
     torch.autograd.Variable._execution_engine.queue_callback(join)
 
 
