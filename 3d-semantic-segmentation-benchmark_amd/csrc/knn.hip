@@ -124,7 +124,10 @@ constexpr int KNN_TC = 32;      // candidates per tile
 constexpr int KNN_WAVES = 4;
 constexpr int KNN_QROWS = 32 * KNN_WAVES;
 constexpr int KNN_NMAX = 64;    // LDS items per row: top-k list + one survivor segment per lane half (<= 64: one per lane in a merge)
-constexpr int KNN_RS = KNN_NMAX;       // row stride in items
+// row stride in items: one item (2 banks) past the capacity.  At 64 items (512 B) every lane's
+// survivor write of a tile hit the same bank pair (SQ_LDS_BANK_CONFLICT 3.3x the LDS-active
+// cycles, round 4; the padding measured neutral on its own)
+constexpr int KNN_RS = KNN_NMAX + 1;
 
 // accumulator register i of lane half h holds candidate acc_row(i, h) of the tile
 // (v_mfma_f32_32x32x2_f32 C/D layout: row = (i & 3) + 8 (i >> 2) + 4 h, column = lane & 31)
@@ -384,6 +387,14 @@ __global__ __launch_bounds__(64 * WPB, 2) void knn_wave_kernel(const float* __re
         }
     };
     fetch(0, cur, cxx_cur);
+    // the first tile lands BEFORE the loop (a use of every loaded register here): with its loads
+    // still pending at the loop header, hipcc's wait insertion merged that state into the loop
+    // body and waited (vmcnt(1) before the MFMAs, vmcnt(0) in the filter) on every iteration for
+    // the NEXT tile's prefetch.  (Measured neutral, round 4: the L2-resident tile lands under the
+    // other wave's work anyway; kept so the prefetch is what the source says.)
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) asm volatile("" ::"v"(cur[q].x), "v"(cur[q].y), "v"(cur[q].z), "v"(cur[q].w));
+    asm volatile("" ::"v"(cxx_cur));
     for (int tt = 0; tt < ntile; ++tt) {
         const int c0 = tile_c0(tt);
         const int nc = min(KNN_TC, N - c0);

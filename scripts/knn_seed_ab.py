@@ -21,8 +21,8 @@ feats, graphs = [], []
 orig = pcseg.models.EdgeConv.forward_graph
 
 
-def rec(self, xp, seeds=None):
-    out, idx = orig(self, xp, seeds)
+def rec(self, xp, seeds=None, **kw):
+    out, idx = orig(self, xp, seeds, **kw)
     feats.append(xp.detach().clone())
     graphs.append(idx)
     return out, idx
