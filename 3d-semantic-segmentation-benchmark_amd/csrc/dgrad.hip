@@ -1,33 +1,32 @@
-// Data-gradient GEMM of a shared-MLP layer with its BN-backward operand, LDS-DMA staged:
-//   dA[M x N] = dZ[M x K] . W[K x N],  dZ = the layer's BN+activation backward rebuilt from
-//   (dy, z) (xform4<OP_BNBWD>), W the layer's weights read k-major (N = its input width);
+// Data-gradient GEMM of a shared-MLP layer, LDS-DMA staged:
+//   dA[M x N] = dZ[M x K] . W[K x N],  W the layer's weights read k-major (N = its input width),
+//   dZ either rebuilt from the layer's (dy, z) by its BN+activation backward (XF: A operand
+//   PCS_OP_BNBWD, xform4<OP_BNBWD>) or read as it lies (a materialised dZ, PCS_OP_PLAIN);
 //   optional epilogue: the previous layer's BN-backward partial sums (sum dy', sum dy'*xhat')
-//   over this block's rows -- exactly gemm_rows_kernel<64, 64, 2, 2, BNBWD, true, EPI> of mlp.hip
-//   (same k order inside a slab, same two-level fp32 accumulation, same epilogue), so the
-//   outputs are bitwise those of that kernel.
+//   over this block's rows -- exactly gemm_rows_kernel<64, 64, 2, 2, BNBWD | PLAIN, true, EPI> of
+//   mlp.hip (same k order inside a slab, same two-level fp32 accumulation, same epilogue), so the
+//   outputs are bitwise those of that kernel (tests/test_gpu_dgrad_dma.py).
 // Reference: the backward of models/utils/common.py:125-178 (MiniPointNet / UnitPointNet:
 // conv -> BN -> ReLU) as autograd runs it.
 //
 // Why a second kernel (VERDICT r3 #1b): the register-staged row GEMM holds one slab of (dy, z, W)
 // in VGPRs while computing the previous one and needs 240 VGPRs with its epilogue -- 2 waves per
-// SIMD, one slab in flight per block: a latency-bound ~0.25 of HBM on the PointNet++ critical
-// path.  Here the raw slabs go global -> LDS by LDS-DMA (global_load_lds_dwordx4, no VGPR
-// destination) through a 3-stage ring, two slabs ahead; the BN-backward transform is applied
-// once per element in a pass over the landed slab (LDS -> VGPR -> LDS, in place), then the MFMAs
-// read the transformed slab.  Per 256-thread block and stage: dy 64x32, z 64x32, the W slab
-// 32x64 and the slab's 5 x 32 BN-backward coefficients (25 KB; 75 KB for 3 stages: 2 blocks per
-// CU).  Every wave issues the same 7 DMA instructions per stage, so a stage is retired by a
-// counted `s_waitcnt vmcnt(7)` (one stage left in flight) + a raw s_barrier -- never
+// SIMD, one slab in flight per block, and over 64-column tiles it reads every row block's
+// operand once per column tile.  Here the raw slabs go global -> LDS by LDS-DMA
+// (global_load_lds_dwordx4, no VGPR destination) through an NS-stage ring; the BN-backward
+// transform (XF) is applied once per element in a pass over the landed slab (LDS -> VGPR -> LDS,
+// in place), then the MFMAs read the slab.  A block covers 64 rows x BN columns (BN = 128 when
+// N > 64: the row block's operand is read once).  Every wave issues the same D DMA instructions
+// per stage, so a stage is retired by a counted `s_waitcnt vmcnt` + a raw s_barrier -- never
 // __syncthreads(), whose fence would drain the ring (cdna_hip_programming.md, glds rules).
 // LDS images are lane-linear (an LDS-DMA writes base + 16 * lane); the dy / z rows (32 floats)
 // have their 16-B chunks XOR-swizzled by (row >> 1) & 7 on the SOURCE address and on every read,
 // so the fragment reads (ds_read_b128 of 16 rows) are bank-conflict free.  The W slab is stored
 // [k][n] as it lies in memory; a lane's B fragment is 4 ds_read_b32 down a column.
-// Grid: (row blocks) x (64-column tiles), persistent over row tiles like the row GEMM; the two
-// column tiles of a row block are adjacent in the XCD-remapped order, so the second read of its
-// (dy, z) rows is an L2 hit.
+// Grid: (row blocks) x (column tiles), persistent over row tiles like the row GEMM, XCD-remapped.
 #include "mlp_common.hpp"
 
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 
@@ -72,15 +71,21 @@ __device__ __forceinline__ unsigned dg_lds_addr(const float* p) {
 
 __device__ __forceinline__ void dg_barrier() { asm volatile("s_barrier" ::: "memory"); }
 
+// LDS floats of one ring stage: A slab (+ z slab + coefficients when XF) + the W slab
+constexpr int dg_stage(int BN, bool XF) { return (XF ? 2 * DG_A + DG_C : DG_A) + DG_BK * BN; }
+// blocks per CU the ring allows (160 KB of LDS)
+constexpr int dg_blocks(int BN, int NS, bool XF) { return NS * dg_stage(BN, XF) * 4 + 4096 <= 80 * 1024 ? 2 : 1; }
+
 // BN = 64 or 128 output columns per block (4 waves as 2 x 2: a wave owns 32 rows x BN/2
-// columns, TN = BN / 64 MFMA blocks), NS ring stages
-template <bool BWD, int BN, int NS>
-__global__ __launch_bounds__(256, BN == 64 || NS == 2 ? 2 : 1) void dgrad_kernel(const DgradArgs g) {
+// columns, TN = BN / 64 MFMA blocks), NS ring stages; XF: A is rebuilt by the BN backward
+template <bool BWD, int BN, int NS, bool XF>
+__global__ __launch_bounds__(256, dg_blocks(BN, NS, XF)) void dgrad_kernel(const DgradArgs g) {
     constexpr int TN = BN / 64;
     constexpr int DB = DG_BK * BN;                      // the W slab
-    constexpr int STAGE = 2 * DG_A + DB + DG_C;         // floats per stage
+    constexpr int AW = XF ? 2 * DG_A : DG_A;            // the A (+ z) slabs
+    constexpr int STAGE = dg_stage(BN, XF);             // floats per stage
     constexpr int BI = BN / 32;                         // W-slab DMA instructions per wave (BN/16 per block)
-    constexpr int D = 5 + BI;                           // DMA instructions per wave and stage
+    constexpr int D = (XF ? 5 : 2) + BI;                // DMA instructions per wave and stage
     constexpr int E = 16 * TN;                          // prefetched Z loads / full-tile stores per lane
     __shared__ __attribute__((aligned(16))) float lds[NS * STAGE];
     __shared__ double red[2][2][BN];
@@ -117,7 +122,7 @@ __global__ __launch_bounds__(256, BN == 64 || NS == 2 ? 2 : 1) void dgrad_kernel
             const int ch = 4 * ((lane & 7) ^ dg_swz(r));
             const unsigned d = __builtin_amdgcn_readfirstlane(sb + 4u * (unsigned)((2 * wave + j) * 256));
             dg_glds16(g.a.data + (size_t)row * g.a.ld + k0 + ch, d);
-            dg_glds16(g.a.z + (size_t)row * g.a.ldz + k0 + ch, d + 4u * DG_A);
+            if (XF) dg_glds16(g.a.z + (size_t)row * g.a.ldz + k0 + ch, d + 4u * DG_A);
         }
         // W slab rows k0 .. k0+31, columns n0 .. n0+BN-1: 64 lanes x 16 B = 256 / BN * 4 rows per
         // instruction, BI instructions per wave
@@ -126,14 +131,14 @@ __global__ __launch_bounds__(256, BN == 64 || NS == 2 ? 2 : 1) void dgrad_kernel
             const int e = (wave * BI + j) * 64 + lane;        // 16-B chunk of the slab
             const int kr = e / (BN / 4), cq = e - kr * (BN / 4);
             const int col = min(n0 + 4 * cq, nlast);
-            const unsigned d = __builtin_amdgcn_readfirstlane(sb + 4u * (unsigned)(2 * DG_A + (wave * BI + j) * 256));
+            const unsigned d = __builtin_amdgcn_readfirstlane(sb + 4u * (unsigned)(AW + (wave * BI + j) * 256));
             dg_glds16(g.W + (size_t)(k0 + kr) * g.ldw + col, d);
         }
         // coefficients: wave 0 s | t, wave 1 mean | alpha, wave 2 kb | kb, wave 3 kb | kb (pad)
-        if (lane < 16) {
+        if (XF && lane < 16) {
             const float* src = wave == 0 ? (lane < 8 ? g.a.s : g.a.t)
                              : wave == 1 ? (lane < 8 ? g.a.mean : g.a.alpha) : g.a.kb;
-            const unsigned d = __builtin_amdgcn_readfirstlane(sb + 4u * (unsigned)(2 * DG_A + DB + wave * 64));
+            const unsigned d = __builtin_amdgcn_readfirstlane(sb + 4u * (unsigned)(AW + DB + wave * 64));
             dg_glds16(src + k0 + 4 * (lane & 7), d);
         }
     };
@@ -187,7 +192,7 @@ __global__ __launch_bounds__(256, BN == 64 || NS == 2 ? 2 : 1) void dgrad_kernel
         }
         dg_barrier();
         // ---- BN-backward transform of the dy slab, in place: thread = (k quad kq, rows r, r + 32)
-        {
+        if constexpr (XF) {
             const int kq = tid & 7;
             const float* cf = st + 2 * DG_A + DB;
             Quad q;
@@ -204,9 +209,9 @@ __global__ __launch_bounds__(256, BN == 64 || NS == 2 ? 2 : 1) void dgrad_kernel
                 const float4 z = *reinterpret_cast<const float4*>(p + DG_A);
                 *reinterpret_cast<float4*>(p) = xform4<OP_BNBWD>(g.a, v, z, 0u, m0 + r, q, ks * DG_BK + 4 * kq, g.K);
             }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            dg_barrier();
         }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        dg_barrier();
         const bool last = ks == nk - 1;
         // the next DMA (into the stage every wave finished reading one iteration ago); after the
         // epilogue's sums instead on a tile's last slab
@@ -224,7 +229,7 @@ __global__ __launch_bounds__(256, BN == 64 || NS == 2 ? 2 : 1) void dgrad_kernel
         // ---- MFMAs: slab into a fresh accumulator, then added (two-level, as the row GEMM)
         {
             const float* As = st;
-            const float* Bs = st + 2 * DG_A;
+            const float* Bs = st + AW;
             const int ar = wm * 32 + l32;
             f32x16 sacc[TN];
 #pragma unroll
@@ -321,15 +326,19 @@ __global__ __launch_bounds__(256, BN == 64 || NS == 2 ? 2 : 1) void dgrad_kernel
 
 bool dgrad_dma_ok(const pcs_operand* a, int M, int K, const float* W, int ldw, int N) {
     auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
-    return a && a->mode == PCS_OP_BNBWD && M >= 1 && K >= DG_BK && K % DG_BK == 0 && N >= 4 && N % 4 == 0 &&
-           ldw % 4 == 0 && ldw >= N && al16(W) && a->ld % 4 == 0 && a->ldz % 4 == 0 && al16(a->data) &&
-           al16(a->z) && al16(a->s) && al16(a->t) && al16(a->mean) && al16(a->alpha) && al16(a->kb);
+    if (!a || (a->mode != PCS_OP_BNBWD && a->mode != PCS_OP_PLAIN)) return false;
+    const bool base = M >= 1 && K >= DG_BK && K % DG_BK == 0 && N >= 4 && N % 4 == 0 && ldw % 4 == 0 && ldw >= N &&
+                      al16(W) && a->ld % 4 == 0 && al16(a->data);
+    if (a->mode == PCS_OP_PLAIN) return base;
+    return base && a->ldz % 4 == 0 && al16(a->z) && al16(a->s) && al16(a->t) && al16(a->mean) && al16(a->alpha) &&
+           al16(a->kb);
 }
 
 // variant: column tile x ring stages.  Default 128 x 2 (N > 64: one column tile reads the row
 // block's dy and Z once; two stages fit two blocks per CU): the PointNet++ 131072 x 128 x 128
 // dgrad 95.5 -> 80.2 us isolated, step 5.05 -> 5.01 ms; 128 x 3 (one block per CU) 105.8 us
-// (profiles/r04_ab_dgrad_variants.txt).  PCS_DGRAD_VAR = "64x3" | "128x2" | "128x3" (A/B)
+// (profiles/r04_ab_dgrad_variants.txt).  A plain A operand has no z slab: 3 stages of 128
+// columns still fit two blocks per CU.  PCS_DGRAD_VAR = "64x3" | "128x2" | "128x3" (A/B)
 static int dgrad_variant() {
     static const int v = [] {
         const char* e = getenv("PCS_DGRAD_VAR");
@@ -342,18 +351,35 @@ static int dgrad_variant() {
 
 int dgrad_dma_bn(int N) { return dgrad_variant() && N > 64 ? 128 : 64; }
 
-const char* dgrad_dma_name(bool bwd, int N) {
-    static const char* const names[2][3] = {
-        {"pcs::dgrad_kernel<false, 64, 3>", "pcs::dgrad_kernel<false, 128, 2>", "pcs::dgrad_kernel<false, 128, 3>"},
-        {"pcs::dgrad_kernel<true, 64, 3>", "pcs::dgrad_kernel<true, 128, 2>", "pcs::dgrad_kernel<true, 128, 3>"}};
-    return names[bwd][dgrad_dma_bn(N) == 64 ? 0 : dgrad_variant()];
+// (BN, NS) of a launch
+static void dgrad_shape(int N, bool xf, int* bn, int* ns) {
+    *bn = dgrad_dma_bn(N);
+    *ns = *bn == 64 ? 3 : (dgrad_variant() == 2 ? 3 : 2);
+    (void)xf;
 }
 
-template <int BN, int NS>
+const char* dgrad_dma_name(bool bwd, bool xf, int N) {
+    int bn, ns;
+    dgrad_shape(N, xf, &bn, &ns);
+    static char names[2][2][3][48];
+    static bool init = false;
+    if (!init) {
+        const int shapes[3][2] = {{64, 3}, {128, 2}, {128, 3}};
+        for (int b = 0; b < 2; ++b)
+            for (int x = 0; x < 2; ++x)
+                for (int v = 0; v < 3; ++v)
+                    snprintf(names[b][x][v], sizeof names[b][x][v], "pcs::dgrad_kernel<%s, %d, %d, %s>",
+                             b ? "true" : "false", shapes[v][0], shapes[v][1], x ? "true" : "false");
+        init = true;
+    }
+    return names[bwd][xf][bn == 64 ? 0 : (ns == 2 ? 1 : 2)];
+}
+
+template <int BN, int NS, bool XF>
 static void launch_dgrad(const DgradArgs& g, bool bwd, hipStream_t st) {
     const unsigned blocks = (unsigned)((long long)g.gx * g.ntn);
-    if (bwd) hipLaunchKernelGGL((dgrad_kernel<true, BN, NS>), dim3(blocks), dim3(256), 0, st, g);
-    else hipLaunchKernelGGL((dgrad_kernel<false, BN, NS>), dim3(blocks), dim3(256), 0, st, g);
+    if (bwd) hipLaunchKernelGGL((dgrad_kernel<true, BN, NS, XF>), dim3(blocks), dim3(256), 0, st, g);
+    else hipLaunchKernelGGL((dgrad_kernel<false, BN, NS, XF>), dim3(blocks), dim3(256), 0, st, g);
 }
 
 int dgrad_dma(const pcs_operand* a, int M, int K, const float* W, int ldw, float* C, int ldc, int N,
@@ -370,14 +396,22 @@ int dgrad_dma(const pcs_operand* a, int M, int K, const float* W, int ldw, float
     if (epi) g.e = to_dev_operand(epi);
     g.bstats = bstats;
     g.gx = gx;
-    const int bn = dgrad_dma_bn(N);
+    const bool xf = a->mode == PCS_OP_BNBWD;
+    int bn, ns;
+    dgrad_shape(N, xf, &bn, &ns);
     g.ntn = (N + bn - 1) / bn;
     const long long blocks = (long long)gx * g.ntn;
     PCS_CHECK_ARG(gx >= 1 && blocks < (1ll << 31), "dgrad_dma: bad grid");
-    const int v = dgrad_variant();
-    if (bn == 64) launch_dgrad<64, 3>(g, bstats != nullptr, st);
-    else if (v == 1) launch_dgrad<128, 2>(g, bstats != nullptr, st);
-    else launch_dgrad<128, 3>(g, bstats != nullptr, st);
+    const bool bw = bstats != nullptr;
+    if (xf) {
+        if (bn == 64) launch_dgrad<64, 3, true>(g, bw, st);
+        else if (ns == 2) launch_dgrad<128, 2, true>(g, bw, st);
+        else launch_dgrad<128, 3, true>(g, bw, st);
+    } else {
+        if (bn == 64) launch_dgrad<64, 3, false>(g, bw, st);
+        else if (ns == 2) launch_dgrad<128, 2, false>(g, bw, st);
+        else launch_dgrad<128, 3, false>(g, bw, st);
+    }
     return 0;
 }
 

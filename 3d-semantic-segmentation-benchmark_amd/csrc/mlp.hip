@@ -1227,8 +1227,9 @@ int pcs::gemm_rows_ex(const pcs_operand* a, int M, int K, const float* W, int ld
         probe_stop(probe, s);
         return e;
     }
-    // the 64 x 64 BN-backward data gradient: LDS-DMA ring kernel (dgrad.hip), bitwise the same
-    if (bt && a->mode == PCS_OP_BNBWD && !stats && !pool_k && !bias && dgrad_dma_enabled() &&
+    // the 64 x 64 data gradient (BN-backward or plain dZ operand): LDS-DMA ring kernel
+    // (dgrad.hip), bitwise the same
+    if (bt && (a->mode == PCS_OP_BNBWD || a->mode == PCS_OP_PLAIN) && !stats && !pool_k && !bias && dgrad_dma_enabled() &&
         dgrad_dma_ok(a, M, K, W, ldw, N)) {
         int bm, bn;
         gemm_tile(M, N, true, &bm, &bn);
@@ -1239,7 +1240,7 @@ int pcs::gemm_rows_ex(const pcs_operand* a, int M, int K, const float* W, int ld
                 const double bytes = operand_bytes(*a, M, K) + 4.0 * M * N * (bstats ? 2 : 1);
                 const pcs_operand ac = *a, ec = epi ? *epi : pcs_operand{};
                 const bool he = epi != nullptr;
-                probe = probe_start(dgrad_dma_name(bstats != nullptr, N), 2.0 * M * K * N,
+                probe = probe_start(dgrad_dma_name(bstats != nullptr, a->mode == PCS_OP_BNBWD, N), 2.0 * M * K * N,
                                     bytes, s, [=]() {
                                         gemm_rows_ex(&ac, M, K, W, ldw, bt, bias, C, ldc, N, stats, he ? &ec : nullptr,
                                                      bstats, stream);

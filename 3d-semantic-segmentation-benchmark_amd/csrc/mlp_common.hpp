@@ -189,7 +189,7 @@ int gemm_rows_ex(const pcs_operand* a, int M, int K, const float* W, int ldw, in
 // gemm_rows_kernel<64, 64, 2, 2, BNBWD, true, 0 | EPI_BWD> for the shapes dgrad_dma_ok accepts;
 // gx = the row blocks (= BN-backward partials per column)
 bool dgrad_dma_ok(const pcs_operand* a, int M, int K, const float* W, int ldw, int N);
-const char* dgrad_dma_name(bool bwd, int N);   // the kernel dgrad_dma launches (probe / profile name)
+const char* dgrad_dma_name(bool bwd, bool xf, int N);   // the kernel dgrad_dma launches (probe / profile name)
 int dgrad_dma(const pcs_operand* a, int M, int K, const float* W, int ldw, float* C, int ldc, int N,
               const pcs_operand* epi, double* bstats, int gx, hipStream_t st);
 // wide-layer GEMM on plain operands (gemm_big.hip): C = A . B^T, A (M x R), B (N x R) row-major
