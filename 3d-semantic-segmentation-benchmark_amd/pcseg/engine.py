@@ -19,6 +19,7 @@ import collections
 import ctypes
 import math
 import struct
+import time
 
 import torch
 
@@ -204,6 +205,7 @@ _join_queued: dict = {}      # device index -> autograd graph task whose backwar
 # (profiles/r04_host_runahead.txt).  The join waits for the pass MAX_INFLIGHT_BACKWARDS back.
 MAX_INFLIGHT_BACKWARDS = 3
 _inflight: dict = {}         # device index -> deque of join events
+inflight_wait_s = [0.0]      # host seconds spent in those waits (bench.py reports it apart)
 
 BWD_FUSE = {'default': 0, 'off': 1, 'all': 2}   # pcs_mlp_layer.bwd_fuse (include/pcseg.h)
 
@@ -239,8 +241,11 @@ def _queue_lane_join(dev: torch.device) -> None:
                 ev.record()
                 q = _inflight.setdefault(idx, collections.deque())
                 q.append(ev)
-                while len(q) > MAX_INFLIGHT_BACKWARDS:
-                    q.popleft().synchronize()
+                if len(q) > MAX_INFLIGHT_BACKWARDS:
+                    t0 = time.perf_counter()
+                    while len(q) > MAX_INFLIGHT_BACKWARDS:
+                        q.popleft().synchronize()
+                    inflight_wait_s[0] += time.perf_counter() - t0
     torch.autograd.Variable._execution_engine.queue_callback(join)
 
 

@@ -13,6 +13,7 @@ graph (pcseg.graphs) replays with the right corrections.
 from __future__ import annotations
 
 import collections
+import time
 
 import torch
 
@@ -35,6 +36,7 @@ class FlatAdam:
         self.grads = grads
         self.max_inflight = int(max_inflight)
         self._inflight: collections.deque = collections.deque()
+        self.wait_s = 0.0                        # host seconds spent waiting on the bound
         self.lr, self.betas, self.eps, self.weight_decay = float(lr), tuple(betas), float(eps), float(weight_decay)
         flat_g = grads.flat
         self.flat = torch.zeros_like(flat_g)       # (alignment pads between parameters stay 0)
@@ -72,5 +74,8 @@ class FlatAdam:
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream(self.flat.device))
             self._inflight.append(ev)
-            while len(self._inflight) > self.max_inflight:
-                self._inflight.popleft().synchronize()
+            if len(self._inflight) > self.max_inflight:
+                t0 = time.perf_counter()
+                while len(self._inflight) > self.max_inflight:
+                    self._inflight.popleft().synchronize()
+                self.wait_s += time.perf_counter() - t0

@@ -357,6 +357,8 @@ def run_workload(key, batch, npoints, args, world, rank, dev):
                                               for f in reversed(traceback.extract_stack(fr)[-8:])))
         wt = threading.Thread(target=watch, daemon=True)
         wt.start()
+    from pcseg import engine as _eng
+    w0 = _eng.inflight_wait_s[0] + getattr(opt, 'wait_s', 0.0)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         cur[0] = time.perf_counter()
@@ -365,7 +367,9 @@ def run_workload(key, batch, npoints, args, world, rank, dev):
             th.append(time.perf_counter())
             mem.append(torch.cuda.memory_reserved(dev) / 2**30)
     cur[0] = None
-    t_host = time.perf_counter() - t0          # host enqueue time (the step has no host sync)
+    t_host = time.perf_counter() - t0          # host time of the K steps (the step has no host sync)
+    # of which waiting on the run-ahead bound (FlatAdam / engine join: max 3 steps ahead)
+    t_wait = _eng.inflight_wait_s[0] + getattr(opt, 'wait_s', 0.0) - w0
     if steplog:
         done.set()
         wt.join()
@@ -397,7 +401,8 @@ def run_workload(key, batch, npoints, args, world, rank, dev):
                       'baseline_config': cfg, 'model': name, 'global_batch': world * batch, 'npoints': npoints,
                       'parallelism': f'dp{world}', 'geometry_prefetch': prefetch, 'hip_graph': use_graph,
                       'stream_priority': args.stream_priority},
-           'host_enqueue_ms_per_step': round(t_host / args.steps * 1e3, 3),
+           'host_enqueue_ms_per_step': round((t_host - t_wait) / args.steps * 1e3, 3),
+           'host_runahead_wait_ms_per_step': round(t_wait / args.steps * 1e3, 3),
            'roofline': roof, 'step_roofline': step_roofline(key, npoints, batch, ms, roof)}
     del model, grads, opt
     torch.cuda.empty_cache()
@@ -430,16 +435,20 @@ def run_drop_in(key, batch, npoints, args, dev):
         opt.step()
         return loss
 
+    from pcseg import engine as _eng
+
     def timed(sync_item):
         for _ in range(args.warmup):
             step()
         torch.cuda.synchronize(dev)
+        w0 = _eng.inflight_wait_s[0]
         t0 = time.perf_counter()
         for _ in range(args.steps):
             loss = step()
             if sync_item:
                 float(loss.item())
-        t_host = time.perf_counter() - t0
+        # host time of the steps, less the engine's run-ahead waits (end-of-backward join)
+        t_host = time.perf_counter() - t0 - (_eng.inflight_wait_s[0] - w0)
         torch.cuda.synchronize(dev)
         return (time.perf_counter() - t0) / args.steps * 1e3, t_host / args.steps * 1e3
 
