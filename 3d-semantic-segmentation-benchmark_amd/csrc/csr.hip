@@ -195,9 +195,13 @@ __global__ __launch_bounds__(256) void inverse_sort_kernel(const int32_t* __rest
 // maps are launch-bound: 10-14 us each alone).  Each map has its own hist region.
 // (Round 4 first fused the scan into the rank kernel for every cloud: each of a cloud's chunks
 // then re-read all its chunks' counts -- quadratic in the chunk count, 0.98 ms per DGCNN map.)
-constexpr int kChunkMin = 4096, kRankMaxTargets = 8192, kInvBatch = 24;
+// a chunk holds two slots per target (>= 4096): the per-target passes of a rank block (LDS
+// counter init, bases) are paid once per 2 x targets slots.  Round 4, batched as the models call
+// it (scripts/inverse_ab.py): PointNet++ 8 maps 90 -> 70 us, DGCNN 4 maps 227 -> 223 us; one
+// slot per target, or chunks of >= 8192 / 16384 slots, measured slower
+constexpr int kChunkMin = 4096, kChunkPerTarget = 2, kRankMaxTargets = 8192, kInvBatch = 24;
 
-static int rank_chunk(int targets) { return std::max(kChunkMin, (targets + 255) / 256 * 256); }
+static int rank_chunk(int targets) { return std::max(kChunkMin, (targets + 255) / 256 * 256 * kChunkPerTarget); }
 
 struct InvMap {
     const int32_t* idx;
