@@ -590,6 +590,7 @@ def main():
                'data': 'synthetic S3DIS-like blocks (pcseg.synthetic), random-init weights',
                'config': dict(prim['config'], rccl_world=dist.get_world_size() if world > 1 else 1),
                'host_enqueue_ms_per_step': prim['host_enqueue_ms_per_step'],
+               'host_runahead_wait_ms_per_step': prim.get('host_runahead_wait_ms_per_step'),
                'roofline': prim['roofline'], 'step_roofline': prim['step_roofline'],
                'drop_in': prim.get('drop_in'),
                'cpu_baseline': cpu_res.get(args.model)}
