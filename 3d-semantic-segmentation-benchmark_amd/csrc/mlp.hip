@@ -795,6 +795,34 @@ __global__ __launch_bounds__(256) void pool_finalize_kernel(const float* __restr
     }
 }
 
+// the same, one channel quad per thread (N % 4 == 0, 16-B aligned pz / out, 4-B aligned pa / arg):
+// 16-B loads and stores and 32-bit quad indexing instead of a 64-bit modulo per element; the min
+// half of pz / pa is read only for a quad with a negative scale.  Same values as above.
+__global__ __launch_bounds__(256) void pool_finalize_q_kernel(const float4* __restrict__ pz,
+                                                              const uchar4* __restrict__ pa, int GN4, int nq,
+                                                              const float* __restrict__ s, const float* __restrict__ t,
+                                                              float slope, float4* __restrict__ out,
+                                                              uchar4* __restrict__ arg) {
+    for (int e = blockIdx.x * 256 + threadIdx.x; e < GN4; e += gridDim.x * 256) {
+        const int c = 4 * (e % nq);
+        const float4 sc = *reinterpret_cast<const float4*>(s + c), tc = *reinterpret_cast<const float4*>(t + c);
+        float4 z = pz[e];
+        uchar4 a = pa[e];
+        if (sc.x < 0.f || sc.y < 0.f || sc.z < 0.f || sc.w < 0.f) {
+            const float4 zn = pz[GN4 + e];
+            const uchar4 an = pa[GN4 + e];
+            if (sc.x < 0.f) { z.x = zn.x; a.x = an.x; }
+            if (sc.y < 0.f) { z.y = zn.y; a.y = an.y; }
+            if (sc.z < 0.f) { z.z = zn.z; a.z = an.z; }
+            if (sc.w < 0.f) { z.w = zn.w; a.w = an.w; }
+        }
+        out[e] = make_float4(act_f(z.x * sc.x + tc.x, 0, slope), act_f(z.y * sc.y + tc.y, 0, slope),
+                             act_f(z.z * sc.z + tc.z, 0, slope), act_f(z.w * sc.w + tc.w, 0, slope));
+        arg[e] = make_uchar4(sc.x == 0.f ? 0 : a.x, sc.y == 0.f ? 0 : a.y, sc.z == 0.f ? 0 : a.z,
+                             sc.w == 0.f ? 0 : a.w);
+    }
+}
+
 __global__ __launch_bounds__(256) void pool_fwd_kernel(const float* __restrict__ Z, int nq, int G, int K,
                                                        const float* __restrict__ s, const float* __restrict__ t,
                                                        int act, float slope, float* __restrict__ out,
@@ -1490,6 +1518,16 @@ int pcs::pool_finalize(const float* pz, const unsigned char* pa, long long G, in
                        int act, float slope, float* out, unsigned char* arg, hipStream_t st) {
     const long long GN = G * N;
     if (GN == 0) return 0;
+    auto al = [](const void* p, uintptr_t a) { return (reinterpret_cast<uintptr_t>(p) & (a - 1)) == 0; };
+    if (N % 4 == 0 && GN / 4 < (1ll << 31) && al(pz, 16) && al(out, 16) && al(pa, 4) && al(arg, 4) && al(s, 16) &&
+        al(t, 16)) {
+        const long long GN4 = GN / 4;
+        const unsigned blocks = (unsigned)std::min<long long>((GN4 + 255) / 256, 8192);
+        hipLaunchKernelGGL(pool_finalize_q_kernel, dim3(blocks), dim3(256), 0, st, reinterpret_cast<const float4*>(pz),
+                           reinterpret_cast<const uchar4*>(pa), (int)GN4, N / 4, s, t, eff_slope(act, slope),
+                           reinterpret_cast<float4*>(out), reinterpret_cast<uchar4*>(arg));
+        return launch_status("pool_finalize");
+    }
     long long blocks = (GN + 255) / 256;
     if (blocks > 8192) blocks = 8192;
     hipLaunchKernelGGL(pool_finalize_kernel, dim3((unsigned)blocks), dim3(256), 0, st, pz, pa, GN, N, s, t,
