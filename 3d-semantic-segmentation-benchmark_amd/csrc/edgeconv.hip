@@ -167,6 +167,48 @@ __global__ __launch_bounds__(256) void edgeconv_bwd_center_kernel(const float* _
     }
 }
 
+// the same, one channel quad per thread (Cout % 4 == 0, 16-B aligned rows): 16-B loads of dout /
+// S / pz, a 16-B store of D and 32-bit quad indexing instead of a 64-bit division per element;
+// the min half of pz is read only for a quad with a negative scale.  Same per-element arithmetic.
+__global__ __launch_bounds__(256) void edgeconv_bwd_center_q_kernel(const float4* __restrict__ dout,
+                                                                    const float4* __restrict__ pz,
+                                                                    const float4* __restrict__ S, int GN4, int nq,
+                                                                    int k, const float* __restrict__ coef,
+                                                                    const float* __restrict__ kBC, float slope,
+                                                                    float4* __restrict__ D, float* __restrict__ Gd) {
+    const int Cout = 4 * nq;
+    for (int e = blockIdx.x * 256 + threadIdx.x; e < GN4; e += gridDim.x * 256) {
+        const int g = e / nq, c = 4 * (e - g * nq);
+        const float4 sv = *reinterpret_cast<const float4*>(coef + c);
+        const float4 tv = *reinterpret_cast<const float4*>(coef + Cout + c);
+        const float4 mv = *reinterpret_cast<const float4*>(coef + 2 * Cout + c);
+        const float4 kbv = *reinterpret_cast<const float4*>(kBC + c);
+        const float4 kcv = *reinterpret_cast<const float4*>(kBC + Cout + c);
+        float4 z = pz[e];
+        if (sv.x < 0.f || sv.y < 0.f || sv.z < 0.f || sv.w < 0.f) {
+            const float4 zn = pz[GN4 + e];
+            if (sv.x < 0.f) z.x = zn.x;
+            if (sv.y < 0.f) z.y = zn.y;
+            if (sv.z < 0.f) z.z = zn.z;
+            if (sv.w < 0.f) z.w = zn.w;
+        }
+        const float4 dv = dout[e], Sv = S[e];
+        const float s4[4] = {sv.x, sv.y, sv.z, sv.w}, t4[4] = {tv.x, tv.y, tv.z, tv.w};
+        const float m4[4] = {mv.x, mv.y, mv.z, mv.w}, kb4[4] = {kbv.x, kbv.y, kbv.z, kbv.w};
+        const float kc4[4] = {kcv.x, kcv.y, kcv.z, kcv.w}, z4[4] = {z.x, z.y, z.z, z.w};
+        const float d4i[4] = {dv.x, dv.y, dv.z, dv.w}, S4[4] = {Sv.x, Sv.y, Sv.z, Sv.w};
+        float d4[4];
+        float* gr = Gd + (size_t)g * 2 * Cout + 2 * c + 1;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            d4[j] = s4[j] * (d4i[j] * dact_f(z4[j] * s4[j] + t4[j], ACT_LRELU, slope));
+            const double dp = (double)d4[j] - (double)k * kb4[j] - (double)kc4[j] * ((double)S4[j] - (double)k * m4[j]);
+            gr[2 * j] = (float)dp;
+        }
+        D[e] = make_float4(d4[0], d4[1], d4[2], d4[3]);
+    }
+}
+
 // per target point m (one wave, lanes over channels): sum over the edges whose neighbour is m
 //   G_in = sum [arg == kk] D_i  - cnt (kB + kC (Y_m - mean)) - kC sum Q_i ,  dY = G_in - dP_m -> G[:, 2c]
 // (z_e = Y_m + Q_i; fp64 accumulation, so the unspecified CSR order does not change the result)
@@ -342,9 +384,20 @@ PCS_API int pcs_edgeconv_bwd(const float* X, int ldx, int C, const int32_t* csr_
                        coef, slope, kEdgeRedRows, part);
     bn_bwd_finalize_launch(part, nb, Cout, G * k, coef, coef + 3 * Cout, dgamma, dbeta, kBC, kBC + Cout, 1, st);
     const long long GN = G * Cout;
-    const unsigned eg = (unsigned)std::min<long long>((GN + 255) / 256, 65536);
-    hipLaunchKernelGGL(edgeconv_bwd_center_kernel, dim3(eg), dim3(256), 0, st, dout, pz, S, G, Cout, k, coef, kBC,
-                       slope, D, Gd);
+    auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+    if (Cout % 4 == 0 && GN / 4 < (1ll << 31) && al16(dout) && al16(pz) && al16(S) && al16(D) && al16(coef) &&
+        al16(kBC)) {
+        const long long GN4 = GN / 4;
+        const unsigned eq = (unsigned)std::min<long long>((GN4 + 255) / 256, 65536);
+        hipLaunchKernelGGL(edgeconv_bwd_center_q_kernel, dim3(eq), dim3(256), 0, st,
+                           reinterpret_cast<const float4*>(dout), reinterpret_cast<const float4*>(pz),
+                           reinterpret_cast<const float4*>(S), (int)GN4, Cout / 4, k, coef, kBC, slope,
+                           reinterpret_cast<float4*>(D), Gd);
+    } else {
+        const unsigned eg = (unsigned)std::min<long long>((GN + 255) / 256, 65536);
+        hipLaunchKernelGGL(edgeconv_bwd_center_kernel, dim3(eg), dim3(256), 0, st, dout, pz, S, G, Cout, k, coef,
+                           kBC, slope, D, Gd);
+    }
     {
         // compulsory bytes: Y, Q, D, arg and the inverse map read once, the (dY | dP) rows written
         ProbeScope pr(st, 0.0, 4.0 * (double)G * Cout * 3 + (double)G * Cout + 4.0 * (double)G * (k + 1) +

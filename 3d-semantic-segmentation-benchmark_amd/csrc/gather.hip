@@ -46,16 +46,18 @@ __global__ void group_fwd_kernel(const float* __restrict__ xyz, const float* __r
 }
 
 // one thread per (row, 4 output channels): same per-element arithmetic, one 16-B store
-// (ld % 4 == 0; rows are 16-B aligned)
+// (ld % 4 == 0; rows are 16-B aligned).  I: the index type -- int whenever the quad count fits
+// (every bench shape): three 64-bit divisions per quad were a large share of its VALU work
+template <typename I>
 __global__ __launch_bounds__(256) void group_fwd_q_kernel(const float* __restrict__ xyz,
                                                           const float* __restrict__ feats,
                                                           const float* __restrict__ cent, const int* __restrict__ idx,
                                                           int C, int N, int K, int D, float r, int normalize,
-                                                          float* __restrict__ out, int nq, long long total) {
-    for (long long t = gtid(); t < total; t += gstride()) {
-        const long long row = t / nq;
+                                                          float* __restrict__ out, int nq, I total) {
+    for (I t = (I)blockIdx.x * 256 + threadIdx.x; t < total; t += (I)gridDim.x * 256) {
+        const I row = t / nq;
         const int q = (int)(t - row * nq);
-        const long long g = row / K;          // centroid row b*C + c
+        const I g = row / K;                  // centroid row b*C + c
         const int b = (int)(g / C);
         const long long pb = (long long)b * N + idx[row];
         float v[4];
@@ -73,7 +75,7 @@ __global__ __launch_bounds__(256) void group_fwd_q_kernel(const float* __restric
             }
             v[e] = x;
         }
-        reinterpret_cast<float4*>(out)[t] = make_float4(v[0], v[1], v[2], v[3]);
+        reinterpret_cast<float4*>(out)[(long long)t] = make_float4(v[0], v[1], v[2], v[3]);
     }
 }
 
@@ -131,15 +133,16 @@ __global__ void interp_fwd_kernel(const float* __restrict__ pts, const int* __re
 // [f1 | IDW-interpolate(pts)] rows in one pass, one thread per (row, 4 channels): the
 // skip features are copied, the interpolated quad uses float4 gathers of the three
 // neighbours with the scalar kernel's per-element arithmetic.  D1, D2, ld_out % 4 == 0.
+template <typename I>
 __global__ __launch_bounds__(256) void interp_cat_q_kernel(const float* __restrict__ f1, int D1,
                                                            const float* __restrict__ pts,
                                                            const int* __restrict__ idx,
                                                            const float* __restrict__ dist, int N, int M, int D2,
-                                                           float* __restrict__ out, int ldq, long long total) {
+                                                           float* __restrict__ out, int ldq, I total) {
     const int q1 = D1 / 4, nq = q1 + D2 / 4;
-    for (long long t = gtid(); t < total; t += gstride()) {
-        const long long row = t / nq;           // b*N + n
-        const int q = (int)(t - row * nq);
+    for (I t = (I)blockIdx.x * 256 + threadIdx.x; t < total; t += (I)gridDim.x * 256) {
+        const long long row = (long long)(t / nq);           // b*N + n
+        const int q = (int)(t - (I)row * nq);
         float4 o;
         if (q < q1) {
             o = reinterpret_cast<const float4*>(f1)[row * q1 + q];
@@ -201,8 +204,12 @@ PCS_API int pcs_group_fwd(const float* xyz, const float* feats, const float* cen
         ProbeScope pr(as_stream(stream), 0.0,
                       4.0 * ((double)B * N * (3 + D) + 3.0 * B * C + (double)B * C * K) + 4.0 * (double)total,
                       "pcs::group_fwd_q_kernel");
-        hipLaunchKernelGGL(group_fwd_q_kernel, grid_for(total / 4), dim3(256), 0, as_stream(stream), xyz, feats,
-                           centroids, idx, C, N, K, D, r, normalize, out, ld_out / 4, total / 4);
+        if (total / 4 < (1ll << 31) - 65536 * 256)
+            hipLaunchKernelGGL(group_fwd_q_kernel<int>, grid_for(total / 4), dim3(256), 0, as_stream(stream), xyz,
+                               feats, centroids, idx, C, N, K, D, r, normalize, out, ld_out / 4, (int)(total / 4));
+        else
+            hipLaunchKernelGGL(group_fwd_q_kernel<long long>, grid_for(total / 4), dim3(256), 0, as_stream(stream), xyz,
+                               feats, centroids, idx, C, N, K, D, r, normalize, out, ld_out / 4, total / 4);
         return launch_status("pcs_group_fwd");
     }
     hipLaunchKernelGGL(group_fwd_kernel, grid_for(total), dim3(256), 0, as_stream(stream), xyz, feats, centroids,
@@ -244,9 +251,14 @@ PCS_API int pcs_interp_fwd(const float* pts, const int32_t* idx, const float* di
     if (D % 4 == 0 && col_off % 4 == 0 && ld_out % 4 == 0 && ((uintptr_t)out | (uintptr_t)pts) % 16 == 0) {
         // the interpolated columns as the f1-less case of the fused kernel, shifted by col_off
         const long long rows = (long long)B * N;
-        hipLaunchKernelGGL(interp_cat_q_kernel, grid_for(rows * (D / 4)), dim3(256), 0, as_stream(stream),
-                           (const float*)nullptr, 0, pts, idx, dist, N, M, D, out + col_off, ld_out / 4,
-                           rows * (D / 4));
+        if (rows * (D / 4) < (1ll << 31) - 65536 * 256)
+            hipLaunchKernelGGL(interp_cat_q_kernel<int>, grid_for(rows * (D / 4)), dim3(256), 0, as_stream(stream),
+                               (const float*)nullptr, 0, pts, idx, dist, N, M, D, out + col_off, ld_out / 4,
+                               (int)(rows * (D / 4)));
+        else
+            hipLaunchKernelGGL(interp_cat_q_kernel<long long>, grid_for(rows * (D / 4)), dim3(256), 0,
+                               as_stream(stream), (const float*)nullptr, 0, pts, idx, dist, N, M, D, out + col_off,
+                               ld_out / 4, rows * (D / 4));
         return launch_status("pcs_interp_fwd");
     }
     hipLaunchKernelGGL(interp_fwd_kernel, grid_for(total), dim3(256), 0, as_stream(stream), pts, idx, dist, N, M, D,
@@ -282,7 +294,11 @@ PCS_API int pcs_interp_cat_fwd(const float* f1, int D1, const float* pts, const 
     ProbeScope pr(as_stream(stream), 9.0 * (double)B * N * D2,
                   4.0 * ((double)B * M * D2 + (double)B * N * D1 + 6.0 * B * N + (double)B * N * (D1 + D2)),
                   "pcs::interp_cat_q_kernel");
-    hipLaunchKernelGGL(interp_cat_q_kernel, grid_for(total), dim3(256), 0, as_stream(stream), f1, D1, pts, idx, dist,
-                       N, M, D2, out, ld_out / 4, total);
+    if (total < (1ll << 31) - 65536 * 256)
+        hipLaunchKernelGGL(interp_cat_q_kernel<int>, grid_for(total), dim3(256), 0, as_stream(stream), f1, D1, pts, idx,
+                           dist, N, M, D2, out, ld_out / 4, (int)total);
+    else
+        hipLaunchKernelGGL(interp_cat_q_kernel<long long>, grid_for(total), dim3(256), 0, as_stream(stream), f1, D1, pts,
+                           idx, dist, N, M, D2, out, ld_out / 4, total);
     return launch_status("pcs_interp_cat_fwd");
 }
