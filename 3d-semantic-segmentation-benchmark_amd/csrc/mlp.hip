@@ -1345,6 +1345,8 @@ static void wgrad_plan(int N, int K, int M, int* BO, int* BI, int* splits, int* 
     *BI = K > 64 ? 128 : 64;
     const int tiles = ((N + *BO - 1) / *BO) * ((K + *BI - 1) / *BI);
     // (512 / 256 blocks for the smaller ones measured +0.3 / +0.8 % on DGCNN, round 3)
+    // (round 4, in-step: 512 / 2048 blocks for the smaller ones were within noise of 1024 on both
+    // models -- shorter lane blocks did not free CUs for the critical path's small kernels sooner)
     const int target = 2.0 * M * N * K >= 1.6e10 ? 2048 : 1024;
     int sp = (target + tiles - 1) / tiles;
     // the partial tiles (sp x N x K floats, written once and read once by the reduce) stay
