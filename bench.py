@@ -489,8 +489,8 @@ def spawn_ranks(n):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=20)
-    ap.add_argument('--warmup', type=int, default=5)
+    ap.add_argument('--steps', type=int, default=30)
+    ap.add_argument('--warmup', type=int, default=10)
     ap.add_argument('--model', default='pointnetpp', choices=sorted(WORKLOADS))
     ap.add_argument('--secondary', default='auto', help="second workload on the same line ('auto': dgcnn when "
                                                         "--model is pointnetpp; 'none' to skip)")
