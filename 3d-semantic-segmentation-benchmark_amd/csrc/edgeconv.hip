@@ -346,7 +346,7 @@ PCS_API int pcs_edgeconv_fwd(const float* X, int ldx, int C, const int32_t* idx,
     }
     bn_finalize_launch(part, nb, Cout, G * k, gamma, beta, eps, momentum, run_mean, run_var, coef, coef + Cout,
                        coef + 2 * Cout, coef + 3 * Cout, num_batches, st);
-    return pool_finalize(pz, pa, G, Cout, coef, coef + Cout, ACT_LRELU, slope, out, arg, st);
+    return pool_finalize(pz, pa, G, Cout, coef, coef + Cout, nullptr, ACT_LRELU, slope, out, arg, st);
 }
 
 // Training-mode EdgeConv backward (the forward's saved tensors; csr_off/csr_ent = pcs_inverse_index

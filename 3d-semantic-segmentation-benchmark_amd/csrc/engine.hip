@@ -335,7 +335,7 @@ PCS_API int pcs_mlp_forward(const float* X, int ldx, int kin, int M, pcs_mlp_lay
         if (P.use_batch) {
             const int nb = pcs_gemm_row_blocks(M, C);
             if (int e = gemm_rows_ex(&a, M, K, P.W, (int)P.ldw, 0, P.bias, P.Z, C, C, part, nullptr, nullptr, stream,
-                                     pz, pa, pk))
+                                     pz, pa, pk, P.gamma))
                 return e;
             const bool track = P.run_mean != nullptr;
             bn_finalize_launch(part, nb, C, M, P.gamma, P.beta, (float)P.eps, track ? (float)P.momentum : 0.f,
@@ -343,7 +343,7 @@ PCS_API int pcs_mlp_forward(const float* X, int ldx, int kin, int M, pcs_mlp_lay
                                reinterpret_cast<long long*>(P.num_batches), st);
         } else {
             if (int e = gemm_rows_ex(&a, M, K, P.W, (int)P.ldw, 0, P.bias, P.Z, C, C, nullptr, nullptr, nullptr, stream,
-                                     pz, pa, pk))
+                                     pz, pa, pk, P.gamma))
                 return e;
             hipLaunchKernelGGL(bn_eval_coef_kernel, dim3((C + 255) / 256), dim3(256), 0, st, P.run_mean, P.run_var,
                                P.gamma, P.beta, (float)P.eps, C, s);
@@ -353,7 +353,7 @@ PCS_API int pcs_mlp_forward(const float* X, int ldx, int kin, int M, pcs_mlp_lay
     const pcs_mlp_layer& T = layers[nl - 1];
     const int C = (int)T.cout;
     if (fuse)
-        return pool_finalize(S.pz, S.pa, M / pool_k, C, T.coef, T.coef + C, (int)T.act, (float)T.slope, out, arg, st);
+        return pool_finalize(S.pz, S.pa, M / pool_k, C, T.coef, T.coef + C, T.gamma, (int)T.act, (float)T.slope, out, arg, st);
     if (pool_k)
         return pcs_pool_fwd(T.Z, C, M / pool_k, pool_k, T.coef, T.coef + C, (int)T.act, (float)T.slope, out, arg,
                             stream);

@@ -252,6 +252,9 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void gemm_rows_kernel(GemmArgs g) 
                     const int colc = cok ? col : g.N - 1;
                     const float bv = (g.bias && cok) ? g.bias[col] : 0.f;
                     float sp = 0.f, tp = 0.f, mp = 0.f, ip = 0.f;
+                    // pooling keeps one extreme per column: the max of C where the consumer's BN scale
+                    // (sign of gamma) is >= 0, else the min -- tracked as the max of -C (sign flip)
+                    const unsigned pflip = (do_pool && g.psign && g.psign[colc] < 0.f) ? 0x80000000u : 0u;
                     if (want_b) { sp = g.e.s[colc]; tp = g.e.t[colc]; mp = g.e.mean[colc]; ip = g.e.inv[colc]; }
 #pragma unroll
                     for (int i = 0; i < TM; ++i) {
@@ -260,11 +263,11 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void gemm_rows_kernel(GemmArgs g) 
                     const float* const Zb = g.e.z + (size_t)rb * g.e.ldz;
                     // fused pooling state of this lane's rows of the 32-row block (a group of 32, or
                     // one group of 16 per hb): running max/min of C and the first row reaching it
-                    float pmx = -INFINITY, pmn = INFINITY;
-                    int imx = 4 * h, imn = 4 * h;
+                    float pmx = -INFINITY;
+                    int imx = 4 * h;
 #pragma unroll
                     for (int hb = 0; hb < 2; ++hb) {     // Z loads batched 8 at a time (register budget)
-                        if (do_pool && g.pool_k == 16 && hb == 1) { pmx = -INFINITY; pmn = INFINITY; imx = imn = 16 + 4 * h; }
+                        if (do_pool && g.pool_k == 16 && hb == 1) { pmx = -INFINITY; imx = 16 + 4 * h; }
                         float zt[8];
                         if (want_b) {
 #pragma unroll
@@ -294,8 +297,8 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void gemm_rows_kernel(GemmArgs g) 
                             }
                             if (do_pool) {
                                 const int rib = rl;                          // increasing in r: first wins
-                                if (v > pmx) { pmx = v; imx = rib; }
-                                if (v < pmn) { pmn = v; imn = rib; }
+                                const float pv = __uint_as_float(__float_as_uint(v) ^ pflip);
+                                if (pv > pmx) { pmx = pv; imx = rib; }
                             }
                             if (want_stats) {
                                 const double d = ok ? (double)v : 0.0;
@@ -314,18 +317,16 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void gemm_rows_kernel(GemmArgs g) 
                         }
                         if (do_pool && (g.pool_k == 16 || hb == 1)) {
                             // merge with the other lane half (same column, the other rows), first row on ties
-                            const float ox = __shfl_xor(pmx, 32), on = __shfl_xor(pmn, 32);
-                            const int oix = __shfl_xor(imx, 32), oin = __shfl_xor(imn, 32);
+                            const float ox = __shfl_xor(pmx, 32);
+                            const int oix = __shfl_xor(imx, 32);
                             if (ox > pmx || (ox == pmx && oix < imx)) { pmx = ox; imx = oix; }
-                            if (on < pmn || (on == pmn && oin < imn)) { pmn = on; imn = oin; }
                             const int r0 = rb + (g.pool_k == 16 ? 16 * hb : 0);
                             if (h == 0 && cok && r0 < g.M) {
                                 const size_t G = (size_t)(g.M / g.pool_k), gi = (size_t)(r0 / g.pool_k);
                                 const int base = g.pool_k == 16 ? 16 * hb : 0;
-                                g.pz[gi * g.N + col] = pmx;
-                                g.pz[(G + gi) * g.N + col] = pmn;
-                                g.pa[gi * g.N + col] = (unsigned char)(imx - base);
-                                g.pa[(G + gi) * g.N + col] = (unsigned char)(imn - base);
+                                const size_t o = ((pflip ? G : 0) + gi) * g.N + col;
+                                g.pz[o] = __uint_as_float(__float_as_uint(pmx) ^ pflip);
+                                g.pa[o] = (unsigned char)(imx - base);
                             }
                         }
                     }
@@ -783,12 +784,12 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restr
 __global__ __launch_bounds__(256) void pool_finalize_kernel(const float* __restrict__ pz,
                                                             const unsigned char* __restrict__ pa, long long GN, int N,
                                                             const float* __restrict__ s, const float* __restrict__ t,
-                                                            float slope, float* __restrict__ out,
-                                                            unsigned char* __restrict__ arg) {
+                                                            const float* __restrict__ sgn, float slope,
+                                                            float* __restrict__ out, unsigned char* __restrict__ arg) {
     for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < GN; e += (long long)gridDim.x * 256) {
         const int c = (int)(e % N);
         const float sc = s[c], tc = t[c];
-        const bool neg = sc < 0.f;
+        const bool neg = (sgn ? sgn[c] : sc) < 0.f;
         const float z = pz[neg ? GN + e : e];
         out[e] = act_f(z * sc + tc, 0, slope);
         arg[e] = sc == 0.f ? (unsigned char)0 : pa[neg ? GN + e : e];
@@ -801,20 +802,23 @@ __global__ __launch_bounds__(256) void pool_finalize_kernel(const float* __restr
 __global__ __launch_bounds__(256) void pool_finalize_q_kernel(const float4* __restrict__ pz,
                                                               const uchar4* __restrict__ pa, int GN4, int nq,
                                                               const float* __restrict__ s, const float* __restrict__ t,
-                                                              float slope, float4* __restrict__ out,
-                                                              uchar4* __restrict__ arg) {
+                                                              const float* __restrict__ sgn, float slope,
+                                                              float4* __restrict__ out, uchar4* __restrict__ arg) {
     for (int e = blockIdx.x * 256 + threadIdx.x; e < GN4; e += gridDim.x * 256) {
         const int c = 4 * (e % nq);
         const float4 sc = *reinterpret_cast<const float4*>(s + c), tc = *reinterpret_cast<const float4*>(t + c);
-        float4 z = pz[e];
-        uchar4 a = pa[e];
-        if (sc.x < 0.f || sc.y < 0.f || sc.z < 0.f || sc.w < 0.f) {
+        const float4 ng = sgn ? *reinterpret_cast<const float4*>(sgn + c) : sc;
+        const bool nx = ng.x < 0.f, ny = ng.y < 0.f, nz = ng.z < 0.f, nw = ng.w < 0.f;
+        float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+        uchar4 a = make_uchar4(0, 0, 0, 0);
+        if (!(nx && ny && nz && nw)) { z = pz[e]; a = pa[e]; }
+        if (nx || ny || nz || nw) {
             const float4 zn = pz[GN4 + e];
             const uchar4 an = pa[GN4 + e];
-            if (sc.x < 0.f) { z.x = zn.x; a.x = an.x; }
-            if (sc.y < 0.f) { z.y = zn.y; a.y = an.y; }
-            if (sc.z < 0.f) { z.z = zn.z; a.z = an.z; }
-            if (sc.w < 0.f) { z.w = zn.w; a.w = an.w; }
+            if (nx) { z.x = zn.x; a.x = an.x; }
+            if (ny) { z.y = zn.y; a.y = an.y; }
+            if (nz) { z.z = zn.z; a.z = an.z; }
+            if (nw) { z.w = zn.w; a.w = an.w; }
         }
         out[e] = make_float4(act_f(z.x * sc.x + tc.x, 0, slope), act_f(z.y * sc.y + tc.y, 0, slope),
                              act_f(z.z * sc.z + tc.z, 0, slope), act_f(z.w * sc.w + tc.w, 0, slope));
@@ -1236,7 +1240,7 @@ int pcs::materialize_dz(const pcs_operand* x, int M, int C, float* out, int ldo,
 // (B[k][n] = W[k*ldw + n], ldw >= N) -- the data-gradient GEMM on the layer's own weights.
 int pcs::gemm_rows_ex(const pcs_operand* a, int M, int K, const float* W, int ldw, int bt, const float* bias, float* C,
                  int ldc, int N, double* stats, const pcs_operand* epi, double* bstats, void* stream, float* pz,
-                 unsigned char* pa, int pool_k) {
+                 unsigned char* pa, int pool_k, const float* psign) {
     PCS_CHECK_ARG(pool_k == 0 || ((pool_k == 16 || pool_k == 32) && M % pool_k == 0 && pz && pa && !bt),
                   "pcs_gemm_rows: fused pooling needs pool_k 16|32 dividing M and pz/pa");
     PCS_CHECK_ARG(M >= 0 && K >= 1 && N >= 1, "pcs_gemm_rows: bad sizes M=%d K=%d N=%d", M, K, N);
@@ -1294,7 +1298,7 @@ int pcs::gemm_rows_ex(const pcs_operand* a, int M, int K, const float* W, int ld
             return launch_status("pcs_gemm_rows");
         }
     }
-    GemmArgs g{to_dev(a), M, K, W, ldw, bias, C, ldc, N, stats, to_dev(epi), bstats, pz, pa, pool_k};
+    GemmArgs g{to_dev(a), M, K, W, ldw, bias, C, ldc, N, stats, to_dev(epi), bstats, pz, pa, pool_k, psign};
     int probe = -1;
     if (probe_enabled()) {
         char nm[96];
@@ -1517,22 +1521,22 @@ PCS_API int pcs_pool_fwd(const float* Z, int N, long long G, int K, const float*
 }
 
 int pcs::pool_finalize(const float* pz, const unsigned char* pa, long long G, int N, const float* s, const float* t,
-                       int act, float slope, float* out, unsigned char* arg, hipStream_t st) {
+                       const float* sgn, int act, float slope, float* out, unsigned char* arg, hipStream_t st) {
     const long long GN = G * N;
     if (GN == 0) return 0;
     auto al = [](const void* p, uintptr_t a) { return (reinterpret_cast<uintptr_t>(p) & (a - 1)) == 0; };
     if (N % 4 == 0 && GN / 4 < (1ll << 31) && al(pz, 16) && al(out, 16) && al(pa, 4) && al(arg, 4) && al(s, 16) &&
-        al(t, 16)) {
+        al(t, 16) && al(sgn, 16)) {
         const long long GN4 = GN / 4;
         const unsigned blocks = (unsigned)std::min<long long>((GN4 + 255) / 256, 8192);
         hipLaunchKernelGGL(pool_finalize_q_kernel, dim3(blocks), dim3(256), 0, st, reinterpret_cast<const float4*>(pz),
-                           reinterpret_cast<const uchar4*>(pa), (int)GN4, N / 4, s, t, eff_slope(act, slope),
+                           reinterpret_cast<const uchar4*>(pa), (int)GN4, N / 4, s, t, sgn, eff_slope(act, slope),
                            reinterpret_cast<float4*>(out), reinterpret_cast<uchar4*>(arg));
         return launch_status("pool_finalize");
     }
     long long blocks = (GN + 255) / 256;
     if (blocks > 8192) blocks = 8192;
-    hipLaunchKernelGGL(pool_finalize_kernel, dim3((unsigned)blocks), dim3(256), 0, st, pz, pa, GN, N, s, t,
+    hipLaunchKernelGGL(pool_finalize_kernel, dim3((unsigned)blocks), dim3(256), 0, st, pz, pa, GN, N, s, t, sgn,
                        eff_slope(act, slope), out, arg);
     return launch_status("pool_finalize");
 }

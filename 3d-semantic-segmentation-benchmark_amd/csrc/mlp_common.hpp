@@ -164,8 +164,10 @@ struct GemmArgs {
     Operand e;
     double* bstats;                            // [2][N][gridDim.x]: sum dy, sum dy*xhat (or null)
     // fused max/min pooling of C over groups of pool_k consecutive rows (pool_k = 16 or 32; 0 = off):
-    // pz [2][M/pool_k][N] (max, min of C), pa [2][M/pool_k][N] (their first row within the group)
-    float* pz; unsigned char* pa; int pool_k;
+    // pz [2][M/pool_k][N] (max, min of C), pa [2][M/pool_k][N] (their first row within the group);
+    // only the half a monotone consumer needs is written: the max for columns with psign[n] >= 0
+    // (or psign null), the min for psign[n] < 0 (pool_finalize reads the half by the same test)
+    float* pz; unsigned char* pa; int pool_k; const float* psign;
 };
 
 // bn_finalize_kernel launch that also bumps BatchNorm.num_batches_tracked (nbt, nullable)
@@ -184,7 +186,7 @@ int materialize_dz(const pcs_operand* x, int M, int C, float* out, int ldo, hipS
 // row GEMM with W row-major N x K (bt = 0, = pcs_gemm_rows) or K x N (bt = 1)
 int gemm_rows_ex(const pcs_operand* a, int M, int K, const float* W, int ldw, int bt, const float* bias, float* C,
                  int ldc, int N, double* stats, const pcs_operand* epi, double* bstats, void* stream,
-                 float* pz = nullptr, unsigned char* pa = nullptr, int pool_k = 0);
+                 float* pz = nullptr, unsigned char* pa = nullptr, int pool_k = 0, const float* psign = nullptr);
 // the 64 x 64 BN-backward data gradient through an LDS-DMA ring (dgrad.hip): bitwise
 // gemm_rows_kernel<64, 64, 2, 2, BNBWD, true, 0 | EPI_BWD> for the shapes dgrad_dma_ok accepts;
 // gx = the row blocks (= BN-backward partials per column)
@@ -206,9 +208,11 @@ int wgrad_nt(const float* X, int ldx, const float* Y, int ldy, int M, int N, int
 const char* wgrad_nt_name(int N, int K, int M);
 // pooled output of a stack from the GEMM's fused z-space max/min (pz/pa of gemm_rows_ex):
 // out = act(s*z + t) with z = max (s > 0), min (s < 0) or any (s == 0, arg 0) -- act(s*z+t) is
-// monotone in z, so this is max_k act(s*z_k + t) with its first argmax
+// monotone in z, so this is max_k act(s*z_k + t) with its first argmax.  The half is chosen by
+// sgn[n] < 0 when sgn is given (the gamma the GEMM's psign used; s = gamma * invstd, invstd > 0,
+// so the signs agree), else by s[n] < 0 (both halves present)
 int pool_finalize(const float* pz, const unsigned char* pa, long long G, int N, const float* s, const float* t,
-                  int act, float slope, float* out, unsigned char* arg, hipStream_t st);
+                  const float* sgn, int act, float slope, float* out, unsigned char* arg, hipStream_t st);
 // engine launch probe: probe_enabled / probe_start / probe_stop (pcs_common.hpp, probe.cpp)
 // weight gradient with deterministic partials: workspace bytes for (N, K, M), and the launch
 size_t wgrad_ws_bytes(int N, int K, int M);
