@@ -8,8 +8,8 @@
 // so the 1x1 convolution runs over the N points (two row GEMMs on the engine, k = 20x fewer
 // flops than over the N k edges) and one gather pass (edgeconv_fwd_kernel) forms every edge
 // value once in registers: BatchNorm statistics (fp64 partials over all B N k edges, as the
-// reference's BatchNorm2d), the running max/min over k with their first index (the pooled
-// output is act(s z + t) at the max for s > 0 and at the min for s < 0, both monotone), and
+// reference's BatchNorm2d), the running max over k (gamma >= 0) or min (gamma < 0) with its
+// first index (the pooled output is act(s z + t), s = gamma invstd: monotone in z), and
 // the per-point sum over k that the backward needs.
 //
 // Backward (training-mode BN): with dy nonzero only at each (i, c)'s argmax edge,
@@ -29,14 +29,25 @@ constexpr int kEdgeFwdBlocks = 1024;
 // one thread = one point x 4 channels; 256 / (Cout/4) points per block, grid-stride over points
 __global__ __launch_bounds__(256) void edgeconv_fwd_kernel(const float* __restrict__ Y, float* __restrict__ PQ,
                                                            const int32_t* __restrict__ idx, int N, int k, int Cout,
-                                                           long long G, float* __restrict__ pz,
-                                                           unsigned char* __restrict__ pa, float* __restrict__ S,
-                                                           double* __restrict__ part) {
+                                                           long long G, const float* __restrict__ sgn,
+                                                           float* __restrict__ pz, unsigned char* __restrict__ pa,
+                                                           float* __restrict__ S, double* __restrict__ part) {
     const int tq = Cout / 4;                       // threads per point
     const int pb = 256 / tq;                       // points per block pass
     const int slot = threadIdx.x / tq;
     const int c = 4 * (threadIdx.x - slot * tq);
     double s1[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0};
+    // one extreme per channel: the max of z where gamma > 0, the min (as the max of -z) where
+    // gamma < 0; where gamma == 0 every edge pools to act(t) and the first (k = 0) is the argmax
+    unsigned flip[4] = {0u, 0u, 0u, 0u};
+    bool keep0[4] = {false, false, false, false};
+    if (sgn && slot < pb) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            flip[q] = sgn[c + q] < 0.f ? 0x80000000u : 0u;
+            keep0[q] = sgn[c + q] == 0.f;
+        }
+    }
     // XCD-aware point order: blocks b, b + 8, ... share an XCD (dispatch round-robin; speed
     // only), so XCD x takes the contiguous range [x Gx, (x+1) Gx) of points and its blocks sweep
     // it together, pb points each per pass: at any time an XCD gathers the Y rows of about one
@@ -51,8 +62,8 @@ __global__ __launch_bounds__(256) void edgeconv_fwd_kernel(const float* __restri
             const float4 yi = *reinterpret_cast<const float4*>(Y + g * Cout + c);
             const float4 pi = *reinterpret_cast<const float4*>(PQ + g * Cout + c);
             const float yv[4] = {yi.x, yi.y, yi.z, yi.w}, pv[4] = {pi.x, pi.y, pi.z, pi.w};
-            float mx[4], mn[4], sm[4];
-            int amx[4] = {0, 0, 0, 0}, amn[4] = {0, 0, 0, 0};
+            float mx[4], sm[4];
+            int amx[4] = {0, 0, 0, 0};
             const int32_t* nb = idx + g * k;
             for (int kk = 0; kk < k; ++kk) {
                 const int j = min(max(nb[kk], 0), N - 1);
@@ -61,23 +72,23 @@ __global__ __launch_bounds__(256) void edgeconv_fwd_kernel(const float* __restri
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
                     const float z = __fadd_rn(__fsub_rn(jv[q], yv[q]), pv[q]);
+                    const float zf = __uint_as_float(__float_as_uint(z) ^ flip[q]);
                     if (kk == 0) {
-                        mx[q] = mn[q] = sm[q] = z;
+                        mx[q] = zf;
+                        sm[q] = z;
                     } else {
-                        if (z > mx[q]) { mx[q] = z; amx[q] = kk; }
-                        if (z < mn[q]) { mn[q] = z; amn[q] = kk; }
+                        if (zf > mx[q] && !keep0[q]) { mx[q] = zf; amx[q] = kk; }
                         sm[q] = __fadd_rn(sm[q], z);
                     }
                     s1[q] += (double)z;
                     s2[q] += (double)z * (double)z;
                 }
             }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) mx[q] = __uint_as_float(__float_as_uint(mx[q]) ^ flip[q]);
             *reinterpret_cast<float4*>(pz + g * Cout + c) = make_float4(mx[0], mx[1], mx[2], mx[3]);
-            *reinterpret_cast<float4*>(pz + (G + g) * Cout + c) = make_float4(mn[0], mn[1], mn[2], mn[3]);
             *reinterpret_cast<uchar4*>(pa + g * Cout + c) =
                 make_uchar4((unsigned char)amx[0], (unsigned char)amx[1], (unsigned char)amx[2], (unsigned char)amx[3]);
-            *reinterpret_cast<uchar4*>(pa + (G + g) * Cout + c) =
-                make_uchar4((unsigned char)amn[0], (unsigned char)amn[1], (unsigned char)amn[2], (unsigned char)amn[3]);
             *reinterpret_cast<float4*>(S + g * Cout + c) = make_float4(sm[0], sm[1], sm[2], sm[3]);
             // P is replaced by Q = P - Y (the backward's per-source-point term)
             *reinterpret_cast<float4*>(PQ + g * Cout + c) =
@@ -109,11 +120,6 @@ __global__ __launch_bounds__(256) void edgeconv_fwd_kernel(const float* __restri
     }
 }
 
-// z of the pooled (argmax) edge: max for s >= 0, min for s < 0 (pool_finalize's choice)
-__device__ __forceinline__ float zsel(const float* pz, long long GN, long long e, float s) {
-    return pz[s < 0.f ? GN + e : e];
-}
-
 // BN-backward sums over the pooled edges (the only ones with dy != 0): part[2][Cout][gridDim.x]
 __global__ __launch_bounds__(256) void edgeconv_bwd_reduce_kernel(const float* __restrict__ dout,
                                                                   const float* __restrict__ pz, long long G, int Cout,
@@ -124,14 +130,13 @@ __global__ __launch_bounds__(256) void edgeconv_bwd_reduce_kernel(const float* _
     const int col = blockIdx.y * 64 + lane;
     const long long gb = (long long)blockIdx.x * rows_per_block;
     const long long ge = min(G, gb + rows_per_block);
-    const long long GN = G * Cout;
     double a = 0.0, b = 0.0;
     if (col < Cout) {
         const float s = coef[col], t = coef[Cout + col], mean = coef[2 * Cout + col], inv = coef[3 * Cout + col];
 #pragma unroll 4
         for (long long g = gb + ph; g < ge; g += 4) {
             const long long e = g * Cout + col;
-            const float z = zsel(pz, GN, e, s);
+            const float z = pz[e];              // the pooled (argmax) edge's z
             const float dy = dout[e] * dact_f(z * s + t, ACT_LRELU, slope);
             a += (double)dy;
             b += (double)dy * (double)((z - mean) * inv);
@@ -159,7 +164,7 @@ __global__ __launch_bounds__(256) void edgeconv_bwd_center_kernel(const float* _
         const long long g = e / Cout;
         const float s = coef[c], t = coef[Cout + c], mean = coef[2 * Cout + c];
         const float kb = kBC[c], kc = kBC[Cout + c];
-        const float z = zsel(pz, GN, e, s);
+        const float z = pz[e];
         const float d = s * (dout[e] * dact_f(z * s + t, ACT_LRELU, slope));
         D[e] = d;
         const double dp = (double)d - (double)k * kb - (double)kc * ((double)S[e] - (double)k * mean);
@@ -169,7 +174,7 @@ __global__ __launch_bounds__(256) void edgeconv_bwd_center_kernel(const float* _
 
 // the same, one channel quad per thread (Cout % 4 == 0, 16-B aligned rows): 16-B loads of dout /
 // S / pz, a 16-B store of D and 32-bit quad indexing instead of a 64-bit division per element;
-// the min half of pz is read only for a quad with a negative scale.  Same per-element arithmetic.
+// Same per-element arithmetic.
 __global__ __launch_bounds__(256) void edgeconv_bwd_center_q_kernel(const float4* __restrict__ dout,
                                                                     const float4* __restrict__ pz,
                                                                     const float4* __restrict__ S, int GN4, int nq,
@@ -184,14 +189,7 @@ __global__ __launch_bounds__(256) void edgeconv_bwd_center_q_kernel(const float4
         const float4 mv = *reinterpret_cast<const float4*>(coef + 2 * Cout + c);
         const float4 kbv = *reinterpret_cast<const float4*>(kBC + c);
         const float4 kcv = *reinterpret_cast<const float4*>(kBC + Cout + c);
-        float4 z = pz[e];
-        if (sv.x < 0.f || sv.y < 0.f || sv.z < 0.f || sv.w < 0.f) {
-            const float4 zn = pz[GN4 + e];
-            if (sv.x < 0.f) z.x = zn.x;
-            if (sv.y < 0.f) z.y = zn.y;
-            if (sv.z < 0.f) z.z = zn.z;
-            if (sv.w < 0.f) z.w = zn.w;
-        }
+        const float4 z = pz[e];
         const float4 dv = dout[e], Sv = S[e];
         const float s4[4] = {sv.x, sv.y, sv.z, sv.w}, t4[4] = {tv.x, tv.y, tv.z, tv.w};
         const float m4[4] = {mv.x, mv.y, mv.z, mv.w}, kb4[4] = {kbv.x, kbv.y, kbv.z, kbv.w};
@@ -310,8 +308,9 @@ PCS_API int pcs_edgeconv_workspace(int B, int N, int C, int Cout, int backward, 
 // Training-mode EdgeConv forward.  X (B*N rows, stride ldx) with C channels, idx (B, N, k)
 // int32 neighbour table (per-cloud indices), W (Cout, 2C) = the Conv2d weight, BN gamma/beta
 // and running stats (updated in place, num_batches_tracked bumped).  Outputs (caller-owned):
-// Y, PQ (B*N x Cout; PQ holds Q = P - Y on return), S (B*N x Cout), pz (2 x B*N x Cout),
-// pa (2 x B*N x Cout u8), coef (4 x Cout: s, t, mean, invstd), out (B*N x Cout) pooled
+// Y, PQ (B*N x Cout; PQ holds Q = P - Y on return), S (B*N x Cout), pz (2 x B*N x Cout; the
+// first B*N x Cout hold the pooled edge's z: max over k (gamma > 0), min (< 0), edge 0 (== 0)),
+// pa (2 x B*N x Cout u8, first half used), coef (4 x Cout: s, t, mean, invstd), out (B*N x Cout) pooled
 // activation, arg (B*N x Cout u8) its neighbour slot.  Reference: dgcnn.py:60-77.
 PCS_API int pcs_edgeconv_fwd(const float* X, int ldx, int C, const int32_t* idx, int B, int N, int k,
                              const float* W, int Cout, const float* gamma, const float* beta, float* run_mean,
@@ -342,11 +341,11 @@ PCS_API int pcs_edgeconv_fwd(const float* X, int ldx, int C, const int32_t* idx,
         // flops: the k edge values (2 adds) and BN sums (3) per (point, channel)
         ProbeScope pr(st, 5.0 * (double)G * k * Cout, 4.0 * (double)G * (2.0 * Cout + k) + 14.0 * (double)G * Cout,
                       "pcs::edgeconv_fwd_kernel");
-        hipLaunchKernelGGL(edgeconv_fwd_kernel, dim3(nb), dim3(256), 0, st, Y, PQ, idx, N, k, Cout, G, pz, pa, S, part);
+        hipLaunchKernelGGL(edgeconv_fwd_kernel, dim3(nb), dim3(256), 0, st, Y, PQ, idx, N, k, Cout, G, gamma, pz, pa, S, part);
     }
     bn_finalize_launch(part, nb, Cout, G * k, gamma, beta, eps, momentum, run_mean, run_var, coef, coef + Cout,
                        coef + 2 * Cout, coef + 3 * Cout, num_batches, st);
-    return pool_finalize(pz, pa, G, Cout, coef, coef + Cout, nullptr, ACT_LRELU, slope, out, arg, st);
+    return pool_finalize(pz, pa, G, Cout, coef, coef + Cout, true, ACT_LRELU, slope, out, arg, st);
 }
 
 // Training-mode EdgeConv backward (the forward's saved tensors; csr_off/csr_ent = pcs_inverse_index

@@ -353,7 +353,8 @@ PCS_API int pcs_mlp_forward(const float* X, int ldx, int kin, int M, pcs_mlp_lay
     const pcs_mlp_layer& T = layers[nl - 1];
     const int C = (int)T.cout;
     if (fuse)
-        return pool_finalize(S.pz, S.pa, M / pool_k, C, T.coef, T.coef + C, T.gamma, (int)T.act, (float)T.slope, out, arg, st);
+        return pool_finalize(S.pz, S.pa, M / pool_k, C, T.coef, T.coef + C, true, (int)T.act,
+                             (float)T.slope, out, arg, st);
     if (pool_k)
         return pcs_pool_fwd(T.Z, C, M / pool_k, pool_k, T.coef, T.coef + C, (int)T.act, (float)T.slope, out, arg,
                             stream);

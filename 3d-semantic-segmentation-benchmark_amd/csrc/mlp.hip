@@ -322,9 +322,9 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void gemm_rows_kernel(GemmArgs g) 
                             if (ox > pmx || (ox == pmx && oix < imx)) { pmx = ox; imx = oix; }
                             const int r0 = rb + (g.pool_k == 16 ? 16 * hb : 0);
                             if (h == 0 && cok && r0 < g.M) {
-                                const size_t G = (size_t)(g.M / g.pool_k), gi = (size_t)(r0 / g.pool_k);
+                                const size_t gi = (size_t)(r0 / g.pool_k);
                                 const int base = g.pool_k == 16 ? 16 * hb : 0;
-                                const size_t o = ((pflip ? G : 0) + gi) * g.N + col;
+                                const size_t o = gi * g.N + col;
                                 g.pz[o] = __uint_as_float(__float_as_uint(pmx) ^ pflip);
                                 g.pa[o] = (unsigned char)(imx - base);
                             }
@@ -784,12 +784,12 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restr
 __global__ __launch_bounds__(256) void pool_finalize_kernel(const float* __restrict__ pz,
                                                             const unsigned char* __restrict__ pa, long long GN, int N,
                                                             const float* __restrict__ s, const float* __restrict__ t,
-                                                            const float* __restrict__ sgn, float slope,
-                                                            float* __restrict__ out, unsigned char* __restrict__ arg) {
+                                                            bool one_half, float slope, float* __restrict__ out,
+                                                            unsigned char* __restrict__ arg) {
     for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < GN; e += (long long)gridDim.x * 256) {
         const int c = (int)(e % N);
         const float sc = s[c], tc = t[c];
-        const bool neg = (sgn ? sgn[c] : sc) < 0.f;
+        const bool neg = !one_half && sc < 0.f;
         const float z = pz[neg ? GN + e : e];
         out[e] = act_f(z * sc + tc, 0, slope);
         arg[e] = sc == 0.f ? (unsigned char)0 : pa[neg ? GN + e : e];
@@ -802,16 +802,15 @@ __global__ __launch_bounds__(256) void pool_finalize_kernel(const float* __restr
 __global__ __launch_bounds__(256) void pool_finalize_q_kernel(const float4* __restrict__ pz,
                                                               const uchar4* __restrict__ pa, int GN4, int nq,
                                                               const float* __restrict__ s, const float* __restrict__ t,
-                                                              const float* __restrict__ sgn, float slope,
-                                                              float4* __restrict__ out, uchar4* __restrict__ arg) {
+                                                              bool one_half, float slope, float4* __restrict__ out,
+                                                              uchar4* __restrict__ arg) {
     for (int e = blockIdx.x * 256 + threadIdx.x; e < GN4; e += gridDim.x * 256) {
         const int c = 4 * (e % nq);
         const float4 sc = *reinterpret_cast<const float4*>(s + c), tc = *reinterpret_cast<const float4*>(t + c);
-        const float4 ng = sgn ? *reinterpret_cast<const float4*>(sgn + c) : sc;
-        const bool nx = ng.x < 0.f, ny = ng.y < 0.f, nz = ng.z < 0.f, nw = ng.w < 0.f;
-        float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-        uchar4 a = make_uchar4(0, 0, 0, 0);
-        if (!(nx && ny && nz && nw)) { z = pz[e]; a = pa[e]; }
+        const bool nx = !one_half && sc.x < 0.f, ny = !one_half && sc.y < 0.f, nz = !one_half && sc.z < 0.f,
+                   nw = !one_half && sc.w < 0.f;
+        float4 z = pz[e];
+        uchar4 a = pa[e];
         if (nx || ny || nz || nw) {
             const float4 zn = pz[GN4 + e];
             const uchar4 an = pa[GN4 + e];
@@ -1521,22 +1520,22 @@ PCS_API int pcs_pool_fwd(const float* Z, int N, long long G, int K, const float*
 }
 
 int pcs::pool_finalize(const float* pz, const unsigned char* pa, long long G, int N, const float* s, const float* t,
-                       const float* sgn, int act, float slope, float* out, unsigned char* arg, hipStream_t st) {
+                       bool one_half, int act, float slope, float* out, unsigned char* arg, hipStream_t st) {
     const long long GN = G * N;
     if (GN == 0) return 0;
     auto al = [](const void* p, uintptr_t a) { return (reinterpret_cast<uintptr_t>(p) & (a - 1)) == 0; };
     if (N % 4 == 0 && GN / 4 < (1ll << 31) && al(pz, 16) && al(out, 16) && al(pa, 4) && al(arg, 4) && al(s, 16) &&
-        al(t, 16) && al(sgn, 16)) {
+        al(t, 16)) {
         const long long GN4 = GN / 4;
         const unsigned blocks = (unsigned)std::min<long long>((GN4 + 255) / 256, 8192);
         hipLaunchKernelGGL(pool_finalize_q_kernel, dim3(blocks), dim3(256), 0, st, reinterpret_cast<const float4*>(pz),
-                           reinterpret_cast<const uchar4*>(pa), (int)GN4, N / 4, s, t, sgn, eff_slope(act, slope),
+                           reinterpret_cast<const uchar4*>(pa), (int)GN4, N / 4, s, t, one_half, eff_slope(act, slope),
                            reinterpret_cast<float4*>(out), reinterpret_cast<uchar4*>(arg));
         return launch_status("pool_finalize");
     }
     long long blocks = (GN + 255) / 256;
     if (blocks > 8192) blocks = 8192;
-    hipLaunchKernelGGL(pool_finalize_kernel, dim3((unsigned)blocks), dim3(256), 0, st, pz, pa, GN, N, s, t, sgn,
+    hipLaunchKernelGGL(pool_finalize_kernel, dim3((unsigned)blocks), dim3(256), 0, st, pz, pa, GN, N, s, t, one_half,
                        eff_slope(act, slope), out, arg);
     return launch_status("pool_finalize");
 }

@@ -163,10 +163,10 @@ struct GemmArgs {
     // uses e.z (its pre-BN Z, M x N), e.s, e.t, e.mean, e.inv, e.act, e.slope
     Operand e;
     double* bstats;                            // [2][N][gridDim.x]: sum dy, sum dy*xhat (or null)
-    // fused max/min pooling of C over groups of pool_k consecutive rows (pool_k = 16 or 32; 0 = off):
-    // pz [2][M/pool_k][N] (max, min of C), pa [2][M/pool_k][N] (their first row within the group);
-    // only the half a monotone consumer needs is written: the max for columns with psign[n] >= 0
-    // (or psign null), the min for psign[n] < 0 (pool_finalize reads the half by the same test)
+    // fused max-or-min pooling of C over groups of pool_k consecutive rows (pool_k = 16 or 32; 0 =
+    // off): pz [M/pool_k][N] = the max of C for columns with psign[n] >= 0 (or psign null), the min
+    // for psign[n] < 0 -- the one extreme a monotone consumer act(s*z+t) with sign(s) = sign(psign)
+    // needs -- and pa [M/pool_k][N] its first row within the group (pool_finalize, one_half)
     float* pz; unsigned char* pa; int pool_k; const float* psign;
 };
 
@@ -208,11 +208,11 @@ int wgrad_nt(const float* X, int ldx, const float* Y, int ldy, int M, int N, int
 const char* wgrad_nt_name(int N, int K, int M);
 // pooled output of a stack from the GEMM's fused z-space max/min (pz/pa of gemm_rows_ex):
 // out = act(s*z + t) with z = max (s > 0), min (s < 0) or any (s == 0, arg 0) -- act(s*z+t) is
-// monotone in z, so this is max_k act(s*z_k + t) with its first argmax.  The half is chosen by
-// sgn[n] < 0 when sgn is given (the gamma the GEMM's psign used; s = gamma * invstd, invstd > 0,
-// so the signs agree), else by s[n] < 0 (both halves present)
+// monotone in z, so this is max_k act(s*z_k + t) with its first argmax.  one_half: the producer
+// already kept the right extreme per channel in the first half (chosen by the sign of gamma;
+// s = gamma * invstd with invstd > 0, so the signs agree), else the half is chosen by s[n] < 0
 int pool_finalize(const float* pz, const unsigned char* pa, long long G, int N, const float* s, const float* t,
-                  const float* sgn, int act, float slope, float* out, unsigned char* arg, hipStream_t st);
+                  bool one_half, int act, float slope, float* out, unsigned char* arg, hipStream_t st);
 // engine launch probe: probe_enabled / probe_start / probe_stop (pcs_common.hpp, probe.cpp)
 // weight gradient with deterministic partials: workspace bytes for (N, K, M), and the launch
 size_t wgrad_ws_bytes(int N, int K, int M);

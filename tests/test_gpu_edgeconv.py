@@ -72,6 +72,29 @@ def test_edgeconv_fused_matches_reference_fp64(C, Cout):
     assert int(bn.num_batches_tracked) == 1
 
 
+def test_edgeconv_fused_negative_gamma():
+    """BN scales of both signs (and a zero): the forward keeps the max over k where gamma >= 0
+    and the min where gamma < 0; output, argmax routing and every gradient against fp64."""
+    x, idx, ref, prod = _case(64, 64, seed=21)
+    with torch.no_grad():
+        w = ref.conv[1].weight
+        w.copy_(w.abs() * torch.tensor([1.0, -1.0]).repeat(w.numel() // 2))
+        w[5] = 0.0
+    prod.load_state_dict(ref.state_dict())
+    prod = prod.to(DEV).train()
+    r64, xr, out64 = _ref_fp64(x, idx, ref)
+    xd = x.to(DEV).requires_grad_(True)
+    with pcseg.replay(pcseg.Replay(knn_idx=[idx])):
+        out = prod(xd)
+    assert rel(out.detach(), out64.detach()) < TOL
+    g = torch.randn(out64.shape, generator=torch.Generator().manual_seed(7), dtype=torch.float64)
+    (out64 * g).sum().backward()
+    (out * g.float().to(DEV)).sum().backward()
+    assert rel(xd.grad, xr.grad) < TOL
+    for (name, p64), p in zip(r64.named_parameters(), prod.parameters()):
+        assert rel(p.grad, p64.grad) < TOL, name
+
+
 def test_edgeconv_fused_equals_materialised_path():
     """Same module, same graph: the fused kernels and the edge-row engine path agree."""
     x, idx, _, prod = _case(64, 64, seed=3)
