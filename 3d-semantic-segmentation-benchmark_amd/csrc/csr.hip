@@ -429,9 +429,14 @@ static size_t rank_batch(const pcs_inverse_map* maps, int n, int B, char* ws, hi
             nchw = std::max(nchw, bw.m[i].nch);
         }
         const size_t lds = ((size_t)W * mt + W) * sizeof(int);
-        if (W == 4)
+        if (W == 4) {
+            // up to (4 * 4096 + 4) ints = 65552 B: above the 64 KB default cap, set like <2>'s
+            static const hipError_t attr = hipFuncSetAttribute(
+                reinterpret_cast<const void*>(&inverse_rank_kernel<4>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                (4 * 4096 + 4) * (int)sizeof(int));
+            (void)attr;
             hipLaunchKernelGGL(inverse_rank_kernel<4>, dim3(nchw, B, n), dim3(256), lds, s, bw, B);
-        else {
+        } else {
             static const hipError_t attr = hipFuncSetAttribute(
                 reinterpret_cast<const void*>(&inverse_rank_kernel<2>), hipFuncAttributeMaxDynamicSharedMemorySize,
                 (2 * kRankMaxTargets + 2) * (int)sizeof(int));
@@ -442,68 +447,74 @@ static size_t rank_batch(const pcs_inverse_map* maps, int n, int B, char* ws, hi
     return off;
 }
 
-// Gather backward over the inverse maps: ONE WAVE PER SOURCE POINT, lanes over channels,
-// so every slot's gradient row is read as contiguous channel runs (coalesced).  The slot
-// list is fetched 64 entries at a time, one per lane (with the entry's per-slot
-// coefficients computed once, lane-parallel), then walked with v_readlane, 4 row loads
-// in flight per lane.
-
-// grad_feats[(b, p), c] = sum over slots s reading p of gout[s][3 + c]  (fp64 accumulation)
-__global__ __launch_bounds__(256) void group_bwd_csr_kernel(const float* __restrict__ gout, int ld,
-                                                            const int32_t* __restrict__ off,
-                                                            const int32_t* __restrict__ ent, int targets, int D,
-                                                            float* __restrict__ gfeats) {
-    const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    if (t >= targets) return;
-    const int a = off[t], z = off[t + 1];
-    for (int c0 = 0; c0 < D; c0 += 64) {
-        const int c = c0 + lane;
-        const int cc = 3 + (c < D ? c : D - 1);
-        double acc = 0.0;
-        for (int base = a; base < z; base += 64) {
-            const int n = min(64, z - base);
-            const int mine = lane < n ? ent[base + lane] : 0;
-            int e = 0;
-            for (; e + 4 <= n; e += 4) {
-                const float v0 = gout[(size_t)__builtin_amdgcn_readlane(mine, e) * ld + cc];
-                const float v1 = gout[(size_t)__builtin_amdgcn_readlane(mine, e + 1) * ld + cc];
-                const float v2 = gout[(size_t)__builtin_amdgcn_readlane(mine, e + 2) * ld + cc];
-                const float v3 = gout[(size_t)__builtin_amdgcn_readlane(mine, e + 3) * ld + cc];
-                acc += (double)v0;
-                acc += (double)v1;
-                acc += (double)v2;
-                acc += (double)v3;
-            }
-            for (; e < n; ++e) acc += (double)gout[(size_t)__builtin_amdgcn_readlane(mine, e) * ld + cc];
-        }
-        if (c < D) gfeats[(size_t)t * D + c] = (float)acc;
-    }
-}
-
-// grad_pts[(b, m), c] = sum over slots s = 3*row + j reading m (fp64 accumulation) of
-//   (gout[row][col_off + c] / norm_row) * w_j      -- the autograd rounding of
-// interpolate's (p*w)/norm (common.py:119-122), as the atomic kernel computes it
-__global__ __launch_bounds__(256) void interp_bwd_csr_kernel(const float* __restrict__ gout, int ld, int col_off,
+// Gather backward over the inverse maps (round 5: streaming).  The lists of consecutive targets
+// are consecutive in `entries`, so one wave walks the lists of TW consecutive targets as ONE
+// contiguous entry range [off[t0], off[t0 + TW]): the entries are fetched 64 at a time, one per
+// lane (with the IDW coefficients of an interpolation slot computed lane-parallel), and walked
+// with v_readlane, U gradient rows in flight per lane; lanes own channels, so every row is read as
+// contiguous channel runs.  A target's list ends where the running entry index reaches the next
+// offset (uniform control: the offsets of the wave's targets sit one per lane), and its fp64 sum
+// is written out then.  Per channel the terms are added in list order -- the same order, per-term
+// rounding and fp64 accumulation as the round-4 one-wave-per-target kernels, so the outputs are
+// bitwise unchanged -- but the wave no longer waits on offsets -> entries -> rows -> store for
+// every target: the per-target latency chain became a stream with U x V loads in flight.
+//
+// V channels per lane: VEC -- V consecutive channels (one float V-vector load per row; rows and
+// col_off 16-B aligned, D = 64 V), else channels lane + 64 v (scalar loads; any col_off, D <= 64 V).
+// IDW: interpolation slots s = 3 * row + j with term (g / norm_row) * w_j (common.py:119-122);
+// otherwise group slots s = row with term g (common.py:64-65).
+template <int V, bool VEC, bool IDW, int U>
+__global__ __launch_bounds__(256) void csr_bwd_stream_kernel(const float* __restrict__ gout, int ld, int col_off,
                                                              const float* __restrict__ dist,
                                                              const int32_t* __restrict__ off,
                                                              const int32_t* __restrict__ ent, int targets, int D,
-                                                             float* __restrict__ gpts) {
-    const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+                                                             int TW, float* __restrict__ out, int ldo) {
+    typedef float fv __attribute__((ext_vector_type(V)));
+    const int wid = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    if (t >= targets) return;
-    const int a = off[t], z = off[t + 1];
-    for (int c0 = 0; c0 < D; c0 += 64) {
-        const int c = c0 + lane;
-        const int cc = col_off + (c < D ? c : D - 1);
-        double acc = 0.0;
-        for (int base = a; base < z; base += 64) {
-            const int n = min(64, z - base);
-            // this lane's entry: its row and IDW coefficients (nrm, w_j)
-            int row = 0;
-            float nrm = 1.f, wj = 0.f;
-            if (lane < n) {
-                const int s = ent[base + lane];
+    const int t0 = wid * TW;
+    if (t0 >= targets) return;
+    const int nt = min(TW, targets - t0);
+    const int ol = off[t0 + min(lane, nt)];             // off[t0 .. t0 + nt], one per lane
+    const int E0 = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_readlane(ol, 0));
+    const int E1 = __builtin_amdgcn_readlane(ol, nt);
+    int cch[V];
+    bool cok[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+        const int c = VEC ? V * lane + v : lane + 64 * v;
+        cok[v] = c < D;
+        cch[v] = col_off + (cok[v] ? c : D - 1);
+    }
+    double acc[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) acc[v] = 0.0;
+    int cur = 0;                                        // the current target, relative to t0
+    int nb = __builtin_amdgcn_readlane(ol, 1);          // its list's end
+    auto flush = [&]() {
+        float* o = out + (size_t)(t0 + cur) * ldo;
+        if (VEC) {
+            fv w;
+#pragma unroll
+            for (int v = 0; v < V; ++v) w[v] = (float)acc[v];
+            *reinterpret_cast<fv*>(o + V * lane) = w;
+        } else {
+#pragma unroll
+            for (int v = 0; v < V; ++v)
+                if (cok[v]) o[lane + 64 * v] = (float)acc[v];
+        }
+#pragma unroll
+        for (int v = 0; v < V; ++v) acc[v] = 0.0;
+        ++cur;
+        nb = __builtin_amdgcn_readlane(ol, min(cur + 1, nt));
+    };
+    for (int base = E0; base < E1; base += 64) {
+        const int n = min(64, E1 - base);
+        int row = 0;
+        float nrm = 1.f, wj = 0.f;
+        if (lane < n) {
+            const int s = ent[base + lane];
+            if (IDW) {
                 row = s / 3;
                 const int j = s - 3 * row;
                 const float w0 = 1.0f / (dist[(size_t)row * 3 + 0] + 1e-9f);
@@ -511,95 +522,43 @@ __global__ __launch_bounds__(256) void interp_bwd_csr_kernel(const float* __rest
                 const float w2 = 1.0f / (dist[(size_t)row * 3 + 2] + 1e-9f);
                 nrm = (w0 + w1) + w2;
                 wj = j == 0 ? w0 : (j == 1 ? w1 : w2);
-            }
-            auto term = [&](int e) {
-                const int r = __builtin_amdgcn_readlane(row, e);
-                const float nv = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(nrm), e));
-                const float wv = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wj), e));
-                return (gout[(size_t)r * ld + cc] / nv) * wv;
-            };
-            int e = 0;
-            for (; e + 4 <= n; e += 4) {
-                const float v0 = term(e), v1 = term(e + 1), v2 = term(e + 2), v3 = term(e + 3);
-                acc += (double)v0;
-                acc += (double)v1;
-                acc += (double)v2;
-                acc += (double)v3;
-            }
-            for (; e < n; ++e) acc += (double)term(e);
-        }
-        if (c < D) gpts[(size_t)t * D + c] = (float)acc;
-    }
-}
-
-// The same for D = 64 V (V = 2, 4: FP1 / FP2-4 of PointNet++): one pass over the slot list,
-// each lane owning V consecutive channels (float2 / float4 loads of a 16-B aligned row run), so
-// the list, the distances and the IDW coefficients are read once instead of D / 64 times.
-// Same per-term rounding and per-channel fp64 summation order as the kernel above.
-template <int V>
-__global__ __launch_bounds__(256) void interp_bwd_csr_vec_kernel(const float* __restrict__ gout, int ld, int col_off,
-                                                                 const float* __restrict__ dist,
-                                                                 const int32_t* __restrict__ off,
-                                                                 const int32_t* __restrict__ ent, int targets,
-                                                                 float* __restrict__ gpts) {
-    typedef float fv __attribute__((ext_vector_type(V)));
-    constexpr int D = 64 * V;
-    const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    if (t >= targets) return;
-    const int a = off[t], z = off[t + 1];
-    double acc[V];
-#pragma unroll
-    for (int v = 0; v < V; ++v) acc[v] = 0.0;
-    const float* g0 = gout + col_off + V * lane;
-    for (int base = a; base < z; base += 64) {
-        const int n = min(64, z - base);
-        int row = 0;
-        float nrm = 1.f, wj = 0.f;
-        if (lane < n) {
-            const int s = ent[base + lane];
-            row = s / 3;
-            const int j = s - 3 * row;
-            const float w0 = 1.0f / (dist[(size_t)row * 3 + 0] + 1e-9f);
-            const float w1 = 1.0f / (dist[(size_t)row * 3 + 1] + 1e-9f);
-            const float w2 = 1.0f / (dist[(size_t)row * 3 + 2] + 1e-9f);
-            nrm = (w0 + w1) + w2;
-            wj = j == 0 ? w0 : (j == 1 ? w1 : w2);
-        }
-        auto term = [&](int e, fv& out) {
-            const int r = __builtin_amdgcn_readlane(row, e);
-            const float nv = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(nrm), e));
-            const float wv = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wj), e));
-            const fv gv = *reinterpret_cast<const fv*>(g0 + (size_t)r * ld);
-#pragma unroll
-            for (int v = 0; v < V; ++v) out[v] = (gv[v] / nv) * wv;
-        };
-        int e = 0;
-        for (; e + 4 <= n; e += 4) {
-            fv t0, t1, t2, t3;
-            term(e, t0);
-            term(e + 1, t1);
-            term(e + 2, t2);
-            term(e + 3, t3);
-#pragma unroll
-            for (int v = 0; v < V; ++v) {
-                acc[v] += (double)t0[v];
-                acc[v] += (double)t1[v];
-                acc[v] += (double)t2[v];
-                acc[v] += (double)t3[v];
+            } else {
+                row = s;
             }
         }
-        for (; e < n; ++e) {
-            fv t0;
-            term(e, t0);
+        for (int e = 0; e < n; e += U) {
+            float val[U][V];
 #pragma unroll
-            for (int v = 0; v < V; ++v) acc[v] += (double)t0[v];
+            for (int u = 0; u < U; ++u) {
+                const int eu = min(e + u, n - 1);
+                const float* g = gout + (size_t)__builtin_amdgcn_readlane(row, eu) * ld;
+                if (VEC) {
+                    const fv gv = *reinterpret_cast<const fv*>(g + col_off + V * lane);
+#pragma unroll
+                    for (int v = 0; v < V; ++v) val[u][v] = gv[v];
+                } else {
+#pragma unroll
+                    for (int v = 0; v < V; ++v) val[u][v] = g[cch[v]];
+                }
+                if (IDW) {
+                    const float nv = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(nrm), eu));
+                    const float wv = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wj), eu));
+#pragma unroll
+                    for (int v = 0; v < V; ++v) val[u][v] = (val[u][v] / nv) * wv;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (e + u < n) {
+                    const int gi = base + e + u;
+                    while (gi == nb) flush();           // the lists that end here (empty ones too)
+#pragma unroll
+                    for (int v = 0; v < V; ++v) acc[v] += (double)val[u][v];
+                }
+            }
         }
     }
-    fv o;
-#pragma unroll
-    for (int v = 0; v < V; ++v) o[v] = (float)acc[v];
-    *reinterpret_cast<fv*>(gpts + (size_t)t * D + V * lane) = o;
+    while (cur < nt) flush();                           // the last list and any empty ones after it
 }
 
 // get_graph_feature backward (dgcnn.py:41-53, rows [x_j - x_i, x_i] of stride ld): point t's
@@ -752,43 +711,101 @@ PCS_API int pcs_inverse_index(const int32_t* idx, int B, int per_batch, int targ
     return pcs_inverse_index_batch(&m, 1, B, workspace, ws_bytes, stream);
 }
 
+// targets per wave of the streaming CSR backward: one.  Several consecutive lists per wave (up to
+// 16, keeping ~16 waves per CU) measured slower in-step: PointNet++ 4.98 vs 4.82 ms with 8 per
+// wave at SA2 (the group backward 174 vs ~60 us: fewer waves hide less latency), 4.93 with 4
+// (profiles/r05_ab_csr_tw.txt)
+static int csr_tw(long long targets) {
+    (void)targets;
+#ifdef PCS_CSR_TW
+    return PCS_CSR_TW;                       // A/B builds (scripts/build_ab.sh) only
+#else
+    return 1;
+#endif
+}
+
+template <int V, bool VEC, bool IDW>
+static void launch_stream(const float* gout, int ld, int col_off, const float* dist, const int32_t* off,
+                          const int32_t* ent, int targets, int D, float* out, int ldo, hipStream_t s) {
+    constexpr int U = VEC ? 16 : (16 / V > 4 ? 16 / V : 4);
+    const int tw = csr_tw(targets);
+    const long long waves = (targets + tw - 1) / tw;
+    hipLaunchKernelGGL((csr_bwd_stream_kernel<V, VEC, IDW, U>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s,
+                       gout, ld, col_off, dist, off, ent, targets, D, tw, out, ldo);
+}
+
+template <bool IDW>
+static int csr_bwd_chunk(const float* gout, int ld, int col_off, const float* dist, const int32_t* off,
+                         const int32_t* ent, int targets, int D, float* out, int ldo, hipStream_t s) {
+    const bool al = ld % 4 == 0 && col_off % 4 == 0 && ldo % 4 == 0 && ((uintptr_t)gout | (uintptr_t)out) % 16 == 0;
+    if (al && D == 64) launch_stream<1, false, IDW>(gout, ld, col_off, dist, off, ent, targets, D, out, ldo, s);
+    else if (al && D == 128) launch_stream<2, true, IDW>(gout, ld, col_off, dist, off, ent, targets, D, out, ldo, s);
+    else if (al && D == 256) launch_stream<4, true, IDW>(gout, ld, col_off, dist, off, ent, targets, D, out, ldo, s);
+    else if (D <= 64) launch_stream<1, false, IDW>(gout, ld, col_off, dist, off, ent, targets, D, out, ldo, s);
+    else if (D <= 128) launch_stream<2, false, IDW>(gout, ld, col_off, dist, off, ent, targets, D, out, ldo, s);
+    else if (D <= 256) launch_stream<4, false, IDW>(gout, ld, col_off, dist, off, ent, targets, D, out, ldo, s);
+    else if (D <= 512) launch_stream<8, false, IDW>(gout, ld, col_off, dist, off, ent, targets, D, out, ldo, s);
+    else PCS_CHECK_ARG(false, "csr backward: D=%d > 512", D);
+    return 0;
+}
+
+// the streaming CSR backward over channels [0, D) of rows at col_off, output rows of stride ldo: one
+// launch per 512 channels, V = the channel chunks per lane
+template <bool IDW>
+static int csr_bwd(const float* gout, int ld, int col_off, const float* dist, const int32_t* off, const int32_t* ent,
+                   int targets, int D, float* out, hipStream_t s) {
+    for (int c0 = 0; c0 < D; c0 += 512)
+        if (int e = csr_bwd_chunk<IDW>(gout, ld, col_off + c0, dist, off, ent, targets, std::min(512, D - c0), out + c0,
+                                       D, s))
+            return e;
+    return 0;
+}
+
+static const char* csr_bwd_name(bool idw, int ld, int col_off, const void* gout, const void* out, int D) {
+    const bool al = ld % 4 == 0 && col_off % 4 == 0 && ((uintptr_t)gout | (uintptr_t)out) % 16 == 0;
+    const int V = D <= 64 ? 1 : D <= 128 ? 2 : D <= 256 ? 4 : 8;
+    const bool vec = al && V > 1 && D == 64 * V && V <= 4;
+    const int U = vec ? 16 : (16 / V > 4 ? 16 / V : 4);
+    static char names[2][4][2][64];
+    const int vi = V == 1 ? 0 : V == 2 ? 1 : V == 4 ? 2 : 3;
+    char* nm = names[idw][vi][vec];
+    snprintf(nm, 64, "pcs::csr_bwd_stream_kernel<%d, %s, %s, %d>", V, vec ? "true" : "false", idw ? "true" : "false", U);
+    return nm;
+}
+
 // grad_feats (B, N, D) = backward of group's feature gather (overwrites; no zero fill needed).
 PCS_API int pcs_group_bwd_csr(const float* grad_out, int ld_gout, const int32_t* offsets, const int32_t* entries,
-                              int B, int N, int D, float* grad_feats, void* stream) {
-    PCS_CHECK_ARG(B >= 1 && N >= 1 && D >= 1 && ld_gout >= 3 + D, "pcs_group_bwd_csr: bad sizes");
+                              int B, int N, int D, long long n_slots, float* grad_feats, void* stream) {
+    PCS_CHECK_ARG(B >= 1 && N >= 1 && D >= 1 && ld_gout >= 3 + D && n_slots >= 0, "pcs_group_bwd_csr: bad sizes");
     const long long total = (long long)B * N * D, targets = (long long)B * N;
-    PCS_CHECK_ARG(total < (1ll << 31), "pcs_group_bwd_csr: too many elements");
+    PCS_CHECK_ARG(total < (1ll << 31) && n_slots < (1ll << 31), "pcs_group_bwd_csr: too many elements");
     PCS_CHECK_ARG(grad_out && offsets && entries && grad_feats, "pcs_group_bwd_csr: null pointer");
-    // algorithmic bytes (SURVEY.md 8(d) group bwd): the D gradient columns of every grouped row
-    // read once, the source gradient written, the map read
-    ProbeScope pr(as_stream(stream), 0.0, 8.0 * (double)total + 4.0 * (double)(targets + 1), "pcs::group_bwd_csr_kernel");
-    hipLaunchKernelGGL(group_bwd_csr_kernel, dim3((unsigned)((targets + 3) / 4)), dim3(256), 0, as_stream(stream),
-                       grad_out, ld_gout, offsets, entries, (int)targets, D, grad_feats);
+    hipStream_t s = as_stream(stream);
+    // algorithmic bytes (SURVEY.md 8(d) group bwd): the D gradient columns of every grouped row (one
+    // per slot) and its entry read once, the source gradient written, the offsets read
+    ProbeScope pr(s, 0.0, 4.0 * (double)n_slots * (D + 1) + 4.0 * (double)total + 4.0 * (double)(targets + 1), "%s",
+                  probe_enabled() ? csr_bwd_name(false, ld_gout, 3, grad_out, grad_feats, D) : "");
+    if (int e = csr_bwd<false>(grad_out, ld_gout, 3, nullptr, offsets, entries, (int)targets, D, grad_feats, s))
+        return e;
     return launch_status("pcs_group_bwd_csr");
 }
 
 // grad_pts (B, M, D) = backward of interpolate's IDW gather (overwrites).
 PCS_API int pcs_interp_bwd_csr(const float* grad_out, int ld_gout, int col_off, const float* dist,
-                               const int32_t* offsets, const int32_t* entries, int B, int M, int D, float* grad_pts,
-                               void* stream) {
-    PCS_CHECK_ARG(B >= 1 && M >= 1 && D >= 1 && ld_gout >= col_off + D && col_off >= 0, "pcs_interp_bwd_csr: bad sizes");
+                               const int32_t* offsets, const int32_t* entries, int B, int M, int D,
+                               long long n_slots, float* grad_pts, void* stream) {
+    PCS_CHECK_ARG(B >= 1 && M >= 1 && D >= 1 && ld_gout >= col_off + D && col_off >= 0 && n_slots >= 0,
+                  "pcs_interp_bwd_csr: bad sizes");
     const long long total = (long long)B * M * D, targets = (long long)B * M;
-    PCS_CHECK_ARG(total < (1ll << 31), "pcs_interp_bwd_csr: too many elements");
+    PCS_CHECK_ARG(total < (1ll << 31) && n_slots < (1ll << 31), "pcs_interp_bwd_csr: too many elements");
     PCS_CHECK_ARG(grad_out && dist && offsets && entries && grad_pts, "pcs_interp_bwd_csr: null pointer");
-    const dim3 grid((unsigned)((targets + 3) / 4));
-    const bool al = ld_gout % 4 == 0 && col_off % 4 == 0 && ((uintptr_t)grad_out | (uintptr_t)grad_pts) % 16 == 0;
-    const int V = al && (D == 128 || D == 256) ? D / 64 : 1;
-    ProbeScope pr(as_stream(stream), 0.0, 8.0 * (double)total + 4.0 * (double)(targets + 1),
-                  V == 1 ? "pcs::interp_bwd_csr_kernel" : "pcs::interp_bwd_csr_vec_kernel<%d>", V);
-    if (V == 2)
-        hipLaunchKernelGGL(interp_bwd_csr_vec_kernel<2>, grid, dim3(256), 0, as_stream(stream), grad_out, ld_gout,
-                           col_off, dist, offsets, entries, (int)targets, grad_pts);
-    else if (V == 4)
-        hipLaunchKernelGGL(interp_bwd_csr_vec_kernel<4>, grid, dim3(256), 0, as_stream(stream), grad_out, ld_gout,
-                           col_off, dist, offsets, entries, (int)targets, grad_pts);
-    else
-        hipLaunchKernelGGL(interp_bwd_csr_kernel, grid, dim3(256), 0, as_stream(stream), grad_out, ld_gout, col_off,
-                           dist, offsets, entries, (int)targets, D, grad_pts);
+    hipStream_t s = as_stream(stream);
+    // algorithmic bytes: per slot its row's D gradient columns, its entry and its row's 3 distances
+    // (read once per slot), the coarse gradient written, the offsets read
+    ProbeScope pr(s, 0.0, 4.0 * (double)n_slots * (D + 4) + 4.0 * (double)total + 4.0 * (double)(targets + 1), "%s",
+                  probe_enabled() ? csr_bwd_name(true, ld_gout, col_off, grad_out, grad_pts, D) : "");
+    if (int e = csr_bwd<true>(grad_out, ld_gout, col_off, dist, offsets, entries, (int)targets, D, grad_pts, s))
+        return e;
     return launch_status("pcs_interp_bwd_csr");
 }
 

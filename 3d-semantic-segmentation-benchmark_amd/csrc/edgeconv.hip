@@ -67,6 +67,8 @@ __global__ __launch_bounds__(256) void edgeconv_fwd_kernel(const float* __restri
             const int32_t* nb = idx + g * k;
             for (int kk = 0; kk < k; ++kk) {
                 const int j = min(max(nb[kk], 0), N - 1);
+                PCS_DCHECK(cloud + j < G && c + 4 <= Cout, "edgeconv fwd Y row %lld col %d outside %lld x %d",
+                           cloud + j, c, G, Cout);
                 const float4 yj = *reinterpret_cast<const float4*>(Y + (cloud + j) * Cout + c);
                 const float jv[4] = {yj.x, yj.y, yj.z, yj.w};
 #pragma unroll
@@ -244,6 +246,7 @@ __global__ __launch_bounds__(256) void edgeconv_bwd_gather_kernel(const float* _
                 const long long r = (long long)__builtin_amdgcn_readlane(row, e);
                 const int kv = __builtin_amdgcn_readlane(kk, e);
                 const size_t o = (size_t)r * Cout + cc;
+                PCS_DCHECK(r >= 0 && r < G, "edgeconv bwd gather row %lld of %lld", r, G);
                 const float dv = D[o];
                 const float qv = Q[o];
                 const int av = arg[o];
@@ -308,9 +311,8 @@ PCS_API int pcs_edgeconv_workspace(int B, int N, int C, int Cout, int backward, 
 // Training-mode EdgeConv forward.  X (B*N rows, stride ldx) with C channels, idx (B, N, k)
 // int32 neighbour table (per-cloud indices), W (Cout, 2C) = the Conv2d weight, BN gamma/beta
 // and running stats (updated in place, num_batches_tracked bumped).  Outputs (caller-owned):
-// Y, PQ (B*N x Cout; PQ holds Q = P - Y on return), S (B*N x Cout), pz (2 x B*N x Cout; the
-// first B*N x Cout hold the pooled edge's z: max over k (gamma > 0), min (< 0), edge 0 (== 0)),
-// pa (2 x B*N x Cout u8, first half used), coef (4 x Cout: s, t, mean, invstd), out (B*N x Cout) pooled
+// Y, PQ (B*N x Cout; PQ holds Q = P - Y on return), S (B*N x Cout), pz (B*N x Cout: the pooled
+// edge's z -- max over k (gamma > 0), min (< 0), edge 0 (== 0)), pa (B*N x Cout u8: its slot), coef (4 x Cout: s, t, mean, invstd), out (B*N x Cout) pooled
 // activation, arg (B*N x Cout u8) its neighbour slot.  Reference: dgcnn.py:60-77.
 PCS_API int pcs_edgeconv_fwd(const float* X, int ldx, int C, const int32_t* idx, int B, int N, int k,
                              const float* W, int Cout, const float* gamma, const float* beta, float* run_mean,
@@ -345,7 +347,7 @@ PCS_API int pcs_edgeconv_fwd(const float* X, int ldx, int C, const int32_t* idx,
     }
     bn_finalize_launch(part, nb, Cout, G * k, gamma, beta, eps, momentum, run_mean, run_var, coef, coef + Cout,
                        coef + 2 * Cout, coef + 3 * Cout, num_batches, st);
-    return pool_finalize(pz, pa, G, Cout, coef, coef + Cout, true, ACT_LRELU, slope, out, arg, st);
+    return pool_finalize(pz, pa, G, Cout, coef, coef + Cout, ACT_LRELU, slope, out, arg, st);
 }
 
 // Training-mode EdgeConv backward (the forward's saved tensors; csr_off/csr_ent = pcs_inverse_index

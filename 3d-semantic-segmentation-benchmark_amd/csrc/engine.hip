@@ -194,8 +194,8 @@ static size_t carve_forward(Carve& cv, int M, int kin, const pcs_mlp_layer* L, i
     s.part = cv.take<double>(max_partials(M, kin, L, nl, pool_k, false));
     if (fused_pool(pool_k)) {
         const size_t gn = (size_t)(M / pool_k) * (size_t)L[nl - 1].cout;
-        s.pz = cv.take<float>(2 * gn);
-        s.pa = cv.take<unsigned char>(2 * gn);
+        s.pz = cv.take<float>(gn);              // the one extreme per channel (gemm_rows_ex's pz / pa)
+        s.pa = cv.take<unsigned char>(gn);
     }
     if (out) *out = s;
     return cv.used;
@@ -353,7 +353,7 @@ PCS_API int pcs_mlp_forward(const float* X, int ldx, int kin, int M, pcs_mlp_lay
     const pcs_mlp_layer& T = layers[nl - 1];
     const int C = (int)T.cout;
     if (fuse)
-        return pool_finalize(S.pz, S.pa, M / pool_k, C, T.coef, T.coef + C, true, (int)T.act,
+        return pool_finalize(S.pz, S.pa, M / pool_k, C, T.coef, T.coef + C, (int)T.act,
                              (float)T.slope, out, arg, st);
     if (pool_k)
         return pcs_pool_fwd(T.Z, C, M / pool_k, pool_k, T.coef, T.coef + C, (int)T.act, (float)T.slope, out, arg,

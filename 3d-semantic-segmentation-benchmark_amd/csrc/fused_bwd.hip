@@ -150,6 +150,8 @@ __global__ __launch_bounds__(256, WIDE ? 1 : 2) void fused_bwd_kernel(FusedBwdAr
 #pragma unroll
         for (int j = 0; j < NJX; ++j) {
             const int rc = min(m0 + s0 + j * RPI, M - 1);
+            PCS_DCHECK(!xin || f.q.rows <= 0 || (rc >= 0 && rc < f.q.rows && 4 * iq + 4 <= ((f.q.cols + 3) & ~3)),
+                       "fused backward input row %d quad %d outside %d x %d", rc, iq, f.q.rows, f.q.cols);
             px[j] = xin ? *reinterpret_cast<const float4*>(f.q.data + (size_t)rc * f.q.ld + 4 * iq)
                         : make_float4(0.f, 0.f, 0.f, 0.f);
         }
@@ -410,7 +412,7 @@ int fused_bwd(const pcs_operand* x, int C, const pcs_operand* q, int CI, const f
     const int G = fused_bwd_grid(M, C, CI, true);
     float* part = reinterpret_cast<float*>((reinterpret_cast<uintptr_t>(ws) + 255) & ~uintptr_t(255));
     float* pdb = db ? part + (size_t)G * C * CI : nullptr;
-    FusedBwdArgs a{to_dev_operand(x), to_dev_operand(q), W, ldw, M, dA, ldd, bstats, part, pdb, CI, CI};
+    FusedBwdArgs a{to_dev_operand(x, M, C), to_dev_operand(q, M, CI), W, ldw, M, dA, ldd, bstats, part, pdb, CI, CI};
     const dim3 grid(G);
     auto launch = [=]() {
         if (C == 32) launch_fused_ci<32>(CI, grid, st, a);
@@ -451,7 +453,8 @@ int fused_wgrad(const pcs_operand* x, int C, const float* X, int ldx, int kin, i
     float* pdb = db ? part + (size_t)G * C * kin : nullptr;
     Operand q{};
     q.data = X; q.ld = ldx; q.slope = 1.f;
-    FusedBwdArgs a{to_dev_operand(x), q, nullptr, 0, M, nullptr, 0, nullptr, part, pdb, kin, kin};
+    q.rows = M; q.cols = kin;
+    FusedBwdArgs a{to_dev_operand(x, M, C), q, nullptr, 0, M, nullptr, 0, nullptr, part, pdb, kin, kin};
     const dim3 grid(G);
     auto launch = [=]() {
         if (C == 32) launch_wgrad_only<32>(grid, st, a);

@@ -95,9 +95,15 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_kernel(const float* __restrict
         const unsigned sa = __builtin_amdgcn_readfirstlane(lbase + 4u * (unsigned)(buf * STAGE + wave * AI * 256));
         const unsigned sb = __builtin_amdgcn_readfirstlane(lbase + 4u * (unsigned)(buf * STAGE + BM * BK + wave * BI * 256));
 #pragma unroll
-        for (int j = 0; j < AI; ++j) glds16(asrc[j] + k0, sa + 1024u * j);
+        for (int j = 0; j < AI; ++j) {
+            PCS_DCHECK_QUAD(asrc[j] + k0, A, M, lda, R, "gemm_nt A");
+            glds16(asrc[j] + k0, sa + 1024u * j);
+        }
 #pragma unroll
-        for (int j = 0; j < BI; ++j) glds16(bsrc[j] + k0, sb + 1024u * j);
+        for (int j = 0; j < BI; ++j) {
+            PCS_DCHECK_QUAD(bsrc[j] + k0, B, N, ldb, R, "gemm_nt B");
+            glds16(bsrc[j] + k0, sb + 1024u * j);
+        }
     };
 
     f32x16 acc[TM][TN];
@@ -310,9 +316,15 @@ __global__ __launch_bounds__(512, 1) void wgrad_nt_kernel(const float* __restric
         const unsigned sy =
             __builtin_amdgcn_readfirstlane(lbase + 4u * (unsigned)(buf * STAGE + BR * BO + wave * YI * 256));
 #pragma unroll
-        for (int j = 0; j < XI; ++j) glds16(xsrc[j] + xo, sx + 1024u * j);
+        for (int j = 0; j < XI; ++j) {
+            PCS_DCHECK_QUAD(xsrc[j] + xo, X, M, ldx, N, "wgrad_nt X");
+            glds16(xsrc[j] + xo, sx + 1024u * j);
+        }
 #pragma unroll
-        for (int j = 0; j < YI; ++j) glds16(ysrc[j] + yo, sy + 1024u * j);
+        for (int j = 0; j < YI; ++j) {
+            PCS_DCHECK_QUAD(ysrc[j] + yo, Y, M, ldy, K, "wgrad_nt Y");
+            glds16(ysrc[j] + yo, sy + 1024u * j);
+        }
     };
 
     f32x16 acc[TM][TN];

@@ -111,11 +111,14 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void gemm_rows_kernel(GemmArgs g) 
                                       // column dx_col0 on, rows of 3 + D): scalar loads
                     const float* wr = g.W + (size_t)gk * g.ldw;
                     const int gn = n0 + 4 * (e % (BN / 4)), nl = g.N - 1;
+                    PCS_DCHECK(gk >= 0 && gk < g.K, "row GEMM k-major W row %d of %d", gk, g.K);
                     if (kBFull || e < BN * GBK / 4)
                         rb[it] = make_float4(wr[min(gn, nl)], wr[min(gn + 1, nl)], wr[min(gn + 2, nl)],
                                              wr[min(gn + 3, nl)]);
                 } else {
                     const int gn = min(n0 + 4 * (e % (BN / 4)), ldw_last);
+                    PCS_DCHECK(gk >= 0 && gk < g.K && gn >= 0 && gn + 4 <= ((g.N + 3) & ~3),
+                               "row GEMM k-major W (%d, %d) outside %d x %d", gk, gn, g.K, g.N);
                     if (kBFull || e < BN * GBK / 4)
                         rb[it] = *reinterpret_cast<const float4*>(g.W + (size_t)gk * g.ldw + gn);
                 }
@@ -124,11 +127,14 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void gemm_rows_kernel(GemmArgs g) 
                 if (g.ldw & 3) {      // unpadded weight rows (a stack's first layer, K = 3 + D): scalar loads
                     const float* wr = g.W + (size_t)gn * g.ldw;
                     const int gk = k0 + 4 * (e & 7), kl = g.K - 1;
+                    PCS_DCHECK(gn >= 0 && gn < g.N, "row GEMM W row %d of %d", gn, g.N);
                     if (kBFull || e < BN * GBK / 4)
                         rb[it] = make_float4(wr[min(gk, kl)], wr[min(gk + 1, kl)], wr[min(gk + 2, kl)],
                                              wr[min(gk + 3, kl)]);
                 } else {
                     const int gk2 = min(k0 + 4 * (e & 7), ldw_last);
+                    PCS_DCHECK(gn >= 0 && gn < g.N && gk2 >= 0 && gk2 + 4 <= ((g.K + 3) & ~3),
+                               "row GEMM W (%d, %d) outside %d x %d", gn, gk2, g.N, g.K);
                     if (kBFull || e < BN * GBK / 4)
                         rb[it] = *reinterpret_cast<const float4*>(g.W + (size_t)gn * g.ldw + gk2);
                 }
@@ -619,21 +625,57 @@ __device__ __forceinline__ double wave_sum_f64(double v) {
     return v;
 }
 
-__device__ __forceinline__ void channel_sums(const double* __restrict__ part, int nb, int N, int n, int lane,
-                                             double& S1, double& S2) {
-    const double* p1 = part + (size_t)n * nb;
-    const double* p2 = part + ((size_t)N + n) * nb;
-    double a0 = 0.0, a1 = 0.0, b0 = 0.0, b1 = 0.0;
-    int i = lane;
-    for (; i + 64 < nb; i += 128) {             // two loads in flight per array
-        a0 += p1[i]; a1 += p1[i + 64];
-        b0 += p2[i]; b1 += p2[i + 64];
+// The two fp64 partial sums of channel n over nb row blocks.  TPC threads per channel (the block's
+// 256 threads cover 256 / TPC channels), sized so a thread holds <= 4 partials per array, all issued
+// before the first add: the partials come from the producing kernel's blocks on every XCD and are
+// read back from HBM / MALL, so each dependent round of loads costs a full memory latency -- one
+// round instead of nb / 128 (round 5: the 1024-partial data-gradient finalizes took ~10 us).  Then
+// a wave reduce and, for TPC > 64, an LDS reduce over the channel's waves.  Fixed order.
+template <int TPC>
+__device__ __forceinline__ void channel_sums(const double* __restrict__ part, int nb, int N, int n, double& S1,
+                                             double& S2) {
+    constexpr int WPC = TPC / 64;                     // waves per channel (TPC = 64, 128, 256)
+    __shared__ double red[2][4];
+    const int r = threadIdx.x % TPC, w = (threadIdx.x / 64) % WPC;
+    const bool ok = n < N;
+    const double* p1 = part + (size_t)(ok ? n : 0) * nb;
+    const double* p2 = part + ((size_t)N + (ok ? n : 0)) * nb;
+    double a[4], b[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int i = r + u * TPC;
+        a[u] = ok && i < nb ? p1[i] : 0.0;
+        b[u] = ok && i < nb ? p2[i] : 0.0;
     }
-    if (i < nb) { a0 += p1[i]; b0 += p2[i]; }
-    S1 = wave_sum_f64(a0 + a1);
-    S2 = wave_sum_f64(b0 + b1);
+    for (int i = r + 4 * TPC; ok && i < nb; i += TPC) {
+        a[0] += p1[i];
+        b[0] += p2[i];
+    }
+    double x = wave_sum_f64((a[0] + a[1]) + (a[2] + a[3]));
+    double y = wave_sum_f64((b[0] + b[1]) + (b[2] + b[3]));
+    if constexpr (WPC > 1) {
+        const int cb = (threadIdx.x / TPC) * WPC;     // this channel's wave slots
+        if ((threadIdx.x & 63) == 0) {
+            red[0][cb + w] = x;
+            red[1][cb + w] = y;
+        }
+        __syncthreads();
+        x = red[0][cb];
+        y = red[1][cb];
+#pragma unroll
+        for (int k = 1; k < WPC; ++k) {
+            x += red[0][cb + k];
+            y += red[1][cb + k];
+        }
+    }
+    S1 = x;
+    S2 = y;
 }
 
+// threads per channel of a finalize over nb partials (<= 4 loads per array and thread up to 1024)
+static int finalize_tpc(int nb) { return nb <= 256 ? 64 : (nb <= 512 ? 128 : 256); }
+
+template <int TPC>
 __global__ __launch_bounds__(256) void bn_finalize_kernel(const double* __restrict__ part, int nb, int N, long long M,
                                                           const float* __restrict__ gamma,
                                                           const float* __restrict__ beta, float eps, float momentum,
@@ -641,12 +683,10 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const double* __restri
                                                           float* __restrict__ s, float* __restrict__ t,
                                                           float* __restrict__ mean_out, float* __restrict__ inv_out,
                                                           long long* __restrict__ nbt) {
-    const int lane = threadIdx.x & 63;
-    const int n = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (n >= N) return;
+    const int n = blockIdx.x * (256 / TPC) + threadIdx.x / TPC;
     double S1, S2;
-    channel_sums(part, nb, N, n, lane, S1, S2);
-    if (lane == 0) {
+    channel_sums<TPC>(part, nb, N, n, S1, S2);
+    if (n < N && threadIdx.x % TPC == 0) {
         if (nbt && n == 0) nbt[0] += 1;         // BatchNorm.num_batches_tracked
         const double mean = S1 / (double)M;
         double var = S2 / (double)M - mean * mean;
@@ -669,19 +709,18 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const double* __restri
 
 // ------------------------------------------------------------------ BN finalize (backward)
 // sums (sum dy, sum dy*xhat) -> dgamma, dbeta (added when `accum`) and the dZ coefficients
-// kB = s*sum_dy/M, kC = s*sum_dyx/M; one wave per channel as above
+// kB = s*sum_dy/M, kC = s*sum_dyx/M; TPC threads per channel as above
+template <int TPC>
 __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const double* __restrict__ part, int nb, int N,
                                                               long long M, const float* __restrict__ s,
                                                               const float* __restrict__ inv,
                                                               float* __restrict__ dgamma, float* __restrict__ dbeta,
                                                               float* __restrict__ kB, float* __restrict__ kC,
                                                               int accum) {
-    const int lane = threadIdx.x & 63;
-    const int n = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (n >= N) return;
+    const int n = blockIdx.x * (256 / TPC) + threadIdx.x / TPC;
     double S1, S2;
-    channel_sums(part, nb, N, n, lane, S1, S2);
-    if (lane == 0) {
+    channel_sums<TPC>(part, nb, N, n, S1, S2);
+    if (n < N && threadIdx.x % TPC == 0) {
         if (dbeta) dbeta[n] = accum ? dbeta[n] + (float)S1 : (float)S1;
         if (dgamma) dgamma[n] = accum ? dgamma[n] + (float)S2 : (float)S2;
         kB[n] = (float)((double)s[n] * S1 / (double)M);
@@ -780,45 +819,33 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restr
 }
 
 // ------------------------------------------------------------------ pooling over K with BN + act
-// pooled[g][c] = max_k act(z*s+t) (first max), argmax u8
+// pooled[g][c] = max_k act(z*s+t) (first max), argmax u8, from the one extreme per channel the
+// producer kept (the max of z where gamma >= 0, the min where gamma < 0: sign(s) = sign(gamma))
 __global__ __launch_bounds__(256) void pool_finalize_kernel(const float* __restrict__ pz,
                                                             const unsigned char* __restrict__ pa, long long GN, int N,
                                                             const float* __restrict__ s, const float* __restrict__ t,
-                                                            bool one_half, float slope, float* __restrict__ out,
+                                                            float slope, float* __restrict__ out,
                                                             unsigned char* __restrict__ arg) {
     for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < GN; e += (long long)gridDim.x * 256) {
         const int c = (int)(e % N);
         const float sc = s[c], tc = t[c];
-        const bool neg = !one_half && sc < 0.f;
-        const float z = pz[neg ? GN + e : e];
-        out[e] = act_f(z * sc + tc, 0, slope);
-        arg[e] = sc == 0.f ? (unsigned char)0 : pa[neg ? GN + e : e];
+        out[e] = act_f(pz[e] * sc + tc, 0, slope);
+        arg[e] = sc == 0.f ? (unsigned char)0 : pa[e];
     }
 }
 
 // the same, one channel quad per thread (N % 4 == 0, 16-B aligned pz / out, 4-B aligned pa / arg):
-// 16-B loads and stores and 32-bit quad indexing instead of a 64-bit modulo per element; the min
-// half of pz / pa is read only for a quad with a negative scale.  Same values as above.
+// 16-B loads and stores and 32-bit quad indexing instead of a 64-bit modulo per element
 __global__ __launch_bounds__(256) void pool_finalize_q_kernel(const float4* __restrict__ pz,
                                                               const uchar4* __restrict__ pa, int GN4, int nq,
                                                               const float* __restrict__ s, const float* __restrict__ t,
-                                                              bool one_half, float slope, float4* __restrict__ out,
+                                                              float slope, float4* __restrict__ out,
                                                               uchar4* __restrict__ arg) {
     for (int e = blockIdx.x * 256 + threadIdx.x; e < GN4; e += gridDim.x * 256) {
         const int c = 4 * (e % nq);
         const float4 sc = *reinterpret_cast<const float4*>(s + c), tc = *reinterpret_cast<const float4*>(t + c);
-        const bool nx = !one_half && sc.x < 0.f, ny = !one_half && sc.y < 0.f, nz = !one_half && sc.z < 0.f,
-                   nw = !one_half && sc.w < 0.f;
-        float4 z = pz[e];
-        uchar4 a = pa[e];
-        if (nx || ny || nz || nw) {
-            const float4 zn = pz[GN4 + e];
-            const uchar4 an = pa[GN4 + e];
-            if (nx) { z.x = zn.x; a.x = an.x; }
-            if (ny) { z.y = zn.y; a.y = an.y; }
-            if (nz) { z.z = zn.z; a.z = an.z; }
-            if (nw) { z.w = zn.w; a.w = an.w; }
-        }
+        const float4 z = pz[e];
+        const uchar4 a = pa[e];
         out[e] = make_float4(act_f(z.x * sc.x + tc.x, 0, slope), act_f(z.y * sc.y + tc.y, 0, slope),
                              act_f(z.z * sc.z + tc.z, 0, slope), act_f(z.w * sc.w + tc.w, 0, slope));
         arg[e] = make_uchar4(sc.x == 0.f ? 0 : a.x, sc.y == 0.f ? 0 : a.y, sc.z == 0.f ? 0 : a.z,
@@ -964,14 +991,26 @@ DropMask drop_mask(double p, long long seed) {
 void bn_finalize_launch(const double* part, int nb, int N, long long M, const float* gamma, const float* beta,
                         float eps, float momentum, float* run_mean, float* run_var, float* s, float* t, float* mean,
                         float* invstd, long long* nbt, hipStream_t st) {
-    hipLaunchKernelGGL(bn_finalize_kernel, dim3((N + 3) / 4), dim3(256), 0, st, part, nb, N, M, gamma, beta, eps, momentum,
-                       run_mean, run_var, s, t, mean, invstd, nbt);
+    const int tpc = finalize_tpc(nb);
+    const dim3 grid((N + 256 / tpc - 1) / (256 / tpc));
+#define PCS_FIN(T) hipLaunchKernelGGL(bn_finalize_kernel<T>, grid, dim3(256), 0, st, part, nb, N, M, gamma, beta, eps, \
+                                      momentum, run_mean, run_var, s, t, mean, invstd, nbt)
+    if (tpc == 64) PCS_FIN(64);
+    else if (tpc == 128) PCS_FIN(128);
+    else PCS_FIN(256);
+#undef PCS_FIN
 }
 
 void bn_bwd_finalize_launch(const double* part, int nb, int N, long long M, const float* s, const float* inv,
                             float* dgamma, float* dbeta, float* kB, float* kC, int accum, hipStream_t st) {
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((N + 3) / 4), dim3(256), 0, st, part, nb, N, M, s, inv, dgamma, dbeta, kB,
-                       kC, accum);
+    const int tpc = finalize_tpc(nb);
+    const dim3 grid((N + 256 / tpc - 1) / (256 / tpc));
+#define PCS_FIN(T) hipLaunchKernelGGL(bn_bwd_finalize_kernel<T>, grid, dim3(256), 0, st, part, nb, N, M, s, inv, dgamma, \
+                                      dbeta, kB, kC, accum)
+    if (tpc == 64) PCS_FIN(64);
+    else if (tpc == 128) PCS_FIN(128);
+    else PCS_FIN(256);
+#undef PCS_FIN
 }
 
 static inline unsigned ew_grid(long long total) {
@@ -1132,15 +1171,6 @@ static double operand_bytes(const pcs_operand& o, int M, int K) {
 // Forward GEMMs in the wide regime (gemm_nt_regime) write one BN partial per 256-row tile,
 // whichever kernel runs them (gemm_nt, or the row GEMM with that many persistent blocks when
 // the operand needs an on-load transform), so the partial count depends on (M, N) only.
-// PCS_DGRAD_DMA=0: the register-staged row GEMM for every data gradient (A/B only)
-static bool dgrad_dma_enabled() {
-    static const bool on = [] {
-        const char* v = getenv("PCS_DGRAD_DMA");
-        return !(v && v[0] == '0');
-    }();
-    return on;
-}
-
 static int row_blocks(int M, int N, bool bwd) {
     if (!bwd && gemm_nt_regime(M, N)) return gemm_nt_row_tiles(M);
     int bm, bn, nt;
@@ -1166,9 +1196,10 @@ static int check_operand(const pcs_operand* o, int K, const char* who, const cha
     return 0;
 }
 
-Operand pcs::to_dev_operand(const pcs_operand* o) {
+Operand pcs::to_dev_operand(const pcs_operand* o, int rows, int cols) {
     Operand r{};
     if (!o) return r;
+    r.rows = rows; r.cols = cols;
     r.data = o->data; r.ld = o->ld; r.mode = o->mode;
     r.s = o->s; r.t = o->t; r.act = o->act; r.slope = eff_slope(o->act, o->slope);
     r.z = o->z; r.ldz = o->ldz;
@@ -1177,7 +1208,7 @@ Operand pcs::to_dev_operand(const pcs_operand* o) {
     return r;
 }
 
-static Operand to_dev(const pcs_operand* o) { return to_dev_operand(o); }
+static Operand to_dev(const pcs_operand* o, int rows, int cols) { return to_dev_operand(o, rows, cols); }
 
 void pcs::wgrad_reduce_launch(const float* part, int splits, long long nk, float* dW, const float* pdb, int N,
                               float* db, hipStream_t st) {
@@ -1221,7 +1252,7 @@ int pcs::materialize_dz(const pcs_operand* x, int M, int C, float* out, int ldo,
     const long long total4 = (long long)M * (C / 4);
     PCS_CHECK_ARG(total4 < (1ll << 31), "materialize_dz: too many elements");
     if (total4 == 0) return 0;
-    const Operand o = to_dev(x);
+    const Operand o = to_dev(x, M, C);
     if (x->mode == PCS_OP_BNBWD)
         hipLaunchKernelGGL(dz_kernel<OP_BNBWD>, dim3(ew_grid(total4)), dim3(256), 0, st, o, (int)total4, C / 4, out,
                            ldo, drop_p > 0.0 ? drop_mask(drop_p, drop_seed) : DropMask{});
@@ -1272,9 +1303,40 @@ int pcs::gemm_rows_ex(const pcs_operand* a, int M, int K, const float* W, int ld
         probe_stop(probe, s);
         return e;
     }
-    // the 64 x 64 data gradient (BN-backward or plain dZ operand): LDS-DMA ring kernel
-    // (dgrad.hip), bitwise the same
-    if (bt && (a->mode == PCS_OP_BNBWD || a->mode == PCS_OP_PLAIN) && !stats && !pool_k && !bias && dgrad_dma_enabled() &&
+    // the forward GEMM of an inner layer (K % 32 == 0, PLAIN or BNACT A) over > 64 outputs and
+    // >= 8192 rows: LDS-DMA ring kernel (fwd_dma.hip) with the row GEMM's epilogue, one BN partial
+    // per row_blocks() block.  Measured in-step on PointNet++ (round 5): 64 -> 128 pooled 114 -> 77 us,
+    // 128 -> 128 35 -> 31, 128 -> 256 pooled 80 -> 61, 256 -> 512 pooled 67 -> 55, FP1-3 -5..-8 us
+    // per layer; the thin ones stay on the row GEMM (32 -> 32 over 1 M rows: 54 vs 117 us, 32 -> 64
+    // pooled 102 vs 128, 64 -> 64 38 vs 42: one slab per 64-row tile, two barriers and an in-place
+    // transform pass per slab are not hidden), as do small M (FP4, 2048 rows: 34 vs 37 us).
+    // Variant 1 (pcs_gemm_rows_variant) takes the DMA kernel wherever it is legal (tests).
+#ifdef PCS_AB_NO_FWD_DMA
+    const int fv = -1;                       // A/B builds only: every forward GEMM on the row GEMM
+#else
+    const int fv = dgrad_forced_variant();
+#endif
+    if (!bt && !bstats && fv >= 0 && (fv >= 1 || (N > 64 && M >= 8192)) &&
+        fwd_dma_ok(a, M, K, W, ldw, N, pool_k, bias)) {
+        const int gx = row_blocks(M, N, false);
+        int probe = -1;
+        if (probe_enabled()) {
+            const pcs_operand ac = *a;
+            probe = probe_start(fwd_dma_name(a->mode == PCS_OP_BNACT, stats != nullptr, pool_k != 0, N),
+                                2.0 * M * K * N, operand_bytes(*a, M, K) + 4.0 * M * N * (pool_k ? 0 : 1) +
+                                (pool_k ? 5.0 * (double)(M / pool_k) * N + 4.0 * M * N : 0.0), s, [=]() {
+                                    gemm_rows_ex(&ac, M, K, W, ldw, 0, bias, C, ldc, N, stats, nullptr, nullptr,
+                                                 stream, pz, pa, pool_k, psign);
+                                });
+        }
+        const int e = fwd_dma(a, M, K, W, ldw, bias, C, ldc, N, stats, gx, pz, pa, pool_k, psign, s);
+        probe_stop(probe, s);
+        if (e) return e;
+        return launch_status("pcs_gemm_rows");
+    }
+    // the 64 x 64 data gradient (BN-backward, pooled BN-backward or plain dZ operand): LDS-DMA ring
+    // kernel (dgrad.hip), bitwise the same (pcs_gemm_rows_kmajor_variant(-1) forces the row GEMM)
+    if (bt && a->mode != PCS_OP_BNACT && !stats && !pool_k && !bias && dgrad_forced_variant() >= 0 &&
         dgrad_dma_ok(a, M, K, W, ldw, N)) {
         int bm, bn;
         gemm_tile(M, N, true, &bm, &bn);
@@ -1285,7 +1347,7 @@ int pcs::gemm_rows_ex(const pcs_operand* a, int M, int K, const float* W, int ld
                 const double bytes = operand_bytes(*a, M, K) + 4.0 * M * N * (bstats ? 2 : 1);
                 const pcs_operand ac = *a, ec = epi ? *epi : pcs_operand{};
                 const bool he = epi != nullptr;
-                probe = probe_start(dgrad_dma_name(bstats != nullptr, a->mode == PCS_OP_BNBWD, N), 2.0 * M * K * N,
+                probe = probe_start(dgrad_dma_name(bstats != nullptr, a->mode, N), 2.0 * M * K * N,
                                     bytes, s, [=]() {
                                         gemm_rows_ex(&ac, M, K, W, ldw, bt, bias, C, ldc, N, stats, he ? &ec : nullptr,
                                                      bstats, stream);
@@ -1297,7 +1359,7 @@ int pcs::gemm_rows_ex(const pcs_operand* a, int M, int K, const float* W, int ld
             return launch_status("pcs_gemm_rows");
         }
     }
-    GemmArgs g{to_dev(a), M, K, W, ldw, bias, C, ldc, N, stats, to_dev(epi), bstats, pz, pa, pool_k, psign};
+    GemmArgs g{to_dev(a, M, K), M, K, W, ldw, bias, C, ldc, N, stats, to_dev(epi, M, N), bstats, pz, pa, pool_k, psign};
     int probe = -1;
     if (probe_enabled()) {
         char nm[96];
@@ -1337,6 +1399,31 @@ PCS_API int pcs_gemm_rows(const pcs_operand* a, int M, int K, const float* W, in
 PCS_API int pcs_gemm_rows_kmajor(const pcs_operand* a, int M, int K, const float* W, int ldw, float* C, int ldc,
                                  int N, const pcs_operand* epi, double* bstats, void* stream) {
     return gemm_rows_ex(a, M, K, W, ldw, 1, nullptr, C, ldc, N, nullptr, epi, bstats, stream);
+}
+
+PCS_API int pcs_gemm_rows_variant(const pcs_operand* a, int M, int K, const float* W, int ldw, const float* bias,
+                                  float* C, int ldc, int N, double* stats, int variant, void* stream) {
+    PCS_CHECK_ARG(variant >= -1 && variant <= 1, "pcs_gemm_rows_variant: variant=%d", variant);
+    dgrad_force_variant(variant);
+    const int e = gemm_rows_ex(a, M, K, W, ldw, 0, bias, C, ldc, N, stats, nullptr, nullptr, stream);
+    dgrad_force_variant(0);
+    return e;
+}
+
+PCS_API int pcs_set_kernel_variant(int variant) {
+    PCS_CHECK_ARG(variant == -1 || variant == 0, "pcs_set_kernel_variant: variant=%d", variant);
+    dgrad_force_variant(variant);
+    return 0;
+}
+
+PCS_API int pcs_gemm_rows_kmajor_variant(const pcs_operand* a, int M, int K, const float* W, int ldw, float* C,
+                                         int ldc, int N, const pcs_operand* epi, double* bstats, int variant,
+                                         void* stream) {
+    PCS_CHECK_ARG(variant >= -1 && variant <= 3, "pcs_gemm_rows_kmajor_variant: variant=%d", variant);
+    dgrad_force_variant(variant);
+    const int e = gemm_rows_ex(a, M, K, W, ldw, 1, nullptr, C, ldc, N, nullptr, epi, bstats, stream);
+    dgrad_force_variant(0);
+    return e;
 }
 
 // wgrad tile (BO x BI) and its row split for N x K over M rows: ~1024 blocks, 2048 for the big
@@ -1426,7 +1513,7 @@ int pcs::wgrad_launch(const pcs_operand* x, int N, const pcs_operand* y, int K, 
     float* pdb = db ? part + (size_t)splits * N * K : nullptr;
     const int tiles = ((N + BO - 1) / BO) * ((K + BI - 1) / BI);
     const dim3 grid(splits, tiles);
-    const Operand xd = to_dev(x), yd = to_dev(y);
+    const Operand xd = to_dev(x, M, N), yd = to_dev(y, M, K);
     // the partial-tile launch alone (the probe's replay rewrites only the workspace)
     auto tiles_launch = [=]() {
         if (BO == 128 && BI == 128) launch_wgrad<128, 128>(grid, st, xd, N, yd, K, M, rows, part, pdb);
@@ -1466,8 +1553,8 @@ PCS_API int pcs_bn_finalize(const double* part, int nb, int N, long long M, cons
                             float eps, float momentum, float* run_mean, float* run_var, float* s, float* t,
                             float* mean, float* invstd, void* stream) {
     PCS_CHECK_ARG(nb >= 1 && N >= 1 && M >= 1, "pcs_bn_finalize: bad sizes");
-    hipLaunchKernelGGL(bn_finalize_kernel, dim3((N + 3) / 4), dim3(256), 0, as_stream(stream), part, nb, N, M, gamma, beta, eps,
-                       momentum, run_mean, run_var, s, t, mean, invstd, (long long*)nullptr);
+    bn_finalize_launch(part, nb, N, M, gamma, beta, eps, momentum, run_mean, run_var, s, t, mean, invstd, nullptr,
+                       as_stream(stream));
     return launch_status("pcs_bn_finalize");
 }
 
@@ -1475,8 +1562,7 @@ PCS_API int pcs_bn_finalize(const double* part, int nb, int N, long long M, cons
 PCS_API int pcs_bn_bwd_finalize(const double* part, int nb, int N, long long M, const float* s, const float* invstd,
                                 float* dgamma, float* dbeta, float* kB, float* kC, int accum, void* stream) {
     PCS_CHECK_ARG(nb >= 1 && N >= 1 && M >= 1, "pcs_bn_bwd_finalize: bad sizes");
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((N + 3) / 4), dim3(256), 0, as_stream(stream), part, nb, N, M, s, invstd,
-                       dgamma, dbeta, kB, kC, accum);
+    bn_bwd_finalize_launch(part, nb, N, M, s, invstd, dgamma, dbeta, kB, kC, accum, as_stream(stream));
     return launch_status("pcs_bn_bwd_finalize");
 }
 
@@ -1520,7 +1606,7 @@ PCS_API int pcs_pool_fwd(const float* Z, int N, long long G, int K, const float*
 }
 
 int pcs::pool_finalize(const float* pz, const unsigned char* pa, long long G, int N, const float* s, const float* t,
-                       bool one_half, int act, float slope, float* out, unsigned char* arg, hipStream_t st) {
+                       int act, float slope, float* out, unsigned char* arg, hipStream_t st) {
     const long long GN = G * N;
     if (GN == 0) return 0;
     auto al = [](const void* p, uintptr_t a) { return (reinterpret_cast<uintptr_t>(p) & (a - 1)) == 0; };
@@ -1529,13 +1615,13 @@ int pcs::pool_finalize(const float* pz, const unsigned char* pa, long long G, in
         const long long GN4 = GN / 4;
         const unsigned blocks = (unsigned)std::min<long long>((GN4 + 255) / 256, 8192);
         hipLaunchKernelGGL(pool_finalize_q_kernel, dim3(blocks), dim3(256), 0, st, reinterpret_cast<const float4*>(pz),
-                           reinterpret_cast<const uchar4*>(pa), (int)GN4, N / 4, s, t, one_half, eff_slope(act, slope),
+                           reinterpret_cast<const uchar4*>(pa), (int)GN4, N / 4, s, t, eff_slope(act, slope),
                            reinterpret_cast<float4*>(out), reinterpret_cast<uchar4*>(arg));
         return launch_status("pool_finalize");
     }
     long long blocks = (GN + 255) / 256;
     if (blocks > 8192) blocks = 8192;
-    hipLaunchKernelGGL(pool_finalize_kernel, dim3((unsigned)blocks), dim3(256), 0, st, pz, pa, GN, N, s, t, one_half,
+    hipLaunchKernelGGL(pool_finalize_kernel, dim3((unsigned)blocks), dim3(256), 0, st, pz, pa, GN, N, s, t,
                        eff_slope(act, slope), out, arg);
     return launch_status("pool_finalize");
 }

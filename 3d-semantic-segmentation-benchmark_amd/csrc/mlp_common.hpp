@@ -37,6 +37,7 @@ struct Operand {
     const float* z; int ldz;
     const float* mean; const float* inv; const float* alpha; const float* kb;
     const unsigned char* arg; int pool_k;
+    int rows, cols;           // the operand's extent (rows x logical channels): debug bounds checks only
 };
 enum { OP_PLAIN = 0, OP_BNACT = 1, OP_BNBWD = 2, OP_POOLBWD = 3 };
 
@@ -78,6 +79,8 @@ __device__ __forceinline__ unsigned pool_slot(const Operand& o, int r) {
 // (callers clamp).  POOLBWD: v = dpool[g][c..], a = the 4 argmax bytes; z only for BNBWD/POOLBWD.
 template <int MODE>
 __device__ __forceinline__ void load_raw(const Operand& o, int r, int c, float4& v, float4& z, unsigned& a) {
+    PCS_DCHECK(o.rows <= 0 || (r >= 0 && r < o.rows && c >= 0 && c + 4 <= ((o.cols + 3) & ~3)),
+               "operand load row %d col %d outside %d x %d (mode %d)", r, c, o.rows, o.cols, MODE);
     if (MODE == OP_POOLBWD) {
         const int g = pool_group(o, r);
         v = *reinterpret_cast<const float4*>(o.data + (size_t)g * o.ld + c);
@@ -166,7 +169,7 @@ struct GemmArgs {
     // fused max-or-min pooling of C over groups of pool_k consecutive rows (pool_k = 16 or 32; 0 =
     // off): pz [M/pool_k][N] = the max of C for columns with psign[n] >= 0 (or psign null), the min
     // for psign[n] < 0 -- the one extreme a monotone consumer act(s*z+t) with sign(s) = sign(psign)
-    // needs -- and pa [M/pool_k][N] its first row within the group (pool_finalize, one_half)
+    // needs -- and pa [M/pool_k][N] its first row within the group (pool_finalize)
     float* pz; unsigned char* pa; int pool_k; const float* psign;
 };
 
@@ -187,13 +190,24 @@ int materialize_dz(const pcs_operand* x, int M, int C, float* out, int ldo, hipS
 int gemm_rows_ex(const pcs_operand* a, int M, int K, const float* W, int ldw, int bt, const float* bias, float* C,
                  int ldc, int N, double* stats, const pcs_operand* epi, double* bstats, void* stream,
                  float* pz = nullptr, unsigned char* pa = nullptr, int pool_k = 0, const float* psign = nullptr);
-// the 64 x 64 BN-backward data gradient through an LDS-DMA ring (dgrad.hip): bitwise
-// gemm_rows_kernel<64, 64, 2, 2, BNBWD, true, 0 | EPI_BWD> for the shapes dgrad_dma_ok accepts;
+// the 64 x 64 data gradient through an LDS-DMA ring (dgrad.hip): bitwise
+// gemm_rows_kernel<64, 64, 2, 2, PLAIN | BNBWD | POOLBWD, true, 0 | EPI_BWD> for the shapes dgrad_dma_ok accepts;
 // gx = the row blocks (= BN-backward partials per column)
 bool dgrad_dma_ok(const pcs_operand* a, int M, int K, const float* W, int ldw, int N);
-const char* dgrad_dma_name(bool bwd, bool xf, int N);   // the kernel dgrad_dma launches (probe / profile name)
+const char* dgrad_dma_name(bool bwd, int mode, int N);  // the kernel dgrad_dma launches (probe / profile name)
+// force a column tile x ring variant for the calling thread's next launches (0 = the policy; 1: 64 x 3,
+// 2: 128 x 2, 3: 128 x 3); -1 = the register-staged row GEMM instead of the DMA kernel
+void dgrad_force_variant(int v);
+int dgrad_forced_variant();
 int dgrad_dma(const pcs_operand* a, int M, int K, const float* W, int ldw, float* C, int ldc, int N,
               const pcs_operand* epi, double* bstats, int gx, hipStream_t st);
+// the forward row GEMM through an LDS-DMA ring (fwd_dma.hip): C = T(A) . W^T + bias with A PLAIN or
+// BNACT, K % 32 == 0, optional fp64 BN partials (stats, gx row blocks) and fused pooling (pz / pa /
+// pool_k 16 | 32 / psign) -- gemm_rows_kernel's epilogue
+bool fwd_dma_ok(const pcs_operand* a, int M, int K, const float* W, int ldw, int N, int pool_k, const float* bias);
+const char* fwd_dma_name(bool xf, bool stats, bool pool, int N);
+int fwd_dma(const pcs_operand* a, int M, int K, const float* W, int ldw, const float* bias, float* C, int ldc, int N,
+            double* stats, int gx, float* pz, unsigned char* pa, int pool_k, const float* psign, hipStream_t st);
 // wide-layer GEMM on plain operands (gemm_big.hip): C = A . B^T, A (M x R), B (N x R) row-major
 bool gemm_nt_regime(int M, int N);                 // (M, N) the wide path is built for
 int gemm_nt_row_tiles(int M);                      // its BN-partial row blocks
@@ -206,21 +220,22 @@ bool wgrad_nt_ok(const float* X, int ldx, const float* Y, int ldy, int M, int N,
 size_t wgrad_nt_ws_bytes(int N, int K, int M);
 int wgrad_nt(const float* X, int ldx, const float* Y, int ldy, int M, int N, int K, float* part, hipStream_t st);
 const char* wgrad_nt_name(int N, int K, int M);
-// pooled output of a stack from the GEMM's fused z-space max/min (pz/pa of gemm_rows_ex):
-// out = act(s*z + t) with z = max (s > 0), min (s < 0) or any (s == 0, arg 0) -- act(s*z+t) is
-// monotone in z, so this is max_k act(s*z_k + t) with its first argmax.  one_half: the producer
-// already kept the right extreme per channel in the first half (chosen by the sign of gamma;
-// s = gamma * invstd with invstd > 0, so the signs agree), else the half is chosen by s[n] < 0
+// pooled output of a stack from the GEMM's fused z-space extreme (pz/pa of gemm_rows_ex): out =
+// act(s*z + t) with z = the max of the group where gamma >= 0, its min where gamma < 0 (the one
+// extreme the producer kept per channel; s = gamma * invstd with invstd > 0, so the signs agree)
+// and arg 0 where s == 0 -- act(s*z+t) is monotone in z, so this is max_k act(s*z_k + t) with its
+// first argmax.  pz / pa: (G, N)
 int pool_finalize(const float* pz, const unsigned char* pa, long long G, int N, const float* s, const float* t,
-                  bool one_half, int act, float slope, float* out, unsigned char* arg, hipStream_t st);
+                  int act, float slope, float* out, unsigned char* arg, hipStream_t st);
 // engine launch probe: probe_enabled / probe_start / probe_stop (pcs_common.hpp, probe.cpp)
 // weight gradient with deterministic partials: workspace bytes for (N, K, M), and the launch
 size_t wgrad_ws_bytes(int N, int K, int M);
 int wgrad_launch(const pcs_operand* x, int N, const pcs_operand* y, int K, int M, float* dW, float* db, void* ws,
                  size_t ws_bytes, void* stream);
 
-// device-side operand of an ABI operand (the activation folded into one slope)
-Operand to_dev_operand(const pcs_operand* o);
+// device-side operand of an ABI operand (the activation folded into one slope) over rows x cols
+// (its extent, for the debug library's bounds checks)
+Operand to_dev_operand(const pcs_operand* o, int rows, int cols);
 // dW[e] += sum_s part[s][e] (e < nk), db[e] += sum_s pdb[s][e] (e < N; pdb/db nullable): fixed order
 void wgrad_reduce_launch(const float* part, int splits, long long nk, float* dW, const float* pdb, int N, float* db,
                          hipStream_t st);

@@ -19,6 +19,35 @@
 
 #define PCS_API extern "C" __attribute__((visibility("default")))
 
+// Device-side bounds checks of the debug library (`make debug` -> libpcseg_debug.so, built with
+// -DPCS_DEBUG_BOUNDS): every clamped operand access of the row GEMM, row / wide weight gradients,
+// LDS-DMA data gradient and EdgeConv is checked against its operand's rows and LOGICAL channel
+// span (rounded to a quad), and a violation prints the site and traps.  Compiled out otherwise.
+#ifdef PCS_DEBUG_BOUNDS
+#define PCS_DCHECK(cond, fmt, ...)                                                                  \
+    do {                                                                                            \
+        if (!(cond)) {                                                                              \
+            printf("pcs bounds: %s:%d: " fmt "\n", __FILE__, __LINE__, ##__VA_ARGS__);             \
+            __builtin_trap();                                                                       \
+        }                                                                                           \
+    } while (0)
+#else
+#define PCS_DCHECK(cond, fmt, ...) \
+    do {                           \
+    } while (0)
+#endif
+
+// debug: the 16-B access at p lies in the first `rows` rows of the row-major operand at base (row
+// stride ld floats) and inside its first `width` channels rounded up to a quad
+#define PCS_DCHECK_QUAD(p, base, rows, ld, width, what)                                                  \
+    do {                                                                                                 \
+        const long long o_ = (long long)((p) - (base));                                                  \
+        const long long r_ = o_ / (ld), c_ = o_ - r_ * (ld);                                             \
+        PCS_DCHECK(o_ >= 0 && r_ < (long long)(rows) && c_ + 4 <= (long long)(((width) + 3) & ~3),       \
+                   "%s: row %lld col %lld outside %lld x %d (ld %d)", what, r_, c_, (long long)(rows),   \
+                   (int)(width), (int)(ld));                                                             \
+    } while (0)
+
 namespace pcs {
 
 // ------------------------------------------------------------ launch probe (probe.cpp)

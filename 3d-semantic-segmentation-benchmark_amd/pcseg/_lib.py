@@ -51,6 +51,9 @@ class InverseMap(ctypes.Structure):
                 ('entries', P)]
 
 
+# the C ABI these bindings are written for (include/pcseg.h pcs_abi_version): 3 = round 5
+# (pcs_group_bwd_csr / pcs_interp_bwd_csr take n_slots; pcs_knn_morton_seeds gone since round 4)
+ABI_VERSION = 3
 OP_PLAIN, OP_BNACT, OP_BNBWD, OP_POOLBWD = 0, 1, 2, 3
 OPP = ctypes.POINTER(Operand)
 
@@ -92,6 +95,9 @@ SIGNATURES = {
     'pcs_mlp_layer_size': [],
     'pcs_gemm_rows': [OPP, I32, I32, P, I32, P, P, I32, I32, P, OPP, P, P],
     'pcs_gemm_rows_kmajor': [OPP, I32, I32, P, I32, P, I32, I32, OPP, P, P],
+    'pcs_gemm_rows_kmajor_variant': [OPP, I32, I32, P, I32, P, I32, I32, OPP, P, I32, P],
+    'pcs_gemm_rows_variant': [OPP, I32, I32, P, I32, P, P, I32, I32, P, I32, P],
+    'pcs_set_kernel_variant': [I32],
     'pcs_gemm_nt': [P, I32, P, I32, I32, I32, I32, P, P, I32, P, P],
     'pcs_gemm_nt_row_tiles': [I32],
     'pcs_wgrad_workspace': [I32, I32, I32, P],
@@ -119,8 +125,8 @@ SIGNATURES = {
     'pcs_inverse_index': [P, I32, I32, I32, P, P, P, ctypes.c_size_t, P],
     'pcs_inverse_index_batch_workspace': [P, I32, I32, P],
     'pcs_inverse_index_batch': [P, I32, I32, P, ctypes.c_size_t, P],
-    'pcs_group_bwd_csr': [P, I32, P, P, I32, I32, I32, P, P],
-    'pcs_interp_bwd_csr': [P, I32, I32, P, P, P, I32, I32, I32, P, P],
+    'pcs_group_bwd_csr': [P, I32, P, P, I32, I32, I32, I64, P, P],
+    'pcs_interp_bwd_csr': [P, I32, I32, P, P, P, I32, I32, I32, I64, P, P],
     # block batches
     'pcs_gather_blocks': [P, P, P, I64, P, P, P],
     'pcs_pad_onehot': [P, I32, P, P, P, I32, I32, I32, P, P, P],
@@ -153,6 +159,9 @@ def load() -> ctypes.CDLL:
             lib.pcs_last_error.restype = ctypes.c_char_p
             lib.pcs_last_error.argtypes = []
             lib.pcs_abi_version.restype = ctypes.c_int
+            if lib.pcs_abi_version() != ABI_VERSION:
+                raise RuntimeError(f'pcseg: {LIB_PATH} has ABI {lib.pcs_abi_version()}, these bindings expect '
+                                   f'{ABI_VERSION}; rebuild the library')
             for name, args in SIGNATURES.items():
                 fn = getattr(lib, name)
                 fn.argtypes = args

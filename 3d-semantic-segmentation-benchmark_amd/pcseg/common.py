@@ -145,6 +145,9 @@ class GeometryPlan:
         made = []
         self.inverse = inverse
         self.fps_idx = []
+        # the native plan builds every inverse map after the last 3-NN when it has both: the
+        # level events then do not cover the ball queries' maps, nn_event does (see sa())
+        self._maps_late = _replay() is None and bool(interp) and bool(inverse)
         if _replay() is None:
             # one native call (pcs_geometry_plan): same kernels, same order, same RNG draws
             self._build_native(coords, levels, interp, inverse, into, main, side)
@@ -334,10 +337,16 @@ class GeometryPlan:
             a.copy_(b)
 
     def sa(self, level: int, q: int = 0):
-        """(centroids, ball idx, inverse map or None) of level >= 1 for its q-th query,
-        after waiting for them."""
+        """(centroids, ball idx, inverse map or None) of level >= 1 for its q-th query.  Waits for
+        the level's event, which covers the centroids and the ball idx.  The inverse map is read
+        only by the gather's backward; where the native plan builds the maps after every 3-NN
+        (interp and inverse, geometry.hip) the level event does not cover it, so it comes as
+        (offsets, entries, event) with the event that does (nn_event), and ops.GroupFn's backward
+        waits on that event before reading it.  Otherwise it is (offsets, entries)."""
         self._wait(self.events[level - 1])
         idx, inv = self.balls[level - 1][q]
+        if inv is not None and self._maps_late:
+            inv = (inv[0], inv[1], self.nn_event)
         return self.coords[level], idx, inv
 
     def fp(self, level: int):

@@ -64,7 +64,10 @@ class FlatGradAllReduce:
     """Flat gradient buffer + bucketed, backward-overlapped all-reduce (mean)."""
 
     def __init__(self, model: torch.nn.Module, bucket_bytes: int = 4 << 20, overlap: bool = True,
-                 broadcast_buffers: bool = True):
+                 broadcast_buffers: bool = True, collectives_at_world_1: bool = False):
+        """collectives_at_world_1: run the bucket all-reduces even in a world of one process (an
+        identity there: the sum of one rank's buffer, divided by 1) -- exercises RCCL's stream
+        ordering against the engine's wgrad lane on a single GPU (tests/test_gpu_rccl.py)."""
         self.params = [p for p in model.parameters() if p.requires_grad]
         # every parameter (and its gradient) starts on a 256-B boundary of the flat buffers: the
         # wide GEMMs stage weights by 16-B LDS-DMA and take only aligned operands
@@ -72,6 +75,7 @@ class FlatGradAllReduce:
         dev = self.params[0].device
         self.flat = torch.zeros(total, dtype=torch.float32, device=dev)
         self.world = dist.get_world_size() if dist.is_initialized() else 1
+        self.collective = self.world > 1 or (collectives_at_world_1 and dist.is_initialized())
         # buckets are laid out in REVERSE parameter order: backward produces the
         # last layers' gradients first, so the first bucket completes earliest.
         order = list(reversed(self.params))
@@ -94,7 +98,7 @@ class FlatGradAllReduce:
         self._launched = [False] * len(self.buckets)
         self._seen: set[int] = set()
         self._handles: list = []
-        self.overlap = overlap and self.world > 1
+        self.overlap = overlap and self.collective
         self.buffers = None
         if broadcast_buffers and self.world > 1 and any(True for _ in model.buffers()):
             # DDP broadcast_buffers: rank 0's buffers at the start of every training forward
@@ -155,7 +159,7 @@ class FlatGradAllReduce:
         """Finish all bucket reductions and average (call before optimizer.step())."""
         if self.flat.is_cuda:
             lane_join(self.flat.device)      # every deferred weight gradient is written
-        if self.world == 1:
+        if not self.collective:
             return
         if self.overlap:
             for h in self._handles:
@@ -166,5 +170,6 @@ class FlatGradAllReduce:
                     dist.all_reduce(self.flat[s:e], op=dist.ReduceOp.SUM)
         else:
             dist.all_reduce(self.flat, op=dist.ReduceOp.SUM)
-        self.flat.div_(self.world)
+        if self.world > 1:
+            self.flat.div_(self.world)
         self._reset()

@@ -157,6 +157,13 @@ def gemm_rows_kmajor(a: Operand, M, K, W, ldw, C, ldc, N, epi: Operand | None = 
     call('pcs_gemm_rows_kmajor', a, M, K, ptr(W), ldw, ptr(C), ldc, N, epi, ptr(bstats), st)
 
 
+def gemm_rows_kmajor_variant(a: Operand, M, K, W, ldw, C, ldc, N, variant, epi: Operand | None = None,
+                             bstats=None, st=None):
+    """gemm_rows_kmajor with its kernel forced for this call: -1 the register-staged row GEMM, 0 the
+    policy, 1 / 2 / 3 the LDS-DMA kernel as 64x3 / 128x2 / 128x3 (column tile x ring stages)."""
+    call('pcs_gemm_rows_kmajor_variant', a, M, K, ptr(W), ldw, ptr(C), ldc, N, epi, ptr(bstats), variant, st)
+
+
 def wgrad_workspace(N, K, M) -> int:
     """Bytes of pcs_wgrad's partial-tile workspace for an N x K gradient over M rows."""
     key = ('wgrad', N, K, M)
@@ -535,8 +542,8 @@ class EdgeConvFn(torch.autograd.Function):
         if not Wm.is_contiguous():
             Wm = Wm.contiguous()
         Y, PQ, S, out = (_f32((M, Cout), dev) for _ in range(4))
-        pz = _f32((2, M, Cout), dev)
-        pa = torch.empty((2, M, Cout), dtype=torch.uint8, device=dev)
+        pz = _f32((M, Cout), dev)                 # the one pooled extreme per channel (edgeconv.hip)
+        pa = torch.empty((M, Cout), dtype=torch.uint8, device=dev)
         arg = torch.empty((M, Cout), dtype=torch.uint8, device=dev)
         coef = _f32((4 * Cout,), dev)
         track = bn.track_running_stats and bn.running_mean is not None

@@ -179,7 +179,10 @@ class GroupFn(torch.autograd.Function):
         out = torch.empty((B * C * K, ld), dtype=torch.float32, device=xyz.device)
         call('pcs_group_fwd', ptr(xyz), ptr(feats), ptr(cent), ptr(idx), B, N, C, K, D, float(np.float32(r)),
              int(bool(normalize)), ptr(out), ld, stream_ptr(xyz.device))
-        ctx.save_for_backward(idx, *(inv if inv is not None else ()))
+        # inv = (offsets, entries) or (offsets, entries, event): the event that covers the map
+        # when it is still being built on the geometry stream (GeometryPlan.sa)
+        ctx.save_for_backward(idx, *(inv[:2] if inv is not None else ()))
+        ctx.inv_event = inv[2] if inv is not None and len(inv) > 2 else None
         ctx.dims = (B, N, C, K, D, ld)
         ctx.has_feats = feats is not None
         ctx.has_inv = inv is not None
@@ -195,14 +198,17 @@ class GroupFn(torch.autograd.Function):
             gout = _c(gout)
             # gather over the inverse map (built here when the forward was not handed one)
             off, ent = saved[1:3] if ctx.has_inv else inverse_index(idx, N)
+            if ctx.inv_event is not None:
+                torch.cuda.current_stream(gout.device).wait_event(ctx.inv_event)
             gfeats = torch.empty((B, N, D), dtype=torch.float32, device=gout.device)
-            call('pcs_group_bwd_csr', ptr(gout), ld, ptr(off), ptr(ent), B, N, D, ptr(gfeats),
+            call('pcs_group_bwd_csr', ptr(gout), ld, ptr(off), ptr(ent), B, N, D, B * C * K, ptr(gfeats),
                  stream_ptr(gout.device))
         return None, gfeats, None, None, None, None, None
 
 
 def group_rows(xyz, feats, cent, idx, r, normalize, inv=None):
-    """inv: optional inverse_index(idx, N) for the atomic-free backward."""
+    """inv: optional inverse_index(idx, N) for the atomic-free backward, optionally with the event
+    that covers it as a third element (waited on by the backward before it reads the map)."""
     check_cuda(xyz, cent, idx)
     xyz, cent = _c(xyz.float()), _c(cent.float())
     feats = _c(feats.float()) if feats is not None else None
@@ -281,7 +287,7 @@ class InterpCatFn(torch.autograd.Function):
             # gather over the inverse map (built here when the forward was not handed one)
             off, ent = saved[2:4] if ctx.has_inv else inverse_index(idx, M)
             g2 = torch.empty((B, M, D2), dtype=torch.float32, device=gout.device)
-            call('pcs_interp_bwd_csr', ptr(gout), W, D1, ptr(dist), ptr(off), ptr(ent), B, M, D2,
+            call('pcs_interp_bwd_csr', ptr(gout), W, D1, ptr(dist), ptr(off), ptr(ent), B, M, D2, 3 * B * N,
                  ptr(g2), stream_ptr(gout.device))
         return g1, g2, None, None, None
 

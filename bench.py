@@ -494,6 +494,11 @@ def main():
     ap.add_argument('--model', default='pointnetpp', choices=sorted(WORKLOADS))
     ap.add_argument('--secondary', default='auto', help="second workload on the same line ('auto': dgcnn when "
                                                         "--model is pointnetpp; 'none' to skip)")
+    ap.add_argument('--others', default='auto',
+                    help="further workloads timed on the same line under `other_configs`, comma-separated "
+                         "('auto': BASELINE configs[3] / configs[4]'s per-GPU halves -- pointnetpp_msg at batch 32, "
+                         "pointnext at batch 16 x 24576 -- when --model is pointnetpp; 'none' to skip); no CPU "
+                         "baseline for them")
     ap.add_argument('--batch', type=int, default=0, help='per-GPU batch (default: the workload\'s)')
     ap.add_argument('--npoints', type=int, default=0, help='points per block (default: the workload\'s)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
@@ -561,8 +566,15 @@ def main():
         if sec not in WORKLOADS:
             raise SystemExit(f'unknown --secondary {sec}')
         keys.append(sec)
+    oth = args.others
+    if oth == 'auto':
+        oth = 'pointnetpp_msg,pointnext' if args.model == 'pointnetpp' else 'none'
+    others = [] if oth == 'none' else [k for k in oth.split(',') if k and k not in keys]
+    for k in others:
+        if k not in WORKLOADS:
+            raise SystemExit(f'unknown --others workload {k}')
     sizes = {k: (args.batch or WORKLOADS[k][3], args.npoints or WORKLOADS[k][4]) if k == args.model
-             else (WORKLOADS[k][3], WORKLOADS[k][4]) for k in keys}
+             else (WORKLOADS[k][3], WORKLOADS[k][4]) for k in keys + others}
 
     cpu_res = {}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -577,9 +589,9 @@ def main():
             raise SystemExit(f'RCCL world {dist.get_world_size()} != --gpus {args.gpus}')
     dev = torch.device('cuda', local)
 
-    results = {k: run_workload(k, *sizes[k], args, world, rank, dev) for k in keys}
+    results = {k: run_workload(k, *sizes[k], args, world, rank, dev) for k in keys + others}
     if world == 1 and not args.no_drop_in:
-        for k in keys:
+        for k in keys + others:
             print(f'[bench] {k}: drop-in harness-A step', file=sys.stderr, flush=True)
             results[k]['drop_in'] = run_drop_in(k, *sizes[k], args, dev)
     if rank == 0:
@@ -599,6 +611,9 @@ def main():
             r['cpu_baseline'] = cpu_res.get(k)
             r['metric'] = METRIC
             res['secondary'] = dict(r, n_gpus=world, dtype='fp32')
+        if others:
+            res['other_configs'] = {k: dict(results[k], metric=METRIC, n_gpus=world, dtype='fp32', cpu_baseline=None)
+                                    for k in others}
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()

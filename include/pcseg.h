@@ -27,6 +27,8 @@ extern "C" {
 #endif
 
 const char* pcs_last_error(void);
+/* 3 since round 5 (pcs_group_bwd_csr / pcs_interp_bwd_csr take n_slots; round 4 dropped
+ * pcs_knn_morton_seeds and added pcs_inverse_index_batch); bindings refuse another version */
 int pcs_abi_version(void);
 /* sizeof(pcs_operand), for bindings to check their struct layout */
 int pcs_operand_size(void);
@@ -77,10 +79,12 @@ int pcs_knn_seeded(const float* x, int B, int N, int F, int k, const int32_t* se
  * centroids (pcs_fps, start = starts[l*B + b]), then its nq ball queries (pcs_ball_query
  * against the previous level's points, or the centroids themselves when on_self -- the
  * InvResMLP grouping, models/utils/common.py:288), then `event` is recorded (nullable);
- * after all levels, when interp, the ball queries' inverse maps (pcs_inverse_index, when
- * inverse) and the 3-NN of each FeaturePropagation from level L-1 down to 0 (pcs_knn_select
- * of level l-1's points (coords for l = 0) among level l's centroids, and its inverse map),
- * then nn_event (without interp each ball query's map follows it, before `event`).  Same kernels and arguments as the per-op calls:
+ * after all levels, when interp: the 3-NN of each FeaturePropagation from level L-1 down to
+ * 0 (pcs_knn_select of level l-1's points (coords for l = 0) among level l's centroids), then
+ * every inverse map -- the ball queries' and the 3-NN's, when inverse -- in one
+ * pcs_inverse_index_batch, then nn_event.  So with interp the level events cover the FPS and
+ * ball queries only and nn_event covers every inverse map; without interp each level's maps
+ * precede its `event`.  Same kernels and arguments as the per-op calls:
  * bitwise the same plan.  Outputs caller-owned; the inverse maps share one workspace of
  * pcs_geometry_plan_workspace bytes.  Replaces pcseg.common.GeometryPlan's ~20 calls. */
 #define PCS_GEO_MAX_LEVELS 6
@@ -188,6 +192,24 @@ int pcs_gemm_rows(const pcs_operand* a, int M, int K, const float* W, int ldw,
 int pcs_gemm_rows_kmajor(const pcs_operand* a, int M, int K, const float* W, int ldw,
                          float* C, int ldc, int N, const pcs_operand* epi,
                          double* bstats, void* stream);
+/* pcs_gemm_rows with its kernel forced for this one call (A/B and tests): variant -1 = the
+ * register-staged row GEMM, 0 = the policy (the LDS-DMA forward kernel for > 64 outputs over
+ * >= 8192 rows), 1 = the LDS-DMA forward kernel wherever it is legal (K % 32 == 0, PLAIN / BNACT
+ * A, 16-B aligned rows). */
+int pcs_gemm_rows_variant(const pcs_operand* a, int M, int K, const float* W, int ldw,
+                          const float* bias, float* C, int ldc, int N, double* stats,
+                          int variant, void* stream);
+/* The calling thread's engine kernels for every later call (A/B and tests only; the product
+ * never calls it): -1 = the register-staged row GEMMs only (no LDS-DMA forward / data-gradient
+ * kernels), 0 = the policy. */
+int pcs_set_kernel_variant(int variant);
+/* pcs_gemm_rows_kmajor with its kernel forced for this one call (A/B measurements and the
+ * bitwise tests; the product always calls the policy): variant -1 = the register-staged row
+ * GEMM, 0 = the policy, 1..3 = the LDS-DMA kernel with 64 x 3 / 128 x 2 / 128 x 3 column tile x
+ * ring stages.  Results are bitwise equal across variants. */
+int pcs_gemm_rows_kmajor_variant(const pcs_operand* a, int M, int K, const float* W, int ldw,
+                                 float* C, int ldc, int N, const pcs_operand* epi,
+                                 double* bstats, int variant, void* stream);
 /* Wide-layer GEMM on plain operands (DGCNN conv5..conv7 forward and data gradient,
  * models/dgcnn/dgcnn.py:188-207 -- the conv1d products the reference runs in ATen):
  * C (M x N, ldc) = A (M x R, lda) . B (N x R, ldb)^T (+ bias), both operands
@@ -358,7 +380,8 @@ int pcs_seg_metrics(const float* pred, const void* labels, int label_u8,
 /* workspace bytes of pcs_edgeconv_fwd (backward = 0) / pcs_edgeconv_bwd (1) */
 int pcs_edgeconv_workspace(int B, int N, int C, int Cout, int backward, size_t* bytes);
 /* forward: Y, PQ (returns Q = P - Y), S = sum_k z (each B*N x Cout), pz / pa
- * (2 x B*N x Cout: max, min of z over k and their first slot), coef (s, t, mean,
+ * (B*N x Cout: the pooled edge's z -- the max over k where gamma > 0, the min where
+ * gamma < 0, edge 0 where gamma == 0 -- and its first slot), coef (s, t, mean,
  * invstd; 4 x Cout), pooled activation out (B*N x Cout) + argmax slot arg (u8);
  * running stats / num_batches updated in place. */
 int pcs_edgeconv_fwd(const float* X, int ldx, int C, const int32_t* idx, int B, int N,
@@ -431,14 +454,17 @@ int pcs_inverse_index_batch_workspace(const pcs_inverse_map* maps, int nmaps, in
 int pcs_inverse_index_batch(const pcs_inverse_map* maps, int nmaps, int B, void* workspace,
                             size_t ws_bytes, void* stream);
 /* common.py:64-65 backward without atomics: grad_feats (B,N,D) = sum of
- * grad_out[slot][3 + c] over the slots reading each point (overwrites). */
+ * grad_out[slot][3 + c] over the slots reading each point (overwrites).  n_slots =
+ * the grouped rows (B*C*K; sizes the launch probe's byte model only).  D <= 512.
+ * (ABI 3: n_slots added.) */
 int pcs_group_bwd_csr(const float* grad_out, int ld_gout, const int32_t* offsets,
-                      const int32_t* entries, int B, int N, int D,
+                      const int32_t* entries, int B, int N, int D, long long n_slots,
                       float* grad_feats, void* stream);
-/* common.py:115-122 backward without atomics: grad_pts (B,M,D) (overwrites). */
+/* common.py:115-122 backward without atomics: grad_pts (B,M,D) (overwrites).
+ * n_slots = 3 x the fine rows.  D <= 512.  (ABI 3: n_slots added.) */
 int pcs_interp_bwd_csr(const float* grad_out, int ld_gout, int col_off,
                        const float* dist, const int32_t* offsets,
-                       const int32_t* entries, int B, int M, int D,
+                       const int32_t* entries, int B, int M, int D, long long n_slots,
                        float* grad_pts, void* stream);
 
 /* ---- block batches --------------------------------------------------------- */

@@ -6,10 +6,10 @@ models=${*:-pointnetpp dgcnn}
 out=gpurun_out/$tag; mkdir -p $out
 export TMPDIR=/tmp
 for m in $models; do
-  timeout -k 10 300 python3 bench.py --model $m --no-cpu-baseline --no-roofline --no-drop-in --secondary none --steps 20 --warmup 5 > $out/b_$m.log 2>&1 || exit $?
+  timeout -k 10 300 python3 bench.py --model $m --no-cpu-baseline --no-roofline --no-drop-in --secondary none --others none --steps 20 --warmup 5 > $out/b_$m.log 2>&1 || exit $?
   tail -1 $out/b_$m.log | cut -c1-150
   cd /tmp && timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$out/prof_$m" -o run --output-format csv -- \
-     python3 "$GRAFT_REPO_ROOT/bench.py" --model $m --no-cpu-baseline --no-roofline --no-drop-in --secondary none --steps 10 --warmup 3 \
+     python3 "$GRAFT_REPO_ROOT/bench.py" --model $m --no-cpu-baseline --no-roofline --no-drop-in --secondary none --others none --steps 10 --warmup 3 \
      > "$GRAFT_REPO_ROOT/$out/prof_$m.log" 2>&1 || exit $?
   cd "$GRAFT_REPO_ROOT"
   f=$(find $out/prof_$m -name '*kernel_trace.csv' | head -1)

@@ -27,5 +27,5 @@ print(f'{n} steps, span (first marker to next) {sum(spans) / max(n, 1):.1f} us/s
 for q in sorted(agg):
     items = sorted(agg[q].items(), key=lambda kv: -kv[1][1])
     print(f'== queue {q}: {sum(v[1] for _, v in items) / n:.0f} us/step of kernels')
-    for name, (c, t) in items[:16]:
+    for name, (c, t) in items[:int(__import__("os").environ.get("QB_TOP", "40"))]:
         print(f'  {t / n:8.1f} us/step {c / n:5.1f}x {t / c:8.1f} us  {name}')

@@ -146,3 +146,42 @@ def test_edgeconv_eval_mode_uses_materialised_path():
         with pcseg.replay(pcseg.Replay(knn_idx=[idx])):
             o = prod(x.to(DEV))
     assert rel(o, o_ref) < TOL
+
+
+@pytest.mark.parametrize('tail', [0, 64])
+@pytest.mark.parametrize('C,Cout', [(64, 64), (3, 64)])
+def test_edgeconv_weight_at_storage_end_in_nan_storage(C, Cout, tail):
+    """Regression guard of the round-4 over-read (the row GEMM's B loads clamped to the weight's
+    row STRIDE, so W + C -- the second half of the (Cout, 2C) EdgeConv weight, read as a column
+    block -- ran up to C floats past the weight's end): the weight is a view into a NaN-filled
+    storage, ending exactly at the storage's end (tail = 0) or followed by NaNs (tail = 64), with
+    NaNs before it.  Any load outside the weight's logical extent reads NaN (or faults at the
+    allocation's end), so outputs and every gradient must be finite and equal the fp64 oracle."""
+    x, idx, ref, prod = _case(C, Cout, seed=11 + C)
+    prod = prod.to(DEV).train()
+    conv = prod.conv[0]
+    w = conv.weight.detach()
+    n = w.numel()
+    store = torch.full((256 + n + tail,), float('nan'), device=DEV)
+    view = store[256:256 + n].view_as(w)
+    view.copy_(w)
+    conv.weight = torch.nn.Parameter(view)
+    assert conv.weight.data_ptr() + 4 * n == store.data_ptr() + 4 * (store.numel() - tail)
+    r64, xr, out64 = _ref_fp64(x, idx, ref)
+    xd = x.to(DEV).requires_grad_(C != 3)
+    with pcseg.replay(pcseg.Replay(knn_idx=[idx])):
+        out = prod(xd)
+    g = torch.randn(out64.shape, generator=torch.Generator().manual_seed(6), dtype=torch.float64)
+    (out64 * g).sum().backward()
+    (out * g.float().to(DEV)).sum().backward()
+    torch.cuda.synchronize()
+    assert torch.isfinite(out).all()
+    assert rel(out.detach(), out64.detach()) < TOL
+    for (name, p64), p in zip(r64.named_parameters(), prod.parameters()):
+        assert torch.isfinite(p.grad).all(), name
+        assert rel(p.grad, p64.grad) < TOL, name
+    if C != 3:
+        assert torch.isfinite(xd.grad).all()
+        assert rel(xd.grad, xr.grad) < TOL
+    # the NaN storage around the weight is untouched (nothing wrote outside the view either)
+    assert torch.isnan(store[:256]).all() and torch.isnan(store[256 + n:]).all()

@@ -496,3 +496,50 @@ def test_fps_sqrt_tie_is_correctly_rounded():
     ref = R.fps_indices(xyz, 1024, start)
     got, _ = ops.fps(xyz.to(DEV), 1024, start.to(DEV))
     assert torch.equal(got.cpu(), ref)
+
+
+@pytest.mark.parametrize('D', [19, 64, 100, 128, 256, 300, 512, 700, 1024])
+@pytest.mark.parametrize('kind', ['random', 'skewed'])
+def test_csr_bwd_stream_all_widths_vs_fp64(D, kind):
+    """The streaming CSR backward (round 5: one wave walks the lists of several consecutive
+    targets as one entry range) against the fp64 sum of the same terms in list order, for every
+    channel template (scalar lanes V = 1 / 2 / 4 / 8, float2 / float4 lanes) of both the group
+    gather (rows [xyz, feats]) and the IDW interpolation, with hub lists, empty lists and more
+    targets than waves (several targets per wave)."""
+    from pcseg._lib import call, ptr, stream_ptr
+    g = torch.Generator().manual_seed(D)
+    B, targets, S, k = 2, 20000, 6000, 5
+    if kind == 'skewed':
+        w = 1.0 / torch.arange(1, targets + 1, dtype=torch.float64) ** 1.1
+        idx = torch.multinomial(w, B * S * k, replacement=True, generator=g).view(B, S * k).to(torch.int32)
+    else:
+        idx = torch.randint(0, targets, (B, S * k), generator=g, dtype=torch.int32)
+    off, ent = ops.inverse_index(idx.view(B, S, k).to(DEV), targets)
+    slots = B * S * k
+    key = (torch.arange(B).unsqueeze(1) * targets + idx.long()).reshape(-1)
+    # group form: rows [xyz, D feats, pad], the gradient columns start at 3
+    ld = (3 + D + 3) // 4 * 4
+    gout = torch.randn(slots, ld, generator=g)
+    gf = torch.full((B, targets, D), float('nan'), device=DEV)
+    call('pcs_group_bwd_csr', ptr(gout.to(DEV)), ld, ptr(off), ptr(ent), B, targets, D, slots, ptr(gf),
+         stream_ptr(torch.device(DEV)))
+    ref = torch.zeros(B * targets, D, dtype=torch.float64).index_add_(0, key, gout[:, 3:3 + D].double())
+    torch.cuda.synchronize()
+    assert torch.equal(gf.cpu().view(-1, D), ref.float())
+    # IDW form: fine rows (S*k/3 per cloud) of [D1 skip, D coarse] channels, slot s = 3 * row + j
+    if (S * k) % 3:
+        return
+    rows = slots // 3
+    D1 = 8
+    W = D1 + D
+    gi = torch.randn(rows, W, generator=g)
+    dist = torch.rand(rows, 3, generator=g) * 0.01
+    gp = torch.full((B, targets, D), float('nan'), device=DEV)
+    call('pcs_interp_bwd_csr', ptr(gi.to(DEV)), W, D1, ptr(dist.to(DEV)), ptr(off), ptr(ent), B, targets, D, slots,
+         ptr(gp), stream_ptr(torch.device(DEV)))
+    wts = 1.0 / (dist + 1e-9)
+    nrm = (wts[:, 0] + wts[:, 1]) + wts[:, 2]
+    terms = (gi[:, D1:].unsqueeze(1) / nrm[:, None, None]) * wts[:, :, None]        # (rows, 3, D) fp32
+    ref = torch.zeros(B * targets, D, dtype=torch.float64).index_add_(0, key, terms.reshape(slots, D).double())
+    torch.cuda.synchronize()
+    assert torch.equal(gp.cpu().view(-1, D), ref.float())
