@@ -130,13 +130,20 @@ __device__ __forceinline__ float4 xform4(const Operand& o, float4 v, float4 z, u
     return in ? out : make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
-// inverted-dropout keep test of element i (counter-based: splitmix64 finaliser of seed + i*phi)
+// inverted-dropout keep test of element i, counter-based: the lowbias32 integer hash (C. Wellons)
+// of a Weyl step of the 32-bit element index, mixed with the 64-bit seed -- 32-bit multiplies only.
+// (Round 4 used the splitmix64 finaliser, whose 64-bit multiplies made the dropout-masked DGCNN
+// conv6 / conv7 reduce and dZ passes VALU-bound: 299 vs ~150 us for conv6's reduce in-step.)  Same
+// Bernoulli(1 - p) keep as torch's nn.Dropout, a different random stream.
 __device__ __forceinline__ bool dropout_keep(unsigned long long seed, unsigned long long i, unsigned thr) {
-    unsigned long long z = seed + i * 0x9E3779B97F4A7C15ull;
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    z ^= z >> 31;
-    return (unsigned)(z >> 32) >= thr;
+    unsigned x = (unsigned)i * 0x9E3779B9u + (unsigned)seed;
+    x ^= (unsigned)(i >> 32) * 0x85EBCA6Bu ^ (unsigned)(seed >> 32);
+    x ^= x >> 16;
+    x *= 0x7FEB352Du;
+    x ^= x >> 15;
+    x *= 0x846CA68Bu;
+    x ^= x >> 16;
+    return x >= thr;
 }
 
 // a stack's fused inverted dropout, applied to its output gradient where that is read

@@ -71,10 +71,16 @@ torch.cuda.synchronize()
 t2 = time.perf_counter()
 print(f'host enqueue {(t1 - t0) / 10 * 1e3:.3f} ms/step, wall {(t2 - t0) / 10 * 1e3:.3f} ms/step')
 pr = cProfile.Profile()
-pr.enable()
-for _ in range(10):
-    step()
-pr.disable()
+# the autograd engine runs the backward of CUDA graphs on its own device thread, where cProfile
+# does not look: profile with the backward on this thread instead
+with torch.autograd.set_multithreading_enabled(False):
+    for _ in range(3):
+        step()
+    torch.cuda.synchronize()
+    pr.enable()
+    for _ in range(10):
+        step()
+    pr.disable()
 torch.cuda.synchronize()
 st = pstats.Stats(pr)
 st.sort_stats('tottime').print_stats(40)
