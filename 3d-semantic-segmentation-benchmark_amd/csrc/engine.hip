@@ -125,19 +125,28 @@ static size_t max_partials(int M, int kin, const pcs_mlp_layer* L, int nl, int p
 // every pass reads two arrays (dy and Z), materialised once (read 2, write 1) every pass
 // reads one.  From 4 passes on the materialised form moves fewer bytes (DGCNN conv5-7:
 // -2.1 ms of GEMM time for +0.5 ms of materialising, scripts/dgcnn_head_ab.py).
+#ifndef PCS_AB_DZ_PASSES
+#define PCS_AB_DZ_PASSES 4                   // (A/B builds only: scripts/build_ab.sh -DPCS_AB_DZ_PASSES=n)
+#endif
 static bool materialize_dz_of(const pcs_mlp_layer& P, int M, bool dgrad) {
-    return dz_passes(M, (int)P.cout, (int)P.cin, dgrad, P.dW != nullptr) >= 4;
+    return dz_passes(M, (int)P.cout, (int)P.cin, dgrad, P.dW != nullptr) >= PCS_AB_DZ_PASSES;
 }
+
+// Rotation depth of a backward's dA / kB / alpha buffers.  The dgrad of layer l reuses the buffers
+// that layer l + kRot - 1's wgrad reads, so it must wait for that wgrad on the lane; with kRot = 6 no
+// stack of the models (<= 5 layers) ever waits.  (Round 4 rotated over 3: the dgrads of FP1's first two
+// layers waited ~90 us each for the lane's wgrads of layers 3 / 4, profiles/r05_main_queue_gaps.txt.)
+constexpr int kRot = 6;
 
 struct BwdScratch {
     float* dz;             // the top layer's materialised dZ (M x cout), when it is wide
     bool dz_ok(bool top) const { return !top || dz != nullptr; }
     double* part;
-    float* kb[3];          // BN-backward coefficients and data gradients rotate over 3
-    float* alpha[3];       // buffers: a layer's wgrad (side stream) may still read one while
-                           // the next two layers' dgrads run
+    float* kb[kRot];       // BN-backward coefficients and data gradients rotate over kRot buffers:
+    float* alpha[kRot];    // a layer's wgrad (side stream) may still read one while the next
+                           // kRot - 1 layers' dgrads run
     float* wt;
-    float* dA[3];
+    float* dA[kRot];
     char* wg;              // wgrad partial tiles (shared by the call's wgrads: one side stream)
     size_t wg_bytes;
     char* wg0;             // the first layer's, when its wgrad runs on the caller's stream
@@ -152,15 +161,15 @@ static size_t carve_backward(Carve& cv, int M, int kin, int ldx, const pcs_mlp_l
     const int mc = std::max(max_cout(L, nl), ldx);
     BwdScratch s{};
     s.part = cv.take<double>(max_partials(M, kin, L, nl, pool_k, true));
-    for (int i = 0; i < 3; ++i) { s.kb[i] = cv.take<float>(mc); s.alpha[i] = cv.take<float>(mc); }
+    for (int i = 0; i < kRot; ++i) { s.kb[i] = cv.take<float>(mc); s.alpha[i] = cv.take<float>(mc); }
     size_t wt = 0, da = 0;
     for (int l = 0; l < nl; ++l) {
         wt = std::max(wt, (size_t)L[l].cout * (size_t)L[l].ldw);
         if (l > 0) da = std::max(da, (size_t)M * (size_t)L[l].cin);
     }
     s.wt = cv.take<float>(wt);
-    // the third buffer only when a stack is deep enough to rotate through it
-    for (int i = 0; i < 3; ++i) s.dA[i] = i < 2 || nl > 3 ? cv.take<float>(da) : nullptr;
+    // as many dA buffers as the stack's dgrads use (nl - 1), at most kRot
+    for (int i = 0; i < kRot; ++i) s.dA[i] = i < std::max(1, std::min(nl - 1, kRot)) ? cv.take<float>(da) : nullptr;
     size_t wg = 0;
     for (int l = 0; l < nl; ++l)
         if (L[l].dW) wg = std::max(wg, wgrad_ws_bytes((int)L[l].cout, (int)L[l].cin, M));
@@ -212,7 +221,7 @@ static size_t carve_forward(Carve& cv, int M, int kin, const pcs_mlp_layer* L, i
 // call's wgrads run in order on the side stream and share one partial-tile workspace.
 struct WgradLane {
     hipStream_t side = nullptr;
-    hipEvent_t ev[8] = {};
+    hipEvent_t ev[16] = {};     // two per forked wgrad: a whole stack's forks before the ring wraps
     int next = 0;
     std::mutex use;
 };
@@ -236,7 +245,7 @@ static WgradLane* wgrad_lane() {
 
 static hipEvent_t lane_event(WgradLane* L) {
     hipEvent_t e = L->ev[L->next];
-    L->next = (L->next + 1) & 7;
+    L->next = (L->next + 1) & 15;
     return e;
 }
 
@@ -441,8 +450,8 @@ static int mlp_backward(const float* X, int ldx, int kin, int M, const pcs_mlp_l
     if (lane) lane_lock = std::unique_lock<std::mutex>(lane->use);
     hipEvent_t pending = nullptr;          // the last wgrad launched on the side stream
     // done[l]: layer l's wgrad finished.  The dgrad of layer l recycles the dA / kb / alpha
-    // buffers (3-way rotation) that layer l + 2's wgrad read, so it waits for that one only:
-    // the layer above's wgrad keeps running under this dgrad.
+    // buffers (kRot-way rotation) that layer l + kRot - 1's wgrad read, so it waits for that one
+    // only: the wgrads above keep running under this dgrad.
     std::vector<hipEvent_t> done(nl, nullptr);
     auto join = [&]() {
         if (pending) {
@@ -507,7 +516,7 @@ static int mlp_backward(const float* X, int ldx, int kin, int M, const pcs_mlp_l
             }
             if (e) return fail(e);
         }
-        if (l + 2 < nl && done[l + 2]) (void)hipStreamWaitEvent(st, done[l + 2], 0);
+        if (l + kRot - 1 < nl && done[l + kRot - 1]) (void)hipStreamWaitEvent(st, done[l + kRot - 1], 0);
         if (l == 0 && !dX) break;
         // dgrad B operand: B[k = cout][n = cin] = W[k][n], read k-major straight from W (bt = 1);
         // a first layer whose row stride is not a multiple of 4 goes through the transpose Wt
@@ -537,14 +546,14 @@ static int mlp_backward(const float* X, int ldx, int kin, int M, const pcs_mlp_l
                 if (int e = gemm_rows_ex(&xop, M, C, Bw, ldb, bt, nullptr, dA, Cin, Cin, nullptr, &epi, S.part, stream))
                     return fail(e);
             }
-            pp = (pp + 1) % 3;
+            pp = (pp + 1) % kRot;
             const float* sq = Q.coef;
             if (int e = pcs_bn_bwd_finalize(S.part, nbg, Cin, M, sq, sq + 3 * Cin, Q.dgamma, Q.dbeta, S.kb[pp],
                                             S.alpha[pp], 1, stream))
                 return fail(e);
             if (!Q.use_batch) { zero_f32(S.kb[pp], Cin, st); zero_f32(S.alpha[pp], Cin, st); }
             xop = bnbwd_op(dA, Cin, Q, S.alpha[pp], S.kb[pp]);
-            da = (da + 1) % 3;
+            da = (da + 1) % kRot;
         } else {
             // dX columns [c0, kin): a caller that reads no gradient of the first c0 input columns
             // (the relative coordinates of grouped rows, pcs_mlp_layer.dx_col0) gets a GEMM of
