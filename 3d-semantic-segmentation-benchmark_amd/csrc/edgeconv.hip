@@ -318,11 +318,13 @@ PCS_API int pcs_edgeconv_fwd(const float* X, int ldx, int C, const int32_t* idx,
                              const float* W, int Cout, const float* gamma, const float* beta, float* run_mean,
                              float* run_var, long long* num_batches, float momentum, float eps, float slope,
                              float* Y, float* PQ, float* S, float* pz, unsigned char* pa, float* coef, float* out,
-                             unsigned char* arg, void* workspace, size_t ws_bytes, void* stream) {
+                             unsigned char* arg, float* out2, int ld2, void* workspace, size_t ws_bytes,
+                             void* stream) {
     PCS_CHECK_ARG(B >= 1 && N >= 1 && k >= 1 && k <= 256 && C >= 1 && Cout >= 4 && Cout % 4 == 0 && Cout <= 1024,
                   "pcs_edgeconv_fwd: bad sizes B=%d N=%d k=%d C=%d Cout=%d", B, N, k, C, Cout);
     PCS_CHECK_ARG(X && idx && W && Y && PQ && S && pz && pa && coef && out && arg && workspace,
                   "pcs_edgeconv_fwd: null pointer");
+    PCS_CHECK_ARG(!out2 || ld2 >= Cout, "pcs_edgeconv_fwd: out2 stride %d < Cout=%d", ld2, Cout);
     const long long G = (long long)B * N;
     PCS_CHECK_ARG(G * k < (1ll << 31), "pcs_edgeconv_fwd: too many edges");
     size_t need = 0;
@@ -347,7 +349,7 @@ PCS_API int pcs_edgeconv_fwd(const float* X, int ldx, int C, const int32_t* idx,
     }
     bn_finalize_launch(part, nb, Cout, G * k, gamma, beta, eps, momentum, run_mean, run_var, coef, coef + Cout,
                        coef + 2 * Cout, coef + 3 * Cout, num_batches, st);
-    return pool_finalize(pz, pa, G, Cout, coef, coef + Cout, ACT_LRELU, slope, out, arg, st);
+    return pool_finalize(pz, pa, G, Cout, coef, coef + Cout, ACT_LRELU, slope, out, arg, st, out2, ld2);
 }
 
 // Training-mode EdgeConv backward (the forward's saved tensors; csr_off/csr_ent = pcs_inverse_index

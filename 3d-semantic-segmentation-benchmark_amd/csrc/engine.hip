@@ -618,6 +618,30 @@ PCS_API int pcs_wgrad_lane(void** side_stream) {
     return 0;
 }
 
+#ifndef PCS_AB_GEO_PRIO
+#define PCS_AB_GEO_PRIO 0   // A/B knob: 1 = lowest priority, 0 = normal (a torch.cuda.Stream's)
+#endif
+
+PCS_API int pcs_geometry_stream(void** stream) {
+    PCS_CHECK_ARG(stream, "pcs_geometry_stream: null pointer");
+    static hipStream_t streams[16];
+    static std::mutex mu;
+    int dev = 0;
+    *stream = nullptr;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return launch_status("pcs_geometry_stream");
+    std::lock_guard<std::mutex> g(mu);
+    if (!streams[dev]) {
+        int least = 0, greatest = 0;
+        if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess ||
+            hipStreamCreateWithPriority(&streams[dev], hipStreamNonBlocking, PCS_AB_GEO_PRIO ? least : 0) != hipSuccess) {
+            streams[dev] = nullptr;
+            return launch_status("pcs_geometry_stream");
+        }
+    }
+    *stream = streams[dev];
+    return 0;
+}
+
 PCS_API int pcs_wgrad_lane_join(void* stream) {
     WgradLane* lane = wgrad_lane();
     if (!lane) return 0;

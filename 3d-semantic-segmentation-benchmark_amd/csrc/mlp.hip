@@ -825,11 +825,14 @@ __global__ __launch_bounds__(256) void pool_finalize_kernel(const float* __restr
                                                             const unsigned char* __restrict__ pa, long long GN, int N,
                                                             const float* __restrict__ s, const float* __restrict__ t,
                                                             float slope, float* __restrict__ out,
-                                                            unsigned char* __restrict__ arg) {
+                                                            unsigned char* __restrict__ arg, float* __restrict__ out2,
+                                                            int ld2) {
     for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < GN; e += (long long)gridDim.x * 256) {
         const int c = (int)(e % N);
         const float sc = s[c], tc = t[c];
-        out[e] = act_f(pz[e] * sc + tc, 0, slope);
+        const float v = act_f(pz[e] * sc + tc, 0, slope);
+        out[e] = v;
+        if (out2) out2[(e / N) * ld2 + c] = v;
         arg[e] = sc == 0.f ? (unsigned char)0 : pa[e];
     }
 }
@@ -840,14 +843,17 @@ __global__ __launch_bounds__(256) void pool_finalize_q_kernel(const float4* __re
                                                               const uchar4* __restrict__ pa, int GN4, int nq,
                                                               const float* __restrict__ s, const float* __restrict__ t,
                                                               float slope, float4* __restrict__ out,
-                                                              uchar4* __restrict__ arg) {
+                                                              uchar4* __restrict__ arg, float* __restrict__ out2,
+                                                              int ld2) {
     for (int e = blockIdx.x * 256 + threadIdx.x; e < GN4; e += gridDim.x * 256) {
-        const int c = 4 * (e % nq);
+        const int g = e / nq, c = 4 * (e - g * nq);
         const float4 sc = *reinterpret_cast<const float4*>(s + c), tc = *reinterpret_cast<const float4*>(t + c);
         const float4 z = pz[e];
         const uchar4 a = pa[e];
-        out[e] = make_float4(act_f(z.x * sc.x + tc.x, 0, slope), act_f(z.y * sc.y + tc.y, 0, slope),
-                             act_f(z.z * sc.z + tc.z, 0, slope), act_f(z.w * sc.w + tc.w, 0, slope));
+        const float4 v = make_float4(act_f(z.x * sc.x + tc.x, 0, slope), act_f(z.y * sc.y + tc.y, 0, slope),
+                                     act_f(z.z * sc.z + tc.z, 0, slope), act_f(z.w * sc.w + tc.w, 0, slope));
+        out[e] = v;
+        if (out2) *reinterpret_cast<float4*>(out2 + (size_t)g * ld2 + c) = v;
         arg[e] = make_uchar4(sc.x == 0.f ? 0 : a.x, sc.y == 0.f ? 0 : a.y, sc.z == 0.f ? 0 : a.z,
                              sc.w == 0.f ? 0 : a.w);
     }
@@ -1437,7 +1443,10 @@ static void wgrad_plan(int N, int K, int M, int* BO, int* BI, int* splits, int* 
     // (512 / 256 blocks for the smaller ones measured +0.3 / +0.8 % on DGCNN, round 3)
     // (round 4, in-step: 512 / 2048 blocks for the smaller ones were within noise of 1024 on both
     // models -- shorter lane blocks did not free CUs for the critical path's small kernels sooner)
-    const int target = 2.0 * M * N * K >= 1.6e10 ? 2048 : 1024;
+#ifndef PCS_AB_WG_BLOCKS
+#define PCS_AB_WG_BLOCKS 1024                // (A/B builds only: -DPCS_AB_WG_BLOCKS=n)
+#endif
+    const int target = 2.0 * M * N * K >= 1.6e10 ? 2048 : PCS_AB_WG_BLOCKS;
     int sp = (target + tiles - 1) / tiles;
     // the partial tiles (sp x N x K floats, written once and read once by the reduce) stay
     // below half the operands' bytes M x (N + K), as long as >= 512 blocks remain
@@ -1606,23 +1615,25 @@ PCS_API int pcs_pool_fwd(const float* Z, int N, long long G, int K, const float*
 }
 
 int pcs::pool_finalize(const float* pz, const unsigned char* pa, long long G, int N, const float* s, const float* t,
-                       int act, float slope, float* out, unsigned char* arg, hipStream_t st) {
+                       int act, float slope, float* out, unsigned char* arg, hipStream_t st, float* out2,
+                       int ld2) {
     const long long GN = G * N;
     if (GN == 0) return 0;
+    PCS_CHECK_ARG(!out2 || ld2 >= N, "pool_finalize: second output stride %d < %d channels", ld2, N);
     auto al = [](const void* p, uintptr_t a) { return (reinterpret_cast<uintptr_t>(p) & (a - 1)) == 0; };
     if (N % 4 == 0 && GN / 4 < (1ll << 31) && al(pz, 16) && al(out, 16) && al(pa, 4) && al(arg, 4) && al(s, 16) &&
-        al(t, 16)) {
+        al(t, 16) && (!out2 || (al(out2, 16) && ld2 % 4 == 0))) {
         const long long GN4 = GN / 4;
         const unsigned blocks = (unsigned)std::min<long long>((GN4 + 255) / 256, 8192);
         hipLaunchKernelGGL(pool_finalize_q_kernel, dim3(blocks), dim3(256), 0, st, reinterpret_cast<const float4*>(pz),
                            reinterpret_cast<const uchar4*>(pa), (int)GN4, N / 4, s, t, eff_slope(act, slope),
-                           reinterpret_cast<float4*>(out), reinterpret_cast<uchar4*>(arg));
+                           reinterpret_cast<float4*>(out), reinterpret_cast<uchar4*>(arg), out2, ld2);
         return launch_status("pool_finalize");
     }
     long long blocks = (GN + 255) / 256;
     if (blocks > 8192) blocks = 8192;
     hipLaunchKernelGGL(pool_finalize_kernel, dim3((unsigned)blocks), dim3(256), 0, st, pz, pa, GN, N, s, t,
-                       eff_slope(act, slope), out, arg);
+                       eff_slope(act, slope), out, arg, out2, ld2);
     return launch_status("pool_finalize");
 }
 

@@ -231,9 +231,11 @@ const char* wgrad_nt_name(int N, int K, int M);
 // act(s*z + t) with z = the max of the group where gamma >= 0, its min where gamma < 0 (the one
 // extreme the producer kept per channel; s = gamma * invstd with invstd > 0, so the signs agree)
 // and arg 0 where s == 0 -- act(s*z+t) is monotone in z, so this is max_k act(s*z_k + t) with its
-// first argmax.  pz / pa: (G, N)
+// first argmax.  pz / pa: (G, N).  out2 (nullable, row stride ld2): a second copy of the pooled
+// rows (the DGCNN EdgeConvs' outputs land in their column block of the head's concatenation too)
 int pool_finalize(const float* pz, const unsigned char* pa, long long G, int N, const float* s, const float* t,
-                  int act, float slope, float* out, unsigned char* arg, hipStream_t st);
+                  int act, float slope, float* out, unsigned char* arg, hipStream_t st, float* out2 = nullptr,
+                  int ld2 = 0);
 // engine launch probe: probe_enabled / probe_start / probe_stop (pcs_common.hpp, probe.cpp)
 // weight gradient with deterministic partials: workspace bytes for (N, K, M), and the launch
 size_t wgrad_ws_bytes(int N, int K, int M);

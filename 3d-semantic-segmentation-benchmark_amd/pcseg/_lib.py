@@ -91,6 +91,7 @@ SIGNATURES = {
                                   ctypes.c_size_t, P],
     'pcs_wgrad_lane': [P],
     'pcs_wgrad_lane_join': [P],
+    'pcs_geometry_stream': [P],
     'pcs_operand_size': [],
     'pcs_mlp_layer_size': [],
     'pcs_gemm_rows': [OPP, I32, I32, P, I32, P, P, I32, I32, P, OPP, P, P],
@@ -117,7 +118,7 @@ SIGNATURES = {
     # fused EdgeConv
     'pcs_edgeconv_workspace': [I32, I32, I32, I32, I32, P],
     'pcs_edgeconv_fwd': [P, I32, I32, P, I32, I32, I32, P, I32, P, P, P, P, P, F32, F32, F32,
-                         P, P, P, P, P, P, P, P, P, ctypes.c_size_t, P],
+                         P, P, P, P, P, P, P, P, P, I32, P, ctypes.c_size_t, P],
     'pcs_edgeconv_bwd': [P, I32, I32, P, P, I32, I32, I32, P, I32, P, P, P, P, P, P, F32,
                          P, P, I32, P, P, P, P, ctypes.c_size_t, P],
     # inverse neighbour maps

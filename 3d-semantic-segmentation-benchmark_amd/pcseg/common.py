@@ -109,12 +109,19 @@ def _event_set(dev, side, L):
 
 
 def side_stream(device) -> torch.cuda.Stream:
-    """One long-lived side stream per device for the neighbour-search work."""
+    """One long-lived side stream per device for the neighbour-search work: the library's
+    geometry stream (pcs_geometry_stream), at the lowest priority -- a prefetched plan's
+    ball-query blocks hold whole compute units for their lifetime and must not be dispatched
+    ahead of the step stream's kernels."""
+    import ctypes
     dev = torch.device(device)
     key = dev.index if dev.index is not None else torch.cuda.current_device()
     st = _side_streams.get(key)
     if st is None:
-        st = torch.cuda.Stream(device=dev)
+        out = ctypes.c_void_p(0)
+        with torch.cuda.device(key):
+            call('pcs_geometry_stream', ctypes.byref(out))
+        st = torch.cuda.ExternalStream(out.value, device=torch.device('cuda', key))
         _side_streams[key] = st
     return st
 

@@ -532,7 +532,7 @@ class EdgeConvFn(torch.autograd.Function):
     (csrc/edgeconv.hip); the backward gathers over the CSR inverse of idx."""
 
     @staticmethod
-    def forward(ctx, X, idx, C, slope, bn, W, gamma, beta, inverse_side=True, holder=None):
+    def forward(ctx, X, idx, C, slope, bn, W, gamma, beta, inverse_side=True, holder=None, also=None):
         dev = X.device
         st = stream_ptr(dev)
         B, N, k = idx.shape
@@ -554,7 +554,9 @@ class EdgeConvFn(torch.autograd.Function):
         call('pcs_edgeconv_fwd', ptr(X), ldx, C, ptr(idx), B, N, k, ptr(Wm), Cout, ptr(gamma), ptr(beta),
              ptr(bn.running_mean) if track else None, ptr(bn.running_var) if track else None,
              ptr(bn.num_batches_tracked) if track else None, float(momentum), float(bn.eps), float(slope),
-             ptr(Y), ptr(PQ), ptr(S), ptr(pz), ptr(pa), ptr(coef), ptr(out), ptr(arg), ptr(ws), ws.numel(), st)
+             ptr(Y), ptr(PQ), ptr(S), ptr(pz), ptr(pa), ptr(coef), ptr(out), ptr(arg),
+             ptr(also[0]) if also is not None else None, also[0].stride(0) if also is not None else 0,
+             ptr(ws), ws.numel(), st)
         record_pool_arg(arg)
         if recording():
             record_act_mask(out > 0)          # LeakyReLU keeps the sign: out > 0 <=> y > 0 at the argmax
@@ -612,7 +614,7 @@ class EdgeConvFn(torch.autograd.Function):
              ptr(pz), ptr(arg), ptr(coef), slope, ptr(gout), ptr(dX), ldx, ptr(dW), ptr(dg), ptr(db), ptr(ws),
              ws.numel(), st)
         notify_grad_ready((W, gamma, beta))
-        return dX, None, None, None, None, None, None, None, None, None
+        return dX, None, None, None, None, None, None, None, None, None, None
 
 
 def edgeconv_fused_ok(conv, bn, cin: int) -> bool:
@@ -622,15 +624,24 @@ def edgeconv_fused_ok(conv, bn, cin: int) -> bool:
 
 
 def edgeconv(x_rows: torch.Tensor, cin: int, idx: torch.Tensor, conv, bn, slope: float,
-             inverse_side: bool = True, holder: list | None = None) -> torch.Tensor:
+             inverse_side: bool = True, holder: list | None = None, also: torch.Tensor | None = None) -> torch.Tensor:
     """x_rows (B*N, ld) point rows, idx (B, N, k) int32 -> pooled (B*N, Cout).  inverse_side: build
-    the backward's inverse map of idx on the side stream during the forward (else in the backward)."""
+    the backward's inverse map of idx on the side stream during the forward (else in the backward).
+    also: an (B*N, Cout) row block (e.g. a storage_alias column block of a concatenation buffer)
+    that receives a second copy of the pooled rows, written by the same kernel -- not an autograd
+    output: the caller connects it (models._CopyColumns with the part marked as written)."""
     if not x_rows.is_cuda:
         raise RuntimeError('pcseg ops run only on the GPU (no CPU fallback); got a CPU tensor')
     if x_rows.shape[1] % 4 or not x_rows.is_contiguous():
         x_rows = pad_rows(x_rows[:, :cin])
+    if also is not None:
+        Cout = conv.weight.shape[0]
+        if (also.dim() != 2 or tuple(also.shape) != (x_rows.shape[0], Cout) or also.stride(1) != 1
+                or also.stride(0) % 4 or also.data_ptr() % 16 or also.device != x_rows.device):
+            raise ValueError(f'edgeconv: `also` must be a 16-B aligned ({x_rows.shape[0]}, {Cout}) row block '
+                             f'with unit column stride, got {tuple(also.shape)} strides {also.stride()}')
     return EdgeConvFn.apply(x_rows, idx.contiguous(), cin, slope, bn, conv.weight, bn.weight, bn.bias, inverse_side,
-                            holder)
+                            holder, (also,) if also is not None else None)
 
 
 class EdgeInverseBatch:

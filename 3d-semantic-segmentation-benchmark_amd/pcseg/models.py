@@ -258,10 +258,13 @@ class EdgeConv(nn.Module):
         """xp point-major (B, N, C) -> (B, N, Cout)."""
         return self.forward_graph(xp)[0]
 
-    def forward_graph(self, xp: torch.Tensor, seeds: torch.Tensor | None = None, inv_batch=None):
+    def forward_graph(self, xp: torch.Tensor, seeds: torch.Tensor | None = None, inv_batch=None,
+                      also: torch.Tensor | None = None):
         """(output (B, N, Cout), this layer's kNN graph (B, N, k) int32).  seeds: the previous
         EdgeConv's graph -- its neighbours' distances in this layer's feature space bound the
-        search threshold from the start (same graph, less merge work)."""
+        search threshold from the start (same graph, less merge work).  also: a (B*N, Cout) row
+        block that receives a copy of the output (the fused kernel writes both; DGCNN's head
+        concatenation), not connected to autograd here."""
         B, N, _ = xp.shape
         rp = _replay()
         if rp is not None and rp.knn_idx:
@@ -274,11 +277,14 @@ class EdgeConv(nn.Module):
         if edgeconv_fused_ok(self.conv[0], self.conv[1], C):
             holder = inv_batch.holder() if (inv_batch is not None and self.edge_inverse == 'deferred') else None
             pooled = edgeconv(xp.reshape(B * N, C), C, idx, self.conv[0], self.conv[1], self.conv[2].negative_slope,
-                              inverse_side=self.edge_inverse == 'side', holder=holder)
+                              inverse_side=self.edge_inverse == 'side', holder=holder, also=also)
             return pooled.view(B, N, -1), idx
         rows = ops.edge_rows(xp, idx)
         pooled = shared_mlp(rows, 2 * C, [self.conv[0]], [self.conv[1]], 'lrelu',
                             self.conv[2].negative_slope, pool_k=self.k)
+        if also is not None:
+            with torch.no_grad():
+                also.copy_(pooled)
         return pooled.view(B, N, -1), idx
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
@@ -286,15 +292,21 @@ class EdgeConv(nn.Module):
 
 
 class _CopyColumns(torch.autograd.Function):
-    """parts (B, N, C_i) copied side by side into the (B*N, sum C_i) row block dest[0]
-    (torch.cat(parts, dim=-1) of dgcnn.py:200 / :245, written into a wider buffer)."""
+    """parts (B, N, C_i) side by side in the (B*N, sum C_i) row block dest[0] (torch.cat(parts,
+    dim=-1) of dgcnn.py:200 / :245, into a wider buffer): copied here unless dest[1] marks the
+    part as already written there by its producer (the EdgeConv kernel's second output, the colour
+    branch's GEMM epilogue).  Backward: each part gets its column slice of the gradient."""
 
     @staticmethod
     def forward(ctx, dest, *parts):
         out = dest[0]
+        written = dest[1] if len(dest) > 1 else (False,) * len(parts)
         off = 0
-        for p in parts:
+        for p, done in zip(parts, written):
             c = p.shape[-1]
+            if done:
+                off += c
+                continue
             src = p.reshape(-1, c)
             blk = out[:, off:off + c]
             if (src.stride(1) == 1 and src.stride(0) % 4 == 0 and c % 4 == 0 and out.stride(0) % 4 == 0
@@ -344,15 +356,30 @@ class _ColumnConcat(torch.autograd.Function):
         return tuple(grads)
 
 
-def _dgcnn_head(self, parts: list[torch.Tensor], B: int, N: int):
-    # conv6 reads cat((x1..x4 [, colour], x5), 1) (dgcnn.py:203-206 / :248-251): one (B*N, 1408)
-    # buffer holds it -- the EdgeConv outputs are copied into its first columns, conv5 writes its
-    # activation straight into the rest, and the concatenation is an alias (no 0.7 GB copy)
+def _head_buffer(self, M: int, widths: list[int], dev):
+    """conv6 reads cat((x1..x4 [, colour], x5), 1) (dgcnn.py:203-206 / :248-251): one (B*N,
+    cxr + emb) buffer H holds it.  The EdgeConv kernels write their outputs into its first
+    columns as a second copy (their dense outputs feed the next kNN / EdgeConv), the colour
+    branch and conv5 write their activations straight into their blocks, and the concatenation
+    is an alias: no copy kernel and no 0.7 GB cat.  -> (H, the parts' column blocks)."""
+    emb = self.conv5[0].weight.shape[0]
+    H = torch.empty((M, sum(widths) + emb), dtype=torch.float32, device=dev)
+    blocks, off = [], 0
+    for w in widths:
+        blocks.append(storage_alias(H, off, w))
+        off += w
+    return H, blocks
+
+
+def _dgcnn_head(self, parts: list[torch.Tensor], B: int, N: int, H: torch.Tensor | None = None):
+    # H: _head_buffer's, the parts already written into its first columns (else copied here)
     M = B * N
     cxr = sum(p.shape[-1] for p in parts)
     emb = self.conv5[0].weight.shape[0]
-    H = torch.empty((M, cxr + emb), dtype=torch.float32, device=parts[0].device)
-    xr = _CopyColumns.apply((storage_alias(H, 0, cxr),), *parts)          # (B*N, 320|384), row stride 1344|1408
+    written = H is not None
+    if H is None:
+        H = torch.empty((M, cxr + emb), dtype=torch.float32, device=parts[0].device)
+    xr = _CopyColumns.apply((storage_alias(H, 0, cxr), (written,) * len(parts)), *parts)  # (B*N, 320|384), stride 1344|1408
     x5 = _seq_rows(xr, self.conv5, out=storage_alias(H, cxr, emb))        # (B*N, emb)
     x6 = _seq_rows(_ColumnConcat.apply(xr, x5), self.conv6)
     x7 = _seq_rows(x6, self.conv7)
@@ -389,12 +416,14 @@ class DGCNN(nn.Module):
         xyz = x[:, :3, :] if x.size(1) == 6 else x
         xp = xyz.transpose(1, 2).contiguous()
         ib = EdgeInverseBatch()
-        x1, g = self.conv1.forward_graph(xp, None, inv_batch=ib)
-        x2, g = self.conv2.forward_graph(x1, g, inv_batch=ib)
-        x3, g = self.conv3.forward_graph(x2, g, inv_batch=ib)
-        x4, _ = self.conv4.forward_graph(x3, g, inv_batch=ib)
+        convs = (self.conv1, self.conv2, self.conv3, self.conv4)
+        H, blk = _head_buffer(self, B * N, [c.conv[0].weight.shape[0] for c in convs], xp.device)
+        x1, g = self.conv1.forward_graph(xp, None, inv_batch=ib, also=blk[0])
+        x2, g = self.conv2.forward_graph(x1, g, inv_batch=ib, also=blk[1])
+        x3, g = self.conv3.forward_graph(x2, g, inv_batch=ib, also=blk[2])
+        x4, _ = self.conv4.forward_graph(x3, g, inv_batch=ib, also=blk[3])
         ib.flush()
-        return _dgcnn_head(self, [x1, x2, x3, x4], B, N)
+        return _dgcnn_head(self, [x1, x2, x3, x4], B, N, H)
 
 
 class DGCNNWithColor(nn.Module):
@@ -424,13 +453,17 @@ class DGCNNWithColor(nn.Module):
         xyz = xp[:, :, :3].contiguous()
         rgb = xp[:, :, 3:6].contiguous()
         ib = EdgeInverseBatch()
-        x1, g = self.conv1.forward_graph(xyz, None, inv_batch=ib)
-        x2, g = self.conv2.forward_graph(x1, g, inv_batch=ib)
-        x3, g = self.conv3.forward_graph(x2, g, inv_batch=ib)
-        x4, _ = self.conv4.forward_graph(x3, g, inv_batch=ib)
+        convs = (self.conv1, self.conv2, self.conv3, self.conv4)
+        H, blk = _head_buffer(self, B * N, [c.conv[0].weight.shape[0] for c in convs] +
+                              [self.color_conv[0].weight.shape[0]], xp.device)
+        x1, g = self.conv1.forward_graph(xyz, None, inv_batch=ib, also=blk[0])
+        x2, g = self.conv2.forward_graph(x1, g, inv_batch=ib, also=blk[1])
+        x3, g = self.conv3.forward_graph(x2, g, inv_batch=ib, also=blk[2])
+        x4, _ = self.conv4.forward_graph(x3, g, inv_batch=ib, also=blk[3])
         ib.flush()
-        color = _seq_rows(pad_rows(rgb.view(B * N, 3)), self.color_conv, 3).view(B, N, -1)
-        return _dgcnn_head(self, [x1, x2, x3, x4, color], B, N)
+        # the colour branch's activation lands in its block directly (the head's only reader)
+        color = _seq_rows(pad_rows(rgb.view(B * N, 3)), self.color_conv, 3, out=blk[4])
+        return _dgcnn_head(self, [x1, x2, x3, x4, color], B, N, H)
 
 
 def get_model(num_classes=13, use_color=True, **kwargs):

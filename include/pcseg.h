@@ -344,6 +344,10 @@ int pcs_mlp_backward_deferred(const float* X, int ldx, int kin, int M,
 int pcs_wgrad_lane(void** side_stream);
 /* `stream` waits for every weight gradient enqueued on the current device's lane so far */
 int pcs_wgrad_lane_join(void* stream);
+/* the current device's geometry stream (FPS, ball queries, 3-NN, inverse maps of a forward,
+ * often the NEXT step's): created once per device at the lowest stream priority, so its long
+ * neighbour-search blocks yield the compute units to the step stream's kernels */
+int pcs_geometry_stream(void** stream);
 
 /* ---- harness-B batch (Training/train_model.py:89-171, preprocess_batch_to_train_format)
  * sample i's rows are packed at [offsets[i], offsets[i] + lengths[i]) of points (rows x D)
@@ -383,14 +387,17 @@ int pcs_edgeconv_workspace(int B, int N, int C, int Cout, int backward, size_t* 
  * (B*N x Cout: the pooled edge's z -- the max over k where gamma > 0, the min where
  * gamma < 0, edge 0 where gamma == 0 -- and its first slot), coef (s, t, mean,
  * invstd; 4 x Cout), pooled activation out (B*N x Cout) + argmax slot arg (u8);
- * running stats / num_batches updated in place. */
+ * out2 (nullable, row stride ld2 >= Cout, 16-B aligned rows for the vector path): a
+ * second copy of `out` -- DGCNN's EdgeConv outputs written straight into their column
+ * block of the head's concatenation (dgcnn.py:200); running stats / num_batches
+ * updated in place. */
 int pcs_edgeconv_fwd(const float* X, int ldx, int C, const int32_t* idx, int B, int N,
                      int k, const float* W, int Cout, const float* gamma,
                      const float* beta, float* run_mean, float* run_var,
                      long long* num_batches, float momentum, float eps, float slope,
                      float* Y, float* PQ, float* S, float* pz, uint8_t* pa,
-                     float* coef, float* out, uint8_t* arg, void* workspace,
-                     size_t ws_bytes, void* stream);
+                     float* coef, float* out, uint8_t* arg, float* out2, int ld2,
+                     void* workspace, size_t ws_bytes, void* stream);
 /* backward from the forward's saved tensors and the CSR inverse of idx
  * (pcs_inverse_index, targets = N): dW (Cout x 2C), dgamma, dbeta accumulate (+=);
  * dX (nullable; C % 4 == 0) is written.  dout: gradient of `out`. */

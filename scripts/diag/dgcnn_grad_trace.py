@@ -48,8 +48,8 @@ prod_out = []
 orig_fg = PM.EdgeConv.forward_graph
 
 
-def fg(self, xp, seeds=None):
-    o, idx = orig_fg(self, xp, seeds)
+def fg(self, xp, seeds=None, **kw):
+    o, idx = orig_fg(self, xp, seeds, **kw)
     o.retain_grad()
     prod_out.append(o)
     return o, idx
