@@ -110,7 +110,7 @@ static size_t max_partials(int M, int kin, const pcs_mlp_layer* L, int nl, int p
         if (backward) m = std::max(m, 2 * c * (size_t)pcs_gemm_row_blocks_dgrad(M, (int)c));
         // a fused inner layer writes its input's BN-backward partials, one per fused block
         if (backward && l > 0)
-            m = std::max(m, 2 * (size_t)L[l].cin * (size_t)fused_bwd_grid(M, (int)L[l].cout, (int)L[l].cin, true));
+            m = std::max(m, 2 * (size_t)L[l].cin * (size_t)fused_bwd_grid(M, (int)L[l].cout, (int)L[l].cin, true, -1));
     }
     if (backward) {
         const size_t c = (size_t)L[nl - 1].cout;
@@ -536,7 +536,7 @@ static int mlp_backward(const float* X, int ldx, int kin, int M, const pcs_mlp_l
             float* dA = S.dA[da];
             int nbg;
             if (fused) {
-                nbg = fused_bwd_grid(M, C, Cin, true);
+                nbg = fused_bwd_grid(M, C, Cin, true, xop.mode);
                 if (int e = fused_bwd(&xop, C, &qop, Cin, P.W, (int)P.ldw, M, dA, Cin, S.part, P.dW, P.db, S.fw,
                                       S.fw_bytes, st))
                     return fail(e);

@@ -57,21 +57,34 @@ __device__ __forceinline__ int acc_row_of(int r, int h) { return (r & 3) + 8 * (
 // WIDE: the wide layers (C + CI > 96) at ONE block per CU (one wave per SIMD, up to 512 VGPRs):
 // the next tile's raw loads are then held in registers under the current tile's MFMAs as on
 // the narrow layers, instead of being staged in chunks after the barrier.
+#ifndef PCS_AB_FB_SPLIT
+#define PCS_AB_FB_SPLIT 1                    // (A/B builds only: 0 = round 4's dW share on every wave)
+#endif
+#ifndef PCS_AB_FB_WLDS
+#define PCS_AB_FB_WLDS 0                     // (A/B builds only: 1 = W's fragments read from LDS, 3 blocks per CU)
+#endif
 template <int C, int CI, int XM, bool DA, bool WIDE = false>
-__global__ __launch_bounds__(256, WIDE ? 1 : 2) void fused_bwd_kernel(FusedBwdArgs f) {
+__global__ __launch_bounds__(256, WIDE ? 1 : (PCS_AB_FB_WLDS ? 3 : 2)) void fused_bwd_kernel(FusedBwdArgs f) {
     constexpr int BM = FB_BM;
     constexpr int ZS = C + 2;                  // row stride = 2 (mod 64) banks: the dA fragment reads
                                                // (32 rows x 2 k) hit 64 distinct banks
     constexpr int XS = CI + 4;                 // float4-aligned rows (row reads only)
     constexpr int NIT = CI / 32, NCT = C / 32;
     constexpr int TW = NCT * NIT;              // 32 x 32 tiles of dW
-    constexpr int WPT = TW >= 4 ? TW / 4 : 1;  // dW tiles per wave
-    constexpr int WR = TW >= 4 ? 1 : 4 / TW;   // waves splitting one dW tile's rows
+    // SPLIT (CI = 32 with a data gradient): the dA strip has only two 32-row tiles, so waves 0, 1
+    // take dA and waves 2, 3 take every dW tile -- C / 2 MFMAs per wave on every SIMD (round 4 gave
+    // all four waves a share of dW, so waves 0, 1 carried dA + dW: 1.5x the MFMA time per tile on
+    // two SIMDs while the other two idled)
+    constexpr bool SPLIT = DA && NIT == 1 && PCS_AB_FB_SPLIT;
+    constexpr int DWW = SPLIT ? 2 : 4;         // waves sharing the dW tiles
+    constexpr int WPT = TW >= DWW ? TW / DWW : 1;  // dW tiles per wave
+    constexpr int WR = TW >= DWW ? 1 : DWW / TW;   // waves splitting one dW tile's rows
     constexpr int NRT = NIT == 4 ? 2 : 1;      // dA row tiles per wave
     static_assert(C % 32 == 0 && CI % 32 == 0 && C <= 128 && CI <= 128, "fused backward widths");
     __shared__ __attribute__((aligned(16))) float Zs[BM * ZS];
     __shared__ __attribute__((aligned(16))) float Xs[BM * XS];
     __shared__ double red[2][4][32];
+    __shared__ float Ws[PCS_AB_FB_WLDS && DA ? C * CI : 1];
     __shared__ float wred[WR > 1 ? (WR - 1) * TW * 1024 : 1];   // per (row subset, tile)
 
     const int tid = threadIdx.x, lane = tid & 63;
@@ -83,22 +96,26 @@ __global__ __launch_bounds__(256, WIDE ? 1 : 2) void fused_bwd_kernel(FusedBwdAr
     const int a_rt0 = NIT == 4 ? 0 : (NIT == 2 ? (w >> 1) : (w & 1));
     const bool a_on = DA && (NIT >= 2 || w < 2);
     const int a_col = a_ct * 32 + l32;
-    float wf[DA ? C / 2 : 1];                  // wf[j] = W[2j + h][a_col]: B fragments of every k step
+    float wf[DA && !PCS_AB_FB_WLDS ? C / 2 : 1];   // wf[j] = W[2j + h][a_col]: B fragments of every k step
     float es = 0.f, et = 0.f, em = 0.f, ei = 0.f;
     if constexpr (DA) {
 #pragma unroll
-        for (int j = 0; j < C / 2; ++j) wf[j] = f.W[(size_t)(2 * j + h) * f.ldw + a_col];
+        for (int j = 0; j < (PCS_AB_FB_WLDS ? 0 : C / 2); ++j) wf[j] = f.W[(size_t)(2 * j + h) * f.ldw + a_col];
+        if (PCS_AB_FB_WLDS)
+            for (int e = tid; e < C * CI; e += 256) Ws[e] = f.W[(size_t)(e / CI) * f.ldw + e % CI];
         // previous layer's BN at this lane's dA column (BN-backward epilogue)
         es = f.q.s[a_col]; et = f.q.t[a_col]; em = f.q.mean[a_col]; ei = f.q.inv[a_col];
     }
     const float qslope = DA ? f.q.slope : 1.f;
 
-    // ---- weight-gradient assignment: tiles t = ct_c * NIT + ct_i.  TW >= 4: wave w takes
-    // t = w + 4u (all share ct_i = w % NIT); TW < 4: wave w takes t = w % TW over the row
-    // pairs p = w / TW (mod WR)
-    const int t_base = TW >= 4 ? w : (w % TW);
+    // ---- weight-gradient assignment over the DWW dW waves (index wd): tiles t = ct_c * NIT + ct_i.
+    // TW >= DWW: wave wd takes t = wd + DWW u (all share ct_i = wd % NIT); TW < DWW: wave wd takes
+    // t = wd % TW over the row pairs p = wd / TW (mod WR).  wsub < 0: no dW on this wave (SPLIT)
+    const bool dw_on = !SPLIT || w >= 2;
+    const int wd = SPLIT ? (w >= 2 ? w - 2 : 0) : w;
+    const int t_base = TW >= DWW ? wd : (wd % TW);
     const int w_i = t_base % NIT;
-    const int wsub = TW >= 4 ? 0 : w / TW;
+    const int wsub = !dw_on ? -1 : (TW >= DWW ? 0 : wd / TW);
     const int b_col = w_i * 32 + l32;
     const float bs = DA ? f.q.s[b_col] : 1.f, bt = DA ? f.q.t[b_col] : 0.f;   // !DA: identity
 
@@ -210,7 +227,8 @@ __global__ __launch_bounds__(256, WIDE ? 1 : 2) void fused_bwd_kernel(FusedBwdAr
                 if (j + PD < C / 2) afrag(j + PD, j % PD);
 #pragma unroll
                 for (int rt = 0; rt < NRT; ++rt)
-                    accA[rt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[rt], wf[j], accA[rt], 0, 0, 0);
+                    accA[rt] = __builtin_amdgcn_mfma_f32_32x32x2f32(
+                        a[rt], PCS_AB_FB_WLDS ? Ws[(2 * j + h) * CI + a_col] : wf[PCS_AB_FB_WLDS ? 0 : j], accA[rt], 0, 0, 0);
             }
 #pragma unroll
             for (int rt = 0; rt < NRT; ++rt) {
@@ -236,14 +254,14 @@ __global__ __launch_bounds__(256, WIDE ? 1 : 2) void fused_bwd_kernel(FusedBwdAr
         }
         // ---- dW += Zs^T . act(Xs*s + t): the fragments of row pair pq + 1 are read while row pair
         // pq's MFMAs run (two register slots), so no MFMA waits on its own LDS reads
-        {
+        if (dw_on) {
             constexpr int NP = BM / 2 / WR;
             float xr[2], za[2][WPT];
             auto frag = [&](int pq, int sl) __attribute__((always_inline)) {
                 const int r = 2 * (pq * WR + wsub) + h;
                 xr[sl] = Xs[r * XS + b_col];
 #pragma unroll
-                for (int u = 0; u < WPT; ++u) za[sl][u] = Zs[r * ZS + ((t_base + 4 * u) / NIT) * 32 + l32];
+                for (int u = 0; u < WPT; ++u) za[sl][u] = Zs[r * ZS + ((t_base + DWW * u) / NIT) * 32 + l32];
             };
             frag(0, 0);
 #pragma unroll
@@ -306,7 +324,7 @@ __global__ __launch_bounds__(256, WIDE ? 1 : 2) void fused_bwd_kernel(FusedBwdAr
     if (wsub == 0) {
 #pragma unroll
         for (int u = 0; u < WPT; ++u) {
-            const int tt = t_base + 4 * u;
+            const int tt = t_base + DWW * u;
             const int c0 = (tt / NIT) * 32, i0 = (tt % NIT) * 32;
 #pragma unroll
             for (int r = 0; r < 16; ++r)
@@ -381,27 +399,37 @@ static const void* fb_kernel(int C, int CI, int xm, bool da) {
 }
 
 // persistent grid: as many blocks per CU as are resident at once (the occupancy query: VGPRs and
-// LDS of the instance; the wide layers run one wave per SIMD), the smallest over the operand
-// modes, so the grid -- and the number of BN-backward partials -- depends on (C, CI, da) only
-int fused_bwd_grid(int M, int C, int CI, bool da) {
-    static int occ[3][3][2];                   // [C][CI][da], 0 = not queried
+// LDS of the instance; the wide layers run one wave per SIMD).  xm = the operand mode of the launch;
+// xm < 0 (workspace sizing): the largest grid over the modes.  The grid is the number of
+// BN-backward partials, which the caller's finalize reads (engine.hip passes the launch's mode).
+// (Round 4 used the smallest grid over the modes for every launch: SA1's middle layer, BNBWD at
+// 164 VGPRs, ran 2 blocks per CU where 3 are resident.)
+#ifndef PCS_AB_FB_MODE_GRID
+#define PCS_AB_FB_MODE_GRID 1                // (A/B builds only: 0 = round 4's smallest grid over the modes)
+#endif
+int fused_bwd_grid(int M, int C, int CI, bool da, int xm) {
+    static int occ[3][3][2][3];                // [C][CI][da][mode], 0 = not queried
     const int ci = C == 32 ? 0 : (C == 64 ? 1 : 2), ii = CI == 32 ? 0 : (CI == 64 ? 1 : 2);
-    int& per_cu = occ[ci][ii][da ? 1 : 0];
-    if (per_cu == 0) {
-        int m = 4;
-        for (int xm : {(int)OP_PLAIN, (int)OP_BNBWD, (int)OP_POOLBWD}) {
-            int n = 0;
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fb_kernel(C, CI, xm, da), 256, 0) != hipSuccess) n = 1;
-            m = std::min(m, std::max(n, 1));
+    const int modes[3] = {(int)OP_PLAIN, (int)OP_BNBWD, (int)OP_POOLBWD};
+    int lo = 4, hi = 1, mine = 0;
+    for (int k = 0; k < 3; ++k) {
+        int& n = occ[ci][ii][da ? 1 : 0][k];
+        if (n == 0) {
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fb_kernel(C, CI, modes[k], da), 256, 0) != hipSuccess)
+                n = 1;
+            n = std::min(std::max(n, 1), 4);
         }
-        per_cu = m;
+        lo = std::min(lo, n);
+        hi = std::max(hi, n);
+        if (modes[k] == xm) mine = n;
     }
+    const int per_cu = !PCS_AB_FB_MODE_GRID ? lo : (xm < 0 || mine == 0 ? hi : mine);
     const int tiles = (M + FB_BM - 1) / FB_BM;
     return std::min(tiles, 256 * per_cu);
 }
 
 size_t fused_bwd_ws_bytes(int M, int C, int CI) {
-    return (size_t)fused_bwd_grid(M, C, CI, true) * ((size_t)C * CI + C) * sizeof(float) + 256;
+    return (size_t)fused_bwd_grid(M, C, CI, true, -1) * ((size_t)C * CI + C) * sizeof(float) + 256;
 }
 
 int fused_bwd(const pcs_operand* x, int C, const pcs_operand* q, int CI, const float* W, int ldw, int M, float* dA,
@@ -409,7 +437,7 @@ int fused_bwd(const pcs_operand* x, int C, const pcs_operand* q, int CI, const f
     PCS_CHECK_ARG(fused_bwd_ok(M, C, CI, ldw, x, q), "fused_bwd: unsupported shape C=%d CI=%d M=%d", C, CI, M);
     PCS_CHECK_ARG(dA && ldd >= CI && ldd % 4 == 0 && bstats && dW && W, "fused_bwd: bad output arguments");
     PCS_CHECK_ARG(ws && ws_bytes >= fused_bwd_ws_bytes(M, C, CI), "fused_bwd: workspace too small");
-    const int G = fused_bwd_grid(M, C, CI, true);
+    const int G = fused_bwd_grid(M, C, CI, true, x->mode);
     float* part = reinterpret_cast<float*>((reinterpret_cast<uintptr_t>(ws) + 255) & ~uintptr_t(255));
     float* pdb = db ? part + (size_t)G * C * CI : nullptr;
     FusedBwdArgs a{to_dev_operand(x, M, C), to_dev_operand(q, M, CI), W, ldw, M, dA, ldd, bstats, part, pdb, CI, CI};
@@ -441,14 +469,14 @@ bool fused_wgrad_ok(int M, int C, int kin, int ldx, const pcs_operand* x) {
 }
 
 size_t fused_wgrad_ws_bytes(int M, int C, int kin) {
-    return (size_t)fused_bwd_grid(M, C, 32, false) * ((size_t)C * kin + C) * sizeof(float) + 256;
+    return (size_t)fused_bwd_grid(M, C, 32, false, -1) * ((size_t)C * kin + C) * sizeof(float) + 256;
 }
 
 int fused_wgrad(const pcs_operand* x, int C, const float* X, int ldx, int kin, int M, float* dW, float* db, void* ws,
                 size_t ws_bytes, hipStream_t st) {
     PCS_CHECK_ARG(fused_wgrad_ok(M, C, kin, ldx, x) && X && dW, "fused_wgrad: unsupported C=%d kin=%d M=%d", C, kin, M);
     PCS_CHECK_ARG(ws && ws_bytes >= fused_wgrad_ws_bytes(M, C, kin), "fused_wgrad: workspace too small");
-    const int G = fused_bwd_grid(M, C, 32, false);
+    const int G = fused_bwd_grid(M, C, 32, false, x->mode);
     float* part = reinterpret_cast<float*>((reinterpret_cast<uintptr_t>(ws) + 255) & ~uintptr_t(255));
     float* pdb = db ? part + (size_t)G * C * kin : nullptr;
     Operand q{};

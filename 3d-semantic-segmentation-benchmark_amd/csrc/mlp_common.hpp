@@ -257,7 +257,7 @@ int bn_act_dropout(const float* Z, int ldz, int M, int N, const float* s, const 
 // rows), PCS_BWD_FUSE_OFF, PCS_BWD_FUSE_ALL (every eligible layer)
 bool fused_bwd_wanted(int policy, int M);
 bool fused_bwd_ok(int M, int C, int CI, int ldw, const pcs_operand* x, const pcs_operand* q);
-int fused_bwd_grid(int M, int C, int CI, bool da);   // blocks = BN-backward partials
+int fused_bwd_grid(int M, int C, int CI, bool da, int xm);   // blocks = BN-backward partials (xm < 0: max)
 size_t fused_bwd_ws_bytes(int M, int C, int CI);
 int fused_bwd(const pcs_operand* x, int C, const pcs_operand* q, int CI, const float* W, int ldw, int M, float* dA,
               int ldd, double* bstats, float* dW, float* db, void* ws, size_t ws_bytes, hipStream_t st);

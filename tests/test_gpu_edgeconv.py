@@ -185,3 +185,61 @@ def test_edgeconv_weight_at_storage_end_in_nan_storage(C, Cout, tail):
         assert rel(xd.grad, xr.grad) < TOL
     # the NaN storage around the weight is untouched (nothing wrote outside the view either)
     assert torch.isnan(store[:256]).all() and torch.isnan(store[256 + n:]).all()
+
+
+@pytest.mark.parametrize('C,Cout,ld,col0', [(64, 64, 1408, 0), (64, 128, 1408, 192), (3, 64, 388, 4)])
+def test_edgeconv_second_output_into_row_block(C, Cout, ld, col0):
+    """`also` (round 5, pcs_edgeconv_fwd's out2): the pooled rows land bit for bit in a column
+    block of a wider buffer too, nothing else of that buffer is touched, and the dense output and
+    every gradient are bitwise those of the call without it."""
+    from pcseg.engine import storage_alias
+    B, N, k = 2, 512, 20
+    x, idx, _, prod = _case(C, Cout, B=B, N=N, k=k, seed=7)
+    prod = prod.to(DEV).train()
+    twin = copy.deepcopy(prod)
+    xp = x.transpose(1, 2).contiguous().to(DEV)
+    gi = idx.to(DEV, torch.int32)
+    H = torch.full((B * N, ld), float('nan'), device=DEV)
+    blk = storage_alias(H, col0, Cout)
+    outs, grads = [], []
+    for m, also in ((prod, blk), (twin, None)):
+        xr = xp.reshape(B * N, C).clone().requires_grad_(True)
+        out = edgeconv(xr, C, gi, m.conv[0], m.conv[1], m.conv[2].negative_slope, also=also)
+        (out * torch.linspace(-1, 1, out.numel(), device=DEV).view_as(out)).sum().backward()
+        outs.append(out.detach())
+        grads.append([xr.grad] + [p.grad for p in m.parameters()])
+    torch.cuda.synchronize()
+    assert torch.equal(blk, outs[0])
+    assert torch.equal(outs[0], outs[1])
+    for a, b in zip(grads[0], grads[1]):
+        assert torch.equal(a, b)
+    rest = torch.cat([H[:, :col0], H[:, col0 + Cout:]], dim=1)
+    assert torch.isnan(rest).all()
+
+
+def test_dgcnn_head_buffer_equals_copied_concatenation():
+    """DGCNN-colour with its parts written into the head buffer by their producers (round 5) against
+    the same model taking the copy path (_dgcnn_head(H=None)): logits, x5 and every gradient bitwise."""
+    import pcseg.models as PM
+    torch.manual_seed(3)
+    m1 = pcseg.DGCNNWithColor(13).to(DEV).train()
+    m2 = copy.deepcopy(m1)
+    x = torch.randn(2, 6, 1024, device=DEV)
+    res = []
+    fg, head = PM.EdgeConv.forward_graph, PM._dgcnn_head
+    for m, old in ((m1, False), (m2, True)):
+        if old:
+            PM.EdgeConv.forward_graph = lambda self, xp, seeds=None, inv_batch=None, also=None: fg(
+                self, xp, seeds, inv_batch=inv_batch)
+            PM._dgcnn_head = lambda self, parts, B, N, H=None: head(self, parts, B, N, None)
+        try:
+            torch.manual_seed(11)           # the same dropout draws in both runs
+            logits, x5, _ = m(x)
+            (logits * torch.linspace(-1, 1, logits.numel(), device=DEV).view_as(logits)).sum().backward()
+        finally:
+            PM.EdgeConv.forward_graph, PM._dgcnn_head = fg, head
+        res.append((logits.detach(), x5.detach(), [p.grad for p in m.parameters()]))
+    torch.cuda.synchronize()
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+    for a, b in zip(res[0][2], res[1][2]):
+        assert torch.equal(a, b)
