@@ -124,6 +124,32 @@ PCS_API int pcs_probe_stream(int i, void** stream) {
     return 0;
 }
 
+// record i's start and end in milliseconds after record 0's start (events on any stream of
+// the device: the overlap of launches on different streams, e.g. a data gradient and the wgrad
+// lane's weight gradient running beside it)
+PCS_API int pcs_probe_times(int i, double* t0_ms, double* t1_ms) {
+    hipEvent_t r0, e0, e1;
+    {
+        std::lock_guard<std::mutex> g(g_probe_mu);
+        PCS_CHECK_ARG(i >= 0 && i < (int)g_probe.size() && t0_ms && t1_ms, "pcs_probe_times: index %d of %zu", i,
+                      g_probe.size());
+        r0 = g_probe[0].e0;
+        e0 = g_probe[i].e0;
+        e1 = g_probe[i].e1;
+    }
+    if (hipEventSynchronize(e1) != hipSuccess) return (int)hipErrorUnknown;
+    float a = 0.f, b = 0.f;
+    hipError_t err = hipEventElapsedTime(&a, r0, e0);
+    if (err == hipSuccess) err = hipEventElapsedTime(&b, r0, e1);
+    if (err != hipSuccess) {
+        set_error("pcs_probe_times: %s", hipGetErrorString(err));
+        return (int)err;
+    }
+    *t0_ms = a;
+    *t1_ms = b;
+    return 0;
+}
+
 // Re-issue every recorded launch of kernel `name` back to back, `reps` times (after one
 // untimed pass), between two events on their stream: the average duration of one launch
 // with the queue kept full, the figure rocprofv3 --stats reports as AverageNs for that

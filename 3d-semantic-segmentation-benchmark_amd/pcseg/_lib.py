@@ -83,6 +83,7 @@ SIGNATURES = {
     'pcs_probe_get': [I32, ctypes.c_char_p, I32, P, P, P],
     'pcs_probe_replay': [ctypes.c_char_p, I32, P, P],
     'pcs_probe_stream': [I32, P],
+    'pcs_probe_times': [I32, P, P],
     'pcs_spin': [I32, P],
     'pcs_mlp_workspace': [I32, I32, I32, ctypes.c_char_p, I32, I32, I32, P],
     'pcs_mlp_forward': [P, I32, I32, I32, ctypes.c_char_p, I32, I32, P, I32, P, P, ctypes.c_size_t, P],

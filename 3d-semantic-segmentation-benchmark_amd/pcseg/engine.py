@@ -120,6 +120,20 @@ class KernelProbe:
             out.append(rec)
         return out
 
+    def timeline(self):
+        """[(name, flops, stream handle, start s, end s)] with starts / ends relative to the
+        first record's start (pcs_probe_times; waits for the launches)."""
+        out = []
+        buf = ctypes.create_string_buffer(128)
+        fl, by, ms = ctypes.c_double(), ctypes.c_double(), ctypes.c_float()
+        sp, t0, t1 = ctypes.c_void_p(), ctypes.c_double(), ctypes.c_double()
+        for i in range(self.n):
+            call('pcs_probe_get', i, buf, 128, ctypes.byref(fl), ctypes.byref(by), ctypes.byref(ms))
+            call('pcs_probe_stream', i, ctypes.byref(sp))
+            call('pcs_probe_times', i, ctypes.byref(t0), ctypes.byref(t1))
+            out.append((buf.value.decode(), fl.value, sp.value or 0, t0.value * 1e-3, t1.value * 1e-3))
+        return out
+
     def replay(self, name: str, reps: int = 20) -> float:
         """Average seconds per launch of kernel `name`, its recorded launches re-issued
         back to back (pcs_probe_replay; comparable with rocprofv3's AverageNs)."""

@@ -196,6 +196,34 @@ def _kernel_entry(name, n, fl, by, sec):
             'achieved_hbm_gbs': round(gbs, 1), 'frac_of_hbm_peak': round(gbs / HBM_PEAK_GBS, 4)}
 
 
+def concurrent_mfma(tl, name, main):
+    """The MFMA work done on the whole GPU while the dominant kernel runs: its own flops plus the
+    flops of the side-stream MFMA launches (the wgrad lane's weight gradients of the same layers)
+    pro rata of their overlap with its launches, over its summed launch time.  The in-step
+    data-gradient GEMMs share the CUs with those weight gradients, so their own fraction
+    understates how busy the matrix cores are."""
+    mine = [(t0, t1, fl) for n, fl, sh, t0, t1 in tl if n == name and sh == main]
+    others = [(t0, t1, fl, n) for n, fl, sh, t0, t1 in tl
+              if sh != main and any(k in n for k in ('gemm', 'wgrad', 'fused_bwd', 'knn_wave'))]
+    if not mine:
+        return None
+    busy = sum(t1 - t0 for t0, t1, _ in mine)
+    own = sum(fl for _, _, fl in mine)
+    side, names = 0.0, set()
+    for a0, a1, _ in mine:
+        for b0, b1, fl, n in others:
+            ov = min(a1, b1) - max(a0, b0)
+            if ov > 0 and b1 > b0:
+                side += fl * ov / (b1 - b0)
+                names.add(n)
+    tf = (own + side) / max(busy, 1e-12) / 1e12
+    return {'tflops': round(tf, 2), 'frac_of_fp32_peak': round(tf / FP32_PEAK_TFLOPS, 4),
+            'own_tflops': round(own / max(busy, 1e-12) / 1e12, 2),
+            'side_gflop_overlapped': round(side / 1e9, 3), 'side_kernels': sorted(names),
+            'note': 'dominant kernel flops + side-stream MFMA flops pro rata of overlap, over the dominant '
+                    'kernel\'s summed launch time (probe events)'}
+
+
 def kernel_roofline(step, dev, key, batch, npoints, replay=False):
     """One more training step with every probed HIP launch -- engine GEMMs, FPS, ball query,
     3-NN, kNN, gathers, inverse maps, EdgeConv -- bracketed by HIP events on its own stream
@@ -230,6 +258,7 @@ def kernel_roofline(step, dev, key, batch, npoints, replay=False):
     if side:
         sn, sv = sorted(side.items(), key=lambda kv: -kv[1][3])[0]
         out['largest_side_stream_kernel'] = _kernel_entry(sn, *sv)
+        out['with_concurrent_side_mfma'] = concurrent_mfma(kp.timeline(), name, int(main))
     gemms = [kv for kv in ranked if any(k in kv[0] for k in ('gemm', 'wgrad', 'fused_bwd'))]
     out['top_kernels'] = [{k: v for k, v in _kernel_entry(nm, *vals).items()
                            if k in ('kernel', 'in_step_ms', 'launches_per_step', 'frac', 'unit', 'compute_unit')}

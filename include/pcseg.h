@@ -422,6 +422,8 @@ int pcs_probe_get(int i, char* name, int cap, double* flops, double* bytes,
 /* Record i's stream (the hipStream_t its launch was enqueued on): bench.py separates the
  * launches on the step's own (critical-path) stream from the side streams'. */
 int pcs_probe_stream(int i, void** stream);
+/* record i's start / end in ms after record 0's start (waits for its stop event) */
+int pcs_probe_times(int i, double* t0_ms, double* t1_ms);
 /* After pcs_probe_end: re-issue every recorded launch of kernel `name` back to back
  * `reps` times (after one untimed pass) between two events on their stream; returns
  * the average microseconds per launch -- comparable with rocprofv3's AverageNs for
