@@ -135,7 +135,7 @@ static bool materialize_dz_of(const pcs_mlp_layer& P, int M, bool dgrad) {
 // Rotation depth of a backward's dA / kB / alpha buffers.  The dgrad of layer l reuses the buffers
 // that layer l + kRot - 1's wgrad reads, so it must wait for that wgrad on the lane; with kRot = 6 no
 // stack of the models (<= 5 layers) ever waits.  (Round 4 rotated over 3: the dgrads of FP1's first two
-// layers waited ~90 us each for the lane's wgrads of layers 3 / 4, profiles/r05_main_queue_gaps.txt.)
+// layers waited ~90 us each for the lane's wgrads of layers 3 / 4; A/B in profiles/r05_ab_rotation.txt.)
 constexpr int kRot = 6;
 
 struct BwdScratch {

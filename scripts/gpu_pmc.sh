@@ -8,7 +8,7 @@ models=${*:-pointnetpp dgcnn}
 out="$GRAFT_REPO_ROOT/gpurun_out/pmc_$tag"; mkdir -p "$out"
 export TMPDIR=/tmp
 for m in $models; do
-  ARGS="--model $m --steps 3 --warmup 2 --no-cpu-baseline --no-roofline --secondary none"
+  ARGS="--model $m --steps 3 --warmup 2 --no-cpu-baseline --no-roofline --no-drop-in --secondary none --others none"
   for c in FETCH_SIZE WRITE_SIZE; do
     cd /tmp && timeout -k 10 300 rocprofv3 --pmc $c --kernel-trace -d "$out/${m}_$c" -o run --output-format csv -- \
        python3 "$GRAFT_REPO_ROOT/bench.py" $ARGS > "$out/${m}_$c.log" 2>&1; rc=$?

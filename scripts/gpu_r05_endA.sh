@@ -1,0 +1,10 @@
+# Round-5 evidence, part A: the whole GPU suite, smoke(), rocprofv3 --stats of the default bench
+# command, and per-queue breakdowns of the PointNet++ / DGCNN bench steps.
+set -u
+cd "$GRAFT_REPO_ROOT"; out=gpurun_out/r05_end; mkdir -p $out
+export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 150 --timeout-method thread > $out/pytest_gpu.log 2>&1; rc=$?
+echo "pytest rc=$rc"; tail -3 $out/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $out/smoke.log 2>&1; rc=$?; echo "smoke rc=$rc"; tail -1 $out/smoke.log; [ $rc -eq 0 ] || exit $rc
+cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$out/prof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline > "$GRAFT_REPO_ROOT/$out/prof.log" 2>&1; rc=$?; echo "prof rc=$rc"; [ $rc -eq 0 ] || exit $rc
+cd "$GRAFT_REPO_ROOT" && bash scripts/gpu_r04_prof.sh r05_endq pointnetpp dgcnn > $out/queues.log 2>&1; echo "queues rc=$?"
