@@ -227,6 +227,24 @@ def test_pointnetpp_three_way_all_tensors(B, N, seed, uniform, pad):
                       f'pointnetpp B={B} N={N}')
 
 
+@pytest.mark.timeout(1200)
+def test_pointnetpp_three_way_b32_bench_dispatch():
+    """BASELINE config 1's dispatch: B = 32 x N = 4096, the bench's own shapes (SA1 over 2^20 grouped
+    rows), so every kernel the timed step runs is exercised -- the LDS-DMA forward (pooled and plain),
+    the DMA data gradients (BNBWD and the pooled POOLBWD form), the fused SA1 backward with its split
+    wave assignment, the streaming CSR gather backward -- and every tensor is checked three-way
+    against the oracle (the reference algorithm, PointNetpp.py) in fp32 and fp64."""
+    from pcseg.engine import KernelProbe
+    with KernelProbe() as kp:
+        rows = three_way(lambda: pcseg.PointNetpp(14), lambda: R.PointNetpp(14), 32, 4096, 131)
+    names = {r[0] for r in kp.records()}
+    for k in ('pcs::fwd_dma_kernel<', 'pcs::dgrad_kernel<true, 128, 2, 1>', 'pcs::dgrad_kernel<true, 64, 3, 2>',
+              'pcs::fused_bwd_kernel<64, 32, 3>', 'pcs::fused_bwd_kernel<32, 32, 2>',
+              'pcs::csr_bwd_stream_kernel<'):
+        assert any(n.startswith(k) for n in names), (k, sorted(names))
+    _assert_three_way(rows, 'pointnetpp B=32 (bench dispatch)')
+
+
 def test_pointnext_three_way_all_tensors():
     _assert_three_way(three_way(lambda: pcseg.PointNeXt(14), lambda: R.PointNeXt(14), 2, 4096, 104), 'pointnext')
 
