@@ -63,8 +63,21 @@ __device__ __forceinline__ int acc_row_of(int r, int h) { return (r & 3) + 8 * (
 #ifndef PCS_AB_FB_WLDS
 #define PCS_AB_FB_WLDS 0                     // (A/B builds only: 1 = W's fragments read from LDS, 3 blocks per CU)
 #endif
+#ifndef PCS_AB_FB_W8
+#define PCS_AB_FB_W8 1                       // (A/B builds only: 0 = the 128 x 128 instance on 4 waves)
+#endif
+// waves per block: the 128 x 128 instance (the widest, MFMA-heaviest: 256 MFMAs per wave and tile on
+// four waves) runs eight waves -- two per SIMD, so one wave's staging, epilogue and LDS reads hide
+// under the other's MFMAs -- each with one dA row tile and two dW tiles (<= 256 registers)
+__host__ __device__ constexpr int fb_waves(int C, int CI, bool da) { return da && C == 128 && CI == 128 && PCS_AB_FB_W8 ? 8 : 4; }
+
 template <int C, int CI, int XM, bool DA, bool WIDE = false>
-__global__ __launch_bounds__(256, WIDE ? 1 : (PCS_AB_FB_WLDS ? 3 : 2)) void fused_bwd_kernel(FusedBwdArgs f) {
+__global__ __launch_bounds__(64 * fb_waves(C, CI, DA), WIDE ? 1 : (PCS_AB_FB_WLDS ? 3 : 2)) void fused_bwd_kernel(
+    FusedBwdArgs f) {
+    constexpr int NWV = fb_waves(C, CI, DA), NT = 64 * NWV;
+    // WL: W (C x CI) staged once in LDS and its B fragments read per MFMA, instead of C / 2 registers
+    // per lane for the whole launch (the eight-wave instance: 256 registers per wave)
+    constexpr bool WL = DA && (PCS_AB_FB_WLDS || NWV == 8);
     constexpr int BM = FB_BM;
     constexpr int ZS = C + 2;                  // row stride = 2 (mod 64) banks: the dA fragment reads
                                                // (32 rows x 2 k) hit 64 distinct banks
@@ -76,15 +89,15 @@ __global__ __launch_bounds__(256, WIDE ? 1 : (PCS_AB_FB_WLDS ? 3 : 2)) void fuse
     // all four waves a share of dW, so waves 0, 1 carried dA + dW: 1.5x the MFMA time per tile on
     // two SIMDs while the other two idled)
     constexpr bool SPLIT = DA && NIT == 1 && PCS_AB_FB_SPLIT;
-    constexpr int DWW = SPLIT ? 2 : 4;         // waves sharing the dW tiles
+    constexpr int DWW = SPLIT ? 2 : NWV;       // waves sharing the dW tiles
     constexpr int WPT = TW >= DWW ? TW / DWW : 1;  // dW tiles per wave
     constexpr int WR = TW >= DWW ? 1 : DWW / TW;   // waves splitting one dW tile's rows
-    constexpr int NRT = NIT == 4 ? 2 : 1;      // dA row tiles per wave
+    constexpr int NRT = NIT == 4 && NWV == 4 ? 2 : 1;   // dA row tiles per wave
     static_assert(C % 32 == 0 && CI % 32 == 0 && C <= 128 && CI <= 128, "fused backward widths");
     __shared__ __attribute__((aligned(16))) float Zs[BM * ZS];
     __shared__ __attribute__((aligned(16))) float Xs[BM * XS];
-    __shared__ double red[2][4][32];
-    __shared__ float Ws[PCS_AB_FB_WLDS && DA ? C * CI : 1];
+    __shared__ double red[2][NWV][32];
+    __shared__ float Ws[WL ? C * CI : 1];
     __shared__ float wred[WR > 1 ? (WR - 1) * TW * 1024 : 1];   // per (row subset, tile)
 
     const int tid = threadIdx.x, lane = tid & 63;
@@ -92,17 +105,17 @@ __global__ __launch_bounds__(256, WIDE ? 1 : (PCS_AB_FB_WLDS ? 3 : 2)) void fuse
     const int h = lane >> 5, l32 = lane & 31;
 
     // ---- data-gradient assignment: column strip a_ct, row tiles a_rt0 .. a_rt0 + NRT - 1
-    const int a_ct = NIT == 4 ? w : (NIT == 2 ? (w & 1) : 0);
-    const int a_rt0 = NIT == 4 ? 0 : (NIT == 2 ? (w >> 1) : (w & 1));
+    const int a_ct = NIT == 4 ? (w & 3) : (NIT == 2 ? (w & 1) : 0);
+    const int a_rt0 = NIT == 4 ? (NWV == 8 ? (w >> 2) : 0) : (NIT == 2 ? (w >> 1) : (w & 1));
     const bool a_on = DA && (NIT >= 2 || w < 2);
     const int a_col = a_ct * 32 + l32;
-    float wf[DA && !PCS_AB_FB_WLDS ? C / 2 : 1];   // wf[j] = W[2j + h][a_col]: B fragments of every k step
+    float wf[DA && !WL ? C / 2 : 1];           // wf[j] = W[2j + h][a_col]: B fragments of every k step
     float es = 0.f, et = 0.f, em = 0.f, ei = 0.f;
     if constexpr (DA) {
 #pragma unroll
-        for (int j = 0; j < (PCS_AB_FB_WLDS ? 0 : C / 2); ++j) wf[j] = f.W[(size_t)(2 * j + h) * f.ldw + a_col];
-        if (PCS_AB_FB_WLDS)
-            for (int e = tid; e < C * CI; e += 256) Ws[e] = f.W[(size_t)(e / CI) * f.ldw + e % CI];
+        for (int j = 0; j < (WL ? 0 : C / 2); ++j) wf[j] = f.W[(size_t)(2 * j + h) * f.ldw + a_col];
+        if (WL)
+            for (int e = tid; e < C * CI; e += NT) Ws[e] = f.W[(size_t)(e / CI) * f.ldw + e % CI];
         // previous layer's BN at this lane's dA column (BN-backward epilogue)
         es = f.q.s[a_col]; et = f.q.t[a_col]; em = f.q.mean[a_col]; ei = f.q.inv[a_col];
     }
@@ -131,8 +144,8 @@ __global__ __launch_bounds__(256, WIDE ? 1 : (PCS_AB_FB_WLDS ? 3 : 2)) void fuse
     const int tiles = (M + BM - 1) / BM;
     // staging: thread = one dZ channel quad over rows r0 + j*RPP (one coefficient quad) and
     // one raw-input quad over rows s0 + j*RPI
-    constexpr int CQ = C / 4, RPP = 256 / CQ, NJ = BM / RPP;
-    constexpr int IQ = CI / 4, RPI = 256 / IQ, NJX = BM / RPI;
+    constexpr int CQ = C / 4, RPP = NT / CQ, NJ = BM / RPP;
+    constexpr int IQ = CI / 4, RPI = NT / IQ, NJX = BM / RPI;
     // PF: the narrow layers (SA1-sized, HBM-bound) hold the NEXT tile's raw loads in registers
     // while the current tile's MFMAs run; the wide ones stage in chunks after the barrier
     constexpr bool PF = C + CI <= 96 || WIDE;
@@ -228,7 +241,7 @@ __global__ __launch_bounds__(256, WIDE ? 1 : (PCS_AB_FB_WLDS ? 3 : 2)) void fuse
 #pragma unroll
                 for (int rt = 0; rt < NRT; ++rt)
                     accA[rt] = __builtin_amdgcn_mfma_f32_32x32x2f32(
-                        a[rt], PCS_AB_FB_WLDS ? Ws[(2 * j + h) * CI + a_col] : wf[PCS_AB_FB_WLDS ? 0 : j], accA[rt], 0, 0, 0);
+                        a[rt], WL ? Ws[(2 * j + h) * CI + a_col] : wf[WL ? 0 : j], accA[rt], 0, 0, 0);
             }
 #pragma unroll
             for (int rt = 0; rt < NRT; ++rt) {
@@ -297,8 +310,8 @@ __global__ __launch_bounds__(256, WIDE ? 1 : (PCS_AB_FB_WLDS ? 3 : 2)) void fuse
         const int ct = tid / 32, lc = tid % 32;
         double a = 0.0, b = 0.0;
 #pragma unroll
-        for (int v = 0; v < 4; ++v) {
-            const int vct = NIT == 4 ? v : (NIT == 2 ? (v & 1) : 0);
+        for (int v = 0; v < NWV; ++v) {
+            const int vct = NIT == 4 ? (v & 3) : (NIT == 2 ? (v & 1) : 0);
             const bool von = NIT >= 2 || v < 2;
             if (von && vct == ct) { a += red[0][v][lc]; b += red[1][v][lc]; }
         }
@@ -336,10 +349,11 @@ __global__ __launch_bounds__(256, WIDE ? 1 : (PCS_AB_FB_WLDS ? 3 : 2)) void fuse
 template <int C, int CI>
 static void launch_fused(dim3 grid, hipStream_t st, const FusedBwdArgs& a) {
     constexpr bool W = C + CI > 96;
+    constexpr int NT = 64 * fb_waves(C, CI, true);
     switch (a.x.mode) {
-    case OP_PLAIN: hipLaunchKernelGGL((fused_bwd_kernel<C, CI, OP_PLAIN, true, W>), grid, dim3(256), 0, st, a); break;
-    case OP_BNBWD: hipLaunchKernelGGL((fused_bwd_kernel<C, CI, OP_BNBWD, true, W>), grid, dim3(256), 0, st, a); break;
-    default: hipLaunchKernelGGL((fused_bwd_kernel<C, CI, OP_POOLBWD, true, W>), grid, dim3(256), 0, st, a); break;
+    case OP_PLAIN: hipLaunchKernelGGL((fused_bwd_kernel<C, CI, OP_PLAIN, true, W>), grid, dim3(NT), 0, st, a); break;
+    case OP_BNBWD: hipLaunchKernelGGL((fused_bwd_kernel<C, CI, OP_BNBWD, true, W>), grid, dim3(NT), 0, st, a); break;
+    default: hipLaunchKernelGGL((fused_bwd_kernel<C, CI, OP_POOLBWD, true, W>), grid, dim3(NT), 0, st, a); break;
     }
 }
 
@@ -415,7 +429,8 @@ int fused_bwd_grid(int M, int C, int CI, bool da, int xm) {
     for (int k = 0; k < 3; ++k) {
         int& n = occ[ci][ii][da ? 1 : 0][k];
         if (n == 0) {
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fb_kernel(C, CI, modes[k], da), 256, 0) != hipSuccess)
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fb_kernel(C, CI, modes[k], da), 64 * fb_waves(C, CI, da),
+                                                             0) != hipSuccess)
                 n = 1;
             n = std::min(std::max(n, 1), 4);
         }
