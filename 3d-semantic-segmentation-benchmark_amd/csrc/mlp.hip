@@ -1125,9 +1125,12 @@ static void gemm_tile(int M, int N, bool bwd, int* bm, int* bn, int* nt = nullpt
     if (nt) *nt = 256;
     bool wide;
     const T* c;
+#ifndef PCS_AB_FWD_MID64
+#define PCS_AB_FWD_MID64 0                   // (A/B builds only: 1 = 64 x 64 first for the thin forward layers)
+#endif
     if (!bwd) {
         wide = N > 64;
-        c = wide ? big : mid;
+        c = wide ? big : (PCS_AB_FWD_MID64 ? mid64 : mid);
     } else {
         wide = N > 64 && N >= 256 && M >= 65536;
         c = wide ? big : mid64;
