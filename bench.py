@@ -177,6 +177,22 @@ def pmc_traffic(kernel, key, batch, npoints):
     return None, None
 
 
+def rocprof_avg_us(kernel, key):
+    """The kernel's average duration in the committed rocprofv3 --stats summary of this workload's
+    bench step (profiles/<round>_<model>_rocprof_stats.txt, scripts/prof_summary.py format): the
+    cross-check of the live HIP-event average (the events bracket each launch, so they also count
+    its dispatch latency)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, 'profiles', f'*_{key}_rocprof_stats.txt')))
+    if not files:
+        return None, None
+    for line in open(files[-1]):
+        parts = line.split()
+        if len(parts) > 5 and parts[1] == 'ms/step' and parts[4] == 'us' and kernel in line:
+            return float(parts[3]), os.path.relpath(files[-1], REPO)
+    return None, None
+
+
 def _kernel_entry(name, n, fl, by, sec):
     """Roofline of one kernel from its summed in-step launches."""
     intensity = fl / by if by else float('inf')
@@ -252,7 +268,9 @@ def kernel_roofline(step, dev, key, batch, npoints, replay=False):
     name, (n, fl, by, sec) = sorted(crit.items(), key=lambda kv: -kv[1][3])[0]
     out = _kernel_entry(name, n, fl, by, sec)
     traffic, src = pmc_traffic(name, key, batch, npoints)
-    out.update({'traffic': traffic, 'traffic_unit': 'bytes/launch', 'traffic_source': src,
+    rp, rsrc = rocprof_avg_us(name, key)
+    out.update({'rocprof_avg_launch_us': rp, 'rocprof_source': rsrc,
+                'traffic': traffic, 'traffic_unit': 'bytes/launch', 'traffic_source': src,
                 'selection': 'largest summed in-step time among the launches on the step\'s own stream',
                 'timing': 'in-step HIP events, step enqueued behind a spin (no host gaps)'})
     if side:

@@ -7,4 +7,9 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider --time
 echo "pytest rc=$rc"; tail -3 $out/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $out/smoke.log 2>&1; rc=$?; echo "smoke rc=$rc"; tail -1 $out/smoke.log; [ $rc -eq 0 ] || exit $rc
 cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$out/prof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline > "$GRAFT_REPO_ROOT/$out/prof.log" 2>&1; rc=$?; echo "prof rc=$rc"; [ $rc -eq 0 ] || exit $rc
-cd "$GRAFT_REPO_ROOT" && bash scripts/gpu_r04_prof.sh r05_endq pointnetpp dgcnn > $out/queues.log 2>&1; echo "queues rc=$?"
+cd "$GRAFT_REPO_ROOT" && bash scripts/gpu_r04_prof.sh r05_endq pointnetpp dgcnn pointnetpp_msg pointnext > $out/queues.log 2>&1; echo "queues rc=$?"
+# per-workload rocprof summaries (bench.py's roofline cross-check reads profiles/<round>_<model>_rocprof_stats.txt)
+for m in pointnetpp dgcnn pointnetpp_msg pointnext; do
+  f=$(find gpurun_out/r05_endq/prof_$m -name '*kernel_stats.csv' | head -1)
+  [ -n "$f" ] && { echo "# rocprofv3 --kernel-trace --stats -- python3 bench.py --model $m --no-cpu-baseline --no-roofline --no-drop-in --secondary none --others none --steps 10 --warmup 3 (this workload only: 13 steps)"; python3 scripts/prof_summary.py "$f" 13 30; } > $out/r05_${m}_rocprof_stats.txt
+done
