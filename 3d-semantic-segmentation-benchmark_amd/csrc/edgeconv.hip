@@ -123,7 +123,7 @@ __global__ __launch_bounds__(256) void edgeconv_fwd_kernel(const float* __restri
 }
 
 // BN-backward sums over the pooled edges (the only ones with dy != 0): part[2][Cout][gridDim.x]
-__global__ __launch_bounds__(256) void edgeconv_bwd_reduce_kernel(const float* __restrict__ dout,
+__global__ __launch_bounds__(256) void edgeconv_bwd_reduce_kernel(const float* __restrict__ dout, int ldo,
                                                                   const float* __restrict__ pz, long long G, int Cout,
                                                                   const float* __restrict__ coef, float slope,
                                                                   int rows_per_block, double* __restrict__ part) {
@@ -139,7 +139,7 @@ __global__ __launch_bounds__(256) void edgeconv_bwd_reduce_kernel(const float* _
         for (long long g = gb + ph; g < ge; g += 4) {
             const long long e = g * Cout + col;
             const float z = pz[e];              // the pooled (argmax) edge's z
-            const float dy = dout[e] * dact_f(z * s + t, ACT_LRELU, slope);
+            const float dy = dout[g * ldo + col] * dact_f(z * s + t, ACT_LRELU, slope);
             a += (double)dy;
             b += (double)dy * (double)((z - mean) * inv);
         }
@@ -154,7 +154,7 @@ __global__ __launch_bounds__(256) void edgeconv_bwd_reduce_kernel(const float* _
 }
 
 // per (point, channel): D = s dy at the argmax edge, dP = D - k kB - kC (S - k mean) -> G[:, 2c+1]
-__global__ __launch_bounds__(256) void edgeconv_bwd_center_kernel(const float* __restrict__ dout,
+__global__ __launch_bounds__(256) void edgeconv_bwd_center_kernel(const float* __restrict__ dout, int ldo,
                                                                   const float* __restrict__ pz,
                                                                   const float* __restrict__ S, long long G, int Cout,
                                                                   int k, const float* __restrict__ coef,
@@ -167,7 +167,7 @@ __global__ __launch_bounds__(256) void edgeconv_bwd_center_kernel(const float* _
         const float s = coef[c], t = coef[Cout + c], mean = coef[2 * Cout + c];
         const float kb = kBC[c], kc = kBC[Cout + c];
         const float z = pz[e];
-        const float d = s * (dout[e] * dact_f(z * s + t, ACT_LRELU, slope));
+        const float d = s * (dout[g * ldo + c] * dact_f(z * s + t, ACT_LRELU, slope));
         D[e] = d;
         const double dp = (double)d - (double)k * kb - (double)kc * ((double)S[e] - (double)k * mean);
         Gd[g * 2 * Cout + 2 * c + 1] = (float)dp;
@@ -177,7 +177,7 @@ __global__ __launch_bounds__(256) void edgeconv_bwd_center_kernel(const float* _
 // the same, one channel quad per thread (Cout % 4 == 0, 16-B aligned rows): 16-B loads of dout /
 // S / pz, a 16-B store of D and 32-bit quad indexing instead of a 64-bit division per element;
 // Same per-element arithmetic.
-__global__ __launch_bounds__(256) void edgeconv_bwd_center_q_kernel(const float4* __restrict__ dout,
+__global__ __launch_bounds__(256) void edgeconv_bwd_center_q_kernel(const float4* __restrict__ dout, int ldo4,
                                                                     const float4* __restrict__ pz,
                                                                     const float4* __restrict__ S, int GN4, int nq,
                                                                     int k, const float* __restrict__ coef,
@@ -192,7 +192,7 @@ __global__ __launch_bounds__(256) void edgeconv_bwd_center_q_kernel(const float4
         const float4 kbv = *reinterpret_cast<const float4*>(kBC + c);
         const float4 kcv = *reinterpret_cast<const float4*>(kBC + Cout + c);
         const float4 z = pz[e];
-        const float4 dv = dout[e], Sv = S[e];
+        const float4 dv = dout[(size_t)g * ldo4 + (c >> 2)], Sv = S[e];
         const float s4[4] = {sv.x, sv.y, sv.z, sv.w}, t4[4] = {tv.x, tv.y, tv.z, tv.w};
         const float m4[4] = {mv.x, mv.y, mv.z, mv.w}, kb4[4] = {kbv.x, kbv.y, kbv.z, kbv.w};
         const float kc4[4] = {kcv.x, kcv.y, kcv.z, kcv.w}, z4[4] = {z.x, z.y, z.z, z.w};
@@ -354,17 +354,19 @@ PCS_API int pcs_edgeconv_fwd(const float* X, int ldx, int C, const int32_t* idx,
 
 // Training-mode EdgeConv backward (the forward's saved tensors; csr_off/csr_ent = pcs_inverse_index
 // of idx with targets N).  Accumulates dW (Cout x 2C), dgamma, dbeta (+=); writes dX (nullable,
-// stride lddx, C % 4 == 0).  dout: gradient of the pooled output (B*N x Cout, dense).
+// stride lddx, C % 4 == 0).  dout: gradient of the pooled output (B*N x Cout, row stride ldo >= Cout: a
+// column block of a wider gradient -- DGCNN's head concatenation -- is read in place).
 PCS_API int pcs_edgeconv_bwd(const float* X, int ldx, int C, const int32_t* csr_off, const int32_t* csr_ent, int B,
                              int N, int k, const float* W, int Cout, const float* Y, const float* Q, const float* S,
                              const float* pz, const unsigned char* arg, const float* coef, float slope,
-                             const float* dout, float* dX, int lddx, float* dW, float* dgamma, float* dbeta,
-                             void* workspace, size_t ws_bytes, void* stream) {
+                             const float* dout, int ldo, float* dX, int lddx, float* dW, float* dgamma,
+                             float* dbeta, void* workspace, size_t ws_bytes, void* stream) {
     PCS_CHECK_ARG(B >= 1 && N >= 1 && k >= 1 && k <= 256 && C >= 1 && Cout >= 4 && Cout % 4 == 0 && Cout <= 1024,
                   "pcs_edgeconv_bwd: bad sizes B=%d N=%d k=%d C=%d Cout=%d", B, N, k, C, Cout);
     PCS_CHECK_ARG(X && csr_off && csr_ent && W && Y && Q && S && pz && arg && coef && dout && dW && workspace,
                   "pcs_edgeconv_bwd: null pointer");
     PCS_CHECK_ARG(!dX || (C % 4 == 0 && lddx >= C && lddx % 4 == 0), "pcs_edgeconv_bwd: dX needs C %% 4 == 0");
+    PCS_CHECK_ARG(ldo >= Cout, "pcs_edgeconv_bwd: dout row stride %d < Cout=%d", ldo, Cout);
     const long long G = (long long)B * N;
     size_t need = 0;
     pcs_edgeconv_workspace(B, N, C, Cout, 1, &need);
@@ -383,22 +385,22 @@ PCS_API int pcs_edgeconv_bwd(const float* X, int ldx, int C, const int32_t* csr_
     w += (size_t)nb * 2 * Cout * sizeof(double);
     w = reinterpret_cast<char*>(((uintptr_t)w + 255) & ~(uintptr_t)255);
     const size_t wg_bytes = wgrad_ws_bytes(2 * Cout, C, (int)G);
-    hipLaunchKernelGGL(edgeconv_bwd_reduce_kernel, dim3(nb, (Cout + 63) / 64), dim3(256), 0, st, dout, pz, G, Cout,
+    hipLaunchKernelGGL(edgeconv_bwd_reduce_kernel, dim3(nb, (Cout + 63) / 64), dim3(256), 0, st, dout, ldo, pz, G, Cout,
                        coef, slope, kEdgeRedRows, part);
     bn_bwd_finalize_launch(part, nb, Cout, G * k, coef, coef + 3 * Cout, dgamma, dbeta, kBC, kBC + Cout, 1, st);
     const long long GN = G * Cout;
     auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
-    if (Cout % 4 == 0 && GN / 4 < (1ll << 31) && al16(dout) && al16(pz) && al16(S) && al16(D) && al16(coef) &&
-        al16(kBC)) {
+    if (Cout % 4 == 0 && ldo % 4 == 0 && GN / 4 < (1ll << 31) && al16(dout) && al16(pz) && al16(S) && al16(D) &&
+        al16(coef) && al16(kBC)) {
         const long long GN4 = GN / 4;
         const unsigned eq = (unsigned)std::min<long long>((GN4 + 255) / 256, 65536);
         hipLaunchKernelGGL(edgeconv_bwd_center_q_kernel, dim3(eq), dim3(256), 0, st,
-                           reinterpret_cast<const float4*>(dout), reinterpret_cast<const float4*>(pz),
+                           reinterpret_cast<const float4*>(dout), ldo / 4, reinterpret_cast<const float4*>(pz),
                            reinterpret_cast<const float4*>(S), (int)GN4, Cout / 4, k, coef, kBC, slope,
                            reinterpret_cast<float4*>(D), Gd);
     } else {
         const unsigned eg = (unsigned)std::min<long long>((GN + 255) / 256, 65536);
-        hipLaunchKernelGGL(edgeconv_bwd_center_kernel, dim3(eg), dim3(256), 0, st, dout, pz, S, G, Cout, k, coef,
+        hipLaunchKernelGGL(edgeconv_bwd_center_kernel, dim3(eg), dim3(256), 0, st, dout, ldo, pz, S, G, Cout, k, coef,
                            kBC, slope, D, Gd);
     }
     {

@@ -121,7 +121,7 @@ SIGNATURES = {
     'pcs_edgeconv_fwd': [P, I32, I32, P, I32, I32, I32, P, I32, P, P, P, P, P, F32, F32, F32,
                          P, P, P, P, P, P, P, P, P, I32, P, ctypes.c_size_t, P],
     'pcs_edgeconv_bwd': [P, I32, I32, P, P, I32, I32, I32, P, I32, P, P, P, P, P, P, F32,
-                         P, P, I32, P, P, P, P, ctypes.c_size_t, P],
+                         P, I32, P, I32, P, P, P, P, ctypes.c_size_t, P],
     # inverse neighbour maps
     'pcs_inverse_index_workspace': [I64, I64, P],
     'pcs_inverse_index': [P, I32, I32, I32, P, P, P, ctypes.c_size_t, P],

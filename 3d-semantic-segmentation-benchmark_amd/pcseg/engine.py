@@ -607,7 +607,11 @@ class EdgeConvFn(torch.autograd.Function):
         B, N, k = idx.shape
         M, ldx = X.shape
         Cout = Wm.shape[0]
-        gout = gout.contiguous()
+        # a row-strided gradient (DGCNN: the EdgeConv's column block of the head's concatenation
+        # gradient) is read in place; anything else is made dense
+        if not (gout.dim() == 2 and gout.stride(1) == 1 and gout.stride(0) >= Cout and gout.stride(0) % 4 == 0
+                and gout.data_ptr() % 16 == 0):
+            gout = gout.contiguous()
         if ctx.inv is None and ctx.holder is not None and len(ctx.holder) == 3:
             ctx.inv = tuple(ctx.holder)
         ctx.holder = None
@@ -625,7 +629,8 @@ class EdgeConvFn(torch.autograd.Function):
         ws = _edge_ws(B, N, C, Cout, 1, dev)
         dW, dg, db = grad_targets((W, gamma, beta))
         call('pcs_edgeconv_bwd', ptr(X), ldx, C, ptr(off), ptr(ent), B, N, k, ptr(Wm), Cout, ptr(Y), ptr(Q), ptr(S),
-             ptr(pz), ptr(arg), ptr(coef), slope, ptr(gout), ptr(dX), ldx, ptr(dW), ptr(dg), ptr(db), ptr(ws),
+             ptr(pz), ptr(arg), ptr(coef), slope, ptr(gout), gout.stride(0), ptr(dX), ldx, ptr(dW), ptr(dg), ptr(db),
+             ptr(ws),
              ws.numel(), st)
         notify_grad_ready((W, gamma, beta))
         return dX, None, None, None, None, None, None, None, None, None, None

@@ -400,14 +400,15 @@ int pcs_edgeconv_fwd(const float* X, int ldx, int C, const int32_t* idx, int B, 
                      void* workspace, size_t ws_bytes, void* stream);
 /* backward from the forward's saved tensors and the CSR inverse of idx
  * (pcs_inverse_index, targets = N): dW (Cout x 2C), dgamma, dbeta accumulate (+=);
- * dX (nullable; C % 4 == 0) is written.  dout: gradient of `out`. */
+ * dX (nullable; C % 4 == 0) is written.  dout: gradient of `out`, row stride
+ * ldo >= Cout (a column block of a wider gradient is read in place). */
 int pcs_edgeconv_bwd(const float* X, int ldx, int C, const int32_t* csr_off,
                      const int32_t* csr_ent, int B, int N, int k, const float* W,
                      int Cout, const float* Y, const float* Q, const float* S,
                      const float* pz, const uint8_t* arg, const float* coef,
-                     float slope, const float* dout, float* dX, int lddx, float* dW,
-                     float* dgamma, float* dbeta, void* workspace, size_t ws_bytes,
-                     void* stream);
+                     float slope, const float* dout, int ldo, float* dX, int lddx,
+                     float* dW, float* dgamma, float* dbeta, void* workspace,
+                     size_t ws_bytes, void* stream);
 
 /* ---- launch probe (measurement) -----------------------------------------------
  * While enabled, every engine GEMM launch (pcs_gemm_rows / pcs_wgrad, also those
