@@ -27,7 +27,9 @@ extern "C" {
 #endif
 
 const char* pcs_last_error(void);
-/* 3 since round 5 (pcs_group_bwd_csr / pcs_interp_bwd_csr take n_slots; round 4 dropped
+/* 3 since round 5 (pcs_group_bwd_csr / pcs_interp_bwd_csr take n_slots, pcs_edgeconv_fwd an
+ * optional second output, pcs_edgeconv_bwd the output gradient's row stride; new:
+ * pcs_geometry_stream, pcs_probe_times and the kernel-variant calls; round 4 dropped
  * pcs_knn_morton_seeds and added pcs_inverse_index_batch); bindings refuse another version */
 int pcs_abi_version(void);
 /* sizeof(pcs_operand), for bindings to check their struct layout */
