@@ -236,7 +236,15 @@ static WgradLane* wgrad_lane() {
     if (!L.side) {
         // lowest priority: a high-priority caller stream keeps the critical path first
         // (the lane at the caller's priority measured slower, profiles/r03_ab_s14_lane_priority.txt)
-        if (hipStreamCreateWithFlags(&L.side, hipStreamNonBlocking) != hipSuccess) { L.side = nullptr; return nullptr; }
+#ifndef PCS_AB_LANE_LOW
+#define PCS_AB_LANE_LOW 0                    // (A/B builds only: 1 = the lane at the lowest stream priority)
+#endif
+        int least = 0, greatest = 0;
+        if (PCS_AB_LANE_LOW && hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) least = 0;
+        if (hipStreamCreateWithPriority(&L.side, hipStreamNonBlocking, PCS_AB_LANE_LOW ? least : 0) != hipSuccess) {
+            L.side = nullptr;
+            return nullptr;
+        }
         for (auto& e : L.ev)
             if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
     }
