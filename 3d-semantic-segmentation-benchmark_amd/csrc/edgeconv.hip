@@ -24,6 +24,11 @@
 
 namespace pcs {
 
+#ifndef PCS_AB_EC_FB
+#define PCS_AB_EC_FB 8                       // (A/B builds only: 1 = one neighbour at a time, round 4)
+#endif
+constexpr int EC_FB = PCS_AB_EC_FB;
+
 constexpr int kEdgeFwdBlocks = 1024;
 
 // one thread = one point x 4 channels; 256 / (Cout/4) points per block, grid-stride over points
@@ -65,25 +70,39 @@ __global__ __launch_bounds__(256) void edgeconv_fwd_kernel(const float* __restri
             float mx[4], sm[4];
             int amx[4] = {0, 0, 0, 0};
             const int32_t* nb = idx + g * k;
-            for (int kk = 0; kk < k; ++kk) {
-                const int j = min(max(nb[kk], 0), N - 1);
-                PCS_DCHECK(cloud + j < G && c + 4 <= Cout, "edgeconv fwd Y row %lld col %d outside %lld x %d",
-                           cloud + j, c, G, Cout);
-                const float4 yj = *reinterpret_cast<const float4*>(Y + (cloud + j) * Cout + c);
-                const float jv[4] = {yj.x, yj.y, yj.z, yj.w};
+            // EC_FB neighbours per batch: the batch's index loads, then all its Y-row gathers, are issued
+            // before its arithmetic, which runs in neighbour order (the same sums and argmax as one
+            // neighbour at a time); k = 20 takes three batches instead of 20 dependent index -> row rounds
+            for (int k0 = 0; k0 < k; k0 += EC_FB) {
+                int jb[EC_FB];
+                float4 yb[EC_FB];
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const float z = __fadd_rn(__fsub_rn(jv[q], yv[q]), pv[q]);
-                    const float zf = __uint_as_float(__float_as_uint(z) ^ flip[q]);
-                    if (kk == 0) {
-                        mx[q] = zf;
-                        sm[q] = z;
-                    } else {
-                        if (zf > mx[q] && !keep0[q]) { mx[q] = zf; amx[q] = kk; }
-                        sm[q] = __fadd_rn(sm[q], z);
+                for (int u = 0; u < EC_FB; ++u) jb[u] = k0 + u < k ? min(max(nb[k0 + u], 0), N - 1) : 0;
+#pragma unroll
+                for (int u = 0; u < EC_FB; ++u) {
+                    PCS_DCHECK(cloud + jb[u] < G && c + 4 <= Cout, "edgeconv fwd Y row %lld col %d outside %lld x %d",
+                               cloud + jb[u], c, G, Cout);
+                    yb[u] = *reinterpret_cast<const float4*>(Y + (cloud + jb[u]) * Cout + c);
+                }
+#pragma unroll
+                for (int u = 0; u < EC_FB; ++u) {
+                    const int kk = k0 + u;
+                    if (kk >= k) break;
+                    const float jv[4] = {yb[u].x, yb[u].y, yb[u].z, yb[u].w};
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const float z = __fadd_rn(__fsub_rn(jv[q], yv[q]), pv[q]);
+                        const float zf = __uint_as_float(__float_as_uint(z) ^ flip[q]);
+                        if (kk == 0) {
+                            mx[q] = zf;
+                            sm[q] = z;
+                        } else {
+                            if (zf > mx[q] && !keep0[q]) { mx[q] = zf; amx[q] = kk; }
+                            sm[q] = __fadd_rn(sm[q], z);
+                        }
+                        s1[q] += (double)z;
+                        s2[q] += (double)z * (double)z;
                     }
-                    s1[q] += (double)z;
-                    s2[q] += (double)z * (double)z;
                 }
             }
 #pragma unroll
@@ -212,6 +231,10 @@ __global__ __launch_bounds__(256) void edgeconv_bwd_center_q_kernel(const float4
 // per target point m (one wave, lanes over channels): sum over the edges whose neighbour is m
 //   G_in = sum [arg == kk] D_i  - cnt (kB + kC (Y_m - mean)) - kC sum Q_i ,  dY = G_in - dP_m -> G[:, 2c]
 // (z_e = Y_m + Q_i; fp64 accumulation, so the unspecified CSR order does not change the result)
+#ifndef PCS_AB_EC_U
+#define PCS_AB_EC_U 4                        // (A/B builds only: slot rows per batch; 16 measured +0.11 ms on DGCNN)
+#endif
+constexpr int EC_U = PCS_AB_EC_U;
 __global__ __launch_bounds__(256) void edgeconv_bwd_gather_kernel(const float* __restrict__ Y,
                                                                   const float* __restrict__ Q,
                                                                   const float* __restrict__ D,
@@ -254,6 +277,28 @@ __global__ __launch_bounds__(256) void edgeconv_bwd_gather_kernel(const float* _
                 aq += (double)qv;
             };
             int e = 0;
+            // EC_U slot rows in flight per lane: all of a batch's loads are issued before its adds, which
+            // then run in list order (the same fp64 sums as one slot at a time).  Lists average k entries,
+            // so one or two batches cover a target instead of k / 4 dependent rounds of loads.
+            for (; e + EC_U <= n; e += EC_U) {
+                float dv[EC_U], qv[EC_U];
+                int av[EC_U], kvs[EC_U];
+#pragma unroll
+                for (int u = 0; u < EC_U; ++u) {
+                    const long long r = (long long)__builtin_amdgcn_readlane(row, e + u);
+                    kvs[u] = __builtin_amdgcn_readlane(kk, e + u);
+                    const size_t o = (size_t)r * Cout + cc;
+                    PCS_DCHECK(r >= 0 && r < G, "edgeconv bwd gather row %lld of %lld", r, G);
+                    dv[u] = D[o];
+                    qv[u] = Q[o];
+                    av[u] = arg[o];
+                }
+#pragma unroll
+                for (int u = 0; u < EC_U; ++u) {
+                    accd += av[u] == kvs[u] ? (double)dv[u] : 0.0;
+                    accq += (double)qv[u];
+                }
+            }
             for (; e + 4 <= n; e += 4) {
                 term(e, accd, accq);
                 term(e + 1, accd, accq);
