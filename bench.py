@@ -163,11 +163,19 @@ def run_cpu_baseline(args, key, batch, npoints):
 
 
 # ----------------------------------------------------------------------------- roofline of the dominant kernel
+def _by_round(files):
+    """Committed profile files sorted by their round number (r05 < r10), last = newest."""
+    import re
+    return sorted(files, key=lambda f: (int(m.group(1)) if (m := re.match(r'r(\d+)_', os.path.basename(f)))
+                                         else -1, f))
+
+
 def pmc_traffic(kernel, key, batch, npoints):
-    """HBM bytes per launch of `kernel` from the committed PMC summary of this workload
-    (scripts/gpu_pmc.sh -> profiles/<round>_pmc_<model>_b<B>_n<N>.json; FETCH_SIZE x2 + WRITE_SIZE)."""
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary of this workload
+    (scripts/gpu_pmc.sh -> profiles/<round>_pmc_<model>_b<B>_n<N>.json; FETCH_SIZE x2 + WRITE_SIZE).
+    Not measured in this run: the PMC passes are separate rocprofv3 runs (MI355X_MICROARCH.md)."""
     import glob
-    files = sorted(glob.glob(os.path.join(REPO, 'profiles', f'*_pmc_{key}_b{batch}_n{npoints}.json')))
+    files = _by_round(glob.glob(os.path.join(REPO, 'profiles', f'*_pmc_{key}_b{batch}_n{npoints}.json')))
     if not files:
         return None, None
     table = json.load(open(files[-1]))
@@ -177,13 +185,13 @@ def pmc_traffic(kernel, key, batch, npoints):
     return None, None
 
 
-def rocprof_avg_us(kernel, key):
-    """The kernel's average duration in the committed rocprofv3 --stats summary of this workload's
-    bench step (profiles/<round>_<model>_rocprof_stats.txt, scripts/prof_summary.py format): the
-    cross-check of the live HIP-event average (the events bracket each launch, so they also count
-    its dispatch latency)."""
+def committed_profile_avg_us(kernel, key):
+    """The kernel's average duration in the newest COMMITTED rocprofv3 --stats summary of this
+    workload's bench step (profiles/<round>_<model>_rocprof_stats.txt, scripts/prof_summary.py
+    format).  Read from the file, not measured in this run: the cross-check of the live HIP-event
+    average (the events bracket each launch, so they also count its dispatch latency)."""
     import glob
-    files = sorted(glob.glob(os.path.join(REPO, 'profiles', f'*_{key}_rocprof_stats.txt')))
+    files = _by_round(glob.glob(os.path.join(REPO, 'profiles', f'*_{key}_rocprof_stats.txt')))
     if not files:
         return None, None
     for line in open(files[-1]):
@@ -268,8 +276,8 @@ def kernel_roofline(step, dev, key, batch, npoints, replay=False):
     name, (n, fl, by, sec) = sorted(crit.items(), key=lambda kv: -kv[1][3])[0]
     out = _kernel_entry(name, n, fl, by, sec)
     traffic, src = pmc_traffic(name, key, batch, npoints)
-    rp, rsrc = rocprof_avg_us(name, key)
-    out.update({'rocprof_avg_launch_us': rp, 'rocprof_source': rsrc,
+    rp, rsrc = committed_profile_avg_us(name, key)
+    out.update({'committed_profile_avg_us': rp, 'committed_profile_source': rsrc,
                 'traffic': traffic, 'traffic_unit': 'bytes/launch', 'traffic_source': src,
                 'selection': 'largest summed in-step time among the launches on the step\'s own stream',
                 'timing': 'in-step HIP events, step enqueued behind a spin (no host gaps)'})
@@ -540,6 +548,134 @@ def run_drop_in(key, batch, npoints, args, dev):
     return out
 
 
+# ----------------------------------------------------------------------------- the JSON line
+LINE_LIMIT = 4096       # the driver reads the last ~10 KB of stdout+stderr: the line stays far below
+
+
+def full_record(results, cpu_res, args, world, rccl_world, keys, others):
+    """Everything the run measured (the detail file's content): the primary workload at the top
+    level, the second half of the metric under `secondary`, the per-GPU halves of configs[3] /
+    configs[4] under `other_configs`."""
+    prim = results[args.model]
+    res = {'metric': METRIC, 'value': prim['value'], 'unit': 'points/s', 'n_gpus': world,
+           'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': prim['ms_per_step'],
+           'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'fp32',
+           'data': 'synthetic S3DIS-like blocks (pcseg.synthetic), random-init weights',
+           'config': dict(prim['config'], rccl_world=rccl_world),
+           'host_enqueue_ms_per_step': prim['host_enqueue_ms_per_step'],
+           'host_runahead_wait_ms_per_step': prim.get('host_runahead_wait_ms_per_step'),
+           'roofline': prim['roofline'], 'step_roofline': prim['step_roofline'],
+           'drop_in': prim.get('drop_in'), 'cpu_baseline': cpu_res.get(args.model)}
+    for k in keys[1:]:
+        res['secondary'] = dict(results[k], metric=METRIC, n_gpus=world, dtype='fp32', cpu_baseline=cpu_res.get(k))
+    if others:
+        res['other_configs'] = {k: dict(results[k], metric=METRIC, n_gpus=world, dtype='fp32', cpu_baseline=None)
+                                for k in others}
+    return res
+
+
+def write_detail(full, path):
+    """The full record (top kernels, side-stream kernels, concurrent MFMA, drop-in rooflines, the
+    all-core CPU leg) as a side file; returns its repo-relative path, or None when not written."""
+    if not path or path == 'none':
+        return None
+    path = path if os.path.isabs(path) else os.path.join(REPO, path)
+    try:
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        with open(path, 'w') as f:
+            json.dump(full, f, indent=1)
+    except OSError as e:
+        print(f'[bench] detail file not written: {e}', file=sys.stderr, flush=True)
+        return None
+    return os.path.relpath(path, REPO)
+
+
+def _r(x, nd=4):
+    return None if x is None else round(x, nd)
+
+
+def compact_roofline(roof):
+    """The dominant kernel's roofline, the contract's fields only."""
+    if not roof:
+        return None
+    out = {'kernel': roof['kernel'].replace('pcs::', ''), 'bound': roof['bound'], 'achieved': roof['achieved'],
+           'peak': roof['peak'], 'unit': roof['unit'], 'frac': roof['frac'], 'traffic': roof.get('traffic'),
+           'avg_launch_us': roof['avg_launch_us'], 'launches_per_step': roof['launches_per_step']}
+    by = roof.get('algo_bytes_per_launch')
+    if out['traffic'] and by:
+        out['traffic_over_algo'] = round(out['traffic'] / by, 3)
+    if roof.get('committed_profile_avg_us') is not None:
+        out['committed_profile_avg_us'] = roof['committed_profile_avg_us']
+    return out
+
+
+def compact_cpu(cb):
+    if not cb:
+        return None
+    return {'value': _r(cb.get('value'), 1), 'unit': cb.get('unit', 'points/s'), 'cores': cb.get('cores'),
+            'kind': cb.get('kind', 'port'), 'sample': (cb.get('sample') or '')[:200]}
+
+
+def compact_workload(r, with_cpu=True):
+    out = {'value': r['value'], 'unit': 'points/s', 'ms_per_step': r['ms_per_step'],
+           'workload': r['config']['workload'], 'roofline': compact_roofline(r.get('roofline'))}
+    sr = r.get('step_roofline')
+    if sr:
+        out['step_frac_fp32'] = sr['frac_of_fp32_peak']
+    if with_cpu:
+        out['cpu_baseline'] = compact_cpu(r.get('cpu_baseline'))
+    di = r.get('drop_in')
+    if di:
+        out['drop_in'] = {'ms_per_step': di['ms_per_step'], 'host_enqueue_ms': di['host_enqueue_ms_per_step']}
+    return out
+
+
+def compact_line(full, detail_path):
+    """The one JSON line bench.py prints last: the contract's keys, the compact roofline and CPU
+    baseline of both halves of the metric, a summary per other config, and the detail file's
+    path.  Kept under LINE_LIMIT bytes (the long strings are trimmed first if it is not)."""
+    line = {k: full[k] for k in ('metric', 'value', 'unit', 'n_gpus', 'steps', 'warmup', 'ms_per_step',
+                                 'higher_is_better', 'scaling', 'vs_baseline', 'dtype', 'data')}
+    c = full['config']
+    line['config'] = {k: c[k] for k in ('workload', 'model', 'global_batch', 'npoints', 'parallelism',
+                                        'rccl_world') if k in c}
+    line['roofline'] = compact_roofline(full.get('roofline'))
+    line['cpu_baseline'] = compact_cpu(full.get('cpu_baseline'))
+    sr = full.get('step_roofline')
+    line['step_frac_fp32'] = sr['frac_of_fp32_peak'] if sr else None
+    di = full.get('drop_in')
+    if di:
+        line['drop_in'] = {'ms_per_step': di['ms_per_step'], 'host_enqueue_ms': di['host_enqueue_ms_per_step']}
+    line['host_enqueue_ms_per_step'] = full.get('host_enqueue_ms_per_step')
+    if full.get('secondary'):
+        line['secondary'] = compact_workload(full['secondary'])
+    if full.get('other_configs'):
+        line['other_configs'] = {
+            k: {'value': r['value'], 'ms_per_step': r['ms_per_step'],
+                'frac': (r.get('roofline') or {}).get('frac'),
+                'drop_in_ms': (r.get('drop_in') or {}).get('ms_per_step')}
+            for k, r in full['other_configs'].items()}
+    line['detail'] = detail_path
+    if len(json.dumps(line, separators=(',', ':'))) > LINE_LIMIT:
+        for blk in (line, line.get('secondary') or {}):
+            if blk.get('cpu_baseline'):
+                blk['cpu_baseline']['sample'] = blk['cpu_baseline']['sample'][:60]
+        line['data'] = 'synthetic'
+    if len(json.dumps(line, separators=(',', ':'))) > LINE_LIMIT:
+        line.pop('other_configs', None)
+    return line
+
+
+def emit_line(full, detail_out):
+    """Write the detail file, then print the compact line as the LAST line of stdout (stderr is
+    flushed first, so no progress line lands after it in a merged log)."""
+    detail = write_detail(full, detail_out)
+    line = json.dumps(compact_line(full, detail), separators=(',', ':'))
+    sys.stderr.flush()
+    print(line, flush=True)
+    return line
+
+
 # ----------------------------------------------------------------------------- launcher
 def _free_port():
     with socket.socket() as s:
@@ -606,6 +742,9 @@ def main():
                          'the backward')
     ap.add_argument('--bwd-fuse', choices=['default', 'off', 'all'], default='default',
                     help='backward kernel choice of the shared-MLP stacks (pcs_mlp_layer.bwd_fuse; A/B runs)')
+    ap.add_argument('--detail-out', default='gpurun_out/bench_detail.json',
+                    help="where the full record (top kernels, side streams, drop-in rooflines, ...) is written; "
+                         "the printed line names it ('none': not written)")
     ap.add_argument('--check-launch', action='store_true',
                     help='launcher self-test: each rank joins a gloo group, prints its env as JSON, exits (no GPU)')
     args = ap.parse_args()
@@ -673,26 +812,9 @@ def main():
             results[k]['drop_in'] = run_drop_in(k, *sizes[k], args, dev)
             release_cached(dev)
     if rank == 0:
-        prim = results[args.model]
-        res = {'metric': METRIC, 'value': prim['value'], 'unit': 'points/s', 'n_gpus': world,
-               'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': prim['ms_per_step'],
-               'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'fp32',
-               'data': 'synthetic S3DIS-like blocks (pcseg.synthetic), random-init weights',
-               'config': dict(prim['config'], rccl_world=dist.get_world_size() if world > 1 else 1),
-               'host_enqueue_ms_per_step': prim['host_enqueue_ms_per_step'],
-               'host_runahead_wait_ms_per_step': prim.get('host_runahead_wait_ms_per_step'),
-               'roofline': prim['roofline'], 'step_roofline': prim['step_roofline'],
-               'drop_in': prim.get('drop_in'),
-               'cpu_baseline': cpu_res.get(args.model)}
-        for k in keys[1:]:
-            r = results[k]
-            r['cpu_baseline'] = cpu_res.get(k)
-            r['metric'] = METRIC
-            res['secondary'] = dict(r, n_gpus=world, dtype='fp32')
-        if others:
-            res['other_configs'] = {k: dict(results[k], metric=METRIC, n_gpus=world, dtype='fp32', cpu_baseline=None)
-                                    for k in others}
-        print(json.dumps(res), flush=True)
+        full = full_record(results, cpu_res, args, world,
+                           dist.get_world_size() if world > 1 else 1, keys, others)
+        emit_line(full, args.detail_out)
     if world > 1:
         dist.destroy_process_group()
     return 0
