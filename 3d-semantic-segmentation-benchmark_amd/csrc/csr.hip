@@ -468,7 +468,7 @@ __global__ __launch_bounds__(256) void csr_bwd_stream_kernel(const float* __rest
                                                              const float* __restrict__ dist,
                                                              const int32_t* __restrict__ off,
                                                              const int32_t* __restrict__ ent, int targets, int D,
-                                                             int TW, float* __restrict__ out, int ldo) {
+                                                             int TW, float* __restrict__ out, int ldo, int n_slots) {
     typedef float fv __attribute__((ext_vector_type(V)));
     const int wid = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
@@ -514,6 +514,9 @@ __global__ __launch_bounds__(256) void csr_bwd_stream_kernel(const float* __rest
         float nrm = 1.f, wj = 0.f;
         if (lane < n) {
             const int s = ent[base + lane];
+            // a stale or corrupt inverse map would read outside the slot rows (debug library only)
+            PCS_DCHECK(s >= 0 && s < n_slots, "csr backward: entry %d = slot %d outside %d slots", base + lane, s,
+                       n_slots);
             if (IDW) {
                 row = s / 3;
                 const int j = s - 3 * row;
@@ -717,34 +720,30 @@ PCS_API int pcs_inverse_index(const int32_t* idx, int B, int per_batch, int targ
 // (profiles/r05_ab_csr_tw.txt)
 static int csr_tw(long long targets) {
     (void)targets;
-#ifdef PCS_CSR_TW
-    return PCS_CSR_TW;                       // A/B builds (scripts/build_ab.sh) only
-#else
     return 1;
-#endif
 }
 
 template <int V, bool VEC, bool IDW>
 static void launch_stream(const float* gout, int ld, int col_off, const float* dist, const int32_t* off,
-                          const int32_t* ent, int targets, int D, float* out, int ldo, hipStream_t s) {
+                          const int32_t* ent, int targets, int D, float* out, int ldo, int n_slots, hipStream_t s) {
     constexpr int U = VEC ? 16 : (16 / V > 4 ? 16 / V : 4);
     const int tw = csr_tw(targets);
     const long long waves = (targets + tw - 1) / tw;
     hipLaunchKernelGGL((csr_bwd_stream_kernel<V, VEC, IDW, U>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s,
-                       gout, ld, col_off, dist, off, ent, targets, D, tw, out, ldo);
+                       gout, ld, col_off, dist, off, ent, targets, D, tw, out, ldo, n_slots);
 }
 
 template <bool IDW>
 static int csr_bwd_chunk(const float* gout, int ld, int col_off, const float* dist, const int32_t* off,
-                         const int32_t* ent, int targets, int D, float* out, int ldo, hipStream_t s) {
+                         const int32_t* ent, int targets, int D, float* out, int ldo, int n_slots, hipStream_t s) {
     const bool al = ld % 4 == 0 && col_off % 4 == 0 && ldo % 4 == 0 && ((uintptr_t)gout | (uintptr_t)out) % 16 == 0;
-    if (al && D == 64) launch_stream<1, false, IDW>(gout, ld, col_off, dist, off, ent, targets, D, out, ldo, s);
-    else if (al && D == 128) launch_stream<2, true, IDW>(gout, ld, col_off, dist, off, ent, targets, D, out, ldo, s);
-    else if (al && D == 256) launch_stream<4, true, IDW>(gout, ld, col_off, dist, off, ent, targets, D, out, ldo, s);
-    else if (D <= 64) launch_stream<1, false, IDW>(gout, ld, col_off, dist, off, ent, targets, D, out, ldo, s);
-    else if (D <= 128) launch_stream<2, false, IDW>(gout, ld, col_off, dist, off, ent, targets, D, out, ldo, s);
-    else if (D <= 256) launch_stream<4, false, IDW>(gout, ld, col_off, dist, off, ent, targets, D, out, ldo, s);
-    else if (D <= 512) launch_stream<8, false, IDW>(gout, ld, col_off, dist, off, ent, targets, D, out, ldo, s);
+    if (al && D == 64) launch_stream<1, false, IDW>(gout, ld, col_off, dist, off, ent, targets, D, out, ldo, n_slots, s);
+    else if (al && D == 128) launch_stream<2, true, IDW>(gout, ld, col_off, dist, off, ent, targets, D, out, ldo, n_slots, s);
+    else if (al && D == 256) launch_stream<4, true, IDW>(gout, ld, col_off, dist, off, ent, targets, D, out, ldo, n_slots, s);
+    else if (D <= 64) launch_stream<1, false, IDW>(gout, ld, col_off, dist, off, ent, targets, D, out, ldo, n_slots, s);
+    else if (D <= 128) launch_stream<2, false, IDW>(gout, ld, col_off, dist, off, ent, targets, D, out, ldo, n_slots, s);
+    else if (D <= 256) launch_stream<4, false, IDW>(gout, ld, col_off, dist, off, ent, targets, D, out, ldo, n_slots, s);
+    else if (D <= 512) launch_stream<8, false, IDW>(gout, ld, col_off, dist, off, ent, targets, D, out, ldo, n_slots, s);
     else PCS_CHECK_ARG(false, "csr backward: D=%d > 512", D);
     return 0;
 }
@@ -753,10 +752,10 @@ static int csr_bwd_chunk(const float* gout, int ld, int col_off, const float* di
 // launch per 512 channels, V = the channel chunks per lane
 template <bool IDW>
 static int csr_bwd(const float* gout, int ld, int col_off, const float* dist, const int32_t* off, const int32_t* ent,
-                   int targets, int D, float* out, hipStream_t s) {
+                   int targets, int D, float* out, int n_slots, hipStream_t s) {
     for (int c0 = 0; c0 < D; c0 += 512)
         if (int e = csr_bwd_chunk<IDW>(gout, ld, col_off + c0, dist, off, ent, targets, std::min(512, D - c0), out + c0,
-                                       D, s))
+                                       D, n_slots, s))
             return e;
     return 0;
 }
@@ -785,7 +784,8 @@ PCS_API int pcs_group_bwd_csr(const float* grad_out, int ld_gout, const int32_t*
     // per slot) and its entry read once, the source gradient written, the offsets read
     ProbeScope pr(s, 0.0, 4.0 * (double)n_slots * (D + 1) + 4.0 * (double)total + 4.0 * (double)(targets + 1), "%s",
                   probe_enabled() ? csr_bwd_name(false, ld_gout, 3, grad_out, grad_feats, D) : "");
-    if (int e = csr_bwd<false>(grad_out, ld_gout, 3, nullptr, offsets, entries, (int)targets, D, grad_feats, s))
+    if (int e = csr_bwd<false>(grad_out, ld_gout, 3, nullptr, offsets, entries, (int)targets, D, grad_feats,
+                               (int)n_slots, s))
         return e;
     return launch_status("pcs_group_bwd_csr");
 }
@@ -804,7 +804,8 @@ PCS_API int pcs_interp_bwd_csr(const float* grad_out, int ld_gout, int col_off, 
     // (read once per slot), the coarse gradient written, the offsets read
     ProbeScope pr(s, 0.0, 4.0 * (double)n_slots * (D + 4) + 4.0 * (double)total + 4.0 * (double)(targets + 1), "%s",
                   probe_enabled() ? csr_bwd_name(true, ld_gout, col_off, grad_out, grad_pts, D) : "");
-    if (int e = csr_bwd<true>(grad_out, ld_gout, col_off, dist, offsets, entries, (int)targets, D, grad_pts, s))
+    if (int e = csr_bwd<true>(grad_out, ld_gout, col_off, dist, offsets, entries, (int)targets, D, grad_pts,
+                              (int)n_slots, s))
         return e;
     return launch_status("pcs_interp_bwd_csr");
 }

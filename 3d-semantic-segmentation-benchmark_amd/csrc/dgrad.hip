@@ -361,9 +361,6 @@ bool dgrad_dma_ok(const pcs_operand* a, int M, int K, const float* W, int ldw, i
     const bool bn = base && a->ldz % 4 == 0 && al16(a->z) && al16(a->s) && al16(a->t) && al16(a->mean) &&
                     al16(a->alpha) && al16(a->kb);
     if (a->mode == PCS_OP_BNBWD) return bn;
-#ifdef PCS_AB_NO_POOL_DMA
-    return false;                            // A/B builds only: the pooled operand on the row GEMM
-#endif
     // POOLBWD: a 64-row tile spans <= 4 groups (pool_k 16 or 32) or lies in one (a multiple of 64);
     // the argmax rows (stride ld bytes) land 16 B at a time
     const int pk = a->pool_k;
@@ -375,7 +372,9 @@ bool dgrad_dma_ok(const pcs_operand* a, int M, int K, const float* W, int ldw, i
 // operand once; two stages fit two blocks per CU), else 64 x 3.  Measured: the PointNet++
 // 131072 x 128 x 128 dgrad 95.5 -> 80.2 us isolated, step 5.05 -> 5.01 ms; 128 x 3 (one block per
 // CU) 105.8 us (profiles/r04_ab_dgrad_variants.txt).  pcs_gemm_rows_kmajor_variant forces one
-// variant for a single call (A/B and the bitwise tests; no process-wide switch).
+// variant for a single call (A/B and the bitwise tests; no process-wide switch).  The switch is
+// per HOST THREAD: pcs_set_kernel_variant covers the launches the calling thread makes (forward
+// passes), not those of PyTorch's autograd device thread (the backward of loss.backward()).
 static thread_local int t_variant = 0;            // 0: policy; 1: 64 x 3; 2: 128 x 2; 3: 128 x 3
 
 void dgrad_force_variant(int v) { t_variant = v; }

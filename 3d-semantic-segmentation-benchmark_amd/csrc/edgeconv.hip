@@ -24,10 +24,9 @@
 
 namespace pcs {
 
-#ifndef PCS_AB_EC_FB
-#define PCS_AB_EC_FB 8                       // (A/B builds only: 1 = one neighbour at a time, round 4)
-#endif
-constexpr int EC_FB = PCS_AB_EC_FB;
+// neighbours per batch of the forward gather (one at a time, round 4, measured slower:
+// profiles/r05_ab_edgeconv_gathers.txt)
+constexpr int EC_FB = 8;
 
 constexpr int kEdgeFwdBlocks = 1024;
 
@@ -231,10 +230,7 @@ __global__ __launch_bounds__(256) void edgeconv_bwd_center_q_kernel(const float4
 // per target point m (one wave, lanes over channels): sum over the edges whose neighbour is m
 //   G_in = sum [arg == kk] D_i  - cnt (kB + kC (Y_m - mean)) - kC sum Q_i ,  dY = G_in - dP_m -> G[:, 2c]
 // (z_e = Y_m + Q_i; fp64 accumulation, so the unspecified CSR order does not change the result)
-#ifndef PCS_AB_EC_U
-#define PCS_AB_EC_U 4                        // (A/B builds only: slot rows per batch; 16 measured +0.11 ms on DGCNN)
-#endif
-constexpr int EC_U = PCS_AB_EC_U;
+constexpr int EC_U = 4;                      // slot rows per batch (16 measured +0.11 ms on DGCNN)
 __global__ __launch_bounds__(256) void edgeconv_bwd_gather_kernel(const float* __restrict__ Y,
                                                                   const float* __restrict__ Q,
                                                                   const float* __restrict__ D,

@@ -109,8 +109,11 @@ static size_t max_partials(int M, int kin, const pcs_mlp_layer* L, int nl, int p
         m = std::max(m, 2 * c * (size_t)pcs_gemm_row_blocks(M, (int)c));
         if (backward) m = std::max(m, 2 * c * (size_t)pcs_gemm_row_blocks_dgrad(M, (int)c));
         // a fused inner layer writes its input's BN-backward partials, one per fused block
-        if (backward && l > 0)
+        if (backward && l > 0) {
             m = std::max(m, 2 * (size_t)L[l].cin * (size_t)fused_bwd_grid(M, (int)L[l].cout, (int)L[l].cin, true, -1));
+            if (L[l].cout == 128 && L[l].cin % 128 == 0)
+                m = std::max(m, 2 * (size_t)L[l].cin * (size_t)bwd_ring_grid(M, (int)L[l].cin));
+        }
     }
     if (backward) {
         const size_t c = (size_t)L[nl - 1].cout;
@@ -125,12 +128,16 @@ static size_t max_partials(int M, int kin, const pcs_mlp_layer* L, int nl, int p
 // every pass reads two arrays (dy and Z), materialised once (read 2, write 1) every pass
 // reads one.  From 4 passes on the materialised form moves fewer bytes (DGCNN conv5-7:
 // -2.1 ms of GEMM time for +0.5 ms of materialising, scripts/dgcnn_head_ab.py).
-#ifndef PCS_AB_DZ_PASSES
-#define PCS_AB_DZ_PASSES 4                   // (A/B builds only: scripts/build_ab.sh -DPCS_AB_DZ_PASSES=n)
-#endif
+// (lower thresholds, 2 and 3 passes, and a byte-model policy measured slower: profiles/r05_ab_dz_threshold.txt,
+// profiles/r05_ab_dz_policy.txt)
+constexpr int kDzPasses = 4;
 static bool materialize_dz_of(const pcs_mlp_layer& P, int M, bool dgrad) {
-    return dz_passes(M, (int)P.cout, (int)P.cin, dgrad, P.dW != nullptr) >= PCS_AB_DZ_PASSES;
+    return dz_passes(M, (int)P.cout, (int)P.cin, dgrad, P.dW != nullptr) >= kDzPasses;
 }
+
+// the ring kernel (bwd_ring.hip) takes every eligible 128-wide BNBWD inner layer unless the layer's
+// policy turns fusion off
+static bool ring_wanted(int policy) { return policy != PCS_BWD_FUSE_OFF; }
 
 // Rotation depth of a backward's dA / kB / alpha buffers.  The dgrad of layer l reuses the buffers
 // that layer l + kRot - 1's wgrad reads, so it must wait for that wgrad on the lane; with kRot = 6 no
@@ -179,7 +186,10 @@ static size_t carve_backward(Carve& cv, int M, int kin, int ldx, const pcs_mlp_l
     s.wg0 = cv.take<char>(s.wg0_bytes);
     size_t fw = 0;
     for (int l = 1; l < nl; ++l)
-        if (L[l].dW) fw = std::max(fw, fused_bwd_ws_bytes(M, (int)L[l].cout, (int)L[l].cin));
+        if (L[l].dW) {
+            fw = std::max(fw, fused_bwd_ws_bytes(M, (int)L[l].cout, (int)L[l].cin));
+            if (L[l].cout == 128 && L[l].cin % 128 == 0) fw = std::max(fw, bwd_ring_ws_bytes(M, 128, (int)L[l].cin));
+        }
     if (L[0].dW && L[0].cin <= 32) fw = std::max(fw, fused_wgrad_ws_bytes(M, (int)L[0].cout, (int)L[0].cin));
     s.fw_bytes = fw;
     s.fw = cv.take<char>(fw);
@@ -234,14 +244,11 @@ static WgradLane* wgrad_lane() {
     std::lock_guard<std::mutex> g(mu);
     WgradLane& L = lanes[dev];
     if (!L.side) {
-        // lowest priority: a high-priority caller stream keeps the critical path first
-        // (the lane at the caller's priority measured slower, profiles/r03_ab_s14_lane_priority.txt)
-#ifndef PCS_AB_LANE_LOW
-#define PCS_AB_LANE_LOW 0                    // (A/B builds only: 1 = the lane at the lowest stream priority)
-#endif
-        int least = 0, greatest = 0;
-        if (PCS_AB_LANE_LOW && hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) least = 0;
-        if (hipStreamCreateWithPriority(&L.side, hipStreamNonBlocking, PCS_AB_LANE_LOW ? least : 0) != hipSuccess) {
+        // normal priority (0), below a high-priority caller stream, so the critical path gets free
+        // CUs first (the lane at the caller's high priority measured slower,
+        // profiles/r03_ab_s14_lane_priority.txt; at the lowest priority it was neutral,
+        // profiles/r05_ab_lane_priority.txt)
+        if (hipStreamCreateWithPriority(&L.side, hipStreamNonBlocking, 0) != hipSuccess) {
             L.side = nullptr;
             return nullptr;
         }
@@ -418,11 +425,13 @@ static int mlp_backward(const float* X, int ldx, int kin, int M, const pcs_mlp_l
         if (T.drop_p > 0.0) {
             const pcs_operand xt = bnbwd_op(gout, ldg, T, S.alpha[0], S.kb[0]);
             bool fused_top = false;
-            if (nl > 1 && T.dW && fused_bwd_wanted((int)T.bwd_fuse, M)) {
+            if (nl > 1 && T.dW) {
                 pcs_operand q = bnbwd_op(nullptr, 0, layers[nl - 2], nullptr, nullptr);
                 q.data = layers[nl - 2].Z;
                 q.ld = (int)T.cin;
-                fused_top = fused_bwd_ok(M, CL, (int)T.cin, (int)T.ldw, &xt, &q);
+                fused_top = ring_wanted((int)T.bwd_fuse) && bwd_ring_ok(M, CL, (int)T.cin, T.W, (int)T.ldw, &xt, &q);
+                fused_top = fused_top || (fused_bwd_wanted((int)T.bwd_fuse, M) &&
+                                          fused_bwd_ok(M, CL, (int)T.cin, (int)T.ldw, &xt, &q));
             }
             drop_on_load = !fused_top && materialize_dz_of(T, M, nl > 1 || dX) && S.dz;
             if (!drop_on_load) {
@@ -483,8 +492,11 @@ static int mlp_backward(const float* X, int ldx, int kin, int M, const pcs_mlp_l
             qop.data = layers[l - 1].Z;
             qop.ld = Cin;
         }
-        const bool fused = l > 0 && P.dW && fused_bwd_wanted((int)P.bwd_fuse, M) &&
-                           fused_bwd_ok(M, C, Cin, (int)P.ldw, &xop, &qop);
+        // a 128-wide BNBWD inner layer: data + weight gradient on the LDS-DMA ring (bwd_ring.hip)
+        const bool ring = l > 0 && P.dW && ring_wanted((int)P.bwd_fuse) &&
+                          bwd_ring_ok(M, C, Cin, P.W, (int)P.ldw, &xop, &qop);
+        const bool fused = ring || (l > 0 && P.dW && fused_bwd_wanted((int)P.bwd_fuse, M) &&
+                                    fused_bwd_ok(M, C, Cin, (int)P.ldw, &xop, &qop));
         if (!fused && materialize_dz_of(P, M, l > 0 || dX) && S.dz_ok(l == nl - 1)) {
             // the top layer's into its own buffer (gout is the caller's), inner ones in place
             // over the dA buffer the rebuilt operand reads
@@ -543,7 +555,12 @@ static int mlp_backward(const float* X, int ldx, int kin, int M, const pcs_mlp_l
             const pcs_mlp_layer& Q = layers[l - 1];
             float* dA = S.dA[da];
             int nbg;
-            if (fused) {
+            if (ring) {
+                nbg = bwd_ring_grid(M, Cin);
+                if (int e = bwd_ring(&xop, &qop, Cin, P.W, (int)P.ldw, M, dA, Cin, S.part, P.dW, P.db, S.fw, S.fw_bytes,
+                                     st))
+                    return fail(e);
+            } else if (fused) {
                 nbg = fused_bwd_grid(M, C, Cin, true, xop.mode);
                 if (int e = fused_bwd(&xop, C, &qop, Cin, P.W, (int)P.ldw, M, dA, Cin, S.part, P.dW, P.db, S.fw,
                                       S.fw_bytes, st))
@@ -626,10 +643,6 @@ PCS_API int pcs_wgrad_lane(void** side_stream) {
     return 0;
 }
 
-#ifndef PCS_AB_GEO_PRIO
-#define PCS_AB_GEO_PRIO 0   // A/B knob: 1 = lowest priority, 0 = normal (a torch.cuda.Stream's)
-#endif
-
 PCS_API int pcs_geometry_stream(void** stream) {
     PCS_CHECK_ARG(stream, "pcs_geometry_stream: null pointer");
     static hipStream_t streams[16];
@@ -639,9 +652,9 @@ PCS_API int pcs_geometry_stream(void** stream) {
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return launch_status("pcs_geometry_stream");
     std::lock_guard<std::mutex> g(mu);
     if (!streams[dev]) {
-        int least = 0, greatest = 0;
-        if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess ||
-            hipStreamCreateWithPriority(&streams[dev], hipStreamNonBlocking, PCS_AB_GEO_PRIO ? least : 0) != hipSuccess) {
+        // normal priority (0, a torch.cuda.Stream's), below the bench's high-priority step stream
+        // (the lowest priority measured neutral, profiles/r05_ab_geometry_blocks.txt)
+        if (hipStreamCreateWithPriority(&streams[dev], hipStreamNonBlocking, 0) != hipSuccess) {
             streams[dev] = nullptr;
             return launch_status("pcs_geometry_stream");
         }

@@ -57,27 +57,22 @@ __device__ __forceinline__ int acc_row_of(int r, int h) { return (r & 3) + 8 * (
 // WIDE: the wide layers (C + CI > 96) at ONE block per CU (one wave per SIMD, up to 512 VGPRs):
 // the next tile's raw loads are then held in registers under the current tile's MFMAs as on
 // the narrow layers, instead of being staged in chunks after the barrier.
-#ifndef PCS_AB_FB_SPLIT
-#define PCS_AB_FB_SPLIT 1                    // (A/B builds only: 0 = round 4's dW share on every wave)
-#endif
-#ifndef PCS_AB_FB_WLDS
-#define PCS_AB_FB_WLDS 0                     // (A/B builds only: 1 = W's fragments read from LDS, 3 blocks per CU)
-#endif
-#ifndef PCS_AB_FB_W8
-#define PCS_AB_FB_W8 1                       // (A/B builds only: 0 = the 128 x 128 instance on 4 waves)
-#endif
 // waves per block: the 128 x 128 instance (the widest, MFMA-heaviest: 256 MFMAs per wave and tile on
 // four waves) runs eight waves -- two per SIMD, so one wave's staging, epilogue and LDS reads hide
-// under the other's MFMAs -- each with one dA row tile and two dW tiles (<= 256 registers)
-__host__ __device__ constexpr int fb_waves(int C, int CI, bool da) { return da && C == 128 && CI == 128 && PCS_AB_FB_W8 ? 8 : 4; }
+// under the other's MFMAs -- each with one dA row tile and two dW tiles (<= 256 registers;
+// profiles/r05_ab_fused_wide_waves.txt).  (The engine runs its 128-wide BNBWD layers on the LDS-DMA
+// ring kernel instead, bwd_ring.hip; this instance serves the PLAIN / POOLBWD operands.)
+__host__ __device__ constexpr int fb_waves(int C, int CI, bool da) { return da && C == 128 && CI == 128 ? 8 : 4; }
 
 template <int C, int CI, int XM, bool DA, bool WIDE = false>
-__global__ __launch_bounds__(64 * fb_waves(C, CI, DA), WIDE ? 1 : (PCS_AB_FB_WLDS ? 3 : 2)) void fused_bwd_kernel(
+__global__ __launch_bounds__(64 * fb_waves(C, CI, DA), WIDE ? 1 : 2) void fused_bwd_kernel(
     FusedBwdArgs f) {
     constexpr int NWV = fb_waves(C, CI, DA), NT = 64 * NWV;
     // WL: W (C x CI) staged once in LDS and its B fragments read per MFMA, instead of C / 2 registers
     // per lane for the whole launch (the eight-wave instance: 256 registers per wave)
-    constexpr bool WL = DA && (PCS_AB_FB_WLDS || NWV == 8);
+    // (W from LDS at three blocks per CU for the narrow instances measured neutral,
+    // profiles/r05_ab_fused_wlds_occupancy.txt)
+    constexpr bool WL = DA && NWV == 8;
     constexpr int BM = FB_BM;
     constexpr int ZS = C + 2;                  // row stride = 2 (mod 64) banks: the dA fragment reads
                                                // (32 rows x 2 k) hit 64 distinct banks
@@ -88,7 +83,7 @@ __global__ __launch_bounds__(64 * fb_waves(C, CI, DA), WIDE ? 1 : (PCS_AB_FB_WLD
     // take dA and waves 2, 3 take every dW tile -- C / 2 MFMAs per wave on every SIMD (round 4 gave
     // all four waves a share of dW, so waves 0, 1 carried dA + dW: 1.5x the MFMA time per tile on
     // two SIMDs while the other two idled)
-    constexpr bool SPLIT = DA && NIT == 1 && PCS_AB_FB_SPLIT;
+    constexpr bool SPLIT = DA && NIT == 1;
     constexpr int DWW = SPLIT ? 2 : NWV;       // waves sharing the dW tiles
     constexpr int WPT = TW >= DWW ? TW / DWW : 1;  // dW tiles per wave
     constexpr int WR = TW >= DWW ? 1 : DWW / TW;   // waves splitting one dW tile's rows
@@ -418,14 +413,11 @@ static const void* fb_kernel(int C, int CI, int xm, bool da) {
 // BN-backward partials, which the caller's finalize reads (engine.hip passes the launch's mode).
 // (Round 4 used the smallest grid over the modes for every launch: SA1's middle layer, BNBWD at
 // 164 VGPRs, ran 2 blocks per CU where 3 are resident.)
-#ifndef PCS_AB_FB_MODE_GRID
-#define PCS_AB_FB_MODE_GRID 1                // (A/B builds only: 0 = round 4's smallest grid over the modes)
-#endif
 int fused_bwd_grid(int M, int C, int CI, bool da, int xm) {
     static int occ[3][3][2][3];                // [C][CI][da][mode], 0 = not queried
     const int ci = C == 32 ? 0 : (C == 64 ? 1 : 2), ii = CI == 32 ? 0 : (CI == 64 ? 1 : 2);
     const int modes[3] = {(int)OP_PLAIN, (int)OP_BNBWD, (int)OP_POOLBWD};
-    int lo = 4, hi = 1, mine = 0;
+    int hi = 1, mine = 0;
     for (int k = 0; k < 3; ++k) {
         int& n = occ[ci][ii][da ? 1 : 0][k];
         if (n == 0) {
@@ -434,11 +426,10 @@ int fused_bwd_grid(int M, int C, int CI, bool da, int xm) {
                 n = 1;
             n = std::min(std::max(n, 1), 4);
         }
-        lo = std::min(lo, n);
         hi = std::max(hi, n);
         if (modes[k] == xm) mine = n;
     }
-    const int per_cu = !PCS_AB_FB_MODE_GRID ? lo : (xm < 0 || mine == 0 ? hi : mine);
+    const int per_cu = xm < 0 || mine == 0 ? hi : mine;
     const int tiles = (M + FB_BM - 1) / FB_BM;
     return std::min(tiles, 256 * per_cu);
 }

@@ -340,12 +340,11 @@ bool fwd_dma_ok(const pcs_operand* a, int M, int K, const float* W, int ldw, int
 }
 
 // column tile: 128 outputs when N > 64 (a row block's A read once for them), else 64
-#ifndef PCS_AB_FWD_NS128
-#define PCS_AB_FWD_NS128 2                   // (A/B builds only: ring stages of the 128-column tiles)
-#endif
+// (a 3-stage ring for the 128-column tiles measured 4.60 vs 4.58 ms, profiles/r05_ab_fwd_dma_stages.txt)
+constexpr int kFwdNs128 = 2;
 static void fwd_shape(int N, int* bn, int* ns) {
     *bn = N > 64 ? 128 : 64;
-    *ns = *bn == 64 ? 3 : PCS_AB_FWD_NS128;
+    *ns = *bn == 64 ? 3 : kFwdNs128;
 }
 
 const char* fwd_dma_name(bool xf, bool stats, bool pool, int N) {
@@ -396,8 +395,8 @@ int fwd_dma(const pcs_operand* a, int M, int K, const float* W, int ldw, const f
         if (xf) launch_fwd<64, 3, true>(g, st);
         else launch_fwd<64, 3, false>(g, st);
     } else {
-        if (xf) launch_fwd<128, PCS_AB_FWD_NS128, true>(g, st);
-        else launch_fwd<128, PCS_AB_FWD_NS128, false>(g, st);
+        if (xf) launch_fwd<128, kFwdNs128, true>(g, st);
+        else launch_fwd<128, kFwdNs128, false>(g, st);
     }
     return 0;
 }

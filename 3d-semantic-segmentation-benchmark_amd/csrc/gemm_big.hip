@@ -217,11 +217,8 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_kernel(const float* __restrict
 
 // the wide path's column tile for N outputs: 256 unless a 128-wide tile wastes less (round 3:
 // 6 x 256 columns for conv6's 1408 measured slower than 11 x 128, profiles/r03_final_checks.txt)
-#ifndef PCS_AB_NT_BN
-#define PCS_AB_NT_BN 0                       // (A/B builds only: 128 / 256 forces the column tile)
-#endif
+// (256- or 128-column tiles throughout measured 16.52 / 16.09 vs 16.07 ms, profiles/r05_ab_nt_column_tile.txt)
 int gemm_nt_bn(int N) {
-    if (PCS_AB_NT_BN) return PCS_AB_NT_BN;
     const int w256 = ((N + 255) / 256) * 256 - N, w128 = ((N + 127) / 128) * 128 - N;
     return w128 < w256 ? 128 : 256;
 }

@@ -1125,12 +1125,11 @@ static void gemm_tile(int M, int N, bool bwd, int* bm, int* bn, int* nt = nullpt
     if (nt) *nt = 256;
     bool wide;
     const T* c;
-#ifndef PCS_AB_FWD_MID64
-#define PCS_AB_FWD_MID64 0                   // (A/B builds only: 1 = 64 x 64 first for the thin forward layers)
-#endif
+    // (64 x 64 tiles first for the thin forward layers measured 4.62 vs 4.58 ms,
+    // profiles/r05_ab_fwd_thin_tiles.txt)
     if (!bwd) {
         wide = N > 64;
-        c = wide ? big : (PCS_AB_FWD_MID64 ? mid64 : mid);
+        c = wide ? big : mid;
     } else {
         wide = N > 64 && N >= 256 && M >= 65536;
         c = wide ? big : mid64;
@@ -1320,11 +1319,7 @@ int pcs::gemm_rows_ex(const pcs_operand* a, int M, int K, const float* W, int ld
     // pooled 102 vs 128, 64 -> 64 38 vs 42: one slab per 64-row tile, two barriers and an in-place
     // transform pass per slab are not hidden), as do small M (FP4, 2048 rows: 34 vs 37 us).
     // Variant 1 (pcs_gemm_rows_variant) takes the DMA kernel wherever it is legal (tests).
-#ifdef PCS_AB_NO_FWD_DMA
-    const int fv = -1;                       // A/B builds only: every forward GEMM on the row GEMM
-#else
     const int fv = dgrad_forced_variant();
-#endif
     if (!bt && !bstats && fv >= 0 && (fv >= 1 || (N > 64 && M >= 8192)) &&
         fwd_dma_ok(a, M, K, W, ldw, N, pool_k, bias)) {
         const int gx = row_blocks(M, N, false);
@@ -1413,9 +1408,10 @@ PCS_API int pcs_gemm_rows_kmajor(const pcs_operand* a, int M, int K, const float
 PCS_API int pcs_gemm_rows_variant(const pcs_operand* a, int M, int K, const float* W, int ldw, const float* bias,
                                   float* C, int ldc, int N, double* stats, int variant, void* stream) {
     PCS_CHECK_ARG(variant >= -1 && variant <= 1, "pcs_gemm_rows_variant: variant=%d", variant);
+    const int prev = dgrad_forced_variant();     // restored, not reset (an earlier pcs_set_kernel_variant holds)
     dgrad_force_variant(variant);
     const int e = gemm_rows_ex(a, M, K, W, ldw, 0, bias, C, ldc, N, stats, nullptr, nullptr, stream);
-    dgrad_force_variant(0);
+    dgrad_force_variant(prev);
     return e;
 }
 
@@ -1429,9 +1425,10 @@ PCS_API int pcs_gemm_rows_kmajor_variant(const pcs_operand* a, int M, int K, con
                                          int ldc, int N, const pcs_operand* epi, double* bstats, int variant,
                                          void* stream) {
     PCS_CHECK_ARG(variant >= -1 && variant <= 3, "pcs_gemm_rows_kmajor_variant: variant=%d", variant);
+    const int prev = dgrad_forced_variant();
     dgrad_force_variant(variant);
     const int e = gemm_rows_ex(a, M, K, W, ldw, 1, nullptr, C, ldc, N, nullptr, epi, bstats, stream);
-    dgrad_force_variant(0);
+    dgrad_force_variant(prev);
     return e;
 }
 
@@ -1446,10 +1443,7 @@ static void wgrad_plan(int N, int K, int M, int* BO, int* BI, int* splits, int* 
     // (512 / 256 blocks for the smaller ones measured +0.3 / +0.8 % on DGCNN, round 3)
     // (round 4, in-step: 512 / 2048 blocks for the smaller ones were within noise of 1024 on both
     // models -- shorter lane blocks did not free CUs for the critical path's small kernels sooner)
-#ifndef PCS_AB_WG_BLOCKS
-#define PCS_AB_WG_BLOCKS 1024                // (A/B builds only: -DPCS_AB_WG_BLOCKS=n)
-#endif
-    const int target = 2.0 * M * N * K >= 1.6e10 ? 2048 : PCS_AB_WG_BLOCKS;
+    const int target = 2.0 * M * N * K >= 1.6e10 ? 2048 : 1024;
     int sp = (target + tiles - 1) / tiles;
     // the partial tiles (sp x N x K floats, written once and read once by the reduce) stay
     // below half the operands' bytes M x (N + K), as long as >= 512 blocks remain

@@ -268,4 +268,13 @@ size_t fused_wgrad_ws_bytes(int M, int C, int kin);
 int fused_wgrad(const pcs_operand* x, int C, const float* X, int ldx, int kin, int M, float* dW, float* db, void* ws,
                 size_t ws_bytes, hipStream_t st);
 
+// fused data + weight gradient of a 128-wide BNBWD inner layer over an LDS-DMA ring (bwd_ring.hip):
+// C = 128, CI = its input width (a multiple of 128); q as fused_bwd's; gx = bwd_ring_grid row blocks
+// (= BN-backward partials per column)
+bool bwd_ring_ok(int M, int C, int CI, const float* W, int ldw, const pcs_operand* x, const pcs_operand* q);
+int bwd_ring_grid(int M, int CI);
+size_t bwd_ring_ws_bytes(int M, int C, int CI);
+int bwd_ring(const pcs_operand* x, const pcs_operand* q, int CI, const float* W, int ldw, int M, float* dA, int ldd,
+             double* bstats, float* dW, float* db, void* ws, size_t ws_bytes, hipStream_t st);
+
 }  // namespace pcs

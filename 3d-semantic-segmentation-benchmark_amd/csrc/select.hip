@@ -468,12 +468,9 @@ __global__ __launch_bounds__(256) void three_nn_kernel(Geo g) {
 }
 
 constexpr int kStageMaxPoints = 8192;  // 96 KB of LDS
-#ifndef PCS_AB_HEAP_RPW
-#define PCS_AB_HEAP_RPW 1   // A/B knob: ball-query rows per wave on the heap path
-#endif
-#ifndef PCS_AB_INTRO_RPW
-#define PCS_AB_INTRO_RPW 1  // A/B knob: rows per wave on the introselect path
-#endif
+// one row per wave on both paths: a prefetched plan's blocks then retire quickly and let the step
+// stream's kernels in (profiles/r05_ab_geometry_blocks.txt)
+constexpr int kRowsPerWave = 1;
 
 static int run_select(Geo g, hipStream_t s, const char* what) {
     PCS_CHECK_ARG(g.B >= 0 && g.R >= 0 && g.N >= 1 && g.K >= 1, "%s: bad sizes B=%d R=%d N=%d K=%d", what, g.B,
@@ -497,7 +494,7 @@ static int run_select(Geo g, hipStream_t s, const char* what) {
     }
     if (heap_path) {
         PCS_CHECK_ARG(g.K <= 64, "%s: k=%d > 64 not supported on the heap path", what, g.K);
-        const int rows_per_wave = PCS_AB_HEAP_RPW;
+        const int rows_per_wave = kRowsPerWave;
         const int waves = (g.R + rows_per_wave - 1) / rows_per_wave;
         constexpr int wpb = kHeapBlock / kWave;
         const dim3 grid((waves + wpb - 1) / wpb, g.B);
@@ -508,7 +505,7 @@ static int run_select(Geo g, hipStream_t s, const char* what) {
     }
     // intro path: n < 64k <= 4096 for k <= 64
     PCS_CHECK_ARG(g.K <= 64, "%s: k=%d > 64 not supported", what, g.K);
-    const int rows_per_wave = PCS_AB_INTRO_RPW;
+    const int rows_per_wave = kRowsPerWave;
     const int waves = (g.R + rows_per_wave - 1) / rows_per_wave;
     const size_t row_lds = (size_t)intro_row_bytes(g.N);
     int wpb = 4;

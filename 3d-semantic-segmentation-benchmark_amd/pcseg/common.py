@@ -110,9 +110,9 @@ def _event_set(dev, side, L):
 
 def side_stream(device) -> torch.cuda.Stream:
     """One long-lived side stream per device for the neighbour-search work: the library's
-    geometry stream (pcs_geometry_stream), at the lowest priority -- a prefetched plan's
-    ball-query blocks hold whole compute units for their lifetime and must not be dispatched
-    ahead of the step stream's kernels."""
+    geometry stream (pcs_geometry_stream), at normal priority -- below the bench's high-priority
+    step stream, so the queue scheduler hands free compute units to the step's kernels first
+    (the lowest priority measured neutral, profiles/r05_ab_geometry_blocks.txt)."""
     import ctypes
     dev = torch.device(device)
     key = dev.index if dev.index is not None else torch.cuda.current_device()

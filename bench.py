@@ -383,7 +383,7 @@ def run_workload(key, batch, npoints, args, world, rank, dev):
     prio = contextlib.ExitStack()
     if args.stream_priority == 'high':
         # the step (its critical path) on a high-priority stream; the geometry side stream and the
-        # wgrad lane keep the default (lowest) priority, so the hardware queue scheduler hands
+        # wgrad lane keep normal priority (0), below it, so the hardware queue scheduler hands
         # free CUs to the critical path first
         hs = step_stream(dev)
         hs.wait_stream(torch.cuda.current_stream(dev))
@@ -735,7 +735,7 @@ def main():
                     help="--graph: capture the next step's neighbour search too, or enqueue it eagerly per step")
     ap.add_argument('--stream-priority', choices=['default', 'high'], default='high',
                     help='run the step on a high-priority stream (default; pcseg\'s side streams -- the next '
-                         'step\'s geometry, the wgrad lane -- keep the lowest priority) or on the default stream')
+                         'step\'s geometry, the wgrad lane -- keep normal priority, below it) or on the default stream')
     ap.add_argument('--edge-inverse', choices=['side', 'backward', 'deferred'], default='deferred',
                     help='DGCNN: where the EdgeConv backward\'s inverse kNN maps are built: on the side stream '
                          'after the last EdgeConv (deferred, default), right after each EdgeConv (side), or in '

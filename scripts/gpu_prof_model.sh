@@ -1,5 +1,5 @@
-# Round 5: per-queue kernel breakdown of one model's bench step (marker = the kernel that starts a step).
-# usage: scripts/gpu_r05_prof_model.sh <tag> <model> <marker>
+# Per-queue kernel breakdown of one model's bench step (marker = the kernel that starts a step).
+# usage: scripts/gpu_prof_model.sh <tag> <model> <marker>
 set -u
 cd "$GRAFT_REPO_ROOT"; tag=$1; m=$2; mk=$3
 out=gpurun_out/$tag; mkdir -p $out

@@ -1,5 +1,5 @@
-# Round-4 clean per-step kernel trace of the bench step (no drop-in, no roofline probe) per model.
-# usage: scripts/gpu_r04_prof.sh <tag> [model ...]
+# Clean per-step kernel trace of the bench step (no drop-in, no roofline probe) per model.
+# usage: scripts/gpu_queues.sh <tag> [model ...]
 set -u
 cd "$GRAFT_REPO_ROOT"; tag=${1:-prof}; shift || true
 models=${*:-pointnetpp dgcnn}

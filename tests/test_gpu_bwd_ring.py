@@ -1,0 +1,79 @@
+"""Fused data + weight gradient of the 128-wide BN layers on the LDS-DMA ring
+(csrc/bwd_ring.hip): one launch gives an inner layer's data gradient, its input layer's
+BN-backward sums and its weight / bias gradient.  Checked through MiniPointNet stacks
+(reference models/utils/common.py:125-150, the FeaturePropagation stacks of
+models/PointNetpp/PointNetpp.py:19-22) against the same stack in fp64 on the CPU: input widths
+128 and 256, the PointNet++ FP1 size (B = 32 x 4096 rows), a ragged row count, bitwise
+reproducibility, the kernel actually launched under the default policy and not under 'off'."""
+import os
+import sys
+
+import pytest
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+if HERE not in sys.path:
+    sys.path.insert(0, HERE)
+
+from test_gpu_fused_bwd import _fp64_stack, _rel, _run  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+def _check(cin, widths, B, H, W, fuse='default', seed=None):
+    from pcseg.engine import KernelProbe
+    with KernelProbe() as kp:
+        mod, x, gout, grads, gx = _run(widths, cin, B, H, W, 0, seed=seed if seed is not None else cin + len(widths),
+                                       fuse=fuse)
+    names = {r[0] for r in kp.records()}
+    xd = x.double().requires_grad_()
+    it = _fp64_stack(mod, xd, 0)
+    params = [next(it) for _ in widths]
+    out = next(it)
+    out.backward(gout.double().view(out.shape))
+    scale = max(float(p[0].grad.norm()) for p in params)
+    # north_star: 1e-3 relative, fp32
+    for l, (got, ref) in enumerate(zip(grads, params)):
+        dw, db, dg, dbe = got
+        assert _rel(dw, ref[0].grad) < 1e-3, (l, 'dW', _rel(dw, ref[0].grad))
+        assert _rel(dg, ref[2].grad) < 1e-3, (l, 'dgamma', _rel(dg, ref[2].grad))
+        assert _rel(dbe, ref[3].grad) < 1e-3, (l, 'dbeta', _rel(dbe, ref[3].grad))
+        assert float((db.double() - ref[1].grad).abs().max()) < 1e-3 * scale, (l, 'db')
+    assert _rel(gx, xd.grad) < 1e-3, ('dX', _rel(gx, xd.grad))
+    return names
+
+
+@pytest.mark.parametrize('cin,widths,B,H,W', [
+    (134, [128, 128, 128], 2, 80, 32),      # FP1-like: two 128 x 128 ring layers
+    (320, [256, 128], 2, 40, 32),            # FP2: the 128 <- 256 layer (two column tiles)
+    (131, [128, 128, 256], 2, 40, 32),       # inner 128 x 128 under a 256-wide top layer
+])
+def test_ring_backward_vs_fp64(cin, widths, B, H, W):
+    names = _check(cin, widths, B, H, W)
+    assert any("bwd_ring_kernel" in n for n in names), names
+
+
+def test_ring_backward_fp1_size_vs_fp64():
+    """PointNet++ FP1 at the bench's batch: 32 x 4096 rows, 128 -> 128 -> 128 -> 128."""
+    names = _check(128, [128, 128, 128, 128], 32, 4096, 1, seed=7)
+    assert any("bwd_ring_kernel" in n for n in names)
+
+
+def test_ring_backward_ragged_rows():
+    """M = 2051: the last 64-row tile holds 3 rows; its missing rows add nothing to dW / db."""
+    names = _check(128, [128, 128], 1, 2051, 1, seed=5)
+    assert any("bwd_ring_kernel" in n for n in names)
+
+
+def test_ring_policy_off_uses_two_gemms():
+    names = _check(134, [128, 128], 2, 40, 32, fuse='off')
+    assert not any("bwd_ring_kernel" in n for n in names)
+
+
+def test_ring_backward_bitwise_reproducible():
+    a = _run([128, 128, 128], 128, 4, 512, 4, 0, seed=9, fuse='default')
+    b = _run([128, 128, 128], 128, 4, 512, 4, 0, seed=9, fuse='default')
+    for ga, gb in zip(a[3], b[3]):
+        for ta, tb in zip(ga, gb):
+            assert torch.equal(ta, tb)
+    assert torch.equal(a[4], b[4])

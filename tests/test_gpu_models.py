@@ -238,7 +238,8 @@ def test_pointnetpp_three_way_b32_bench_dispatch():
     with KernelProbe() as kp:
         rows = three_way(lambda: pcseg.PointNetpp(14), lambda: R.PointNetpp(14), 32, 4096, 131)
     names = {r[0] for r in kp.records()}
-    for k in ('pcs::fwd_dma_kernel<', 'pcs::dgrad_kernel<true, 128, 2, 1>', 'pcs::dgrad_kernel<true, 64, 3, 2>',
+    for k in ('pcs::fwd_dma_kernel<', 'pcs::bwd_ring_kernel<128>', 'pcs::bwd_ring_kernel<256>',
+              'pcs::dgrad_kernel<true, 64, 3, 2>',
               'pcs::fused_bwd_kernel<64, 32, 3>', 'pcs::fused_bwd_kernel<32, 32, 2>',
               'pcs::csr_bwd_stream_kernel<'):
         assert any(n.startswith(k) for n in names), (k, sorted(names))
@@ -280,6 +281,26 @@ def test_dgcnn_color_three_way_wide_regime_b16():
         assert k in names, (k, sorted(names))
     print('wide kernels exercised:', sorted(n for n in names if '_nt_' in n))
     _assert_three_way(rows, 'dgcnn B=16 (M = 65536)')
+
+
+@pytest.mark.timeout(1800)
+def test_dgcnn_color_three_way_b32_bench_dispatch():
+    """BASELINE config 2 at the bench's own shape: DGCNNWithColor, B = 32 x N = 4096, k = 20 (M =
+    131 072 rows) -- the column-tile rule and the dZ materialisation policy of conv5-7 depend on M,
+    so this is the dispatch the timed step runs: the wide data gradients, conv6 / conv7's weight
+    gradients on the lane's row kernel and the wide one, the EdgeConv gathers.  Every tensor
+    three-way against the oracle (dgcnn.py:165-257) on the oracle's own kNN graphs (replayed)."""
+    from pcseg.engine import KernelProbe
+    with KernelProbe() as kp:
+        rows = three_way(lambda: pcseg.DGCNNWithColor(14), lambda: R.DGCNNWithColor(14), 32, 4096, 112,
+                         chfirst=True)
+    names = {r[0] for r in kp.records()}
+    for k in ('pcs::gemm_nt_kernel<128, 4, 2, false>', 'pcs::gemm_nt_kernel<256, 2, 4, false>',
+              'pcs::gemm_nt_kernel<256, 2, 4, true>', 'pcs::wgrad_nt_kernel<128, 4, 2>',
+              'pcs::wgrad_kernel<128, 128, 0, 0, 1>', 'pcs::edgeconv_fwd_kernel', 'pcs::edgeconv_bwd_gather_kernel'):
+        assert k in names, (k, sorted(names))
+    print('kernels exercised:', sorted(names))
+    _assert_three_way(rows, 'dgcnn B=32 (bench dispatch, M = 131072)')
 
 
 def test_dgcnn_xyz_three_way_all_tensors():
