@@ -33,11 +33,10 @@ namespace pcs {
 constexpr int BR_C = 128;                      // the layer's width: dZ columns, the data gradient's K
 constexpr int BR_BM = 64, BR_BK = 32;          // rows per tile, dZ columns per slab
 constexpr int BR_NK = BR_C / BR_BK;            // slabs per tile
-constexpr int BR_NS = 3;                       // ring stages
+constexpr int BR_NS = 5;                       // ring stages (four slabs in flight)
 constexpr int BR_SLAB = BR_BM * BR_BK;         // floats of one dy (or z) slab: 8 KB
 constexpr int BR_STAGE = 2 * BR_SLAB;          // dy + z
 constexpr int BR_X = BR_BM * 128;              // the input tile (64 rows x the 128-column tile): 32 KB
-constexpr int BR_W = BR_C * 128;               // W's column tile: 64 KB
 constexpr int BR_THREADS = 512;
 
 struct BwdRingArgs {
@@ -59,35 +58,35 @@ struct BwdRingArgs {
 __device__ __forceinline__ int br_xswz(int r) { return ((r ^ (r >> 2)) & 1) << 3; }
 __device__ __forceinline__ int br_acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
-// s_waitcnt vmcnt(n) for the few counts the ring uses (the immediate must be a constant)
+// s_waitcnt vmcnt(n), n even in [0, 42] (the immediate must be a constant)
 __device__ __forceinline__ void br_vm_wait(int n) {
     switch (n) {
-    case 2: __builtin_amdgcn_s_waitcnt(dg_vmcnt(2)); break;
-    case 4: __builtin_amdgcn_s_waitcnt(dg_vmcnt(4)); break;
-    case 6: __builtin_amdgcn_s_waitcnt(dg_vmcnt(6)); break;
-    case 32: __builtin_amdgcn_s_waitcnt(dg_vmcnt(32)); break;
-    case 34: __builtin_amdgcn_s_waitcnt(dg_vmcnt(34)); break;
-    case 36: __builtin_amdgcn_s_waitcnt(dg_vmcnt(36)); break;
-    case 38: __builtin_amdgcn_s_waitcnt(dg_vmcnt(38)); break;
+#define BR_W(k) \
+    case k: __builtin_amdgcn_s_waitcnt(dg_vmcnt(k)); break;
+    BR_W(2) BR_W(4) BR_W(6) BR_W(8) BR_W(10) BR_W(12) BR_W(14) BR_W(32) BR_W(34) BR_W(36) BR_W(38) BR_W(40) BR_W(42)
+#undef BR_W
     default: __builtin_amdgcn_s_waitcnt(dg_vmcnt(0)); break;
     }
     asm volatile("" ::: "memory");
 }
 
-// CI: the input width (128 or 256), also the row stride of dA and of the previous layer's Z
+// CI: the input width (128 or 256), also the row stride of dA and of the previous layer's Z.
+// Waves 0-3 (data gradient): wave v owns dA columns n0 + 32v .. +31 over all 64 rows (two 32-row
+// MFMA blocks) and holds its W fragments -- W[32 ks + 16 h + 4 qq + u][n0 + 32 v + l32], 64 values
+// -- in registers for the whole launch.  Waves 4-7 (weight gradient): wave 4 + v owns dW columns
+// n0 + 32v .. +31, one 32 x 32 accumulator per slab.  Per slab every wave waits only for its OWN
+// slab DMAs (the rows it rebuilds into dZ are the rows it loaded), rebuilds them, and one barrier
+// publishes the slab.
 template <int CI>
 __global__ __launch_bounds__(BR_THREADS, 1) void bwd_ring_kernel(const BwdRingArgs g) {
-    __shared__ __attribute__((aligned(16))) float Wl[BR_W];
     __shared__ __attribute__((aligned(16))) float ring[BR_NS * BR_STAGE];
-    __shared__ __attribute__((aligned(16))) float Xl[BR_X];
+    __shared__ __attribute__((aligned(16))) float Xl[2][BR_X];
     __shared__ __attribute__((aligned(16))) float cf[5 * BR_C];     // s | t | mean | alpha | kb
     __shared__ float qc[4][128];                   // layer l-1's s | t | mean | inv over the column tile
-    __shared__ double red[2][2][128];
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const bool awave = wave < 4;                   // data gradient (else weight gradient)
-    const int wm = (wave >> 1) & 1, wn = wave & 1;
     const int v = wave & 3;
     const int h = lane >> 5, l32 = lane & 31;
 
@@ -102,21 +101,14 @@ __global__ __launch_bounds__(BR_THREADS, 1) void bwd_ring_kernel(const BwdRingAr
     const int my_tiles = rb < tiles ? (tiles - 1 - rb) / g.gx + 1 : 0;
     const int total = my_tiles * BR_NK;
 
-    // ---- resident operands and per-lane coefficients, all loaded before the first DMA (a plain
-    // load issued later would make the compiler's wait for it drain the ring)
-    for (int e = tid; e < BR_C * 32; e += BR_THREADS) {
-        const int k = e >> 5, n = 4 * (e & 31);
-        PCS_DCHECK_QUAD(g.W + (size_t)k * g.ldw + n0 + n, g.W, BR_C, g.ldw, g.CI, "bwd_ring W");
-        const float4 w = *reinterpret_cast<const float4*>(g.W + (size_t)k * g.ldw + n0 + n);
-        *reinterpret_cast<float4*>(&Wl[k * 128 + (n ^ (((k >> 4) & 1) << 5))]) = w;
-    }
+    // ---- resident operands, all loaded before the first DMA (a plain load issued later would make
+    // the compiler's wait for it drain the ring): the dZ coefficients and layer l-1's BN over the
+    // column tile in LDS, the data-gradient waves' W fragments in registers
     for (int e = tid; e < 5 * BR_C; e += BR_THREADS) {
         const int c = e & (BR_C - 1), f = e >> 7;
         const float* src = f == 0 ? g.a.s : f == 1 ? g.a.t : f == 2 ? g.a.mean : f == 3 ? g.a.alpha : g.a.kb;
         cf[e] = src[c];
     }
-    // (read from LDS where used: registers kept across the loop would spill, and a spill reload is a
-    // vector-memory load whose compiler-inserted wait drains the ring)
     for (int e = tid; e < 4 * 128; e += BR_THREADS) {
         const int c = e & 127, f = e >> 7;
         const float* src = f == 0 ? g.q.s : f == 1 ? g.q.t : f == 2 ? g.q.mean : g.q.inv;
@@ -126,24 +118,26 @@ __global__ __launch_bounds__(BR_THREADS, 1) void bwd_ring_kernel(const BwdRingAr
     __builtin_amdgcn_s_waitcnt(dg_vmcnt(0));
     __syncthreads();
 
-    const unsigned rbase = dg_lds_addr(ring), xbase = dg_lds_addr(Xl);
+    const unsigned rbase = dg_lds_addr(ring), xbase = dg_lds_addr(&Xl[0][0]);
     // per-lane float offsets of the input-tile reads (row part + swizzled chunk; the two variants are
     // the two values of the row's swizzle bit, br_xswz):
-    //   data gradient, row wm*32 + acc_row(r, h), column wn*64 + 32j + l32: swizzle bit (r & 1) ^ h,
-    //     chunk bit 3 = j ^ that bit -> xa0 (j ^ r even) / xa1 (odd), + 128 * ((r & 3) + 8 * (r >> 2));
+    //   data gradient, row 32 rb2 + acc_row(r, h), column 32v + l32: swizzle bit (r & 1) ^ h -> xa0
+    //     (r even) / xa1 (r odd), + 4096 rb2 + 128 * ((r & 3) + 8 * (r >> 2));
     //   weight gradient, row 2p + h, column 32v + l32: swizzle bit ((p >> 1) & 1) ^ h -> xw0 / xw1, + 256 p
-    const int xa0 = wm * 4096 + 512 * h + 4 * (16 * wn + (l32 >> 2) + 8 * h) + (l32 & 3);
-    const int xa1 = wm * 4096 + 512 * h + 4 * (16 * wn + (l32 >> 2) + 8 * (1 - h)) + (l32 & 3);
-    const int xw0 = 128 * h + 4 * ((8 * v + (l32 >> 2)) ^ (8 * h)) + (l32 & 3);
-    const int xw1 = 128 * h + 4 * ((8 * v + (l32 >> 2)) ^ (8 * (1 - h))) + (l32 & 3);
+    const int xa0 = 512 * h + 4 * (8 * (v ^ h) + (l32 >> 2)) + (l32 & 3);
+    const int xa1 = 512 * h + 4 * (8 * (v ^ h ^ 1) + (l32 >> 2)) + (l32 & 3);
+    const int xw0 = 128 * h + 4 * (8 * (v ^ h) + (l32 >> 2)) + (l32 & 3);
+    const int xw1 = 128 * h + 4 * (8 * (v ^ h ^ 1) + (l32 >> 2)) + (l32 & 3);
+
     // dy / z slabs of flattened iteration it (row tile it / 4, slab it % 4) into stage it % NS:
-    // thread = (row tid >> 3, 16-B chunk tid & 7), one DMA of dy and one of z per wave
+    // thread = (row tid >> 3, 16-B chunk tid & 7), one DMA of dy and one of z per wave -- a wave's
+    // DMAs land exactly the rows its threads rebuild
+    const int tr = tid >> 3, tkq = tid & 7;
     auto issue_stage = [&](int it) __attribute__((always_inline)) {
         const int ti = it >> 2, ks = it & 3;
         const int m0 = (rb + ti * g.gx) * BR_BM, k0 = ks * BR_BK;
-        const int r = tid >> 3;
-        const int row = min(m0 + r, M - 1);
-        const int ch = 4 * ((tid & 7) ^ dg_swz(r));
+        const int row = min(m0 + tr, M - 1);
+        const int ch = 4 * (tkq ^ dg_swz(tr));
         const unsigned d = __builtin_amdgcn_readfirstlane(rbase + 4u * (unsigned)((it % BR_NS) * BR_STAGE + wave * 256));
         const unsigned oy = (unsigned)(row * g.a.ld + k0 + ch), oz = (unsigned)(row * g.a.ldz + k0 + ch);
         PCS_DCHECK_QUAD(g.a.data + oy, g.a.data, M, g.a.ld, BR_C, "bwd_ring dy");
@@ -151,9 +145,10 @@ __global__ __launch_bounds__(BR_THREADS, 1) void bwd_ring_kernel(const BwdRingAr
         dg_glds16(g.a.data + oy, d);
         dg_glds16(g.a.z + oz, d + 4u * BR_SLAB);
     };
-    // the input tile of row tile ti: 2048 chunks, 4 DMAs per wave (each two 128-float rows)
+    // the input tile of row tile ti into buffer ti & 1: 2048 chunks, 4 DMAs per wave (each two rows)
     auto issue_x = [&](int ti) __attribute__((always_inline)) {
         const int m0 = (rb + ti * g.gx) * BR_BM;
+        const unsigned xb = xbase + 4u * (unsigned)((ti & 1) * BR_X);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int e = (wave * 4 + j) * 64 + lane;
@@ -161,192 +156,211 @@ __global__ __launch_bounds__(BR_THREADS, 1) void bwd_ring_kernel(const BwdRingAr
             const int row = min(m0 + r, M - 1);
             const float* src = g.q.data + (unsigned)(row * CI + n0 + 4 * (c ^ br_xswz(r)));
             PCS_DCHECK_QUAD(src, g.q.data, M, CI, CI, "bwd_ring input");
-            dg_glds16(src, __builtin_amdgcn_readfirstlane(xbase + 4u * (unsigned)((wave * 4 + j) * 256)));
+            dg_glds16(src, __builtin_amdgcn_readfirstlane(xb + 4u * (unsigned)((wave * 4 + j) * 256)));
         }
     };
-
-    // role registers, shared: R[0..1] the data gradient's accumulators and R[2..3] its per-slab sums
-    // (data-gradient waves) or R[ks] the weight gradient's accumulator of slab ks (weight-gradient
-    // waves); F the input tile's values -- raw Z at the epilogue's rows (data gradient) or the B
-    // fragments act(BN(Z)) (weight gradient).  One register set for both roles keeps the kernel
-    // within the 256 registers of two waves per SIMD.
-    f32x16 R[BR_NK];
+    // role registers: R[0..1] the data gradient's row-block accumulators (data-gradient waves), or
+    // R[ks] and R[4 + ks] the weight gradient's two accumulators of slab ks (even / odd row pairs:
+    // ONE dependent chain of v_mfma_f32_32x32x2_f32 issues at half the matrix pipe's rate, measured
+    // with in-kernel stamps).  The input tile is read from its LDS buffer where used (it stays there
+    // for the whole tile: the next one fills the other buffer), so the kernel fits the 256 registers
+    // of two waves per SIMD.
+    f32x16 R[2 * BR_NK];
 #pragma unroll
-    for (int j = 0; j < BR_NK; ++j) R[j] = f32x16{};
-    float F[32];
-    double s1[2] = {0.0, 0.0}, s2[2] = {0.0, 0.0};
-    float4 dbv[BR_NK];
+    for (int j = 0; j < 2 * BR_NK; ++j) R[j] = f32x16{};
+    double s1 = 0.0, s2 = 0.0;
+    // db: the column sums of this wave's 8 dZ rows per slab (lane-group reduction), lane group ks
+    // (lanes 8 ks .. 8 ks + 7) accumulating slab ks's column quad tkq over the tiles
+    float4 dbv = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float bs = qc[0][32 * v + l32], bt = qc[1][32 * v + l32];     // (weight gradient's B transform)
+
+    // refill j (after the barrier that ends iteration j; j = -5 .. -1 is the prologue): at a tile's
+    // first slab that tile's input tile (its buffer was last read by the tile two before, done by
+    // now), then stage j + 5 into the stage iteration j's MFMAs just finished with
+    auto refill = [&](int j) __attribute__((always_inline)) {
+        const int sj = j + BR_NS;
+        if ((sj & 3) == 0 && (sj >> 2) < my_tiles) issue_x(sj >> 2);
+        if (sj < total) issue_stage(sj);
+    };
+    // vector-memory ops a wave has issued after stage i's two DMAs when it waits for them (in
+    // iteration i - 1): refills i - 4 .. i - 2 (4 for an input tile, 2 per stage) and the
+    // data-gradient waves' full-tile stores of iterations i - 4 .. i - 1 (32)
+    auto younger = [&](int i) __attribute__((always_inline)) {
+        int n = 0;
 #pragma unroll
-    for (int j = 0; j < BR_NK; ++j) dbv[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-    bool stores_full = false;
-
-    if (total > 0) {
-        issue_stage(0);
-        issue_x(0);
-    }
-    if (total > 1) issue_stage(1);
-
-    const int tr = tid >> 3, tkq = tid & 7;        // this thread's (row, k quad) of the dZ pass
-    for (int ti = 0; ti < my_tiles; ++ti) {
+        for (int j = i - 4; j <= i - 2; ++j) {
+            const int sj = j + BR_NS;
+            if (j >= -BR_NS) {
+                if ((sj & 3) == 0 && (sj >> 2) < my_tiles) n += 4;
+                if (sj < total) n += 2;
+            }
+        }
+#pragma unroll
+        for (int j = i - 4; j <= i - 1; ++j)
+            if (awave && j >= 0 && (j & 3) == 3 && (rb + (j >> 2) * g.gx) * BR_BM + BR_BM <= M) n += 32;
+        return n;
+    };
+    // this wave's rows of slab i: wait for its own DMAs (its rows are exactly the ones it loaded, so no
+    // barrier is needed before the rebuild), then dZ in place: BN backward of (dy, z), rows past M zeroed
+    auto rebuild = [&](int i) __attribute__((always_inline)) {
+        br_vm_wait(younger(i));
+        const int ti = i >> 2, ks = i & 3;
         const int m0 = (rb + ti * g.gx) * BR_BM;
+        float* p = ring + (i % BR_NS) * BR_STAGE + tr * BR_BK + 4 * (tkq ^ dg_swz(tr));
+        const float4 dy = *reinterpret_cast<const float4*>(p);
+        const float4 z = *reinterpret_cast<const float4*>(p + BR_SLAB);
+        const int k = ks * BR_BK + 4 * tkq;
+        Quad qd;
+        qd.s = *reinterpret_cast<const float4*>(&cf[k]);
+        qd.t = *reinterpret_cast<const float4*>(&cf[BR_C + k]);
+        qd.mean = *reinterpret_cast<const float4*>(&cf[2 * BR_C + k]);
+        qd.alpha = *reinterpret_cast<const float4*>(&cf[3 * BR_C + k]);
+        qd.kb = *reinterpret_cast<const float4*>(&cf[4 * BR_C + k]);
+        float4 o = xform4<OP_BNBWD>(g.a, dy, z, 0u, m0 + tr, qd, k, BR_C);
+        if (m0 + tr >= M) o = make_float4(0.f, 0.f, 0.f, 0.f);
+        *reinterpret_cast<float4*>(p) = o;
 #pragma unroll
-        for (int ks = 0; ks < BR_NK; ++ks) {
-            const int it = ti * BR_NK + ks;
-            // ---- stage it landed (with it, at a tile's first slab, the input tile issued before it).
-            // A wave's vector-memory ops per tile, in order: slab 0 -> stage it + 2, the next input
-            // tile (4); slabs 1, 2 -> stage it + 2; slab 3 -> stage it + 2, the data-gradient waves'
-            // 32 full-tile stores.  Those issued after stage it may stay in flight:
-            {
-                const int s2 = it + 1 < total ? 2 : 0;
-                const int x4 = ti + 1 < my_tiles ? 4 : 0;
-                const int st32 = awave && ti > 0 && stores_full ? 32 : 0;
-                const int n = ks == 0 ? s2 + st32 : ks == 1 ? st32 + s2 + x4 : ks == 2 ? x4 + s2 : s2;
-                br_vm_wait(n);
-            }
-            dg_barrier();
-            float* st = ring + (it % BR_NS) * BR_STAGE;
-            // ---- dZ in place: BN backward of (dy, z), rows past M zeroed
-            {
-                float* p = st + tr * BR_BK + 4 * (tkq ^ dg_swz(tr));
-                const float4 dy = *reinterpret_cast<const float4*>(p);
-                const float4 z = *reinterpret_cast<const float4*>(p + BR_SLAB);
-                const int k = ks * BR_BK + 4 * tkq;
-                Quad qd;
-                qd.s = *reinterpret_cast<const float4*>(&cf[k]);
-                qd.t = *reinterpret_cast<const float4*>(&cf[BR_C + k]);
-                qd.mean = *reinterpret_cast<const float4*>(&cf[2 * BR_C + k]);
-                qd.alpha = *reinterpret_cast<const float4*>(&cf[3 * BR_C + k]);
-                qd.kb = *reinterpret_cast<const float4*>(&cf[4 * BR_C + k]);
-                float4 o = xform4<OP_BNBWD>(g.a, dy, z, 0u, m0 + tr, qd, k, BR_C);
-                if (m0 + tr >= M) o = make_float4(0.f, 0.f, 0.f, 0.f);
-                *reinterpret_cast<float4*>(p) = o;
-                dbv[ks].x += o.x; dbv[ks].y += o.y; dbv[ks].z += o.z; dbv[ks].w += o.w;
-            }
-            // ---- at a tile's first slab: the input tile into registers -- the epilogue's raw Z
-            // (data-gradient waves) or the weight gradient's act(BN(Z)) B fragments -- so its LDS
-            // buffer can take the next tile
-            if (ks == 0) {
-                if (awave) {
-#pragma unroll
-                    for (int j = 0; j < 2; ++j)
-#pragma unroll
-                        for (int r = 0; r < 16; ++r)
-                            F[16 * j + r] = Xl[((j ^ r) & 1 ? xa1 : xa0) + 128 * ((r & 3) + 8 * (r >> 2))];
-                } else {
-                    const float bs = qc[0][32 * v + l32], bt = qc[1][32 * v + l32];
-#pragma unroll
-                    for (int p = 0; p < 32; ++p)
-                        F[p] = act_f(Xl[((p >> 1) & 1 ? xw1 : xw0) + 256 * p] * bs + bt, 0, qslope);
-                }
-            }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            dg_barrier();
-            // ---- refill: the stage every wave finished reading one iteration ago; at a tile's first
-            // slab also the next input tile (every wave has its copy of this one)
-            if (it + 2 < total) issue_stage(it + 2);
-            if (ks == 0 && ti + 1 < my_tiles) issue_x(ti + 1);
+        for (int m = 8; m < 64; m <<= 1) {
+            o.x += __shfl_xor(o.x, m); o.y += __shfl_xor(o.y, m);
+            o.z += __shfl_xor(o.z, m); o.w += __shfl_xor(o.w, m);
+        }
+        if ((lane >> 3) == ks) { dbv.x += o.x; dbv.y += o.y; dbv.z += o.z; dbv.w += o.w; }
+    };
+    // the end of iteration i: every wave's rows of slab i + 1 rebuilt and its MFMAs on slab i issued
+    auto publish = [&](int i) __attribute__((always_inline)) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        dg_barrier();
+        refill(i);
+    };
 
-            if (awave) {
-                // ---- data gradient: 32 rows x 64 columns of dZ . W (the slab into a fresh
-                // accumulator, then added: dgrad_kernel's two-level fp32 sum)
-                const int ar = wm * 32 + l32;
+    // Software pipeline, per iteration i: MFMAs on slab i (rebuilt and published last iteration) and
+    // the rebuild of slab i + 1, then one barrier.  The two waves of a SIMD take the two in opposite
+    // order -- a data-gradient wave issues its MFMAs first, a weight-gradient wave rebuilds first --
+    // so each one's rebuild (VALU + LDS) runs under the other's MFMAs and the matrix pipe stays busy.
+    if (awave) {
+        // data-gradient waves: W's fragments held in registers for the whole launch (landed before
+        // the first DMA, so no later wait for them counts the ring)
+        float Wr[BR_NK * 16];
 #pragma unroll
-                for (int qq = 0; qq < 4; ++qq) {
-                    const float4 a = *reinterpret_cast<const float4*>(st + ar * BR_BK + 4 * ((4 * h + qq) ^ dg_swz(ar)));
-                    const int kr = ks * BR_BK + 16 * h + 4 * qq;
+        for (int j = 0; j < BR_NK * 16; ++j) {
+            const int k = 32 * (j >> 4) + 16 * h + (j & 15);
+            PCS_DCHECK(k < BR_C && n0 + 32 * v + l32 < g.CI, "bwd_ring W row %d col %d", k, n0 + 32 * v + l32);
+            Wr[j] = g.W[(size_t)k * g.ldw + n0 + 32 * v + l32];
+        }
+        __builtin_amdgcn_s_waitcnt(dg_vmcnt(0));
 #pragma unroll
-                    for (int j = 0; j < 2; ++j) {
-                        const int bc = (wn * 64 + 32 * j + l32) ^ (h << 5);
-                        const float b0 = Wl[(kr + 0) * 128 + bc], b1 = Wl[(kr + 1) * 128 + bc];
-                        const float b2 = Wl[(kr + 2) * 128 + bc], b3 = Wl[(kr + 3) * 128 + bc];
-                        const f32x16 c0 = {};
-                        R[2 + j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, b0, qq == 0 ? c0 : R[2 + j], 0, 0, 0);
-                        R[2 + j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b1, R[2 + j], 0, 0, 0);
-                        R[2 + j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, b2, R[2 + j], 0, 0, 0);
-                        R[2 + j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b3, R[2 + j], 0, 0, 0);
+        for (int j = -BR_NS; j < 0; ++j) refill(j);
+        if (total > 0) rebuild(0);
+        publish(-1);
+        const int c = 32 * v + l32;
+        for (int ti = 0; ti < my_tiles; ++ti) {
+            const int m0 = (rb + ti * g.gx) * BR_BM;
+            const float* xl = &Xl[ti & 1][0];
+#pragma unroll
+            for (int ks = 0; ks < BR_NK; ++ks) {
+                const int i = ti * BR_NK + ks;
+                const float* st = ring + (i % BR_NS) * BR_STAGE;
+                // ---- data gradient: dA[64 rows][32v + l32] += dZ_slab . W_slab, both row blocks
+#pragma unroll
+                for (int b2 = 0; b2 < 2; ++b2) {
+                    const int ar = 32 * b2 + l32;
+#pragma unroll
+                    for (int qq = 0; qq < 4; ++qq) {
+                        const float4 a = *reinterpret_cast<const float4*>(st + ar * BR_BK + 4 * ((4 * h + qq) ^ dg_swz(ar)));
+                        const float* w = &Wr[16 * ks + 4 * qq];
+                        R[b2] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, w[0], R[b2], 0, 0, 0);
+                        R[b2] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, w[1], R[b2], 0, 0, 0);
+                        R[b2] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, w[2], R[b2], 0, 0, 0);
+                        R[b2] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, w[3], R[b2], 0, 0, 0);
                     }
                 }
-#pragma unroll
-                for (int j = 0; j < 2; ++j) R[j] += R[2 + j];
                 if (ks == BR_NK - 1) {
-                    // ---- tile epilogue: layer l-1's BN-backward sums, then the stores --
-                    // unconditional on a full tile, so the next wait can count them
-                    const int rb0 = m0 + wm * 32;
+                    // ---- tile epilogue: layer l-1's BN-backward sums (per tile in fp32, then into the
+                    // fp64 totals), then the stores -- unconditional on a full tile, so later waits
+                    // can count them
                     const bool full = m0 + BR_BM <= M;
+                    const float sp = qc[0][c], tp = qc[1][c], mp = qc[2][c], ip = qc[3][c];
+                    float t1 = 0.f, t2 = 0.f;
 #pragma unroll
-                    for (int j = 0; j < 2; ++j) {
-                        const int c = wn * 64 + 32 * j + l32;
-                        const float sp = qc[0][c], tp = qc[1][c], mp = qc[2][c], ip = qc[3][c];
+                    for (int b2 = 0; b2 < 2; ++b2)
 #pragma unroll
                         for (int r = 0; r < 16; ++r) {
-                            const float o = R[j][r] + 0.f;
-                            R[j][r] = o;
-                            const bool ok = full || rb0 + br_acc_row(r, h) < M;
-                            const float z = F[16 * j + r];
-                            const float dy = o * dact_f(z * sp + tp, 0, qslope);
-                            const float xh = (z - mp) * ip;
-                            const double dd = ok ? (double)dy : 0.0;
-                            s1[j] += dd;
-                            s2[j] += dd * (double)xh;
+                            const float o = R[b2][r] + 0.f;
+                            R[b2][r] = o;
+                            const bool ok = full || m0 + 32 * b2 + br_acc_row(r, h) < M;
+                            const float z = xl[(r & 1 ? xa1 : xa0) + 4096 * b2 + 128 * ((r & 3) + 8 * (r >> 2))];
+                            const float dy = ok ? o * dact_f(z * sp + tp, 0, qslope) : 0.f;
+                            t1 += dy;
+                            t2 += dy * ((z - mp) * ip);
                         }
-                    }
-                    stores_full = full;
+                    s1 += (double)t1;
+                    s2 += (double)t2;
 #pragma unroll
-                    for (int j = 0; j < 2; ++j) {
-                        float* cb = g.dA + (size_t)(rb0 + 4 * h) * CI + n0 + wn * 64 + 32 * j + l32;
+                    for (int b2 = 0; b2 < 2; ++b2) {
+                        float* cb = g.dA + (size_t)(m0 + 32 * b2 + 4 * h) * CI + n0 + c;
                         if (full) {
 #pragma unroll
-                            for (int r = 0; r < 16; ++r) cb[((r & 3) + 8 * (r >> 2)) * CI] = R[j][r];
+                            for (int r = 0; r < 16; ++r) cb[((r & 3) + 8 * (r >> 2)) * CI] = R[b2][r];
                         } else {
 #pragma unroll
                             for (int r = 0; r < 16; ++r)
-                                if (rb0 + br_acc_row(r, h) < M) cb[((r & 3) + 8 * (r >> 2)) * CI] = R[j][r];
+                                if (m0 + 32 * b2 + br_acc_row(r, h) < M) cb[((r & 3) + 8 * (r >> 2)) * CI] = R[b2][r];
                         }
-                        R[j] = f32x16{};
+                        R[b2] = f32x16{};
                     }
                 }
-            } else {
+                if (i + 1 < total) rebuild(i + 1);
+                publish(i);
+            }
+        }
+    } else {
+#pragma unroll
+        for (int j = -BR_NS; j < 0; ++j) refill(j);
+        if (total > 0) rebuild(0);
+        publish(-1);
+        for (int ti = 0; ti < my_tiles; ++ti) {
+            const float* xl = &Xl[ti & 1][0];
+#pragma unroll
+            for (int ks = 0; ks < BR_NK; ++ks) {
+                const int i = ti * BR_NK + ks;
+                const float* st = ring + (i % BR_NS) * BR_STAGE;
+                if (i + 1 < total) rebuild(i + 1);
                 // ---- weight gradient: dW[32 ks .. +31][n0 + 32 v .. +31] += dZ_slab^T . X, 2 rows per MFMA
 #pragma unroll
                 for (int p = 0; p < 32; ++p) {
                     const int zr = 2 * p + h;
                     const float a = st[zr * BR_BK + 4 * ((l32 >> 2) ^ dg_swz(zr)) + (l32 & 3)];
-                    R[ks] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, F[p], R[ks], 0, 0, 0);
+                    const float b = act_f(xl[((p >> 1) & 1 ? xw1 : xw0) + 256 * p] * bs + bt, 0, qslope);
+                    R[ks + 4 * (p & 1)] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, R[ks + 4 * (p & 1)], 0, 0, 0);
                 }
+                publish(i);
             }
         }
     }
     br_vm_wait(0);
     __syncthreads();
 
-    // ---- layer l-1's BN-backward partials of this row block (both lane halves, both row halves)
+    // ---- layer l-1's BN-backward partials of this row block: a data-gradient wave owns its 32 columns
     if (awave) {
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const double a = s1[j] + __shfl_xor(s1[j], 32);
-            const double b = s2[j] + __shfl_xor(s2[j], 32);
-            if (lane < 32) {
-                red[0][wm][wn * 64 + 32 * j + l32] = a;
-                red[1][wm][wn * 64 + 32 * j + l32] = b;
-            }
+        const double a = s1 + __shfl_xor(s1, 32);
+        const double b = s2 + __shfl_xor(s2, 32);
+        if (lane < 32) {
+            const int cl = n0 + 32 * v + l32;
+            g.bstats[(size_t)cl * g.gx + rb] = a;
+            g.bstats[((size_t)CI + cl) * g.gx + rb] = b;
         }
     }
-    // db partial: each thread's column-quad sums over its rows, added in row order through LDS
-    float* dbs = ring;                             // [4][64 rows][32]
-#pragma unroll
-    for (int ks = 0; ks < BR_NK; ++ks)
-        *reinterpret_cast<float4*>(&dbs[(ks * BR_BM + tr) * BR_BK + 4 * tkq]) = dbv[ks];
+    // db partial: the waves' column-quad sums (lane 8 ks + tkq of each wave holds slab ks, quad
+    // tkq), added in wave order
+    float* dbs = ring;                             // [8 waves][4 slabs][32]
+    if (lane < 32)
+        *reinterpret_cast<float4*>(&dbs[(wave * BR_NK + (lane >> 3)) * BR_BK + 4 * tkq]) = dbv;
     __syncthreads();
-    if (tid < 128) {
-        const int cl = n0 + tid;
-        g.bstats[(size_t)cl * g.gx + rb] = red[0][0][tid] + red[0][1][tid];
-        g.bstats[((size_t)CI + cl) * g.gx + rb] = red[1][0][tid] + red[1][1][tid];
-        if (g.pdb && ct == 0) {
-            const int ks = tid >> 5, kk = tid & 31;
-            float s = 0.f;
-            for (int r = 0; r < BR_BM; ++r) s += dbs[(ks * BR_BM + r) * BR_BK + kk];
-            g.pdb[(size_t)rb * BR_C + tid] = s;
-        }
+    if (tid < 128 && g.pdb && ct == 0) {
+        const int ks = tid >> 5, kk = tid & 31;
+        float sum = 0.f;
+        for (int w = 0; w < 8; ++w) sum += dbs[(w * BR_NK + ks) * BR_BK + kk];
+        g.pdb[(size_t)rb * BR_C + tid] = sum;
     }
     // dW partial: this workgroup's 128 x 128 column tile of its row block's slot
     if (!awave) {
@@ -354,7 +368,7 @@ __global__ __launch_bounds__(BR_THREADS, 1) void bwd_ring_kernel(const BwdRingAr
 #pragma unroll
         for (int ks = 0; ks < BR_NK; ++ks)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) part[(ks * 32 + br_acc_row(r, h)) * CI] = R[ks][r];
+            for (int r = 0; r < 16; ++r) part[(ks * 32 + br_acc_row(r, h)) * CI] = R[ks][r] + R[4 + ks][r];
     }
 }
 

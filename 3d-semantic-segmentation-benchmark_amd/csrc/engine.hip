@@ -135,9 +135,10 @@ static bool materialize_dz_of(const pcs_mlp_layer& P, int M, bool dgrad) {
     return dz_passes(M, (int)P.cout, (int)P.cin, dgrad, P.dW != nullptr) >= kDzPasses;
 }
 
-// the ring kernel (bwd_ring.hip) takes every eligible 128-wide BNBWD inner layer unless the layer's
-// policy turns fusion off
-static bool ring_wanted(int policy) { return policy != PCS_BWD_FUSE_OFF; }
+// the ring kernel (bwd_ring.hip) takes the eligible 128-wide BNBWD inner layers under policy 'all'
+// only: isolated it runs 127 us per FP1 layer (0.43 of the fp32 MFMA peak) and the PointNet++ step
+// measured 4.80 ms with it against 4.55 ms on the default dgrad + lane-wgrad pair
+static bool ring_wanted(int policy) { return policy == PCS_BWD_FUSE_ALL; }
 
 // Rotation depth of a backward's dA / kB / alpha buffers.  The dgrad of layer l reuses the buffers
 // that layer l + kRot - 1's wgrad reads, so it must wait for that wgrad on the lane; with kRot = 6 no

@@ -27,6 +27,9 @@
 // up to fp32 summation order.
 #include "pcs_common.hpp"
 
+#include <algorithm>
+#include <cmath>
+
 namespace pcs {
 
 constexpr unsigned kInfBits = 0x7f800000u;
@@ -409,6 +412,286 @@ __device__ __forceinline__ void adjust3(H3& h, float v, int i) {
 
 __device__ __forceinline__ bool lt_vi(float va, int ia, float vb, int ib) { return va < vb || (va == vb && ia < ib); }
 
+// ------------------------------------------------------------------ heap path over a cell grid
+// The heap select (partial_sort) on a ball: the heap starts as the first k queue entries
+// (indices 0..k-1, out-of-radius ones at +inf) and entry i >= k replaces the top only when its
+// value is strictly below it -- an out-of-radius entry (+inf) never is.  So the only entries that
+// can change the heap are the IN-RADIUS points with index >= k, and they act in ascending index
+// order.  This kernel visits just those: one workgroup bins its cloud into cells of edge >= r
+// (counting sort in LDS), so every in-radius point of a centroid lies in the 3 x 3 x 3 cells
+// around the centroid's cell; a wave marks the in-radius points >= k of those cells in a bitmap
+// of the cloud's indices, walks the bitmap in ascending index order (compacted into a list) and
+// runs the same lane-heap surgery as heap_select_kernel on them -- the same heap states, so the
+// same index set, ties and underfull balls included.  Work per centroid: the points of 27 cells
+// instead of all N (PointNeXt SA1: ~600 of 24 576).
+constexpr int kGridBlock = 1024;               // 16 waves share the cloud's grid
+constexpr int kGridWaves = kGridBlock / kWave;
+constexpr int kGridList = 512;                 // per-wave candidate list (u16), filled in rounds
+constexpr int kGridU = 4;                      // 64-candidate batches with their loads in flight together
+
+struct GridLds {
+    int* cend;                 // [ncells]: end of cell c in `sorted` (start = cend[c - 1], 0 for c = 0)
+    unsigned short* sorted;    // [N]: point indices grouped by cell
+    unsigned* bm;              // [waves][nw] candidate bitmaps
+    unsigned short* list;      // [waves][kGridList]
+};
+
+__device__ __forceinline__ int grid_axis(float x, float lo, float inv, int n) {
+    const float u = (x - lo) * inv;
+    // NaN and below-range coordinates -> 0, above-range -> n - 1
+    return u >= 1.f ? (int)fminf(u, (float)(n - 1)) : 0;
+}
+
+__global__ __launch_bounds__(kGridBlock) void grid_heap_select_kernel(Geo g, float cs0, int max_cells,
+                                                                      int rows_per_wave) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char g_lds[];
+    __shared__ float s_box[kGridWaves][6];
+    __shared__ float s_geo[4];                 // lo x, y, z, 1 / cell edge
+    __shared__ int s_dim[3];
+    const int b = blockIdx.y, N = g.N, K = g.K;
+    const int nw = (N + 31) >> 5;
+    const float* X = g.xyz + (size_t)b * N * 3;
+    GridLds L;
+    size_t off = 0;
+    L.cend = reinterpret_cast<int*>(g_lds + off);
+    off += (size_t)max_cells * 4;
+    L.sorted = reinterpret_cast<unsigned short*>(g_lds + off);
+    off += ((size_t)N * 2 + 15) / 16 * 16;
+    L.bm = reinterpret_cast<unsigned*>(g_lds + off);
+    off += (size_t)kGridWaves * nw * 4;
+    L.list = reinterpret_cast<unsigned short*>(g_lds + off);
+    const float* P = X;                        // (clouds past 8192 points: coordinates from L2)
+    const int tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
+
+    // ---- bounding box (NaN coordinates ignored by fminf / fmaxf)
+    float bx[6] = {__builtin_inff(), __builtin_inff(), __builtin_inff(), -__builtin_inff(), -__builtin_inff(),
+                   -__builtin_inff()};
+    for (int p = tid; p < N; p += kGridBlock) {
+        const float x = X[3 * p], y = X[3 * p + 1], z = X[3 * p + 2];
+        bx[0] = fminf(bx[0], x); bx[1] = fminf(bx[1], y); bx[2] = fminf(bx[2], z);
+        bx[3] = fmaxf(bx[3], x); bx[4] = fmaxf(bx[4], y); bx[5] = fmaxf(bx[5], z);
+    }
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1)
+#pragma unroll
+        for (int k = 0; k < 6; ++k) bx[k] = k < 3 ? fminf(bx[k], __shfl_xor(bx[k], m)) : fmaxf(bx[k], __shfl_xor(bx[k], m));
+    if (lane == 0)
+        for (int k = 0; k < 6; ++k) s_box[wv][k] = bx[k];
+    __syncthreads();
+    if (tid == 0) {
+        float lo[3], ext[3];
+        bool fin = true;
+        for (int k = 0; k < 3; ++k) {
+            float a = s_box[0][k], c = s_box[0][k + 3];
+            for (int w = 1; w < kGridWaves; ++w) { a = fminf(a, s_box[w][k]); c = fmaxf(c, s_box[w][k + 3]); }
+            lo[k] = a;
+            ext[k] = c - a;
+            fin = fin && ext[k] >= 0.f && ext[k] < 3.0e38f;
+        }
+        // cell edge: >= 1.02 r (cs0), and >= 2^-16 of the largest extent, so that with the fp32
+        // rounding of (x - lo) * inv (<= 2^-22 of the extent / edge) two points within r land in
+        // cells at most one apart on every axis; grown until the cell count fits the LDS table
+        double cs = cs0;
+        if (fin) cs = fmax(cs, (double)fmaxf(ext[0], fmaxf(ext[1], ext[2])) * (1.0 / 65536.0));
+        long long n[3] = {1, 1, 1};
+        for (int guard = 0; fin && guard < 64; ++guard) {
+            for (int k = 0; k < 3; ++k) n[k] = (long long)((double)ext[k] / cs) + 1;
+            if (n[0] * n[1] * n[2] <= max_cells) break;
+            cs *= 1.25;
+        }
+        if (!fin || n[0] * n[1] * n[2] > max_cells) n[0] = n[1] = n[2] = 1;
+        for (int k = 0; k < 3; ++k) { s_geo[k] = fin ? lo[k] : 0.f; s_dim[k] = (int)n[k]; }
+        s_geo[3] = fin ? (float)(1.0 / cs) : 0.f;
+    }
+    __syncthreads();
+    const float lox = s_geo[0], loy = s_geo[1], loz = s_geo[2], inv = s_geo[3];
+    const int gx = s_dim[0], gy = s_dim[1], gz = s_dim[2];
+    const int nc = gx * gy * gz;
+    auto cell_of = [&](float x, float y, float z) {
+        return grid_axis(x, lox, inv, gx) + gx * (grid_axis(y, loy, inv, gy) + gy * grid_axis(z, loz, inv, gz));
+    };
+    // ---- counting sort of the point indices by cell (the order inside a cell is irrelevant: the
+    // bitmap restores index order)
+    for (int c = tid; c < nc; c += kGridBlock) L.cend[c] = 0;
+    __syncthreads();
+    for (int p = tid; p < N; p += kGridBlock) atomicAdd(&L.cend[cell_of(P[3 * p], P[3 * p + 1], P[3 * p + 2])], 1);
+    __syncthreads();
+    {
+        // exclusive scan of the counts: each thread a run of consecutive cells, then the runs
+        const int per = (nc + kGridBlock - 1) / kGridBlock;
+        const int c0 = tid * per, c1 = min(c0 + per, nc);
+        int sum = 0;
+        for (int c = c0; c < c1; ++c) sum += L.cend[c];
+        int inc = sum;
+#pragma unroll
+        for (int m = 1; m < 64; m <<= 1) {
+            const int o = __shfl_up(inc, m);
+            inc += lane >= m ? o : 0;
+        }
+        __shared__ int s_ws[kGridWaves];
+        if (lane == 63) s_ws[wv] = inc;
+        __syncthreads();
+        int base = 0;
+        for (int w = 0; w < wv; ++w) base += s_ws[w];
+        int run = base + inc - sum;
+        for (int c = c0; c < c1; ++c) {
+            const int n = L.cend[c];
+            L.cend[c] = run;                   // start of cell c, advanced to its end by the scatter
+            run += n;
+        }
+    }
+    __syncthreads();
+    for (int p = tid; p < N; p += kGridBlock) {
+        const int c = cell_of(P[3 * p], P[3 * p + 1], P[3 * p + 2]);
+        L.sorted[atomicAdd(&L.cend[c], 1)] = (unsigned short)p;
+    }
+    __syncthreads();
+
+    // ---- the rows: one wave each
+    unsigned* bm = L.bm + (size_t)wv * nw;
+    unsigned short* list = L.list + (size_t)wv * kGridList;
+    const int wave = blockIdx.x * kGridWaves + wv;
+    for (int rr = 0; rr < rows_per_wave; ++rr) {
+        const int row = wave * rows_per_wave + rr;
+        if (row >= g.R) break;
+        const float* c = g.cent + ((size_t)b * g.R + row) * 3;
+        const float cx = c[0], cy = c[1], cz = c[2];
+        // the heap: the first K queue entries (K <= 64 <= N)
+        LaneHeap h;
+        {
+            const unsigned v = dist_bits(sqdist_unfused(P[3 * lane], P[3 * lane + 1], P[3 * lane + 2], cx, cy, cz), g);
+            h.v = v;
+            h.i = (unsigned)lane;
+            h.make(K);
+        }
+        unsigned top = h.gv(0);
+        for (int w = lane; w < nw; w += kWave) bm[w] = 0u;
+        wave_sync();
+        // in-radius points >= K of the 27 cells -> bitmap.  The x-adjacent cells of one (y, z) are one
+        // run of `sorted`: lane q < 9 takes run q, the 9 runs are flattened into one index space and
+        // walked GU x 64 entries at a time, all their coordinate loads in flight together
+        const int ix = grid_axis(cx, lox, inv, gx), iy = grid_axis(cy, loy, inv, gy), iz = grid_axis(cz, loz, inv, gz);
+        const int xl = max(ix - 1, 0), xh = min(ix + 1, gx - 1);
+        int rbeg = 0, rlen = 0;
+        if (lane < 9) {
+            const int y = iy + lane % 3 - 1, z = iz + lane / 3 - 1;
+            if (y >= 0 && y < gy && z >= 0 && z < gz) {
+                const int cl = xl + gx * (y + gy * z), ch = xh + gx * (y + gy * z);
+                rbeg = cl == 0 ? 0 : L.cend[cl - 1];
+                rlen = L.cend[ch] - rbeg;
+            }
+        }
+        int rinc = rlen;
+#pragma unroll
+        for (int m = 1; m < 16; m <<= 1) {
+            const int o = __shfl_up(rinc, m);
+            rinc += lane >= m ? o : 0;
+        }
+        const int T = __builtin_amdgcn_readlane(rinc, 8);
+        int pre[9], bg[9];
+#pragma unroll
+        for (int q = 0; q < 9; ++q) {
+            pre[q] = __builtin_amdgcn_readlane(rinc - rlen, q);
+            bg[q] = __builtin_amdgcn_readlane(rbeg, q);
+        }
+        for (int j0 = 0; j0 < T; j0 += kGridU * kWave) {
+            int pp[kGridU];
+            float qx[kGridU], qy[kGridU], qz[kGridU];
+#pragma unroll
+            for (int u = 0; u < kGridU; ++u) {
+                const int j = j0 + u * kWave + lane;
+                int b0 = bg[0], p0 = pre[0];
+#pragma unroll
+                for (int q = 1; q < 9; ++q)
+                    if (j >= pre[q]) { b0 = bg[q]; p0 = pre[q]; }
+                pp[u] = j < T ? (int)L.sorted[b0 + j - p0] : -1;
+            }
+#pragma unroll
+            for (int u = 0; u < kGridU; ++u) {
+                const int p = pp[u] < 0 ? 0 : pp[u];
+                qx[u] = P[3 * p]; qy[u] = P[3 * p + 1]; qz[u] = P[3 * p + 2];
+            }
+#pragma unroll
+            for (int u = 0; u < kGridU; ++u) {
+                const int p = pp[u];
+                if (p >= K && sqdist_unfused(qx[u], qy[u], qz[u], cx, cy, cz) <= g.r2)
+                    atomicOr(&bm[p >> 5], 1u << (p & 31));
+            }
+        }
+        wave_sync();
+        // ascending walk: lane l owns words [l * wpl, (l + 1) * wpl), its candidates land in the list
+        // at its exclusive prefix; rounds of kGridList list entries
+        const int wpl = (nw + kWave - 1) / kWave;
+        const int w0 = min(lane * wpl, nw), w1 = min(w0 + wpl, nw);
+        int cnt = 0;
+        for (int w = w0; w < w1; ++w) cnt += __popc(bm[w]);
+        int incl = cnt;
+#pragma unroll
+        for (int m = 1; m < 64; m <<= 1) {
+            const int o = __shfl_up(incl, m);
+            incl += lane >= m ? o : 0;
+        }
+        const int total = __builtin_amdgcn_readlane(incl, 63);
+        const int first = incl - cnt;
+        for (int r0 = 0; r0 < total; r0 += kGridList) {
+            // this round's entries [r0, r0 + kGridList)
+            if (first < r0 + kGridList && first + cnt > r0) {
+                int pos = first;
+                for (int w = w0; w < w1 && pos < r0 + kGridList; ++w) {
+                    unsigned m = bm[w];
+                    while (m) {
+                        const int bit = __ffs(m) - 1;
+                        m &= m - 1;
+                        if (pos >= r0 && pos < r0 + kGridList) list[pos - r0] = (unsigned short)(32 * w + bit);
+                        ++pos;
+                    }
+                }
+            }
+            wave_sync();
+            const int n = min(kGridList, total - r0);
+            for (int base = 0; base < n; base += kGridU * kWave) {
+                // GU x 64 candidates' coordinates in flight together, then the heap in list order
+                unsigned vv[kGridU], pv[kGridU];
+#pragma unroll
+                for (int u = 0; u < kGridU; ++u) {
+                    const int j = base + u * kWave + lane;
+                    pv[u] = j < n ? list[j] : 0u;
+                }
+#pragma unroll
+                for (int u = 0; u < kGridU; ++u) {
+                    const int j = base + u * kWave + lane;
+                    const unsigned p = pv[u];
+                    vv[u] = j < n ? dist_bits(sqdist_unfused(P[3 * p], P[3 * p + 1], P[3 * p + 2], cx, cy, cz), g)
+                                  : kInfBits;
+                }
+#pragma unroll
+                for (int u = 0; u < kGridU; ++u) {
+                    unsigned long long mk = ballot(vv[u] < top);
+                    while (mk) {
+                        const int l = ffs64(mk);
+                        mk &= mk - 1;
+                        const unsigned v = readlane_u(vv[u], l);
+                        if (v < top) {
+                            h.adjust(0, K, v, readlane_u(pv[u], l));
+                            top = h.gv(0);
+                        }
+                    }
+                }
+            }
+            wave_sync();
+        }
+        emit_sorted(h.v, h.i, K, g.out_idx + ((size_t)b * g.R + row) * K,
+                    g.out_dist ? g.out_dist + ((size_t)b * g.R + row) * K : nullptr);
+    }
+}
+
+// LDS bytes of a grid launch (grid_heap_select_kernel's layout)
+static size_t grid_lds_bytes(int N, int max_cells) {
+    const size_t nw = (size_t)(N + 31) / 32;
+    return (size_t)max_cells * 4 + ((size_t)N * 2 + 15) / 16 * 16 + (size_t)kGridWaves * nw * 4 +
+           (size_t)kGridWaves * kGridList * 2;
+}
+
 template <bool STAGE>
 __global__ __launch_bounds__(256) void three_nn_kernel(Geo g) {
     extern __shared__ __attribute__((aligned(16))) float s_xyz[];
@@ -468,6 +751,11 @@ __global__ __launch_bounds__(256) void three_nn_kernel(Geo g) {
 }
 
 constexpr int kStageMaxPoints = 8192;  // 96 KB of LDS
+// the grid kernel where the exhaustive heap kernel cannot stage the cloud in LDS (N > 8192: it then
+// streams every point of the cloud from L2 for every centroid); up to 8192 points the staged
+// exhaustive scan measured as fast (PointNet++ SA1: 312 vs 280 us, profiles/r06_ballq.txt)
+constexpr int kGridMinPoints = kStageMaxPoints + 1;
+constexpr size_t kGridLdsMax = 160 * 1024 - 1024;   // dynamic LDS cap (the kernel's static arrays take < 1 KB)
 // one row per wave on both paths: a prefetched plan's blocks then retire quickly and let the step
 // stream's kernels in (profiles/r05_ab_geometry_blocks.txt)
 constexpr int kRowsPerWave = 1;
@@ -491,6 +779,25 @@ static int run_select(Geo g, hipStream_t s, const char* what) {
         if (stage) hipLaunchKernelGGL(three_nn_kernel<true>, grid, dim3(256), xyz_lds, s, g);
         else hipLaunchKernelGGL(three_nn_kernel<false>, grid, dim3(256), 0, s, g);
         return launch_status(what);
+    }
+    if (heap_path && g.use_radius && g.K <= 64 && g.N >= kGridMinPoints) {
+        // ball query on the heap path: over the cell grid (grid_heap_select_kernel), when its LDS fits
+        const int cells = 8192;
+        const size_t lds = grid_lds_bytes(g.N, cells);
+        if (lds <= kGridLdsMax) {
+            // rows per wave: about one workgroup per CU over the launch (each builds its cloud's grid)
+            const long long waves_total = (long long)kGridWaves * 256;
+            const int rpw = (int)std::max<long long>(1, ((long long)g.B * g.R + waves_total - 1) / waves_total);
+            const int waves = (g.R + rpw - 1) / rpw;
+            const dim3 grid((waves + kGridWaves - 1) / kGridWaves, g.B);
+            const float cs0 = (float)(std::sqrt((double)g.r2) * 1.02) + 1e-30f;
+            ProbeScope pr(s, flops, bytes, "pcs::grid_heap_select_kernel");
+            static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&grid_heap_select_kernel),
+                                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kGridLdsMax);
+            (void)attr;
+            hipLaunchKernelGGL(grid_heap_select_kernel, grid, dim3(kGridBlock), lds, s, g, cs0, cells, rpw);
+            return launch_status(what);
+        }
     }
     if (heap_path) {
         PCS_CHECK_ARG(g.K <= 64, "%s: k=%d > 64 not supported on the heap path", what, g.K);

@@ -238,8 +238,7 @@ def test_pointnetpp_three_way_b32_bench_dispatch():
     with KernelProbe() as kp:
         rows = three_way(lambda: pcseg.PointNetpp(14), lambda: R.PointNetpp(14), 32, 4096, 131)
     names = {r[0] for r in kp.records()}
-    for k in ('pcs::fwd_dma_kernel<', 'pcs::bwd_ring_kernel<128>', 'pcs::bwd_ring_kernel<256>',
-              'pcs::dgrad_kernel<true, 64, 3, 2>',
+    for k in ('pcs::fwd_dma_kernel<', 'pcs::dgrad_kernel<true, 128, 2, 1>', 'pcs::dgrad_kernel<true, 64, 3, 2>',
               'pcs::fused_bwd_kernel<64, 32, 3>', 'pcs::fused_bwd_kernel<32, 32, 2>',
               'pcs::csr_bwd_stream_kernel<'):
         assert any(n.startswith(k) for n in names), (k, sorted(names))

@@ -69,11 +69,33 @@ def test_ball_query_golden(golden, case):
     (4, 4096, 1024, 0.1, 32, 'surface'), (4, 1024, 256, 0.2, 32, 'surface'), (4, 256, 64, 0.4, 32, 'surface'),
     (4, 64, 16, 0.8, 32, 'surface'), (2, 1024, 1024, 0.1, 32, 'surface'), (2, 4096, 512, 0.1, 32, 'uniform'),
     (2, 2047, 300, 0.3, 32, 'dup'), (2, 2048, 300, 0.3, 32, 'dup'), (2, 16, 16, 0.8, 16, 'surface'),
-    (2, 3000, 100, 0.05, 16, 'surface'), (1, 24576, 1024, 0.1, 32, 'surface'), (2, 100, 50, 2.0, 32, 'uniform')])
+    (2, 3000, 100, 0.05, 16, 'surface'), (1, 24576, 1024, 0.1, 32, 'surface'), (2, 100, 50, 2.0, 32, 'uniform'),
+    (2, 8192, 512, 0.1, 32, 'surface'), (2, 4096, 256, 0.8, 32, 'surface'), (1, 24576, 512, 0.1, 32, 'dup'),
+    (2, 12000, 700, 0.8, 32, 'surface'), (2, 9000, 400, 0.1, 16, 'uniform'),
+    (2, 6000, 300, 0.1, 64, 'uniform')])
 def test_ball_query_matches_oracle(B, N, C, r, K, kind):
+    """Index sets equal to the reference's (topk over the radius-masked distances).  N > 8192 with
+    k * 64 <= N runs the cell-grid heap path (grid_heap_select_kernel): underfull (uniform) and
+    duplicate-heavy clouds, r = 0.8 (few cells), k = 16 and 32; smaller clouds the staged exhaustive
+    heap kernel."""
     xyz = cloud(B, N, seed=7 * N + C, kind=kind)
     start = torch.zeros(B, dtype=torch.int32)
     cent = xyz[torch.arange(B).view(B, 1), R.fps_indices(xyz, C, start).long()]
+    ref = R.ball_query(cent, xyz, r, K)
+    got = ops.ball_query(cent.to(DEV), xyz.to(DEV), r, K).cpu()
+    assert torch.equal(sorted_rows(got), sorted_rows(ref))
+
+
+@pytest.mark.parametrize('N,r,K', [(12000, 0.2, 32), (24576, 0.1, 32), (9000, 0.05, 32)])
+def test_ball_query_arbitrary_centroids(N, r, K):
+    """Centroids that are not cloud points, some outside the cloud's box (clamped to its edge
+    cells), some on cell boundaries: the grid path's candidate cells still hold every in-radius point."""
+    B, C = 2, 300
+    xyz = cloud(B, N, seed=N + 3)
+    g = torch.Generator().manual_seed(N)
+    cent = torch.rand(B, C, 3, generator=g) * torch.tensor([1.4, 1.4, 3.4]) - 0.2
+    cent[:, :40] = xyz[:, :40] + r * (torch.rand(B, 40, 3, generator=g) - 0.5)
+    cent[:, 40:60] = torch.round(cent[:, 40:60] / r) * r
     ref = R.ball_query(cent, xyz, r, K)
     got = ops.ball_query(cent.to(DEV), xyz.to(DEV), r, K).cpu()
     assert torch.equal(sorted_rows(got), sorted_rows(ref))
