@@ -113,10 +113,99 @@ __device__ __forceinline__ void emit_sorted(unsigned v, unsigned i, int k, int* 
     }
 }
 
+
+// ------------------------------------------------------------------ ball query: the unambiguous case
+// A ball's candidates held in (value, index) slots: slot 0 = the queue's first K entries (lanes < K;
+// +inf out of radius), slots 1..S = in-radius entries of index >= K, list entry 64 (s - 1) + lane in
+// ascending index order (n of them).  When at least K of them are finite and the K-th smallest value
+// is strictly below the (K+1)-th, BOTH libstdc++ selections the reference's topk runs (SURVEY.md
+// Appendix A) return exactly the K smallest: partial_sort's heap keeps every excluded entry at or
+// above its final top (entries only enter strictly below the top, and the top never rises), and
+// nth_element partitions around the K-th.  Then the set is found by a radix search for the K-th
+// smallest value bits -- no heap surgery.  Ties at the boundary and underfull balls (whose surviving
+// infs the heap order picks) take the exact emulation.
+template <int S>
+__device__ bool ball_unambiguous(const unsigned (&vs)[S + 1], const unsigned (&xs)[S + 1], int K, int n, uint2* scratch,
+                                 int* out_idx, float* out_dist) {
+    const int lane = lane_id();
+    int finite = 0;
+#pragma unroll
+    for (int u = 0; u <= S; ++u) finite += popc64(ballot(vs[u] != kInfBits && (u > 0 || lane < K)));
+    if (finite < K) return false;
+    // T = the smallest value bits with count(v <= T) >= K (values finite, below +inf bits)
+    unsigned lo = 0u, hi = kInfBits - 1u;
+    while (lo < hi) {
+        const unsigned mid = lo + ((hi - lo) >> 1);
+        int c = 0;
+#pragma unroll
+        for (int u = 0; u <= S; ++u) c += popc64(ballot(vs[u] <= mid && (u > 0 || lane < K)));
+        if (c >= K) hi = mid;
+        else lo = mid + 1u;
+    }
+    int base = 0;
+    unsigned long long sel[S + 1];
+#pragma unroll
+    for (int u = 0; u <= S; ++u) {
+        sel[u] = ballot(vs[u] <= lo && (u > 0 || lane < K));
+        base += popc64(sel[u]);
+    }
+    if (base != K) return false;               // a tie straddles the K-th value
+    base = 0;
+#pragma unroll
+    for (int u = 0; u <= S; ++u) {
+        if ((sel[u] >> lane) & 1ull) scratch[base + popc64(sel[u] & lanemask_lt())] = make_uint2(vs[u], xs[u]);
+        base += popc64(sel[u]);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (lane < K) {
+        // canonical order: ascending value, then index
+        const uint2 me = scratch[lane];
+        int rank = 0;
+        for (int j = 0; j < K; ++j) {
+            const uint2 o = scratch[j];
+            rank += (o.x < me.x || (o.x == me.x && o.y < me.y)) ? 1 : 0;
+        }
+        out_idx[rank] = (int)me.y;
+        if (out_dist) out_dist[rank] = __uint_as_float(me.x);
+    }
+    return true;
+}
+
+// the exact heap select over the same slots (partial_sort's make_heap on the first K entries, then
+// the in-radius entries of index >= K in index order)
+template <int S>
+__device__ void ball_heap_slots(const unsigned (&vs)[S + 1], const unsigned (&xs)[S + 1], int K, int n, int* out_idx,
+                                float* out_dist) {
+    LaneHeap h;
+    h.v = vs[0];
+    h.i = xs[0];
+    h.make(K);
+    unsigned top = h.gv(0);
+#pragma unroll
+    for (int u = 1; u <= S; ++u) {
+        unsigned long long mk = ballot(64 * (u - 1) + lane_id() < n && vs[u] < top);
+        while (mk) {
+            const int l = ffs64(mk);
+            mk &= mk - 1;
+            const unsigned v = readlane_u(vs[u], l);
+            if (v < top) {
+                h.adjust(0, K, v, readlane_u(xs[u], l));
+                top = h.gv(0);
+            }
+        }
+    }
+    emit_sorted(h.v, h.i, K, out_idx, out_dist);
+}
+
 // 1024-thread blocks: 16 waves share one staged cloud (48 KB at N = 4096), so LDS allows
 // 8 waves per SIMD instead of 3 -- the heap surgery is a latency-bound chain of
 // v_readlane / SALU hops per wave, and occupancy is what hides it.
 constexpr int kHeapBlock = 1024;
+
+constexpr int kFastS = 2;                      // list slots per lane of the staged ball path (128 entries: 24 KB per
+                                               // block, so two 1024-thread blocks still share a CU at N = 4096)
 
 template <bool STAGE>
 __global__ __launch_bounds__(kHeapBlock) void heap_select_kernel(Geo g, int rows_per_wave) {
@@ -131,11 +220,51 @@ __global__ __launch_bounds__(kHeapBlock) void heap_select_kernel(Geo g, int rows
     const int lane = lane_id();
     const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int K = g.K;
+    // ball queries (staged cloud): per wave a 64 * kFastS-entry list of the in-radius entries of index >= K
+    // and K output slots, after the cloud in the dynamic LDS
+    uint2* wl = reinterpret_cast<uint2*>(s_xyz + ((size_t)g.N * 3 + 3) / 4 * 4) + (size_t)(threadIdx.x >> 6) * (64 * kFastS + 64);
     for (int rr = 0; rr < rows_per_wave; ++rr) {
         const int row = wave * rows_per_wave + rr;
         if (row >= g.R) break;
         const float* c = g.cent + ((size_t)b * g.R + row) * 3;
         const float cx = c[0], cy = c[1], cz = c[2];
+        int* oi = g.out_idx + ((size_t)b * g.R + row) * K;
+        float* od = g.out_dist ? g.out_dist + ((size_t)b * g.R + row) * K : nullptr;
+
+        if (STAGE && g.use_radius) {
+            // one pass over the cloud: the first K entries, and the in-radius ones of index >= K in order
+            // (into a 64 * kFastS-entry list)
+            unsigned vs[kFastS + 1], xs[kFastS + 1];
+            int n = 0;
+            for (int base = 0; base < g.N; base += kWave) {
+                const int p = base + lane;
+                unsigned v = kInfBits;
+                if (p < g.N) v = dist_bits(sqdist_unfused(P[3 * p], P[3 * p + 1], P[3 * p + 2], cx, cy, cz), g);
+                if (base == 0) { vs[0] = lane < K ? v : kInfBits; xs[0] = (unsigned)lane; }
+                const bool in = p >= K && p < g.N && v != kInfBits;
+                const unsigned long long m = ballot(in);
+                const int pos = n + popc64(m & lanemask_lt());
+                if (in && pos < 64 * kFastS) wl[pos] = make_uint2(v, (unsigned)p);
+                n += popc64(m);
+            }
+            if (n <= 64 * kFastS) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+                for (int u = 1; u <= kFastS; ++u) {
+                    const int j = 64 * (u - 1) + lane;
+                    const uint2 e = j < n ? wl[j] : make_uint2(kInfBits, 0u);
+                    vs[u] = e.x;
+                    xs[u] = e.y;
+                }
+                __builtin_amdgcn_wave_barrier();
+                if (!ball_unambiguous<kFastS>(vs, xs, K, n, wl + 64 * kFastS, oi, od))
+                    ball_heap_slots<kFastS>(vs, xs, K, n, oi, od);
+                continue;
+            }
+            // (more than 64 * kFastS in-radius entries: the exhaustive heap pass below)
+        }
 
         LaneHeap h;
         h.v = kInfBits;
@@ -163,8 +292,7 @@ __global__ __launch_bounds__(kHeapBlock) void heap_select_kernel(Geo g, int rows
                 }
             }
         }
-        emit_sorted(h.v, h.i, K, g.out_idx + ((size_t)b * g.R + row) * K,
-                    g.out_dist ? g.out_dist + ((size_t)b * g.R + row) * K : nullptr);
+        emit_sorted(h.v, h.i, K, oi, od);
     }
 }
 
@@ -428,6 +556,7 @@ constexpr int kGridBlock = 1024;               // 16 waves share the cloud's gri
 constexpr int kGridWaves = kGridBlock / kWave;
 constexpr int kGridList = 512;                 // per-wave candidate list (u16), filled in rounds
 constexpr int kGridU = 4;                      // 64-candidate batches with their loads in flight together
+constexpr int kGridS = kGridList / 64;         // list slots per lane of the one-list (fast) path
 
 struct GridLds {
     int* cend;                 // [ncells]: end of cell c in `sorted` (start = cend[c - 1], 0 for c = 0)
@@ -556,15 +685,8 @@ __global__ __launch_bounds__(kGridBlock) void grid_heap_select_kernel(Geo g, flo
         if (row >= g.R) break;
         const float* c = g.cent + ((size_t)b * g.R + row) * 3;
         const float cx = c[0], cy = c[1], cz = c[2];
-        // the heap: the first K queue entries (K <= 64 <= N)
-        LaneHeap h;
-        {
-            const unsigned v = dist_bits(sqdist_unfused(P[3 * lane], P[3 * lane + 1], P[3 * lane + 2], cx, cy, cz), g);
-            h.v = v;
-            h.i = (unsigned)lane;
-            h.make(K);
-        }
-        unsigned top = h.gv(0);
+        // the queue's first K entries (K <= 64 <= N): the heap's initial contents
+        const unsigned v0 = dist_bits(sqdist_unfused(P[3 * lane], P[3 * lane + 1], P[3 * lane + 2], cx, cy, cz), g);
         for (int w = lane; w < nw; w += kWave) bm[w] = 0u;
         wave_sync();
         // in-radius points >= K of the 27 cells -> bitmap.  The x-adjacent cells of one (y, z) are one
@@ -633,6 +755,47 @@ __global__ __launch_bounds__(kGridBlock) void grid_heap_select_kernel(Geo g, flo
         }
         const int total = __builtin_amdgcn_readlane(incl, 63);
         const int first = incl - cnt;
+        int* oi = g.out_idx + ((size_t)b * g.R + row) * K;
+        float* od = g.out_dist ? g.out_dist + ((size_t)b * g.R + row) * K : nullptr;
+        if (total <= kGridList) {
+            // one list: the candidates' values into slots, then the unambiguous K smallest or the heap
+            int pos = first;
+            for (int w = w0; w < w1; ++w) {
+                unsigned m = bm[w];
+                while (m) {
+                    const int bit = __ffs(m) - 1;
+                    m &= m - 1;
+                    list[pos++] = (unsigned short)(32 * w + bit);
+                }
+            }
+            wave_sync();
+            unsigned vs[kGridS + 1], xs[kGridS + 1];
+            vs[0] = lane < K ? v0 : kInfBits;
+            xs[0] = (unsigned)lane;
+#pragma unroll
+            for (int u = 1; u <= kGridS; ++u) {
+                const int j = 64 * (u - 1) + lane;
+                xs[u] = j < total ? list[j] : 0u;
+            }
+#pragma unroll
+            for (int u = 1; u <= kGridS; ++u) {
+                const int j = 64 * (u - 1) + lane;
+                const unsigned p = xs[u];
+                vs[u] = j < total ? dist_bits(sqdist_unfused(P[3 * p], P[3 * p + 1], P[3 * p + 2], cx, cy, cz), g)
+                                  : kInfBits;
+            }
+            wave_sync();
+            if (!ball_unambiguous<kGridS>(vs, xs, K, total, reinterpret_cast<uint2*>(list), oi, od))
+                ball_heap_slots<kGridS>(vs, xs, K, total, oi, od);
+            wave_sync();
+            continue;
+        }
+        // more candidates than one list: the exact heap over rounds of the list
+        LaneHeap h;
+        h.v = v0;
+        h.i = (unsigned)lane;
+        h.make(K);
+        unsigned top = h.gv(0);
         for (int r0 = 0; r0 < total; r0 += kGridList) {
             // this round's entries [r0, r0 + kGridList)
             if (first < r0 + kGridList && first + cnt > r0) {
@@ -680,8 +843,7 @@ __global__ __launch_bounds__(kGridBlock) void grid_heap_select_kernel(Geo g, flo
             }
             wave_sync();
         }
-        emit_sorted(h.v, h.i, K, g.out_idx + ((size_t)b * g.R + row) * K,
-                    g.out_dist ? g.out_dist + ((size_t)b * g.R + row) * K : nullptr);
+        emit_sorted(h.v, h.i, K, oi, od);
     }
 }
 
@@ -806,7 +968,15 @@ static int run_select(Geo g, hipStream_t s, const char* what) {
         constexpr int wpb = kHeapBlock / kWave;
         const dim3 grid((waves + wpb - 1) / wpb, g.B);
         ProbeScope pr(s, flops, bytes, "pcs::heap_select_kernel<%s>", stage ? "true" : "false");
-        if (stage) hipLaunchKernelGGL(heap_select_kernel<true>, grid, dim3(kHeapBlock), xyz_lds, s, g, rows_per_wave);
+        // (ball queries: per wave 64 * kFastS list entries + 64 output slots of 8 B after the cloud)
+        const size_t hl = xyz_lds + (g.use_radius ? (size_t)wpb * (64 * kFastS + 64) * 8 : 0);
+        if (stage) {
+            static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&heap_select_kernel<true>),
+                                                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                               (int)(kStageMaxPoints * 12 + wpb * (64 * kFastS + 64) * 8));
+            (void)attr;
+            hipLaunchKernelGGL(heap_select_kernel<true>, grid, dim3(kHeapBlock), hl, s, g, rows_per_wave);
+        }
         else hipLaunchKernelGGL(heap_select_kernel<false>, grid, dim3(kHeapBlock), 0, s, g, rows_per_wave);
         return launch_status(what);
     }
