@@ -309,6 +309,275 @@ __global__ __launch_bounds__(BLOCK) void fps_kernel(const float* __restrict__ xy
     }
 }
 
+// ------------------------------------------------------------------ FPS with spatial culling
+// The same selection as fps_kernel (squared running minima as float bits, the window / flag fast
+// path, the exact sqrt slow path) with the points of a cloud REORDERED spatially: a counting sort
+// by a 16 x 16 x 16 Morton-ordered cell grid over the cloud's box gives each thread PPT consecutive
+// points of that order, i.e. a compact region, and its bounding box.  A step's new centroid can
+// lower a point's minimum only if its distance is below that minimum, so a thread whose box lies
+// farther from the centroid than its largest minimum skips the update (a wave whose threads all
+// skip issues nothing): after the first few dozen steps most of the cloud is far from each new
+// centroid.  The skip test keeps a 2^-18 relative margin over the box distance, which covers the
+// fp32 rounding of both the box distance and the point distance, so a skipped point's minimum is
+// exactly what the update would have left.  Ties and the window test use the points' ORIGINAL
+// indices (looked up in the sorted-index table), so the pick -- the reference's first index of
+// the largest sqrt distance -- does not depend on the storage order, and the in-cell order of the
+// (atomic) counting sort does not matter.
+constexpr int kCullCells = 4096;              // 16^3 Morton cells
+constexpr float kCullMargin = 0.999996f;      // 1 - 2^-18
+constexpr size_t kCullLdsMax = 160 * 1024 - 1024;   // dynamic LDS cap (the static slots take < 1 KB)
+
+__device__ __forceinline__ unsigned morton16(unsigned x, unsigned y, unsigned z) {
+    auto spread = [](unsigned v) {             // 4 bits -> every third bit
+        v = (v | (v << 4)) & 0x0C3u;
+        v = (v | (v << 2)) & 0x249u;
+        return v;
+    };
+    return spread(x) | (spread(y) << 1) | (spread(z) << 2);
+}
+
+template <int BLOCK, int PPT, bool LDSC>
+__global__ __launch_bounds__(BLOCK) void fps_cull_kernel(const float* __restrict__ xyz, int N, int C,
+                                                         const int* __restrict__ start, int* __restrict__ out_idx,
+                                                         float* __restrict__ out_xyz) {
+    constexpr int NW = BLOCK / kWave;
+    static_assert(NW == 4 || NW == 8 || NW == 16, "slot reduction width");
+    __shared__ __attribute__((aligned(16))) uint2 s_slot[2][NW];
+    __shared__ __attribute__((aligned(16))) uint2 s_key[NW];
+    __shared__ float s_box[NW][6];
+    // dynamic LDS: [C centroids (16 B) | sorted original index per position (u16, N) | cell counts
+    // (kCullCells ints) | x | y | z of the N points (LDSC)]
+    extern __shared__ float4 fps_lds[];
+    const bool lds_out = C <= kFpsLdsOut;
+    float4* s_out = fps_lds;
+    unsigned short* s_ord = reinterpret_cast<unsigned short*>(fps_lds + (lds_out ? C : 0));
+    int* s_cnt = reinterpret_cast<int*>(s_ord + ((N + 7) & ~7));
+    float* s_px = reinterpret_cast<float*>(s_cnt + kCullCells);
+    float* s_py = s_px + N;
+    float* s_pz = s_py + N;
+
+    const int b = blockIdx.x;
+    const int t = threadIdx.x;
+    const int w = t >> 6, lane = t & 63;
+    const float* P = xyz + (size_t)b * N * 3;
+
+    // ---- the cloud's box and the cell of every point (16 cells per axis over the box)
+    float bx[6] = {__builtin_inff(), __builtin_inff(), __builtin_inff(), -__builtin_inff(), -__builtin_inff(),
+                   -__builtin_inff()};
+    for (int p = t; p < N; p += BLOCK) {
+        const float x = P[3 * p], y = P[3 * p + 1], z = P[3 * p + 2];
+        if (LDSC) { s_px[p] = x; s_py[p] = y; s_pz[p] = z; }
+        bx[0] = fminf(bx[0], x); bx[1] = fminf(bx[1], y); bx[2] = fminf(bx[2], z);
+        bx[3] = fmaxf(bx[3], x); bx[4] = fmaxf(bx[4], y); bx[5] = fmaxf(bx[5], z);
+    }
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1)
+#pragma unroll
+        for (int k = 0; k < 6; ++k) bx[k] = k < 3 ? fminf(bx[k], __shfl_xor(bx[k], m)) : fmaxf(bx[k], __shfl_xor(bx[k], m));
+    if (lane == 0)
+        for (int k = 0; k < 6; ++k) s_box[w][k] = bx[k];
+    for (int c = t; c < kCullCells; c += BLOCK) s_cnt[c] = 0;
+    __syncthreads();
+    float lo[3], sc[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        float a = s_box[0][k], e = s_box[0][k + 3];
+        for (int v = 1; v < NW; ++v) { a = fminf(a, s_box[v][k]); e = fmaxf(e, s_box[v][k + 3]); }
+        lo[k] = a;
+        const float ext = e - a;
+        sc[k] = ext > 0.f && ext < 3.0e38f ? 16.f / ext : 0.f;   // degenerate / non-finite: one cell
+    }
+    auto cell_of = [&](float x, float y, float z) {
+        const float u[3] = {(x - lo[0]) * sc[0], (y - lo[1]) * sc[1], (z - lo[2]) * sc[2]};
+        unsigned c[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) c[k] = u[k] >= 1.f ? (unsigned)fminf(u[k], 15.f) : 0u;
+        return morton16(c[0], c[1], c[2]);
+    };
+    for (int p = t; p < N; p += BLOCK) atomicAdd(&s_cnt[cell_of(P[3 * p], P[3 * p + 1], P[3 * p + 2])], 1);
+    __syncthreads();
+    if (w == 0) {
+        // exclusive scan of the 4096 counts by one wave: 64 runs of 64
+        int sum = 0;
+        for (int c = 64 * lane; c < 64 * lane + 64; ++c) sum += s_cnt[c];
+        int inc = sum;
+#pragma unroll
+        for (int m = 1; m < 64; m <<= 1) {
+            const int o = __shfl_up(inc, m);
+            inc += lane >= m ? o : 0;
+        }
+        int run = inc - sum;
+        for (int c = 64 * lane; c < 64 * lane + 64; ++c) {
+            const int n = s_cnt[c];
+            s_cnt[c] = run;
+            run += n;
+        }
+    }
+    __syncthreads();
+    for (int p = t; p < N; p += BLOCK)
+        s_ord[atomicAdd(&s_cnt[cell_of(P[3 * p], P[3 * p + 1], P[3 * p + 2])], 1)] = (unsigned short)p;
+    __syncthreads();
+
+    // ---- this thread's PPT consecutive points of the spatial order, their box
+    float px[PPT], py[PPT], pz[PPT];
+    unsigned best[PPT];
+    float tb[6] = {__builtin_inff(), __builtin_inff(), __builtin_inff(), -__builtin_inff(), -__builtin_inff(),
+                   -__builtin_inff()};
+#pragma unroll
+    for (int j = 0; j < PPT; ++j) {
+        const int q = t * PPT + j;
+        if (q < N) {
+            const int p = s_ord[q];
+            px[j] = LDSC ? s_px[p] : P[3 * p];
+            py[j] = LDSC ? s_py[p] : P[3 * p + 1];
+            pz[j] = LDSC ? s_pz[p] : P[3 * p + 2];
+            best[j] = 0x7f800000u;
+            tb[0] = fminf(tb[0], px[j]); tb[1] = fminf(tb[1], py[j]); tb[2] = fminf(tb[2], pz[j]);
+            tb[3] = fmaxf(tb[3], px[j]); tb[4] = fmaxf(tb[4], py[j]); tb[5] = fmaxf(tb[5], pz[j]);
+        } else {
+            px[j] = py[j] = pz[j] = 0.f;
+            best[j] = 0u;                      // padding: never above a real point, never a candidate
+        }
+    }
+    // NaN coordinates make the box test fail (never skip) -- the update then runs as fps_kernel's
+    unsigned Mt = 0x7f800000u;                // this thread's largest minimum (bits)
+
+    int far = start[b];
+    far = far < 0 ? 0 : (far >= N ? N - 1 : far);
+    float cx = LDSC ? s_px[far] : P[3 * far], cy = LDSC ? s_py[far] : P[3 * far + 1],
+          cz = LDSC ? s_pz[far] : P[3 * far + 2];
+    const int q0 = t * PPT;
+
+    for (int i = 0; i < C; ++i) {
+        if (t == 0) {
+            if (lds_out) {
+                s_out[i] = make_float4(cx, cy, cz, __int_as_float(far));
+            } else {
+                out_idx[(size_t)b * C + i] = far;
+                float* o = out_xyz + ((size_t)b * C + i) * 3;
+                o[0] = cx;
+                o[1] = cy;
+                o[2] = cz;
+            }
+        }
+        if (i == C - 1) break;
+
+        // ---- update (skipped when the box is provably farther than every minimum of the thread)
+        const float ex = fmaxf(fmaxf(tb[0] - cx, cx - tb[3]), 0.f);
+        const float ey = fmaxf(fmaxf(tb[1] - cy, cy - tb[4]), 0.f);
+        const float ez = fmaxf(fmaxf(tb[2] - cz, cz - tb[5]), 0.f);
+        const float d2b = (ex * ex + ey * ey + ez * ez) * kCullMargin;
+        if (!(d2b > __uint_as_float(Mt))) {
+            unsigned M = 0u;
+            if constexpr (PPT % 2 == 0) {
+                const f32x2 c2x = {cx, cx}, c2y = {cy, cy}, c2z = {cz, cz};
+#pragma unroll
+                for (int j = 0; j < PPT; j += 2) {
+                    const f32x2 dx = f32x2{px[j], px[j + 1]} - c2x;
+                    const f32x2 dy = f32x2{py[j], py[j + 1]} - c2y;
+                    const f32x2 dz = f32x2{pz[j], pz[j + 1]} - c2z;
+                    const f32x2 d = __builtin_elementwise_fma(dz, dz, __builtin_elementwise_fma(dy, dy, dx * dx));
+                    best[j] = min(__float_as_uint(d.x), best[j]);
+                    best[j + 1] = min(__float_as_uint(d.y), best[j + 1]);
+                    M = max(M, max(best[j], best[j + 1]));
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < PPT; ++j) {
+                    const float dx = px[j] - cx, dy = py[j] - cy, dz = pz[j] - cz;
+                    const float d = __fmaf_rn(dz, dz, __fmaf_rn(dy, dy, __fmul_rn(dx, dx)));
+                    best[j] = min(__float_as_uint(d), best[j]);
+                    M = max(M, best[j]);
+                }
+            }
+            Mt = M;
+        }
+        const unsigned wk = wave_umax(q0 < N ? Mt + 1u : 0u);
+        const unsigned mw = wk - 1u;
+        const unsigned wlo = wk == 0u ? 0xFFFFFFFFu : (mw > kFpsWin ? mw - kFpsWin : 0u);
+        // lowest ORIGINAL index of this thread whose value lies in the window, and that value
+        unsigned ci = 0xFFFFFFFFu, cv = 0u;
+        if (Mt >= wlo && q0 < N) {
+#pragma unroll
+            for (int j = 0; j < PPT; ++j) {
+                if (best[j] >= wlo) {
+                    const unsigned id = s_ord[q0 + j];
+                    cv = id < ci ? best[j] : cv;
+                    ci = id < ci ? id : ci;
+                }
+            }
+        }
+        const unsigned key = (ci << 1) | (cv != mw ? 1u : 0u);
+        const unsigned wkey = wave_umin(key);
+        const int buf = i & 1;
+        if (lane == 0) s_slot[buf][w] = make_uint2(wk, wkey);
+        __syncthreads();
+        const uint2 sl = lane < NW ? s_slot[buf][lane] : make_uint2(0u, 0xFFFFFFFFu);
+        const unsigned Ms = slot_umax<NW>(sl.x);
+        const unsigned slo = Ms > kFpsWin + 1u ? Ms - kFpsWin : 1u;
+        const bool near = sl.x >= slo && (sl.x != Ms || (sl.y & 1u));
+        const unsigned fk = slot_umin<NW>(sl.x == Ms ? sl.y : 0xFFFFFFFFu);
+        if (__builtin_expect(ballot(near) == 0ull, 1)) {
+            far = (int)(fk >> 1);
+        } else {
+            unsigned kx = 0u, ky = 0xFFFFFFFFu;
+            if (wk != 0u) {
+                const float S = sqrt_cr(__uint_as_float(mw));
+                const unsigned lo2 = sqrt_class_lo(S);
+                unsigned cand = 0xFFFFFFFFu;
+                if (Mt >= lo2 && q0 < N) {
+#pragma unroll
+                    for (int j = 0; j < PPT; ++j)
+                        if (best[j] >= lo2) cand = min(cand, (unsigned)s_ord[q0 + j]);
+                }
+                kx = __float_as_uint(S) + 1u;
+                ky = wave_umin(cand);
+            }
+            if (lane == 0) s_key[w] = make_uint2(kx, ky);
+            __syncthreads();
+            const uint2 k2 = lane < NW ? s_key[lane] : make_uint2(0u, 0xFFFFFFFFu);
+            const unsigned bs = slot_umax<NW>(k2.x);
+            far = (int)slot_umin<NW>(k2.x == bs ? k2.y : 0xFFFFFFFFu);
+        }
+        if constexpr (LDSC) {
+            cx = s_px[far];
+            cy = s_py[far];
+            cz = s_pz[far];
+        } else {
+            cx = P[3 * far + 0];
+            cy = P[3 * far + 1];
+            cz = P[3 * far + 2];
+        }
+    }
+    if (lds_out) {
+        __syncthreads();
+        for (int i = t; i < C; i += BLOCK) {
+            const float4 q = s_out[i];
+            out_idx[(size_t)b * C + i] = __float_as_int(q.w);
+            float* o = out_xyz + ((size_t)b * C + i) * 3;
+            o[0] = q.x;
+            o[1] = q.y;
+            o[2] = q.z;
+        }
+    }
+}
+
+static size_t fps_cull_lds_bytes(int N, int C, bool ldsc) {
+    return (C <= kFpsLdsOut ? (size_t)C * 16 : 0) + (size_t)((N + 7) & ~7) * 2 + (size_t)kCullCells * 4 +
+           (ldsc ? (size_t)N * 12 : 0);
+}
+
+template <int BLOCK, int PPT, bool LDSC>
+static void launch_fps_cull(const float* xyz, int B, int N, int C, const int* start, int* out_idx, float* out_xyz,
+                            hipStream_t s) {
+    static const hipError_t attr = hipFuncSetAttribute(
+        reinterpret_cast<const void*>(&fps_cull_kernel<BLOCK, PPT, LDSC>), hipFuncAttributeMaxDynamicSharedMemorySize,
+        (int)kCullLdsMax);
+    (void)attr;
+    hipLaunchKernelGGL((fps_cull_kernel<BLOCK, PPT, LDSC>), dim3(B), dim3(BLOCK), fps_cull_lds_bytes(N, C, LDSC), s,
+                       xyz, N, C, start, out_idx, out_xyz);
+}
+
 // dynamic LDS of one FPS launch (fps_kernel's layout)
 static size_t fps_lds_bytes(int N, int C) {
     return (C <= kFpsLdsOut ? (size_t)C * 16 : 0) + (N <= kFpsLdsCloud ? (size_t)N * 12 : 0);
@@ -325,9 +594,21 @@ static void launch_fps_lds(const float* xyz, int B, int N, int C, const int* sta
                        out_idx, out_xyz);
 }
 
+// the culled kernel for clouds past the LDS copy (N > 8192; PointNeXt's 24 576: 1.91 -> 1.57 ms at
+// B = 16, C = 1024); at 4 096 points its sort and box tests cost more than the culling saves
+// (0.82 vs 0.69 ms at B = 32), so smaller clouds keep fps_kernel
+constexpr int kCullMinPoints = kFpsLdsCloud + 1;
+
 template <int BLOCK, int PPT>
 static void launch_fps(const float* xyz, int B, int N, int C, const int* start, int* out_idx, float* out_xyz,
                        hipStream_t s) {
+    if constexpr (BLOCK >= 256) {
+        if (N >= kCullMinPoints && fps_cull_lds_bytes(N, C, N <= kFpsLdsCloud) <= kCullLdsMax) {
+            if (N <= kFpsLdsCloud) launch_fps_cull<BLOCK, PPT, true>(xyz, B, N, C, start, out_idx, out_xyz, s);
+            else launch_fps_cull<BLOCK, PPT, false>(xyz, B, N, C, start, out_idx, out_xyz, s);
+            return;
+        }
+    }
     if (N <= kFpsLdsCloud) launch_fps_lds<BLOCK, PPT, true>(xyz, B, N, C, start, out_idx, out_xyz, s);
     else launch_fps_lds<BLOCK, PPT, false>(xyz, B, N, C, start, out_idx, out_xyz, s);
 }
@@ -351,7 +632,9 @@ PCS_API int pcs_fps(const float* xyz, int B, int N, int C, const int32_t* start,
     const double flops = 8.0 * B * (double)N * C, bytes = (double)B * (12.0 * N + 16.0 * C);
 #define PCS_FPS_CASE(BL, PP)                                                                    \
     if (blk == BL && ppt <= PP) {                                                               \
-        ProbeScope pr(s, flops, bytes, "pcs::fps_kernel<%d, %d, %s>", BL, PP,                 \
+        ProbeScope pr(s, flops, bytes, "pcs::%s<%d, %d, %s>",                                    \
+                      BL >= 256 && N >= kCullMinPoints && fps_cull_lds_bytes(N, C, N <= kFpsLdsCloud) <= \
+                      kCullLdsMax ? "fps_cull_kernel" : "fps_kernel", BL, PP,                    \
                       N <= kFpsLdsCloud ? "true" : "false");                                    \
         launch_fps<BL, PP>(xyz, B, N, C, start, out_idx, out_xyz, s);                           \
     } else

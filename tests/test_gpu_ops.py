@@ -35,7 +35,8 @@ def sorted_rows(idx):
 # ----------------------------------------------------------------------------- FPS
 @pytest.mark.parametrize('B,N,C,kind', [(2, 4096, 1024, 'surface'), (3, 1024, 256, 'surface'), (2, 256, 64, 'uniform'),
                                         (2, 64, 16, 'surface'), (2, 1000, 333, 'dup'), (1, 24576, 1024, 'surface'),
-                                        (2, 5000, 1200, 'uniform'), (1, 37, 37, 'dup'), (4, 2048, 512, 'dup')])
+                                        (2, 5000, 1200, 'uniform'), (1, 37, 37, 'dup'), (4, 2048, 512, 'dup'),
+                                        (2, 12000, 700, 'dup'), (1, 9000, 2000, 'uniform'), (1, 30000, 1024, 'surface')])
 def test_fps_bit_exact(B, N, C, kind):
     xyz = cloud(B, N, seed=N + C, kind=kind)
     start = torch.randint(0, N, (B,), dtype=torch.int32, generator=torch.Generator().manual_seed(N))
