@@ -1,6 +1,6 @@
 """Host-side (Python) profile of the drop-in harness-A step (bench.run_drop_in: torch.optim.Adam,
 zero_grad, forward, criterion, backward, step on the default stream, no prefetch): where the
-enqueue time goes.  usage: python scripts/host_profile_dropin.py [model] [batch]"""
+enqueue time goes.  usage: python scripts/host_profile_dropin.py [model] [batch] [points]"""
 import cProfile
 import os
 import pstats
@@ -18,12 +18,13 @@ from pcseg.synthetic import make_batch  # noqa: E402
 
 key = sys.argv[1] if len(sys.argv) > 1 else 'pointnetpp'
 B = int(sys.argv[2]) if len(sys.argv) > 2 else 32
+NPTS = int(sys.argv[3]) if len(sys.argv) > 3 else 4096
 name, ctor, kind = bench.WORKLOADS[key][:3]
 dev = torch.device('cuda', 0)
 torch.manual_seed(0)
 model = ctor(pcseg).to(dev).train()
 opt = torch.optim.Adam(model.parameters(), lr=1e-3)
-pts, labels, lengths = make_batch(B, 4096, seed=2000)
+pts, labels, lengths = make_batch(B, NPTS, seed=2000)
 x = bench.model_input(pts.to(dev), kind)
 lab = (labels.float() if kind == 'chfirst6' else labels).to(dev)
 lengths = lengths.to(dev)
