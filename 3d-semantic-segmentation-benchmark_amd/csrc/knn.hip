@@ -24,6 +24,7 @@
 // candidate still passes the (lower) threshold.
 // knn_kernel (k = 40): one thread per query row with a sorted register list.
 #include "pcs_common.hpp"
+#include <algorithm>
 
 namespace pcs {
 
@@ -526,6 +527,567 @@ __global__ __launch_bounds__(256) void knn_sqnorm_kernel(const float* __restrict
     }
 }
 
+// ----------------------------------------------------------------------------- pruned kNN
+// The same lists as knn_wave_kernel from a fraction of its tiles.  pcs_knn_order sorts each
+// cloud's points by the Morton code of their xyz; in that order 32 consecutive points form a
+// compact tile in coordinate space, and -- DGCNN's EdgeConv features being functions of the local
+// geometry -- mostly in feature space too.  knn_tiles_kernel summarises every tile in feature space
+// (centroid, bounding radius, axis-aligned box, largest squared norm); knn_pruned_kernel gives each
+// wave one tile of query rows, sorts the candidate tiles by a lower bound of the squared distance
+// between the two tiles (sphere and box bounds), and scans them nearest first until a tile's bound
+// exceeds the loosest row's threshold: every later tile is then provably worse than each row's
+// current k-th best.  Skipping is exact: the bound is deflated for its own fp32 rounding and for
+// the rounding of the scan's pd (2^-13 (|x_q|^2 + |x_c|^2) covers it, cf. the seeded margin), a
+// skipped candidate's pd is strictly below the row's running threshold (so it could not even tie
+// the final k-th), and the survivors that remain are ranked by the same (pd, original index) order.
+// Any order is correct (a permutation of the cloud); a good one makes the scan short.
+constexpr int KO_MAX = 8192;                 // points per cloud the LDS Morton sort takes
+constexpr int KP_NT = KO_MAX / KNN_TC;       // candidate tiles per cloud of the pruned kernel
+
+__host__ __device__ constexpr int knn_tile_stride(int F) { return ((3 * F + 2) + 3) & ~3; }
+
+__device__ __forceinline__ void knn_wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ unsigned knn_spread3(unsigned v) {
+    v &= 1023u;
+    v = (v | (v << 16)) & 0x030000FFu;
+    v = (v | (v << 8)) & 0x0300F00Fu;
+    v = (v | (v << 4)) & 0x030C30C3u;
+    v = (v | (v << 2)) & 0x09249249u;
+    return v;
+}
+
+// one cloud per block: 10-bit-per-axis Morton keys of the first three features over the cloud's
+// bounding cube, bitonic-sorted in LDS as (key, index) pairs (ties: lower index first); P = the
+// padded power of two.  Non-finite coordinates quantise to cell 0.
+__global__ __launch_bounds__(1024) void knn_order_kernel(const float* __restrict__ x, int N, int F, int P,
+                                                         int* __restrict__ order) {
+    extern __shared__ unsigned long long s_key[];
+    __shared__ float s_red[16][6];
+    const int b = blockIdx.x, tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+    const float* X = x + (size_t)b * N * F;
+    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int i = tid; i < N; i += 1024) {
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            const float v = X[(size_t)i * F + a];
+            if (fabsf(v) <= 3.4e38f) {
+                lo[a] = fminf(lo[a], v);
+                hi[a] = fmaxf(hi[a], v);
+            }
+        }
+    }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = fminf(lo[a], __shfl_xor(lo[a], m));
+            hi[a] = fmaxf(hi[a], __shfl_xor(hi[a], m));
+        }
+    }
+    if (l == 0) {
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            s_red[w][a] = lo[a];
+            s_red[w][3 + a] = hi[a];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        float mn = s_red[0][a], mx = s_red[0][3 + a];
+        for (int j = 1; j < 16; ++j) {
+            mn = fminf(mn, s_red[j][a]);
+            mx = fmaxf(mx, s_red[j][3 + a]);
+        }
+        lo[a] = mn;
+        hi[a] = mx;
+    }
+    const float ext = fmaxf(fmaxf(hi[0] - lo[0], hi[1] - lo[1]), hi[2] - lo[2]);
+    const float scale = ext > 0.f && ext <= 3.4e38f ? 1023.f / ext : 0.f;
+    for (int i = tid; i < P; i += 1024) {
+        unsigned long long key = ~0ull;
+        if (i < N) {
+            unsigned m = 0;
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                float t = (X[(size_t)i * F + a] - lo[a]) * scale;
+                t = t == t ? fminf(fmaxf(t, 0.f), 1023.f) : 0.f;
+                m |= knn_spread3((unsigned)t) << a;
+            }
+            key = ((unsigned long long)m << 32) | (unsigned)i;
+        }
+        s_key[i] = key;
+    }
+    __syncthreads();
+    for (int k = 2; k <= P; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = tid; i < (P >> 1); i += 1024) {
+                const int a = 2 * j * (i / j) + (i % j), c = a + j;
+                const unsigned long long u = s_key[a], v = s_key[c];
+                if ((u > v) == ((a & k) == 0)) {
+                    s_key[a] = v;
+                    s_key[c] = u;
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (int i = tid; i < N; i += 1024) order[(size_t)b * N + i] = (int)(unsigned)(s_key[i] & 0xffffffffull);
+}
+
+__global__ __launch_bounds__(256) void knn_identity_order_kernel(long long P, int N, int* __restrict__ order) {
+    const long long p = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (p < P) order[p] = (int)(p % N);
+}
+
+// one wave per (tile, cloud): lane d < F owns feature d.  Per cloud, field-major (element [f][t] at
+// f * nt + t, so a wave reading one field of 64 tiles reads 256 contiguous bytes): centroid rows
+// [0, F), box low [F, 2F), box high [2F, 3F), radius (3F), largest |x|^2 (3F + 1); a cloud spans
+// knn_tile_stride(F) * nt floats.  A tile with a non-finite feature gets a NaN radius (its bounds
+// are never used to skip).
+template <int F>
+__global__ __launch_bounds__(64) void knn_tiles_kernel(const float* __restrict__ x, int N, const int* __restrict__ order,
+                                                       const float* __restrict__ xx, float* __restrict__ tinfo) {
+    static_assert(F <= 64, "one lane per feature");
+    constexpr int TS = knn_tile_stride(F);
+    const int t = blockIdx.x, b = blockIdx.y, l = threadIdx.x;
+    const int nt = (N + KNN_TC - 1) / KNN_TC;
+    const int p0 = t * KNN_TC, np = min(KNN_TC, N - p0);
+    const float* X = x + (size_t)b * N * F;
+    const int* O = order + (size_t)b * N;
+    float lo = INFINITY, hi = -INFINITY, sum = 0.f;
+    bool bad = false;
+    for (int j = 0; j < np; ++j) {
+        const int oi = min(max(O[p0 + j], 0), N - 1);
+        const float v = l < F ? X[(size_t)oi * F + l] : 0.f;
+        bad = bad || !(fabsf(v) <= 3.4e38f);
+        lo = fminf(lo, v);
+        hi = fmaxf(hi, v);
+        sum += v;
+    }
+    const float cen = sum / (float)np;
+    float r2 = 0.f;
+    for (int j = 0; j < np; ++j) {
+        const int oi = min(max(O[p0 + j], 0), N - 1);
+        const float v = l < F ? X[(size_t)oi * F + l] : 0.f;
+        float d = l < F ? (v - cen) * (v - cen) : 0.f;
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) d += __shfl_xor(d, m);
+        r2 = fmaxf(r2, d);
+    }
+    float mxx = l < np ? xx[(size_t)b * N + min(max(O[p0 + l], 0), N - 1)] : 0.f;
+    bad = bad || !(fabsf(mxx) <= 3.4e38f);
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) mxx = fmaxf(mxx, __shfl_xor(mxx, m));
+    bad = ballot(bad) != 0ull;
+    float* rec = tinfo + (size_t)b * nt * TS + t;
+    if (l < F) {
+        rec[(size_t)l * nt] = cen;
+        rec[(size_t)(F + l) * nt] = lo;
+        rec[(size_t)(2 * F + l) * nt] = hi;
+    }
+    if (l == 0) {
+        rec[(size_t)(3 * F) * nt] = bad ? NAN : sqrtf(r2) * (1.f + 0x1p-10f);
+        rec[(size_t)(3 * F + 1) * nt] = mxx;
+    }
+}
+
+// lower bound of the pd margin below which tile `ti` cannot reach any row of tile `tq` (squared
+// feature distance, deflated for rounding); -inf when unusable (NaN / overflow)
+template <int F>
+__device__ __forceinline__ float knn_tile_bound(const float* __restrict__ TI, int nt, int tq, int t) {
+    float cd = 0.f, gap = 0.f;
+#pragma unroll 8
+    for (int d = 0; d < F; ++d) {
+        const float cq = TI[d * nt + tq], ct = TI[d * nt + t];
+        const float lq = TI[(F + d) * nt + tq], hq = TI[(2 * F + d) * nt + tq];
+        const float lt = TI[(F + d) * nt + t], ht = TI[(2 * F + d) * nt + t];
+        const float df = cq - ct;
+        cd = fmaf(df, df, cd);
+        const float g = fmaxf(fmaxf(lq - ht, lt - hq), 0.f);
+        gap = fmaf(g, g, gap);
+    }
+    const float rs = TI[3 * F * nt + tq] + TI[3 * F * nt + t];
+    float sph = fmaxf(sqrtf(cd) * (1.f - 0x1p-10f) - rs, 0.f);
+    sph *= sph;
+    const float lb = fmaxf(sph, gap) * (1.f - 0x1p-10f) - 0x1p-13f * (TI[(3 * F + 1) * nt + tq] + TI[(3 * F + 1) * nt + t]);
+    return (lb == lb && rs == rs && cd == cd) ? lb : -INFINITY;
+}
+
+// The k-th largest of a row's values over one or two tiles: M = 16 or 32 per lane half (-inf for
+// invalid slots).  Each half sorts its M (bitonic network, descending), takes the partner half's
+// sorted M by shuffles, and k-th(A u B) = max over splits i of min(A[i-1], B[k-i-1]).  All
+// indices compile-time.
+template <int K, int M>
+__device__ __forceinline__ float knn_tile_kth(const float (&pd)[M]) {
+    static_assert(K <= 2 * M, "k-th of 2M");
+    float v[M];
+#pragma unroll
+    for (int r = 0; r < M; ++r) v[r] = pd[r];
+#pragma unroll
+    for (int k = 2; k <= M; k <<= 1)
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1)
+#pragma unroll
+            for (int i = 0; i < M; ++i) {
+                const int p = i ^ j;
+                if (p > i) {
+                    const bool desc = (i & k) == 0;
+                    const float x = v[i], y = v[p];
+                    v[i] = desc ? fmaxf(x, y) : fminf(x, y);
+                    v[p] = desc ? fminf(x, y) : fmaxf(x, y);
+                }
+            }
+    float best = -INFINITY;
+#pragma unroll
+    for (int i = 0; i <= K; ++i) {
+        const int j = K - i;                               // taken from the partner's list
+        if (i > M || j > M) continue;
+        const float av = i == 0 ? INFINITY : v[i - 1];
+        const float bv = j == 0 ? INFINITY : __shfl_xor(v[j - 1], 32);
+        best = fmaxf(best, fminf(av, bv));
+    }
+    return best;
+}
+
+// Per cloud and query tile: every candidate tile's bound (knn_tile_bound), sorted ascending (ties by
+// tile) -> the scan order of the pruned kernel, (B, nt, nt) tile ids and their bounds.  One block
+// per (KP_PQ query tiles, cloud): thread t reads candidate tile t's fields once (coalesced) for all
+// KP_PQ query tiles, then ranks within LDS.
+constexpr int KP_PQ = 4;
+template <int F>
+__global__ __launch_bounds__(KP_NT) void knn_pairs_kernel(const float* __restrict__ tinfo, int N, int* __restrict__ sorted_t,
+                                                       float* __restrict__ sorted_lb) {
+    constexpr int TS = knn_tile_stride(F);
+    __shared__ float s_b[KP_PQ][KP_NT];
+    const int b = blockIdx.y, t = threadIdx.x;
+    const int nt = (N + KNN_TC - 1) / KNN_TC;
+    const int tq0 = blockIdx.x * KP_PQ;
+    const float* TI = tinfo + (size_t)b * nt * TS;
+#pragma unroll
+    for (int r = 0; r < KP_PQ; ++r) {
+        const int tq = min(tq0 + r, nt - 1);
+        s_b[r][t] = t < nt ? knn_tile_bound<F>(TI, nt, tq, t) : INFINITY;
+    }
+    __syncthreads();
+    if (t >= nt) return;
+#pragma unroll
+    for (int r = 0; r < KP_PQ; ++r) {
+        const int tq = tq0 + r;
+        if (tq >= nt) break;
+        const float v = s_b[r][t];
+        int rk = 0;
+        for (int u = 0; u < nt; u += 4) {
+            const float4 o = *reinterpret_cast<const float4*>(&s_b[r][u]);
+            rk += (u + 0 < nt && (o.x < v || (o.x == v && u + 0 < t))) ? 1 : 0;
+            rk += (u + 1 < nt && (o.y < v || (o.y == v && u + 1 < t))) ? 1 : 0;
+            rk += (u + 2 < nt && (o.z < v || (o.z == v && u + 2 < t))) ? 1 : 0;
+            rk += (u + 3 < nt && (o.w < v || (o.w == v && u + 3 < t))) ? 1 : 0;
+        }
+        const size_t row = ((size_t)b * nt + tq) * nt;
+        sorted_t[row + rk] = t;
+        sorted_lb[row + rk] = v;
+    }
+}
+
+#ifdef PCS_KNN_DIAG
+// diagnostic build: per wave (b, tile) 8 ints: tiles scanned, running merges, then the cycles of
+// setup (seeds, bounds, sort), scan and final merge
+__device__ int g_knn_diag[8 << 13];
+#define KNN_STAMP(v) do { asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory"); } while (0)
+#else
+#define KNN_STAMP(v) do { (void)(v); } while (0)
+#endif
+
+// knn_wave_kernel's scan (PRE norms) over the candidate tiles of a Morton-ordered cloud, nearest
+// first, stopping at the first tile whose bound exceeds every row's threshold.  Rows and
+// candidates are addressed through `order`; survivors carry original indices.
+template <int F, int K, int WPB, bool SEEDED>
+__global__ __launch_bounds__(64 * WPB, 2) void knn_pruned_kernel(const float* __restrict__ x, int B, int N, int rblocks,
+                                                              int* __restrict__ out_idx, const float* __restrict__ xx_pre,
+                                                              const int* __restrict__ order,
+                                                              const int* __restrict__ sorted_t,
+                                                              const float* __restrict__ sorted_lb,
+                                                              const int* __restrict__ seeds, int ks) {
+    constexpr bool MF = (F % 4 == 0);
+    static_assert(MF || F == 3, "F must be 3 or a multiple of 4");
+    constexpr int FH = MF ? F / 2 : 2;
+    constexpr int NQ = MF ? FH / 4 : 1;
+    constexpr int SEG = (KNN_NMAX - K) / 2;
+    constexpr int CAP = SEG - 1;
+    static_assert(CAP >= 16, "a segment must take one tile's 16 candidates after a merge");
+    __shared__ float2 s_cc[WPB][KNN_TC];          // (|x_c|^2, original index) of the tile in the MFMA
+    __shared__ float2 s_it[32 * WPB * KNN_RS];
+    __shared__ float s_lb[WPB][KP_NT];            // this wave's scan order (knn_pairs_kernel): bounds
+    __shared__ int s_tl[WPB][KP_NT];              // and candidate tiles, ascending
+
+    const int L = blockIdx.x;
+    const int total = B * rblocks;
+    int b, rb;
+    if (total % 8 == 0 && (total / 8) % rblocks == 0) {
+        const int per = total / 8;
+        const int j = (L % 8) * per + L / 8;
+        b = j / rblocks;
+        rb = j - b * rblocks;
+    } else {
+        b = L / rblocks;
+        rb = L - b * rblocks;
+    }
+    const int tid = threadIdx.x;
+    const int w = tid >> 6, l = tid & 63, h = l >> 5, l32 = l & 31;
+    const int tq = rb * WPB + w;                                  // this wave's query tile
+    const int nt = (N + KNN_TC - 1) / KNN_TC;
+    if (tq >= nt) return;                                         // (no barriers below)
+    unsigned long long st0 = 0, st1 = 0, st2 = 0, st3 = 0, sta = 0, stb = 0;
+    int merges = 0;
+    KNN_STAMP(st0);
+    const float* X = x + (size_t)b * N * F;
+    const int* O = order + (size_t)b * N;
+    const int pq = tq * KNN_TC + l32;
+    // order entries are clamped into the cloud (memory safety; a non-permutation gives wrong lists)
+    const int qi = min(max(O[min(pq, N - 1)], 0), N - 1);
+    PCS_DCHECK(O[min(pq, N - 1)] == qi, "knn order entry %d outside the cloud (N %d)", O[min(pq, N - 1)], N);
+    float2* const wl = s_it + (w * 32) * KNN_RS;
+    float2* const sg = wl + l32 * KNN_RS + K + h * SEG;
+
+    float a[FH];
+    if constexpr (MF) {
+        const float* xr = X + (size_t)qi * F + h * FH;
+#pragma unroll
+        for (int s = 0; s < FH; s += 4) {
+            const float4 v = *reinterpret_cast<const float4*>(xr + s);
+            a[s] = v.x; a[s + 1] = v.y; a[s + 2] = v.z; a[s + 3] = v.w;
+        }
+    } else {
+        const float* xr = X + (size_t)qi * 3;
+        a[0] = h ? xr[2] : xr[0];
+        a[1] = h ? 0.f : xr[1];
+    }
+    const float xxq = xx_pre[(size_t)b * N + qi];
+    float tau = -INFINITY;
+    if constexpr (SEEDED) {
+        const int* sr = seeds + ((size_t)b * N + qi) * ks;
+        float t0 = INFINITY;
+        bool ok = ks >= K;
+        int prev[K];
+        const int nsd = ks < K ? 0 : K;
+        for (int j = 0; j < nsd; ++j) {
+            const int sj = sr[j];
+            ok = ok && sj >= 0 && sj < N;
+            const int sc = (sj >= 0 && sj < N) ? sj : 0;
+#pragma unroll
+            for (int u = 0; u < K; ++u) ok = ok && !(u < j && prev[u] == sc);
+#pragma unroll
+            for (int u = 0; u < K; ++u) prev[u] = u == j ? sc : prev[u];
+            float part = 0.f;
+            if constexpr (MF) {
+                const float4* src = reinterpret_cast<const float4*>(X + (size_t)sc * F + h * FH);
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) {
+                    const float4 v = src[q];
+                    part = __fmaf_rn(a[4 * q], v.x, part);
+                    part = __fmaf_rn(a[4 * q + 1], v.y, part);
+                    part = __fmaf_rn(a[4 * q + 2], v.z, part);
+                    part = __fmaf_rn(a[4 * q + 3], v.w, part);
+                }
+            } else {
+                const float* sp = X + (size_t)sc * 3;
+                part = __fmaf_rn(a[1], h ? 0.f : sp[1], __fmul_rn(a[0], h ? sp[2] : sp[0]));
+            }
+            const float dot = __fadd_rn(part, __shfl_xor(part, 32));
+            const float cx = xx_pre[(size_t)b * N + sc];
+            const float pd = __fsub_rn(__fsub_rn(-xxq, -2.f * dot), cx);
+            t0 = fminf(t0, __fsub_rn(pd, ldexpf(__fadd_rn(xxq, cx), -14)));
+        }
+        tau = ok ? t0 : -INFINITY;
+    }
+    // the loosest row's threshold as a squared distance: -min over rows of tau (+inf while any
+    // row has fewer than k candidates)
+    auto loosest = [&]() {
+        float m = tau;
+#pragma unroll
+        for (int s = 32; s >= 1; s >>= 1) m = fminf(m, __shfl_xor(m, s));
+        return -m;
+    };
+
+    // this wave's scan order: the candidate tiles by ascending bound (knn_pairs_kernel)
+    KNN_STAMP(sta);
+    {
+        const size_t row = ((size_t)b * nt + tq) * nt;
+        for (int i = l; i < nt; i += 64) {
+            s_tl[w][i] = sorted_t[row + i];
+            s_lb[w][i] = sorted_lb[row + i];
+        }
+    }
+    KNN_STAMP(stb);
+    knn_wave_sync();
+
+    int cnt = 0, nl = 0;
+    float thr = loosest();
+    float4 cur[NQ], nxt[NQ];
+    int ci_cur = 0, ci_nxt = 0;                  // this lane's candidate (original index)
+    float cxx_cur = 0.f, cxx_nxt = 0.f;
+    auto fetch = [&](int t, float4* dst, int& ci, float& cxx) __attribute__((always_inline)) {
+        const int c0 = t * KNN_TC;
+        ci = min(max(O[c0 + min(l32, N - c0 - 1)], 0), N - 1);
+        cxx = xx_pre[(size_t)b * N + ci];
+        if constexpr (MF) {
+            const float4* src = reinterpret_cast<const float4*>(X + (size_t)ci * F + h * FH);
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) dst[q] = src[q];
+        } else {
+            const float* xr = X + (size_t)ci * 3;
+            dst[0] = h ? make_float4(xr[2], 0.f, 0.f, 0.f) : make_float4(xr[0], xr[1], 0.f, 0.f);
+        }
+    };
+    int tcur = s_tl[w][0];
+    constexpr int KTILES = MF ? 1 : 2;
+    float v2[16 * KTILES];                       // the first tiles' pd (threshold start)
+    KNN_STAMP(st1);
+    fetch(tcur, cur, ci_cur, cxx_cur);
+    int scanned = 0;
+    for (int i = 0; i < nt; ++i) {
+        if (s_lb[w][i] > thr) break;             // sorted: every remaining tile is farther
+        ++scanned;
+        const int c0 = tcur * KNN_TC;
+        const int nc = min(KNN_TC, N - c0);
+        const int tnext = i + 1 < nt ? s_tl[w][i + 1] : tcur;
+        if (i + 1 < nt) fetch(tnext, nxt, ci_nxt, cxx_nxt);
+        float pd[16];
+        {
+            typedef float f32x16 __attribute__((ext_vector_type(16)));
+            f32x16 acc = {};
+            if constexpr (!MF) {
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cur[0].x, a[0], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cur[0].y, a[1], acc, 0, 0, 0);
+            } else {
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) {
+                    const float4 v = cur[q];
+                    const int s = 4 * q;
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(v.x, a[s], acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(v.y, a[s + 1], acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(v.z, a[s + 2], acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(v.w, a[s + 3], acc, 0, 0, 0);
+                }
+            }
+            if (h == 0) s_cc[w][l32] = make_float2(cxx_cur, __int_as_float(ci_cur));
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float inner = -2.f * acc[r];
+                pd[r] = __fsub_rn(__fsub_rn(-xxq, inner), s_cc[w][acc_row(r, h)].x);
+            }
+        }
+        if (i < KTILES) {
+            // the first (nearest) tile's k-th best pd of each row, then (F = 3) the first two tiles':
+            // lower bounds of the row's final k-th best -- the same pd values the scan compares, so
+            // no margin -- that start the threshold tight (no running merges to establish it).  F =
+            // 64 stops at one tile: the second tile's 16 registers cost more than its tighter start
+            // (637 vs 620 us seeded, graph 2)
+            if (i == 0) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) v2[r] = (acc_row(r, h) < nc && pd[r] == pd[r]) ? pd[r] : -INFINITY;
+                float v1[16];
+#pragma unroll
+                for (int r = 0; r < 16; ++r) v1[r] = v2[r];
+                tau = fmaxf(tau, knn_tile_kth<K, 16>(v1));
+            } else if constexpr (KTILES == 2) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) v2[16 + r] = (acc_row(r, h) < nc && pd[r] == pd[r]) ? pd[r] : -INFINITY;
+                tau = fmaxf(tau, knn_tile_kth<K, 16 * KTILES>(v2));
+            }
+            thr = loosest();
+        }
+        unsigned pm = 0;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) pm |= (acc_row(r, h) < nc && pd[r] >= tau) ? (1u << r) : 0u;
+        unsigned dropped = 0;
+        if (!ballot(cnt + __builtin_popcount(pm) > CAP)) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                sg[cnt] = make_float2(pd[r], s_cc[w][acc_row(r, h)].y);
+                cnt += (pm >> r) & 1u;
+            }
+        } else {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const bool p = (pm >> r) & 1u;
+                sg[min(cnt, CAP)] = make_float2(pd[r], s_cc[w][acc_row(r, h)].y);
+                dropped |= (p && cnt >= CAP) ? (1u << r) : 0u;
+                cnt += (p && cnt < CAP) ? 1 : 0;
+            }
+        }
+        const unsigned long long nm = ballot(dropped != 0 || cnt > CAP);
+        if (nm) {
+            unsigned rows = (unsigned)nm | (unsigned)(nm >> 32);
+            while (rows) {
+                const int r = __ffs(rows) - 1;
+                rows &= rows - 1;
+                const int c0n = (int)readlane_u((unsigned)cnt, r);
+                const int c1n = (int)readlane_u((unsigned)cnt, r + 32);
+                const int nlr = (int)readlane_u((unsigned)nl, r);
+                const float ntau = knn_select_row<K, SEG>(wl + r * KNN_RS, nlr, c0n, c1n, l);
+                ++merges;
+                const bool mine = l32 == r;
+                tau = mine ? ntau : tau;
+                cnt = mine ? 0 : cnt;
+                nl = mine ? min(nlr + c0n + c1n, K) : nl;
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const bool p = ((dropped >> r) & 1u) && pd[r] >= tau;
+                sg[min(cnt, CAP)] = make_float2(pd[r], s_cc[w][acc_row(r, h)].y);
+                cnt += p ? 1 : 0;
+            }
+            thr = loosest();
+        }
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) cur[q] = nxt[q];
+        ci_cur = ci_nxt;
+        cxx_cur = cxx_nxt;
+        tcur = tnext;
+    }
+    KNN_STAMP(st2);
+    for (int r = 0; r < 32; ++r) {
+        const int c0n = (int)readlane_u((unsigned)cnt, r);
+        const int c1n = (int)readlane_u((unsigned)cnt, r + 32);
+        const int nlr = (int)readlane_u((unsigned)nl, r);
+        const int p = tq * KNN_TC + r;
+        if (p >= N) continue;
+        const int q = (int)readlane_u((unsigned)qi, r);
+        int* o = out_idx + ((size_t)b * N + q) * K;
+        if (nlr + c0n + c1n > K) {
+            knn_select_row<K, SEG>(wl + r * KNN_RS, nlr, c0n, c1n, l);
+            knn_merge_row<K, SEG>(wl + r * KNN_RS, K, 0, 0, l, o);
+            continue;
+        }
+        knn_merge_row<K, SEG>(wl + r * KNN_RS, nlr, c0n, c1n, l, o);
+    }
+    KNN_STAMP(st3);
+#ifdef PCS_KNN_DIAG
+    if (l == 0) {
+        int* dg = g_knn_diag + 8 * ((b * nt + tq) & ((1 << 13) - 1));
+        dg[0] = scanned;
+        dg[1] = merges;
+        dg[2] = (int)(st1 - st0);
+        dg[3] = (int)(st2 - st1);
+        dg[4] = (int)(st3 - st2);
+        dg[5] = (int)(sta - st0);
+        dg[6] = (int)(stb - sta);
+    }
+#else
+    (void)scanned;
+    (void)merges;
+    (void)sta;
+    (void)stb;
+#endif
+}
+
 template <int K>
 constexpr bool knn_tiled() { return (KNN_NMAX - K) / 2 - 1 >= 16; }
 
@@ -558,6 +1120,50 @@ static void launch_knn(const float* x, int B, int N, int* out, float* xx, const 
         return;
     }
     hipLaunchKernelGGL((knn_kernel<F, K>), dim3((N + 255) / 256, B), dim3(256), 0, s, x, N, out);
+}
+
+template <int F, int K>
+static void launch_knn_pruned(const float* x, int B, int N, int* out, float* xx, const int* order, float* tinfo,
+                              const int* seeds, int ks, hipStream_t s) {
+    if constexpr (knn_tiled<K>()) {
+        if (N <= KO_MAX) {
+            const long long P = (long long)B * N;
+            const int nt = (N + KNN_TC - 1) / KNN_TC;
+            const int rb = (nt + KNN_WAVES - 1) / KNN_WAVES;
+            hipLaunchKernelGGL((knn_sqnorm_kernel<F>), dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, x, P, xx);
+            hipLaunchKernelGGL((knn_tiles_kernel<F>), dim3(nt, B), dim3(64), 0, s, x, N, order, (const float*)xx, tinfo);
+            int* sorted_t = reinterpret_cast<int*>(tinfo + (size_t)B * nt * knn_tile_stride(F));
+            float* sorted_lb = reinterpret_cast<float*>(sorted_t + (size_t)B * nt * nt);
+            hipLaunchKernelGGL((knn_pairs_kernel<F>), dim3((nt + KP_PQ - 1) / KP_PQ, B), dim3(KP_NT), 0, s,
+                               (const float*)tinfo, N, sorted_t, sorted_lb);
+            ProbeScope pr(s, 2.0 * F * (double)N * N * B, 4.0 * (double)B * N * (F + K), "pcs::knn_pruned_kernel<%d, %d, %d, %s>",
+                          F, K, KNN_WAVES, seeds ? "true" : "false");
+            if (seeds)
+                hipLaunchKernelGGL((knn_pruned_kernel<F, K, KNN_WAVES, true>), dim3(rb * B), dim3(64 * KNN_WAVES), 0, s, x, B,
+                                   N, rb, out, (const float*)xx, order, (const int*)sorted_t, (const float*)sorted_lb,
+                                   seeds, ks);
+            else
+                hipLaunchKernelGGL((knn_pruned_kernel<F, K, KNN_WAVES, false>), dim3(rb * B), dim3(64 * KNN_WAVES), 0, s, x,
+                                   B, N, rb, out, (const float*)xx, order, (const int*)sorted_t, (const float*)sorted_lb,
+                                   (const int*)nullptr, 0);
+            return;
+        }
+    }
+    launch_knn<F, K>(x, B, N, out, xx, seeds, ks, s);
+}
+
+template <int F>
+static int dispatch_pruned(const float* x, int B, int N, int k, int* out, float* xx, const int* order, float* tinfo,
+                           const int* seeds, int ks, hipStream_t s) {
+    switch (k) {
+        case 16: launch_knn_pruned<F, 16>(x, B, N, out, xx, order, tinfo, seeds, ks, s); return 0;
+        case 20: launch_knn_pruned<F, 20>(x, B, N, out, xx, order, tinfo, seeds, ks, s); return 0;
+        case 32: launch_knn<F, 32>(x, B, N, out, xx, seeds, ks, s); return 0;
+        case 40: launch_knn<F, 40>(x, B, N, out, xx, seeds, ks, s); return 0;
+        default:
+            set_error("pcs_knn_pruned: k=%d not instantiated (16, 20, 32, 40)", k);
+            return (int)hipErrorInvalidValue;
+    }
 }
 
 template <int F>
@@ -627,3 +1233,78 @@ PCS_API int pcs_knn_seeded(const float* x, int B, int N, int F, int k, const int
     float* xx = reinterpret_cast<float*>((reinterpret_cast<uintptr_t>(ws) + 255) & ~uintptr_t(255));
     return knn_run(x, B, N, F, k, out_idx, xx, seeds, ks, stream);
 }
+
+// ----------------------------------------------------------------------------- pruned kNN API
+static size_t knn_align256(size_t n) { return (n + 255) & ~size_t(255); }
+
+// Morton order of each cloud's points by their first three features (DGCNN: the xyz graph's
+// input), (B, N) int32 -- the order pcs_knn_pruned scans in.  Clouds past 8192 points get the
+// identity order (correct, unpruned in effect).
+PCS_API int pcs_knn_order(const float* x, int B, int N, int F, int32_t* order, void* stream) {
+    using namespace pcs;
+    PCS_CHECK_ARG(B >= 0 && N >= 1 && F >= 3, "pcs_knn_order: bad sizes B=%d N=%d F=%d", B, N, F);
+    PCS_CHECK_ARG(x && order, "pcs_knn_order: null pointer");
+    if (B == 0) return 0;
+    hipStream_t s = as_stream(stream);
+    if (N > KO_MAX) {
+        const long long P = (long long)B * N;
+        hipLaunchKernelGGL(knn_identity_order_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, P, N, order);
+        return launch_status("pcs_knn_order");
+    }
+    int P = 64;
+    while (P < N) P <<= 1;
+    const size_t lds = (size_t)P * sizeof(unsigned long long);
+    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&knn_order_kernel),
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                       (int)(KO_MAX * sizeof(unsigned long long)));
+    (void)attr;
+    hipLaunchKernelGGL(knn_order_kernel, dim3(B), dim3(1024), lds, s, x, N, F, P, order);
+    return launch_status("pcs_knn_order");
+}
+
+PCS_API int pcs_knn_pruned_workspace(int B, int N, int F, size_t* bytes) {
+    using namespace pcs;
+    PCS_CHECK_ARG(bytes && B >= 0 && N >= 0 && F >= 1, "pcs_knn_pruned_workspace: bad arguments");
+    const size_t nt = ((size_t)N + KNN_TC - 1) / KNN_TC;
+    // squared norms | tile fields (B, TS, nt) | scan orders (B, nt, nt) tile ids | their bounds
+    *bytes = knn_align256((size_t)B * N * sizeof(float)) + 256;
+    if (N <= KO_MAX)    // (larger clouds take the unpruned kernel: norms only)
+        *bytes += (size_t)B * nt * knn_tile_stride(F) * sizeof(float) + 2 * (size_t)B * nt * nt * sizeof(float);
+    return 0;
+}
+
+// pcs_knn_seeded (seeds nullable) scanning each cloud in `order` (pcs_knn_order's output, a
+// permutation of 0..N-1 per cloud) with tile pruning: the same lists from a fraction of the
+// candidate tiles.  Workspace: pcs_knn_pruned_workspace(B, N, F) bytes.
+PCS_API int pcs_knn_pruned(const float* x, int B, int N, int F, int k, const int32_t* order, const int32_t* seeds,
+                           int ks, int32_t* out_idx, void* ws, size_t ws_bytes, void* stream) {
+    using namespace pcs;
+    PCS_CHECK_ARG(B >= 0 && N >= 1 && k >= 1 && k <= N, "pcs_knn_pruned: bad sizes B=%d N=%d k=%d", B, N, k);
+    PCS_CHECK_ARG(x && out_idx && order, "pcs_knn_pruned: null pointer");
+    PCS_CHECK_ARG(!seeds || ks >= 1, "pcs_knn_pruned: ks < 1");
+    size_t need = 0;
+    pcs_knn_pruned_workspace(B, N, F, &need);
+    PCS_CHECK_ARG(ws && ws_bytes >= need, "pcs_knn_pruned: workspace too small (%zu < %zu)", ws_bytes, need);
+    if (B == 0) return 0;
+    hipStream_t s = as_stream(stream);
+    const uintptr_t base = (reinterpret_cast<uintptr_t>(ws) + 255) & ~uintptr_t(255);
+    float* xx = reinterpret_cast<float*>(base);
+    float* tinfo = reinterpret_cast<float*>(base + knn_align256((size_t)B * N * sizeof(float)));
+    int rc;
+    switch (F) {
+        case 3: rc = dispatch_pruned<3>(x, B, N, k, out_idx, xx, order, tinfo, seeds, ks, s); break;
+        case 64: rc = dispatch_pruned<64>(x, B, N, k, out_idx, xx, order, tinfo, seeds, ks, s); break;
+        default:
+            set_error("pcs_knn_pruned: F=%d not instantiated (3, 64)", F);
+            return (int)hipErrorInvalidValue;
+    }
+    if (rc) return rc;
+    return launch_status("pcs_knn_pruned");
+}
+
+#ifdef PCS_KNN_DIAG
+// diagnostic build only: the per-wave scanned-tile counts of the last pruned launch ((b, tile) order)
+PCS_API int pcs_knn_diag(int* out, int n) {
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(pcs::g_knn_diag), sizeof(int) * (size_t)std::min(n, 8 << 13));
+}
+#endif

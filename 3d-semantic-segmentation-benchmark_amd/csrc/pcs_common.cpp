@@ -29,7 +29,7 @@ int launch_status(const char* what) {
 
 PCS_API const char* pcs_last_error(void) { return g_err; }
 
-PCS_API int pcs_abi_version(void) { return 3; }
+PCS_API int pcs_abi_version(void) { return 4; }
 
 PCS_API int pcs_operand_size(void) { return (int)sizeof(pcs_operand); }
 

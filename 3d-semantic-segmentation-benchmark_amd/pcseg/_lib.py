@@ -51,9 +51,9 @@ class InverseMap(ctypes.Structure):
                 ('entries', P)]
 
 
-# the C ABI these bindings are written for (include/pcseg.h pcs_abi_version): 3 = round 5
-# (pcs_group_bwd_csr / pcs_interp_bwd_csr take n_slots; pcs_knn_morton_seeds gone since round 4)
-ABI_VERSION = 3
+# the C ABI these bindings are written for (include/pcseg.h pcs_abi_version): 4 = round 6
+# (pcs_knn_order / pcs_knn_pruned added; round 5: pcs_group_bwd_csr / pcs_interp_bwd_csr take n_slots)
+ABI_VERSION = 4
 OP_PLAIN, OP_BNACT, OP_BNBWD, OP_POOLBWD = 0, 1, 2, 3
 OPP = ctypes.POINTER(Operand)
 
@@ -68,6 +68,9 @@ SIGNATURES = {
     'pcs_copy_cols': [P, I32, I32, I32, P, I32, P],
     'pcs_knn_ws': [P, I32, I32, I32, I32, P, P, ctypes.c_size_t, P],
     'pcs_knn_seeded': [P, I32, I32, I32, I32, P, I32, P, P, ctypes.c_size_t, P],
+    'pcs_knn_order': [P, I32, I32, I32, P, P],
+    'pcs_knn_pruned_workspace': [I32, I32, I32, P],
+    'pcs_knn_pruned': [P, I32, I32, I32, I32, P, P, I32, P, P, ctypes.c_size_t, P],
     'pcs_group_fwd': [P, P, P, P, I32, I32, I32, I32, I32, F32, I32, P, I32, P],
     'pcs_maxk_fwd': [P, I64, I32, I32, P, P, P],
     'pcs_maxk_bwd': [P, P, I64, I32, I32, P, P],

@@ -75,19 +75,45 @@ def knn_select(query: torch.Tensor, ref: torch.Tensor, k: int = 3, out=None):
     return idx, dist
 
 
-def knn(x: torch.Tensor, k: int, seeds: torch.Tensor | None = None) -> torch.Tensor:
+def knn_order(xyz: torch.Tensor) -> torch.Tensor:
+    """Morton order (B, N) int32 of each cloud's points by their first three features (the xyz
+    graph's input): the scan order of knn(..., order=)."""
+    check_cuda(xyz)
+    xyz = _c(xyz.float())
+    B, N, Fd = xyz.shape
+    order = torch.empty((B, N), dtype=torch.int32, device=xyz.device)
+    call('pcs_knn_order', ptr(xyz), B, N, Fd, ptr(order), stream_ptr(xyz.device))
+    return order
+
+
+def knn(x: torch.Tensor, k: int, seeds: torch.Tensor | None = None,
+        order: torch.Tensor | None = None) -> torch.Tensor:
     """DGCNN feature-space kNN; x point-major (B,N,F) -> idx (B,N,k) int32.  seeds (B,N,ks)
-    int32 (the previous graph) only speed the search up: the lists are the same."""
+    int32 (the previous graph) and order (B,N) int32 (knn_order of the cloud's xyz: candidate
+    tiles are scanned nearest first and the provably farther ones skipped) only speed the
+    search up: the lists are the same."""
     check_cuda(x)
     x = _c(x.float())
     B, N, Fd = x.shape
     out = torch.empty((B, N, k), dtype=torch.int32, device=x.device)
-    ws = torch.empty((B * N + 64,), dtype=torch.float32, device=x.device)    # per-point squared norms
     if seeds is not None:
         if seeds.dtype != torch.int32 or seeds.shape[:2] != (B, N) or seeds.device != x.device:
             raise ValueError(f'knn seeds must be int32 (B, N, ks) on {x.device}, got {seeds.dtype} '
                              f'{tuple(seeds.shape)} on {seeds.device}')
         seeds = _c(seeds)
+    if order is not None:
+        if order.dtype != torch.int32 or tuple(order.shape) != (B, N) or order.device != x.device:
+            raise ValueError(f'knn order must be int32 (B, N) on {x.device}, got {order.dtype} '
+                             f'{tuple(order.shape)} on {order.device}')
+        order = _c(order)
+        nbytes = ctypes.c_size_t()
+        call('pcs_knn_pruned_workspace', B, N, Fd, ctypes.byref(nbytes))
+        ws = torch.empty(((nbytes.value + 3) // 4,), dtype=torch.float32, device=x.device)
+        call('pcs_knn_pruned', ptr(x), B, N, Fd, k, ptr(order), ptr(seeds) if seeds is not None else None,
+             seeds.shape[2] if seeds is not None else 0, ptr(out), ptr(ws), ws.numel() * 4, stream_ptr(x.device))
+        return out
+    ws = torch.empty((B * N + 64,), dtype=torch.float32, device=x.device)    # per-point squared norms
+    if seeds is not None:
         call('pcs_knn_seeded', ptr(x), B, N, Fd, k, ptr(seeds), seeds.shape[2], ptr(out), ptr(ws), ws.numel() * 4,
              stream_ptr(x.device))
         return out

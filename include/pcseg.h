@@ -27,7 +27,8 @@ extern "C" {
 #endif
 
 const char* pcs_last_error(void);
-/* 3 since round 5 (pcs_group_bwd_csr / pcs_interp_bwd_csr take n_slots, pcs_edgeconv_fwd an
+/* 4 since round 6 (added pcs_knn_order, pcs_knn_pruned, pcs_knn_pruned_workspace).
+ * 3 since round 5 (pcs_group_bwd_csr / pcs_interp_bwd_csr take n_slots, pcs_edgeconv_fwd an
  * optional second output, pcs_edgeconv_bwd the output gradient's row stride; new:
  * pcs_geometry_stream, pcs_probe_times and the kernel-variant calls; round 4 dropped
  * pcs_knn_morton_seeds and added pcs_inverse_index_batch); bindings refuse another version */
@@ -74,6 +75,18 @@ int pcs_knn_ws(const float* x, int B, int N, int F, int k, int32_t* out_idx,
  * Rows whose seeds are out of range, repeated or fewer than k search unseeded. */
 int pcs_knn_seeded(const float* x, int B, int N, int F, int k, const int32_t* seeds,
                    int ks, int32_t* out_idx, void* ws, size_t ws_bytes, void* stream);
+/* Morton order (B,N) int32 of each cloud's points by their first three features (x (B,N,F),
+ * F >= 3: DGCNN's xyz, dgcnn.py:183 / :228 graph input); clouds past 8192 points get the
+ * identity order.  Computed once per forward and shared by its four graphs. */
+int pcs_knn_order(const float* x, int B, int N, int F, int32_t* order, void* stream);
+/* pcs_knn_seeded (seeds nullable) scanning each cloud in `order` (a permutation of 0..N-1 per
+ * cloud, pcs_knn_order's output) nearest tiles first, skipping the candidate tiles that are
+ * provably farther than every row's k-th best: the same lists as pcs_knn.  Workspace:
+ * pcs_knn_pruned_workspace(B, N, F) bytes. */
+int pcs_knn_pruned_workspace(int B, int N, int F, size_t* bytes);
+int pcs_knn_pruned(const float* x, int B, int N, int F, int k, const int32_t* order,
+                   const int32_t* seeds, int ks, int32_t* out_idx, void* ws, size_t ws_bytes,
+                   void* stream);
 
 /* ---- geometry plan of a PointNet++-family forward --------------------------
  * One call enqueues, on one stream and in this order, every neighbour structure of a

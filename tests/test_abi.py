@@ -32,7 +32,7 @@ def test_library_exports_every_header_symbol():
         assert hasattr(lib, s), s
     # every typed binding corresponds to a header declaration and vice versa
     assert set(_lib.SIGNATURES) | {'pcs_last_error', 'pcs_abi_version'} == set(syms)
-    assert lib.pcs_abi_version() == _lib.ABI_VERSION == 3
+    assert lib.pcs_abi_version() == _lib.ABI_VERSION == 4
     assert lib.pcs_operand_size() == ctypes.sizeof(_lib.Operand)
 
 

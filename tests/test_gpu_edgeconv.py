@@ -230,8 +230,8 @@ def test_dgcnn_head_buffer_equals_copied_concatenation():
     fg, head = PM.EdgeConv.forward_graph, PM._dgcnn_head
     for m, old in ((m1, False), (m2, True)):
         if old:
-            PM.EdgeConv.forward_graph = lambda self, xp, seeds=None, inv_batch=None, also=None: fg(
-                self, xp, seeds, inv_batch=inv_batch)
+            PM.EdgeConv.forward_graph = lambda self, xp, seeds=None, inv_batch=None, also=None, order=None: fg(
+                self, xp, seeds, inv_batch=inv_batch, order=order)
             PM._dgcnn_head = lambda self, parts, B, N, H=None: head(self, parts, B, N, None)
         try:
             torch.manual_seed(11)           # the same dropout draws in both runs

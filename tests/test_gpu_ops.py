@@ -252,6 +252,10 @@ def test_dgcnn_knn_selection_exact_on_integer_grids(F_, lo, hi, N):
     exp = torch.sort(d.round(), dim=-1, stable=True).indices[..., :k]
     got = ops.knn(x.contiguous().to(DEV), k).cpu().long()
     assert torch.equal(got, exp)
+    # the pruned scan (Morton order of the first three features) through the same ties
+    xd_ = x.contiguous().to(DEV)
+    got_p = ops.knn(xd_, k, order=ops.knn_order(xd_)).cpu().long()
+    assert torch.equal(got_p, exp)
 
 
 @pytest.mark.parametrize('F_', [3, 64])
@@ -292,6 +296,91 @@ def test_dgcnn_knn_seeded_bitwise_equal(k):
     assert torch.equal(ops.knn(xi, k, seeds=bi), bi)
 
 
+def _knn_order_cases():
+    # (name, x (B, N, F) on DEV, xyz the order is built from)
+    g = torch.Generator().manual_seed(77)
+    out = []
+    for N in (4096, 2051, 333, 31, 8192):
+        xyz = make_batch(2, N, seed=N)[0][:, :, :3].contiguous().to(DEV)
+        out.append((f'xyz{N}', xyz, xyz))
+    xyz = make_batch(2, 4096, seed=5)[0][:, :, :3].contiguous()
+    W1, W2 = torch.randn(3, 32, generator=g), torch.randn(32, 64, generator=g)
+    smooth = (torch.tanh(xyz @ W1 * 4.0) @ W2).contiguous()            # features of the geometry
+    out.append(('smooth64', smooth.to(DEV), xyz.to(DEV)))
+    out.append(('random64', torch.randn(2, 4096, 64, generator=g).to(DEV), xyz.to(DEV)))   # no locality
+    dup = smooth.clone()
+    dup[:, 1000:1600] = dup[:, 1000:1001]                                # 600 identical points
+    out.append(('dup64', dup.contiguous().to(DEV), xyz.to(DEV)))
+    grid = torch.randint(0, 3, (2, 4096, 64), generator=g).float()
+    out.append(('grid64', grid.to(DEV), grid[:, :, :3].contiguous().to(DEV)))
+    far = xyz.clone()
+    far[:, :7] += 1e4                                                    # outliers: huge bounds / norms
+    out.append(('outliers3', far.contiguous().to(DEV), far.contiguous().to(DEV)))
+    return out
+
+
+@pytest.mark.parametrize('k', [16, 20, 32])
+def test_dgcnn_knn_pruned_bitwise_equal(k):
+    """pcs_knn_pruned (candidate tiles scanned in a per-cloud Morton order, the provably farther
+    ones skipped) gives bitwise the same lists as the full scan: clouds of 4096 / ragged / tiny /
+    8192 points (the LDS sort's limit), 64-wide features that follow the geometry, random
+    features (nothing to prune), 600 identical points, integer features (exact ties on the k-th
+    value), far outliers; with and without seeds; k = 32 takes the unpruned kernel."""
+    for name, x, xyz in _knn_order_cases():
+        if x.shape[1] < k:
+            continue
+        od = ops.knn_order(xyz)
+        base = ops.knn(x, k)
+        got = ops.knn(x, k, order=od)
+        assert torch.equal(got, base), name
+        if x.shape[2] == 64:
+            near = ops.knn((x + 0.1 * torch.randn_like(x)).contiguous(), k)
+            assert torch.equal(ops.knn(x, k, seeds=near, order=od), base), name
+
+
+def test_dgcnn_knn_order_is_a_permutation():
+    """pcs_knn_order: per cloud a permutation of 0..N-1 (ragged and tiny clouds), consecutive
+    points close in space (Morton locality); past 8192 points the identity; any permutation is
+    a valid scan order (a random one gives the same lists)."""
+    for N in (4096, 333, 5, 8192):
+        xyz = make_batch(3, N, seed=N + 1)[0][:, :, :3].contiguous().to(DEV)
+        od = ops.knn_order(xyz).long().cpu()
+        assert torch.equal(od.sort(-1).values, torch.arange(N).expand(3, N))
+        if N >= 4096:
+            p = xyz.cpu().gather(1, od[..., None].expand(-1, -1, 3))
+            step = (p[:, 1:] - p[:, :-1]).norm(dim=-1).median()
+            rnd = (xyz.cpu()[:, 1:] - xyz.cpu()[:, :-1]).norm(dim=-1).median()
+            assert step < 0.25 * rnd, (float(step), float(rnd))
+    xyz = make_batch(2, 9000, seed=3)[0][:, :, :3].contiguous().to(DEV)
+    assert torch.equal(ops.knn_order(xyz).long().cpu(), torch.arange(9000).expand(2, 9000))
+    x = make_batch(2, 4096, seed=8)[0][:, :, :3].contiguous().to(DEV)
+    perm = torch.stack([torch.randperm(4096) for _ in range(2)]).to(torch.int32).to(DEV)
+    assert torch.equal(ops.knn(x, 20, order=perm), ops.knn(x, 20))
+
+
+def test_dgcnn_knn_pruned_kernel_runs_in_model():
+    """DGCNN's forward builds one Morton order; graphs 1-3 take the pruned kernel, graph 4 the
+    seeded full scan (models.py, the note above DGCNN)."""
+    from pcseg import _lib
+    torch.manual_seed(0)
+    m = pcseg.DGCNNWithColor(14).to(DEV).train()
+    x = make_batch(2, 4096, seed=31)[0][:, :, :6].contiguous().transpose(1, 2).to(DEV)
+    names = []
+    orig = _lib.call
+
+    def spy(name, *a):
+        names.append(name)
+        return orig(name, *a)
+    pcseg.ops.call = spy
+    try:
+        with torch.no_grad():
+            m(x)
+    finally:
+        pcseg.ops.call = orig
+    assert names.count('pcs_knn_order') == 1 and names.count('pcs_knn_pruned') == 3, names
+    assert names.count('pcs_knn_seeded') == 1, names
+
+
 def test_dgcnn_model_seeded_graphs_equal_unseeded():
     """DGCNNWithColor's graphs 2-4 (seeded by the previous graph) equal the unseeded search on
     the same features (B=2, N=4096)."""
@@ -314,7 +403,7 @@ def test_dgcnn_model_seeded_graphs_equal_unseeded():
     finally:
         pcseg.models.EdgeConv.forward_graph = orig
     assert len(graphs) == 4
-    for f, gidx in zip(feats[1:], graphs[1:]):
+    for f, gidx in zip(feats, graphs):               # graph 1: pruned, unseeded; 2-4: pruned + seeded
         assert torch.equal(gidx, ops.knn(f, 20))
 
 
