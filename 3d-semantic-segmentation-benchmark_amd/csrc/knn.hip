@@ -624,17 +624,22 @@ __global__ __launch_bounds__(1024) void knn_order_kernel(const float* __restrict
         s_key[i] = key;
     }
     __syncthreads();
+    // bitonic network.  Thread t handles pairs i = t + 1024 m, so for j < 64 a wave only touches its
+    // own 128-key blocks: stages between two such stages need no block barrier (a wave's LDS
+    // accesses complete in order), only a wave-level fence; a barrier follows every stage whose
+    // successor may be j >= 64 (j >= 64 itself, and j = 1, the last stage of a merge)
     for (int k = 2; k <= P; k <<= 1) {
         for (int j = k >> 1; j > 0; j >>= 1) {
             for (int i = tid; i < (P >> 1); i += 1024) {
-                const int a = 2 * j * (i / j) + (i % j), c = a + j;
+                const int a = ((i & ~(j - 1)) << 1) | (i & (j - 1)), c = a + j;
                 const unsigned long long u = s_key[a], v = s_key[c];
                 if ((u > v) == ((a & k) == 0)) {
                     s_key[a] = v;
                     s_key[c] = u;
                 }
             }
-            __syncthreads();
+            if (j >= 64 || j == 1) __syncthreads();
+            else knn_wave_sync();
         }
     }
     for (int i = tid; i < N; i += 1024) order[(size_t)b * N + i] = (int)(unsigned)(s_key[i] & 0xffffffffull);
