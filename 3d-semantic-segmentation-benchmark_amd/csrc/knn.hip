@@ -660,32 +660,45 @@ __global__ __launch_bounds__(64) void knn_tiles_kernel(const float* __restrict__
                                                        const float* __restrict__ xx, float* __restrict__ tinfo) {
     static_assert(F <= 64, "one lane per feature");
     constexpr int TS = knn_tile_stride(F);
+    __shared__ float s_t[KNN_TC][F + 1];           // the tile minus its centroid, point-major
     const int t = blockIdx.x, b = blockIdx.y, l = threadIdx.x;
     const int nt = (N + KNN_TC - 1) / KNN_TC;
     const int p0 = t * KNN_TC, np = min(KNN_TC, N - p0);
     const float* X = x + (size_t)b * N * F;
     const int* O = order + (size_t)b * N;
+    // lane j < np holds point j's index; the feature loads then need no dependent index load
+    const int myo = l < np ? min(max(O[p0 + l], 0), N - 1) : 0;
+    float v[KNN_TC];
+#pragma unroll
+    for (int j = 0; j < KNN_TC; ++j) {
+        const int oi = (int)readlane_u((unsigned)myo, j);
+        v[j] = (j < np && l < F) ? X[(size_t)oi * F + l] : 0.f;
+    }
     float lo = INFINITY, hi = -INFINITY, sum = 0.f;
     bool bad = false;
-    for (int j = 0; j < np; ++j) {
-        const int oi = min(max(O[p0 + j], 0), N - 1);
-        const float v = l < F ? X[(size_t)oi * F + l] : 0.f;
-        bad = bad || !(fabsf(v) <= 3.4e38f);
-        lo = fminf(lo, v);
-        hi = fmaxf(hi, v);
-        sum += v;
+#pragma unroll
+    for (int j = 0; j < KNN_TC; ++j) {
+        if (j < np) {
+            bad = bad || !(fabsf(v[j]) <= 3.4e38f);
+            lo = fminf(lo, v[j]);
+            hi = fmaxf(hi, v[j]);
+            sum += v[j];
+        }
     }
     const float cen = sum / (float)np;
-    float r2 = 0.f;
-    for (int j = 0; j < np; ++j) {
-        const int oi = min(max(O[p0 + j], 0), N - 1);
-        const float v = l < F ? X[(size_t)oi * F + l] : 0.f;
-        float d = l < F ? (v - cen) * (v - cen) : 0.f;
+    if (l < F) {
 #pragma unroll
-        for (int m = 32; m >= 1; m >>= 1) d += __shfl_xor(d, m);
-        r2 = fmaxf(r2, d);
+        for (int j = 0; j < KNN_TC; ++j) s_t[j][l] = v[j] - cen;
     }
-    float mxx = l < np ? xx[(size_t)b * N + min(max(O[p0 + l], 0), N - 1)] : 0.f;
+    __syncthreads();
+    float r2 = 0.f;                                  // lane j: point j's squared distance to the centroid
+    if (l < np) {
+#pragma unroll 8
+        for (int d = 0; d < F; ++d) r2 = fmaf(s_t[l][d], s_t[l][d], r2);
+    }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) r2 = fmaxf(r2, __shfl_xor(r2, m));
+    float mxx = l < np ? xx[(size_t)b * N + myo] : 0.f;
     bad = bad || !(fabsf(mxx) <= 3.4e38f);
 #pragma unroll
     for (int m = 32; m >= 1; m >>= 1) mxx = fmaxf(mxx, __shfl_xor(mxx, m));
@@ -702,27 +715,11 @@ __global__ __launch_bounds__(64) void knn_tiles_kernel(const float* __restrict__
     }
 }
 
-// lower bound of the pd margin below which tile `ti` cannot reach any row of tile `tq` (squared
-// feature distance, deflated for rounding); -inf when unusable (NaN / overflow)
-template <int F>
-__device__ __forceinline__ float knn_tile_bound(const float* __restrict__ TI, int nt, int tq, int t) {
-    float cd = 0.f, gap = 0.f;
-#pragma unroll 8
-    for (int d = 0; d < F; ++d) {
-        const float cq = TI[d * nt + tq], ct = TI[d * nt + t];
-        const float lq = TI[(F + d) * nt + tq], hq = TI[(2 * F + d) * nt + tq];
-        const float lt = TI[(F + d) * nt + t], ht = TI[(2 * F + d) * nt + t];
-        const float df = cq - ct;
-        cd = fmaf(df, df, cd);
-        const float g = fmaxf(fmaxf(lq - ht, lt - hq), 0.f);
-        gap = fmaf(g, g, gap);
-    }
-    const float rs = TI[3 * F * nt + tq] + TI[3 * F * nt + t];
-    float sph = fmaxf(sqrtf(cd) * (1.f - 0x1p-10f) - rs, 0.f);
-    sph *= sph;
-    const float lb = fmaxf(sph, gap) * (1.f - 0x1p-10f) - 0x1p-13f * (TI[(3 * F + 1) * nt + tq] + TI[(3 * F + 1) * nt + t]);
-    return (lb == lb && rs == rs && cd == cd) ? lb : -INFINITY;
-}
+// The tile-pair bound (knn_pairs_kernel): a lower bound of the squared feature distance between any
+// row of query tile q and any candidate of tile c -- the larger of the sphere bound
+// (|cen_q - cen_c| - r_q - r_c)^2 and the box-gap bound sum_d max(lo_q - hi_c, lo_c - hi_q, 0)^2,
+// deflated by 2^-10 for its own fp32 rounding and by 2^-13 (max|x_q|^2 + max|x_c|^2) for the
+// rounding of the pd the scan computes; -inf when unusable (NaN / overflow).
 
 // The k-th largest of a row's values over one or two tiles: M = 16 or 32 per lane half (-inf for
 // invalid slots).  Each half sorts its M (bitonic network, descending), takes the partner half's
@@ -760,43 +757,91 @@ __device__ __forceinline__ float knn_tile_kth(const float (&pd)[M]) {
     return best;
 }
 
-// Per cloud and query tile: every candidate tile's bound (knn_tile_bound), sorted ascending (ties by
-// tile) -> the scan order of the pruned kernel, (B, nt, nt) tile ids and their bounds.  One block
-// per (KP_PQ query tiles, cloud): thread t reads candidate tile t's fields once (coalesced) for all
-// KP_PQ query tiles, then ranks within LDS.
-constexpr int KP_PQ = 4;
+// Per cloud and query tile: every candidate tile's bound (the tile-pair bound above), sorted
+// ascending (ties by tile) -> the scan order of the pruned kernel, (B, nt, nt) tile ids and their
+// bounds.  One block of 4 waves per (KP_PQ query tiles, cloud): thread t computes candidate tile t's
+// bounds against all KP_PQ query tiles (its fields read once, coalesced, dimension-outer; the query
+// tiles' fields are block-uniform), as (order-preserving bound bits, tile) 64-bit keys in LDS; then
+// each wave bitonic-sorts KP_PQ / 4 rows of keys (one compare-exchange pair per lane and stage, wave
+// fences only).
+constexpr int KP_PQ = 8;
 template <int F>
-__global__ __launch_bounds__(KP_NT) void knn_pairs_kernel(const float* __restrict__ tinfo, int N, int* __restrict__ sorted_t,
-                                                       float* __restrict__ sorted_lb) {
+__global__ __launch_bounds__(256) void knn_pairs_kernel(const float* __restrict__ tinfo, int N, int* __restrict__ sorted_t,
+                                                     float* __restrict__ sorted_lb) {
     constexpr int TS = knn_tile_stride(F);
-    __shared__ float s_b[KP_PQ][KP_NT];
-    const int b = blockIdx.y, t = threadIdx.x;
+    __shared__ unsigned long long s_k[KP_PQ][KP_NT];
+    __shared__ __attribute__((aligned(16))) float s_q[3][F][KP_PQ];     // the query tiles' fields, row-minor
+    const int b = blockIdx.y, tid = threadIdx.x, w = tid >> 6, l = tid & 63;
     const int nt = (N + KNN_TC - 1) / KNN_TC;
+    int P = 64;                                    // keys per row: nt padded to a power of two
+    while (P < nt) P <<= 1;
     const int tq0 = blockIdx.x * KP_PQ;
     const float* TI = tinfo + (size_t)b * nt * TS;
-#pragma unroll
-    for (int r = 0; r < KP_PQ; ++r) {
-        const int tq = min(tq0 + r, nt - 1);
-        s_b[r][t] = t < nt ? knn_tile_bound<F>(TI, nt, tq, t) : INFINITY;
+    float* const sq = &s_q[0][0][0];
+    for (int e = tid; e < 3 * F * KP_PQ; e += 256) {
+        const int r = e % KP_PQ, fd = e / KP_PQ;                       // fd = field * F + d
+        sq[e] = TI[fd * nt + min(tq0 + r, nt - 1)];
     }
     __syncthreads();
-    if (t >= nt) return;
+    for (int t = tid; t < P; t += 256) {
+        if (t >= nt) {
 #pragma unroll
-    for (int r = 0; r < KP_PQ; ++r) {
+            for (int r = 0; r < KP_PQ; ++r) s_k[r][t] = ~0ull;
+            continue;
+        }
+        int tqr[KP_PQ];
+#pragma unroll
+        for (int r = 0; r < KP_PQ; ++r) tqr[r] = min(tq0 + r, nt - 1);
+        float cd[KP_PQ], gap[KP_PQ];
+#pragma unroll
+        for (int r = 0; r < KP_PQ; ++r) cd[r] = gap[r] = 0.f;
+#pragma unroll 4
+        for (int d = 0; d < F; ++d) {
+            const float ct = TI[d * nt + t], lt = TI[(F + d) * nt + t], ht = TI[(2 * F + d) * nt + t];
+#pragma unroll
+            for (int r = 0; r < KP_PQ; ++r) {
+                const float cq = s_q[0][d][r], lq = s_q[1][d][r], hq = s_q[2][d][r];
+                const float df = cq - ct;
+                cd[r] = fmaf(df, df, cd[r]);
+                const float g = fmaxf(fmaxf(lq - ht, lt - hq), 0.f);
+                gap[r] = fmaf(g, g, gap[r]);
+            }
+        }
+        const float rt = TI[3 * F * nt + t], mt = TI[(3 * F + 1) * nt + t];
+#pragma unroll
+        for (int r = 0; r < KP_PQ; ++r) {
+            const float rs = TI[3 * F * nt + tqr[r]] + rt;
+            float sph = fmaxf(sqrtf(cd[r]) * (1.f - 0x1p-10f) - rs, 0.f);
+            sph *= sph;
+            float lb = fmaxf(sph, gap[r]) * (1.f - 0x1p-10f) - 0x1p-13f * (TI[(3 * F + 1) * nt + tqr[r]] + mt);
+            lb = (lb == lb && rs == rs && cd[r] == cd[r]) ? lb : -INFINITY;
+            s_k[r][t] = ((unsigned long long)knn_key(lb) << 32) | (unsigned)t;     // ascending bound, then tile
+        }
+    }
+    __syncthreads();
+    for (int r = w; r < KP_PQ; r += 4) {
         const int tq = tq0 + r;
         if (tq >= nt) break;
-        const float v = s_b[r][t];
-        int rk = 0;
-        for (int u = 0; u < nt; u += 4) {
-            const float4 o = *reinterpret_cast<const float4*>(&s_b[r][u]);
-            rk += (u + 0 < nt && (o.x < v || (o.x == v && u + 0 < t))) ? 1 : 0;
-            rk += (u + 1 < nt && (o.y < v || (o.y == v && u + 1 < t))) ? 1 : 0;
-            rk += (u + 2 < nt && (o.z < v || (o.z == v && u + 2 < t))) ? 1 : 0;
-            rk += (u + 3 < nt && (o.w < v || (o.w == v && u + 3 < t))) ? 1 : 0;
+        unsigned long long* K = s_k[r];
+        for (int k = 2; k <= P; k <<= 1) {
+            for (int j = k >> 1; j > 0; j >>= 1) {
+                for (int i = l; i < (P >> 1); i += 64) {
+                    const int a = ((i & ~(j - 1)) << 1) | (i & (j - 1)), c = a + j;
+                    const unsigned long long u = K[a], v = K[c];
+                    if ((u > v) == ((a & k) == 0)) {
+                        K[a] = v;
+                        K[c] = u;
+                    }
+                }
+                knn_wave_sync();
+            }
         }
         const size_t row = ((size_t)b * nt + tq) * nt;
-        sorted_t[row + rk] = t;
-        sorted_lb[row + rk] = v;
+        for (int i = l; i < nt; i += 64) {
+            const unsigned long long key = K[i];
+            sorted_t[row + i] = (int)(unsigned)(key & 0xffffffffull);
+            sorted_lb[row + i] = knn_unkey((unsigned)(key >> 32));
+        }
     }
 }
 
@@ -1139,7 +1184,7 @@ static void launch_knn_pruned(const float* x, int B, int N, int* out, float* xx,
             hipLaunchKernelGGL((knn_tiles_kernel<F>), dim3(nt, B), dim3(64), 0, s, x, N, order, (const float*)xx, tinfo);
             int* sorted_t = reinterpret_cast<int*>(tinfo + (size_t)B * nt * knn_tile_stride(F));
             float* sorted_lb = reinterpret_cast<float*>(sorted_t + (size_t)B * nt * nt);
-            hipLaunchKernelGGL((knn_pairs_kernel<F>), dim3((nt + KP_PQ - 1) / KP_PQ, B), dim3(KP_NT), 0, s,
+            hipLaunchKernelGGL((knn_pairs_kernel<F>), dim3((nt + KP_PQ - 1) / KP_PQ, B), dim3(256), 0, s,
                                (const float*)tinfo, N, sorted_t, sorted_lb);
             ProbeScope pr(s, 2.0 * F * (double)N * N * B, 4.0 * (double)B * N * (F + K), "pcs::knn_pruned_kernel<%d, %d, %d, %s>",
                           F, K, KNN_WAVES, seeds ? "true" : "false");

@@ -399,8 +399,8 @@ def _head_seq(cin, cout, dropout):
 # Graphs 1-3 of a DGCNN forward take the pruned kNN (ops.knn(order=): candidate tiles of the
 # Morton-ordered cloud scanned nearest first, the provably farther ones skipped; the same lists).
 # The fourth graph is built on conv3's features, which follow the geometry least: the pruned scan
-# still reads 0.57 of its tiles (block-max; 0.25-0.34 for graphs 1-3) and measured slower than
-# the seeded full scan (1006 vs 951 us at B=32, profiles/r06_knn_pruned.txt).
+# still reads 0.57 of its tiles (block-max; 0.25-0.34 for graphs 1-3) and measured no faster than
+# the seeded full scan (956 vs 953 us at B=32, profiles/r06_knn_pruned.txt).
 
 
 class DGCNN(nn.Module):

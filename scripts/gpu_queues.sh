@@ -13,7 +13,7 @@ for m in $models; do
      > "$GRAFT_REPO_ROOT/$out/prof_$m.log" 2>&1 || exit $?
   cd "$GRAFT_REPO_ROOT"
   f=$(find $out/prof_$m -name '*kernel_trace.csv' | head -1)
-  mk=fps_kernel\<512; [ $m = dgcnn ] && mk=knn_wave_kernel\<3; [ $m = pointnext ] && mk=fps_cull_kernel\<1024
+  mk=fps_kernel\<512; [ $m = dgcnn ] && mk=knn_order_kernel; [ $m = pointnext ] && mk=fps_cull_kernel\<1024
   python3 scripts/queue_breakdown.py "$f" "$mk" > $out/queue_$m.txt; head -40 $out/queue_$m.txt
   python3 scripts/timeline.py "$f" 2 "$mk" > $out/timeline_$m.txt
 done
